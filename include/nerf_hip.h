@@ -1,0 +1,174 @@
+/*
+ * nerf_hip.h -- C-ABI of the MI355X-native NoPe-NeRF render + training hot path.
+ *
+ * The reference (js0n-lai/my-nope-nerf) is pure Python/PyTorch and has no FFI; its
+ * "plugin boundary" for this path is the Python call chain
+ *   Trainer.train_step -> nope_nerf.forward -> Renderer.nope_nerf -> OfficialStaticNerf.forward
+ *   -> Loss.forward -> loss.backward -> Adam.step
+ * (model/training.py:70-100, model/network.py:19-33, model/rendering.py:36-168,
+ *  model/official_nerf.py:60-119, model/losses.py:164-228).  Each entry point below
+ * replaces the ATen work one of those functions launches;
+ * the replaced reference lines are cited per function.  The host side that binds
+ * these symbols is my-nope-nerf_amd/model/_hip.py (ctypes); INTEGRATION.md shows it.
+ *
+ * Conventions (all entry points):
+ *  - plain device pointers (fp32 unless stated, row-major, 16-byte aligned),
+ *    element counts / leading dimensions in elements, a hipStream_t passed as void*;
+ *  - nothing allocates, nothing synchronises the host: work is enqueued on `stream`;
+ *  - return 0 on success, a negative NERF_E* code on a bad argument or launch
+ *    failure; nerf_hip_last_error() returns the message (thread-local).
+ */
+#ifndef NERF_HIP_H
+#define NERF_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NERF_OK 0
+#define NERF_EINVAL (-1)   /* bad argument (null pointer, shape, alignment) */
+#define NERF_ELAUNCH (-2)  /* hipGetLastError after a launch */
+
+/* Row tile of every per-sample GEMM: sample buffers are padded to a multiple of it. */
+#define NERF_ROW_TILE 128
+
+int nerf_hip_abi_version(void);
+const char* nerf_hip_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * Samples + positional encodings.
+ * Replaces Renderer.sample_uniform / sample_ndc z + pts (rendering.py:169-198,
+ * linspace :89-90) and encode_position (official_nerf.py:99-119, L=10 / L=4).
+ * pts = pts_o[r] + pts_d[r] * z[r,s];  z = lerp(near,far,s/(S-1)) jittered by
+ * noise[r,s] in its stratified bin when noise != NULL (rendering.py:187-191).
+ * view[r] is the (already negated) direction fed to the colour branch.
+ * enc_p : [n_pad][64]  = [x(3), sin(2^i x)(3), cos(2^i x)(3) ... i<10, 0]   (63 + 1 pad)
+ * enc_d : [n_pad][64]  = same with L=4 on view (27 + 37 pad)
+ * z     : [n_pad]; rows >= R*S of all outputs are written as 0.
+ */
+int nerf_encode_samples(const float* pts_o, const float* pts_d, const float* view,
+                        const float* noise, int n_rays, int n_samples, int n_pad,
+                        float near_z, float far_z, float* z, float* enc_p, float* enc_d,
+                        void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Linear layer forward on FP32 MFMA (v_mfma_f32_32x32x2_f32).
+ * Replaces nn.Linear (+ReLU) and the skip / colour torch.cat of
+ * OfficialStaticNerf.infer_occ / forward (official_nerf.py:62-64, 88-91).
+ *   y[m, n] = act( sum_k x1[m,k] w[n,k] + sum_k x2[m,k] w[n,k1+k] + bias[n] )
+ * x1: [m][ldx1] (k1 cols used), x2: [m][ldx2] (k2 cols, may be NULL with k2 = 0),
+ * w : [n][k1+k2] (padded packed weight), y: [m][ldy]. m % 128 == 0, n % 64 == 0,
+ * k1 % 32 == 0, k2 % 32 == 0. relu: 0/1.
+ */
+int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2, int k2,
+                    const float* w, const float* bias, float* y, int ldy, int m, int n,
+                    int relu, void* stream);
+
+/* Backward w.r.t. the layer input (autograd of official_nerf.py:62-91).
+ *   dx[m, j] = ( sum_o dy[m,o] wt[j,o]  + (u ? u[m*ldu] * v[j] : 0) ) * (mask ? (mask[m,j] > 0) : 1)
+ * wt: [n][k] = transpose of the packed weight restricted to the wanted input columns
+ * (n = number of input columns produced, k = layer outputs), mask: post-ReLU
+ * activation of the previous layer ([m][ldmask]) or NULL.  m%128==0, n%64==0, k%32==0. */
+int nerf_linear_bwd_data(const float* dy, int lddy, int k, const float* wt,
+                         const float* u, int ldu, const float* v, const float* mask, int ldmask,
+                         float* dx, int lddx, int m, int n, void* stream);
+
+/* Backward w.r.t. weight and bias, split over sample rows:
+ *   slab[split][o][col0 + j] = sum_{rows of split} dy[row, o] * x[row, j]   (j < kin)
+ *   bslab[split][o]          = sum_{rows of split} dy[row, o]   (if bslab != NULL)
+ * dy: [m][lddy] (nout columns), x: [m][ldx] (kin columns), slab row stride ldslab.
+ * Rows are split into `splits` equal chunks; nout % 64 == 0, kin % 64 == 0,
+ * m % (32*splits) == 0. */
+int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const float* x, int ldx,
+                           int kin, int m, int splits, float* slab, int ldslab, int col0,
+                           float* bslab, void* stream);
+
+/* Sum the split-K slabs (slab[split][nout][ldslab], bslab[split][nout]) into a
+ * parameter gradient in the reference layout (unpadded gw[nout_ref][kin_ref],
+ * gb[nout_ref]); accumulate != 0 adds into gw/gb. */
+int nerf_slab_reduce(const float* slab, int splits, int nout, int ldslab, int nout_ref,
+                     int kin_ref, const float* bslab, float* gw, float* gb, int accumulate,
+                     void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Output heads (density + colour logits), forward and backward.
+ * Replaces fc_density and fc_rgb (official_nerf.py:66, 91).
+ *   raw4[s] = ( h8[s].wd + bd,  hr[s].Wc[c] + bc[c] for c<3 )
+ * h8: [n_pad][256] trunk output, hr: [n_pad][128] colour hidden (D/2), hidden = D. */
+int nerf_heads_fwd(const float* h8, int ld8, const float* hr, int ldr, int hidden,
+                   const float* wd, const float* bd, const float* wc, const float* bc,
+                   float* raw4, int n_pad, void* stream);
+
+/* graw4[s] = dL/draw4[s].  Writes dyr = (graw4[s,1:4] @ Wc) * (hr > 0)  [n_pad][hidden/2]
+ * and per-block partial sums of dWc (3 x hidden/2), dbc (3), dwd (hidden), dbd (1) into
+ * part[blocks][4*hidden/2... ] -- see nerf_heads_part_size(). */
+int nerf_heads_part_size(int hidden, int n_pad);
+int nerf_heads_bwd(const float* graw4, const float* h8, int ld8, const float* hr, int ldr,
+                   int hidden, const float* wc, float* dyr, int lddyr, float* part, int n_pad,
+                   void* stream);
+/* Reduce the heads partials into gwd[hidden], gbd[1], gwc[3][hidden/2], gbc[3]. */
+int nerf_heads_reduce(const float* part, int hidden, int n_pad, float* gwd, float* gbd,
+                      float* gwc, float* gbc, int accumulate, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Fused per-ray compositing: sigma->alpha, exclusive transmittance product with
+ * eps = 1e-6, weighted sums (rendering.py:113-141, official_nerf.py:77-83, 92).
+ *   flags bit0: dist_alpha (alpha = 1-exp(-sigma*delta), delta_last = 1e10, alpha_last = 1)
+ *         bit1: white_background       bit2: occ_activation relu (else softplus)
+ * Outputs rgb[R][3], dist[R], alpha[R*S]. One wavefront per ray (S <= 1024). */
+int nerf_composite_fwd(const float* raw4, const float* z, int n_rays, int n_samples, int flags,
+                       float* rgb, float* dist, float* alpha, void* stream);
+
+/* Backward of nerf_composite_fwd: grad_rgb[R][3], grad_dist[R] -> graw4[R*S][4]
+ * (rows >= R*S up to n_pad are zeroed). */
+int nerf_composite_bwd(const float* raw4, const float* z, int n_rays, int n_samples, int flags,
+                       const float* grad_rgb, const float* grad_dist, float* graw4, int n_pad,
+                       void* stream);
+
+/* Gradient w.r.t. the ray inputs of nerf_encode_samples (pose learning):
+ * genc_p[s][64], genc_d[s][64] -> per ray g_pts_o[R][3] = sum_s dL/dpts,
+ * g_pts_d[R][3] = sum_s z dL/dpts, g_view[R][3] = sum_s dL/dview. */
+int nerf_encode_bwd(const float* pts_o, const float* pts_d, const float* view, const float* z,
+                    const float* genc_p, const float* genc_d, int n_rays, int n_samples,
+                    float* g_pts_o, float* g_pts_d, float* g_view, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Weight packing: src [rows][cols] (reference nn.Linear layout) -> dst [rows][ld_dst]
+ * zero padded, and (if dst_t != NULL) its transpose dst_t[c][r] (row stride ld_t,
+ * rows c >= cols zero).  Padding rows/cols outside the written ranges keep their
+ * previous contents (callers zero the buffers once).  Up to NERF_MAX_PACK descriptors. */
+#define NERF_MAX_PACK 16
+typedef struct {
+    const float* src;
+    float* dst;    /* [rows][ld_dst] */
+    float* dst_t;  /* [rows_t][ld_t] or NULL */
+    int rows, cols, ld_dst, rows_t, ld_t;
+} nerf_pack_desc;
+int nerf_pack_weights(const nerf_pack_desc* descs, int n, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Adam (torch.optim.Adam semantics, amsgrad False) over one flat fp32 buffer.
+ * Replaces optimizer.step() (training.py:93-99). */
+int nerf_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                   int64_t n, float lr, float beta1, float beta2, float eps,
+                   float weight_decay, int step, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Brute-force nearest neighbour for the dense point-cloud loss
+ * (losses.py:129-150): idx[i] = argmin_j |x[i] - y[j]| (first index on ties).
+ * x: [p][3], y: [q][3] fp32, idx: int64 [p]. */
+int nerf_chamfer_nn(const float* x, int p, const float* y, int q, int64_t* idx, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Timing hooks for bench.py: when enabled, every GEMM launch is bracketed by
+ * hipEvents on its stream; nerf_prof_read returns the summed milliseconds and
+ * launch count of the GEMM family since the last reset (synchronises events). */
+int nerf_prof_enable(int on);
+int nerf_prof_read(double* gemm_ms, int64_t* gemm_launches, double* gemm_flops);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NERF_HIP_H */

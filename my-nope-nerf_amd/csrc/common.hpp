@@ -1,0 +1,62 @@
+// Shared helpers for the nerf_hip C-ABI (error reporting, argument checks, wave utilities).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstdarg>
+
+#include "../../include/nerf_hip.h"
+
+namespace nerf {
+
+// thread-local last error message (nerf_hip_last_error)
+void set_error(const char* fmt, ...);
+
+#define NERF_CHECK(cond, ...)                     \
+    do {                                          \
+        if (!(cond)) {                            \
+            ::nerf::set_error(__VA_ARGS__);       \
+            return NERF_EINVAL;                   \
+        }                                         \
+    } while (0)
+
+#define NERF_CHECK_PTR(p) NERF_CHECK((p) != nullptr, "%s: null pointer '%s'", __func__, #p)
+#define NERF_CHECK_ALIGN16(p) \
+    NERF_CHECK((((uintptr_t)(p)) & 15u) == 0, "%s: pointer '%s' not 16-byte aligned", __func__, #p)
+
+inline int check_launch(const char* fn) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("%s: launch failed: %s", fn, hipGetErrorString(e));
+        return NERF_ELAUNCH;
+    }
+    return NERF_OK;
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// GEMM timing hooks (prof.cpp)
+void prof_begin(hipStream_t s);
+void prof_end(hipStream_t s, double flops);
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// torch.nn.functional.softplus(x, beta=1, threshold=20)
+__device__ __forceinline__ float softplus_f(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+// its derivative as torch computes it (z = exp(x); z / (z + 1)), 1 above the threshold
+__device__ __forceinline__ float softplus_grad_f(float x) {
+    if (x > 20.f) return 1.f;
+    float z = expf(x);
+    return z / (z + 1.f);
+}
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + expf(-x)); }
+
+}  // namespace nerf

@@ -1,0 +1,425 @@
+// FP32 MFMA GEMMs for the NeRF field MLP (forward, backward-data, backward-weight).
+//
+// Replaces the cuBLAS SGEMM (addmm) + ReLU + torch.cat work of
+// OfficialStaticNerf.infer_occ/forward (official_nerf.py:60-96) and its autograd
+// backward (training.py:92), SURVEY.md section 2.1 K4/K12.
+//
+// Design (gfx950):
+//  * exact-f32 v_mfma_f32_32x32x2_f32 (64 FLOP/clk/SIMD, the f32 peak; no xf32 on
+//    CDNA4) so results stay an f32 fma chain -> 1e-4 parity with the fp32 reference;
+//  * 256-thread workgroups (4 waves), block tile BM x BN, BK = 32, LDS k-major
+//    images As[k][m], Bs[k][n] double-buffered, register-staged global loads issued
+//    before the MFMA block of the current tile (one barrier per K tile);
+//  * K-contiguous operands (activations [m][k], weights [n][k]) are transposed while
+//    staging: 16-B global loads, 4 ds_write_b32 into rows padded to BM+1 floats,
+//    which keeps both the stores and the per-lane MFMA operand reads conflict-free;
+//  * sample-major operands of the weight gradient (dy[s][o], x[s][j]) are already
+//    k-major: 16-B loads and ds_write_b128 into rows padded to BM+4 floats;
+//  * fused epilogues: +bias/ReLU (forward), rank-1 add + ReLU-mask (backward-data),
+//    split-K slab + bias-gradient column sums (backward-weight).
+#include "common.hpp"
+
+namespace nerf {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BK = 32;
+constexpr int kThreads = 256;
+
+// ---------------------------------------------------------------------------
+// shared MFMA block: acc[TM][TN] += As[k][wm0..] x Bs[k][wn0..] over BK
+// ---------------------------------------------------------------------------
+template <int TM, int TN, int LDA, int LDB>
+__device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const float* __restrict__ Bs,
+                                          int wm0, int wn0, f32x16 (&acc)[TM][TN]) {
+    const int lane = lane_id();
+    const int l32 = lane & 31;
+    const int hi = lane >> 5;
+#pragma unroll
+    for (int kp = 0; kp < BK / 2; ++kp) {
+        const int k = 2 * kp + hi;
+        float a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = As[k * LDA + wm0 + 32 * i + l32];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = Bs[k * LDB + wn0 + 32 * j + l32];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+}
+
+// accumulator register r of a 32x32 tile -> row offset inside the tile (gfx950 C/D map)
+__device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
+
+// ---------------------------------------------------------------------------
+// NT GEMM: C[m][n] = epi( sum_k A[m][k] B[n][k] ), A from up to two K segments.
+// ---------------------------------------------------------------------------
+struct NTArgs {
+    const float* a1; int lda1; int k1;
+    const float* a2; int lda2; int k2;
+    const float* b;  int ldb;           // [n][k1+k2]
+    const float* bias;                  // fwd
+    const float* u;  const float* v;    // bwd-data rank-1 term u[m*ldu] v[n]
+    int ldu;
+    const float* mask; int ldmask;      // bwd-data ReLU mask (x > 0)
+    float* c; int ldc;
+    int m, n;
+    int relu;
+};
+
+enum { EPI_FWD = 0, EPI_BWD = 1 };
+
+template <int BM, int BN, int WAVES_M, int EPI>
+__global__ __launch_bounds__(kThreads) void k_gemm_nt(NTArgs p) {
+    constexpr int WAVES_N = 4 / WAVES_M;
+    constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int LDA = BM + 1, LDB = BN + 1;
+    constexpr int A_F4 = BM * BK / 4 / kThreads;  // float4 per thread
+    constexpr int B_F4 = BN * BK / 4 / kThreads;
+    static_assert(A_F4 >= 1 && B_F4 >= 1, "tile too small");
+
+    __shared__ __attribute__((aligned(16))) float smem[2 * BK * (LDA + LDB)];
+    auto As = [&](int buf) { return smem + buf * BK * LDA; };
+    auto Bs = [&](int buf) { return smem + 2 * BK * LDA + buf * BK * LDB; };
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int wm0 = (wave / WAVES_N) * WTM;
+    const int wn0 = (wave % WAVES_N) * WTN;
+    const int m0 = blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const int ktot = p.k1 + p.k2;
+    const int nkt = ktot / BK;
+
+    float4 ra[A_F4], rb[B_F4];
+
+    auto load_tile = [&](int kt) {
+        const int kk = kt * BK;
+        const float* abase;
+        int lda, kc0;
+        if (kk < p.k1) { abase = p.a1; lda = p.lda1; kc0 = kk; }
+        else           { abase = p.a2; lda = p.lda2; kc0 = kk - p.k1; }
+#pragma unroll
+        for (int i = 0; i < A_F4; ++i) {
+            const int idx = tid + kThreads * i;
+            const int row = idx >> 3, kc = idx & 7;
+            ra[i] = *reinterpret_cast<const float4*>(abase + (size_t)(m0 + row) * lda + kc0 + 4 * kc);
+        }
+#pragma unroll
+        for (int i = 0; i < B_F4; ++i) {
+            const int idx = tid + kThreads * i;
+            const int row = idx >> 3, kc = idx & 7;
+            rb[i] = *reinterpret_cast<const float4*>(p.b + (size_t)(n0 + row) * p.ldb + kk + 4 * kc);
+        }
+    };
+    auto store_tile = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < A_F4; ++i) {
+            const int idx = tid + kThreads * i;
+            const int row = idx >> 3, kc = idx & 7;
+            float* d = As(buf) + (4 * kc) * LDA + row;
+            d[0] = ra[i].x; d[LDA] = ra[i].y; d[2 * LDA] = ra[i].z; d[3 * LDA] = ra[i].w;
+        }
+#pragma unroll
+        for (int i = 0; i < B_F4; ++i) {
+            const int idx = tid + kThreads * i;
+            const int row = idx >> 3, kc = idx & 7;
+            float* d = Bs(buf) + (4 * kc) * LDB + row;
+            d[0] = rb[i].x; d[LDB] = rb[i].y; d[2 * LDB] = rb[i].z; d[3 * LDB] = rb[i].w;
+        }
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nkt) load_tile(kt + 1);
+        mfma_tile<TM, TN, LDA, LDB>(As(cur), Bs(cur), wm0, wn0, acc);
+        if (kt + 1 < nkt) store_tile(cur ^ 1);
+        __syncthreads();
+    }
+
+    // epilogue
+    const int lane = lane_id();
+    const int l32 = lane & 31, hi = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn0 + 32 * j + l32;
+        float bcol = 0.f, vcol = 0.f;
+        if (EPI == EPI_FWD) bcol = p.bias ? p.bias[col] : 0.f;
+        if (EPI == EPI_BWD) vcol = p.u ? p.v[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm0 + 32 * i + acc_row(r, hi);
+                float x = acc[i][j][r];
+                if (EPI == EPI_FWD) {
+                    x = x + bcol;
+                    if (p.relu) x = fmaxf(x, 0.f);
+                } else {
+                    if (p.u) x = x + p.u[(size_t)row * p.ldu] * vcol;
+                    if (p.mask) x = (p.mask[(size_t)row * p.ldmask + col] > 0.f) ? x : 0.f;
+                }
+                p.c[(size_t)row * p.ldc + col] = x;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// TN GEMM (weight gradient): slab[split][o][col0+j] = sum_s dy[s][o] x[s][j]
+// ---------------------------------------------------------------------------
+struct TNArgs {
+    const float* dy; int lddy;   // A[m=o][k=s] = dy[s][o]
+    const float* x;  int ldx;    // B[k=s][n=j] = x[s][j]
+    int rows_per_split;
+    float* slab; int ldslab; int col0; size_t slab_stride;
+    float* bslab; int nout;
+};
+
+template <int BM, int BN, int WAVES_M>
+__global__ __launch_bounds__(kThreads) void k_gemm_tn(TNArgs p) {
+    constexpr int WAVES_N = 4 / WAVES_M;
+    constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int LDA = BM + 4, LDB = BN + 4;
+    constexpr int A_F4 = BM * BK / 4 / kThreads;
+    constexpr int B_F4 = BN * BK / 4 / kThreads;
+    constexpr int A_C4 = BM / 4, B_C4 = BN / 4;  // float4 per k-row
+
+    __shared__ __attribute__((aligned(16))) float smem[2 * BK * (LDA + LDB)];
+    auto As = [&](int buf) { return smem + buf * BK * LDA; };
+    auto Bs = [&](int buf) { return smem + 2 * BK * LDA + buf * BK * LDB; };
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int wm0 = (wave / WAVES_N) * WTM;
+    const int wn0 = (wave % WAVES_N) * WTN;
+    const int o0 = blockIdx.x * BM;
+    const int j0 = blockIdx.y * BN;
+    const int split = blockIdx.z;
+    const size_t s0 = (size_t)split * p.rows_per_split;
+    const int nkt = p.rows_per_split / BK;
+    const bool do_bias = (p.bslab != nullptr) && (blockIdx.y == 0);
+
+    float4 ra[A_F4], rb[B_F4];
+    auto load_tile = [&](int kt) {
+        const size_t sb = s0 + (size_t)kt * BK;
+#pragma unroll
+        for (int i = 0; i < A_F4; ++i) {
+            const int idx = tid + kThreads * i;
+            const int row = idx / A_C4, c4 = idx % A_C4;
+            ra[i] = *reinterpret_cast<const float4*>(p.dy + (sb + row) * p.lddy + o0 + 4 * c4);
+        }
+#pragma unroll
+        for (int i = 0; i < B_F4; ++i) {
+            const int idx = tid + kThreads * i;
+            const int row = idx / B_C4, c4 = idx % B_C4;
+            rb[i] = *reinterpret_cast<const float4*>(p.x + (sb + row) * p.ldx + j0 + 4 * c4);
+        }
+    };
+    auto store_tile = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < A_F4; ++i) {
+            const int idx = tid + kThreads * i;
+            const int row = idx / A_C4, c4 = idx % A_C4;
+            *reinterpret_cast<float4*>(As(buf) + row * LDA + 4 * c4) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < B_F4; ++i) {
+            const int idx = tid + kThreads * i;
+            const int row = idx / B_C4, c4 = idx % B_C4;
+            *reinterpret_cast<float4*>(Bs(buf) + row * LDB + 4 * c4) = rb[i];
+        }
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    float bsum = 0.f;
+
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nkt) load_tile(kt + 1);
+        mfma_tile<TM, TN, LDA, LDB>(As(cur), Bs(cur), wm0, wn0, acc);
+        if (do_bias && tid < BM) {
+#pragma unroll 8
+            for (int k = 0; k < BK; ++k) bsum += As(cur)[k * LDA + tid];
+        }
+        if (kt + 1 < nkt) store_tile(cur ^ 1);
+        __syncthreads();
+    }
+
+    float* slab = p.slab + (size_t)split * p.slab_stride;
+    const int lane = lane_id();
+    const int l32 = lane & 31, hi = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int o = o0 + wm0 + 32 * i + acc_row(r, hi);
+                const int c = p.col0 + j0 + wn0 + 32 * j + l32;
+                slab[(size_t)o * p.ldslab + c] = acc[i][j][r];
+            }
+    if (do_bias && tid < BM) p.bslab[(size_t)split * p.nout + o0 + tid] = bsum;
+}
+
+// sum split-K slabs into the reference-layout gradient
+__global__ void k_slab_reduce(const float* __restrict__ slab, int splits, int nout, int ldslab,
+                              int nout_ref, int kin_ref, const float* __restrict__ bslab,
+                              float* __restrict__ gw, float* __restrict__ gb, int accumulate) {
+    const size_t stride = (size_t)nout * ldslab;
+    const int total = nout_ref * kin_ref;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total + nout_ref; e += gridDim.x * blockDim.x) {
+        if (e < total) {
+            const int o = e / kin_ref, j = e % kin_ref;
+            const float* s = slab + (size_t)o * ldslab + j;
+            float acc = 0.f;
+            for (int q = 0; q < splits; ++q) acc += s[q * stride];
+            gw[e] = accumulate ? gw[e] + acc : acc;
+        } else if (bslab != nullptr && gb != nullptr) {
+            const int o = e - total;
+            float acc = 0.f;
+            for (int q = 0; q < splits; ++q) acc += bslab[(size_t)q * nout + o];
+            gb[o] = accumulate ? gb[o] + acc : acc;
+        }
+    }
+}
+
+}  // namespace nerf
+
+using namespace nerf;
+
+template <int BM, int BN, int WM, int EPI>
+static int launch_nt(const NTArgs& a, hipStream_t s, double flops) {
+    dim3 grid(a.m / BM, a.n / BN);
+    prof_begin(s);
+    hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, EPI>), grid, dim3(kThreads), 0, s, a);
+    prof_end(s, flops);
+    return check_launch("k_gemm_nt");
+}
+
+static int check_nt(const NTArgs& a, const char* fn) {
+    NERF_CHECK(a.a1 && a.b && a.c, "%s: null operand", fn);
+    NERF_CHECK(a.m > 0 && a.m % 128 == 0, "%s: m=%d must be a positive multiple of 128", fn, a.m);
+    NERF_CHECK(a.n > 0 && a.n % 64 == 0, "%s: n=%d must be a positive multiple of 64", fn, a.n);
+    NERF_CHECK(a.k1 > 0 && a.k1 % 32 == 0 && a.k2 % 32 == 0 && a.k2 >= 0,
+               "%s: k1=%d k2=%d must be multiples of 32", fn, a.k1, a.k2);
+    NERF_CHECK(a.k2 == 0 || a.a2 != nullptr, "%s: k2>0 needs x2", fn);
+    NERF_CHECK(a.lda1 % 4 == 0 && a.lda2 % 4 == 0 && a.ldb % 4 == 0 && a.ldc >= a.n,
+               "%s: leading dimensions must be multiples of 4", fn);
+    NERF_CHECK(a.lda1 >= a.k1 && (a.k2 == 0 || a.lda2 >= a.k2) && a.ldb >= a.k1 + a.k2,
+               "%s: leading dimension smaller than K", fn);
+    NERF_CHECK((((uintptr_t)a.a1 | (uintptr_t)a.b | (uintptr_t)(a.a2 ? a.a2 : a.a1)) & 15u) == 0,
+               "%s: operands must be 16-byte aligned", fn);
+    return NERF_OK;
+}
+
+extern "C" int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2, int k2,
+                               const float* w, const float* bias, float* y, int ldy, int m, int n,
+                               int relu, void* stream) {
+    NTArgs a{};
+    a.a1 = x1; a.lda1 = ldx1; a.k1 = k1;
+    a.a2 = x2; a.lda2 = x2 ? ldx2 : 0; a.k2 = x2 ? k2 : 0;
+    a.b = w; a.ldb = k1 + a.k2;
+    a.bias = bias; a.c = y; a.ldc = ldy; a.m = m; a.n = n; a.relu = relu;
+    int rc = check_nt(a, __func__);
+    if (rc) return rc;
+    const double fl = 2.0 * m * n * (double)(k1 + a.k2);
+    hipStream_t s = as_stream(stream);
+    if (n % 128 == 0) return launch_nt<128, 128, 2, EPI_FWD>(a, s, fl);
+    return launch_nt<128, 64, 4, EPI_FWD>(a, s, fl);
+}
+
+extern "C" int nerf_linear_bwd_data(const float* dy, int lddy, int k, const float* wt,
+                                    const float* u, int ldu, const float* v, const float* mask,
+                                    int ldmask, float* dx, int lddx, int m, int n, void* stream) {
+    NTArgs a{};
+    a.a1 = dy; a.lda1 = lddy; a.k1 = k;
+    a.a2 = nullptr; a.lda2 = 0; a.k2 = 0;
+    a.b = wt; a.ldb = k;
+    a.u = u; a.ldu = ldu; a.v = v; a.mask = mask; a.ldmask = ldmask;
+    a.c = dx; a.ldc = lddx; a.m = m; a.n = n;
+    int rc = check_nt(a, __func__);
+    if (rc) return rc;
+    NERF_CHECK(u == nullptr || v != nullptr, "%s: u without v", __func__);
+    const double fl = 2.0 * m * n * (double)k;
+    hipStream_t s = as_stream(stream);
+    if (n % 128 == 0) return launch_nt<128, 128, 2, EPI_BWD>(a, s, fl);
+    return launch_nt<128, 64, 4, EPI_BWD>(a, s, fl);
+}
+
+extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const float* x, int ldx,
+                                      int kin, int m, int splits, float* slab, int ldslab, int col0,
+                                      float* bslab, void* stream) {
+    NERF_CHECK_PTR(dy);
+    NERF_CHECK_PTR(x);
+    NERF_CHECK_PTR(slab);
+    NERF_CHECK(nout > 0 && nout % 64 == 0, "%s: nout=%d must be a multiple of 64", __func__, nout);
+    NERF_CHECK(kin > 0 && kin % 64 == 0, "%s: kin=%d must be a multiple of 64", __func__, kin);
+    NERF_CHECK(splits > 0 && m % splits == 0 && (m / splits) % BK == 0,
+               "%s: m=%d not divisible into %d splits of a multiple of %d rows", __func__, m, splits, BK);
+    NERF_CHECK(lddy % 4 == 0 && ldx % 4 == 0 && ldslab >= col0 + kin, "%s: bad leading dims", __func__);
+    NERF_CHECK_ALIGN16(dy);
+    NERF_CHECK_ALIGN16(x);
+    TNArgs a{};
+    a.dy = dy; a.lddy = lddy; a.x = x; a.ldx = ldx;
+    a.rows_per_split = m / splits;
+    a.slab = slab; a.ldslab = ldslab; a.col0 = col0; a.slab_stride = (size_t)nout * ldslab;
+    a.bslab = bslab; a.nout = nout;
+    hipStream_t s = as_stream(stream);
+    const double fl = 2.0 * m * nout * (double)kin;
+    prof_begin(s);
+    if (nout % 128 == 0 && kin % 128 == 0) {
+        dim3 grid(nout / 128, kin / 128, splits);
+        hipLaunchKernelGGL((k_gemm_tn<128, 128, 2>), grid, dim3(kThreads), 0, s, a);
+    } else if (nout % 128 == 0) {
+        dim3 grid(nout / 128, kin / 64, splits);
+        hipLaunchKernelGGL((k_gemm_tn<128, 64, 4>), grid, dim3(kThreads), 0, s, a);
+    } else if (kin % 128 == 0) {
+        dim3 grid(nout / 64, kin / 128, splits);
+        hipLaunchKernelGGL((k_gemm_tn<64, 128, 2>), grid, dim3(kThreads), 0, s, a);
+    } else {
+        dim3 grid(nout / 64, kin / 64, splits);
+        hipLaunchKernelGGL((k_gemm_tn<64, 64, 2>), grid, dim3(kThreads), 0, s, a);
+    }
+    prof_end(s, fl);
+    return check_launch(__func__);
+}
+
+extern "C" int nerf_slab_reduce(const float* slab, int splits, int nout, int ldslab, int nout_ref,
+                                int kin_ref, const float* bslab, float* gw, float* gb, int accumulate,
+                                void* stream) {
+    NERF_CHECK_PTR(slab);
+    NERF_CHECK_PTR(gw);
+    NERF_CHECK(splits > 0 && nout > 0 && kin_ref > 0 && ldslab >= kin_ref && nout_ref <= nout,
+               "%s: bad sizes", __func__);
+    const int total = nout_ref * kin_ref + nout_ref;
+    const int blocks = (total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048;
+    hipLaunchKernelGGL(k_slab_reduce, dim3(blocks), dim3(256), 0, as_stream(stream), slab, splits,
+                       nout, ldslab, nout_ref, kin_ref, bslab, gw, gb, accumulate);
+    return check_launch(__func__);
+}

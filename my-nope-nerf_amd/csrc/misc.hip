@@ -1,0 +1,116 @@
+// Weight packing, the Adam step and the point-cloud nearest-neighbour kernel.
+#include "common.hpp"
+
+#include <cmath>
+
+namespace nerf {
+
+struct PackBatch {
+    nerf_pack_desc d[NERF_MAX_PACK];
+    int n;
+};
+
+// blockIdx.y selects the descriptor; grid-stride over the padded destination
+__global__ void k_pack(PackBatch pb) {
+    const nerf_pack_desc& d = pb.d[blockIdx.y];
+    const int total = d.rows * d.ld_dst;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        const int r = e / d.ld_dst, c = e % d.ld_dst;
+        d.dst[e] = c < d.cols ? d.src[(size_t)r * d.cols + c] : 0.f;
+    }
+    if (d.dst_t != nullptr) {
+        const int tt = d.rows_t * d.rows;  // dst_t[c][r], c < rows_t, r < rows
+        for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < tt; e += gridDim.x * blockDim.x) {
+            const int c = e / d.rows, r = e % d.rows;
+            d.dst_t[(size_t)c * d.ld_t + r] = c < d.cols ? d.src[(size_t)r * d.cols + c] : 0.f;
+        }
+    }
+}
+
+// torch.optim.Adam (amsgrad=False, maximize=False), single-tensor formulation:
+//   g += wd*p; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2
+//   denom = sqrt(v)/sqrt(bc2) + eps;  p -= (lr/bc1) * m / denom
+__global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                       float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
+                       float wd, float step_size, float sbc2) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        float gi = g[i];
+        if (wd != 0.f) gi = gi + wd * p[i];
+        const float mi = m[i] + (1.f - b1) * (gi - m[i]);   // lerp_ as torch does
+        const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        const float denom = sqrtf(vi) / sbc2 + eps;
+        p[i] = p[i] + (-step_size * mi) / denom;  // addcdiv_(m, denom, value=-step_size)
+    }
+}
+
+// nearest neighbour, one thread per query point, reference points staged through LDS
+constexpr int NN_TILE = 256;
+__global__ __launch_bounds__(256) void k_chamfer_nn(const float* __restrict__ x, int P,
+                                                    const float* __restrict__ y, int Q,
+                                                    int64_t* __restrict__ idx) {
+    __shared__ float4 ys[NN_TILE];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    float px = 0.f, py = 0.f, pz = 0.f;
+    if (i < P) { px = x[3 * i]; py = x[3 * i + 1]; pz = x[3 * i + 2]; }
+    float best = INFINITY;
+    int bi = 0;
+    for (int t0 = 0; t0 < Q; t0 += NN_TILE) {
+        const int j = t0 + threadIdx.x;
+        if (j < Q) ys[threadIdx.x] = make_float4(y[3 * j], y[3 * j + 1], y[3 * j + 2], 0.f);
+        __syncthreads();
+        const int nt = min(NN_TILE, Q - t0);
+        for (int k = 0; k < nt; ++k) {
+            const float4 q = ys[k];
+            const float dx = px - q.x, dy = py - q.y, dz = pz - q.z;
+            const float d = sqrtf(__fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
+            if (d < best) { best = d; bi = t0 + k; }  // strict: first index wins ties (torch.argmin)
+        }
+        __syncthreads();
+    }
+    if (i < P) idx[i] = bi;
+}
+
+}  // namespace nerf
+
+using namespace nerf;
+
+extern "C" int nerf_pack_weights(const nerf_pack_desc* descs, int n, void* stream) {
+    NERF_CHECK_PTR(descs);
+    NERF_CHECK(n > 0 && n <= NERF_MAX_PACK, "%s: n=%d outside 1..%d", __func__, n, NERF_MAX_PACK);
+    PackBatch pb{};
+    pb.n = n;
+    for (int i = 0; i < n; ++i) {
+        const nerf_pack_desc& d = descs[i];
+        NERF_CHECK(d.src && d.dst && d.rows > 0 && d.cols > 0 && d.ld_dst >= d.cols,
+                   "%s: bad descriptor %d", __func__, i);
+        NERF_CHECK(d.dst_t == nullptr || (d.rows_t >= d.cols && d.ld_t >= d.rows),
+                   "%s: descriptor %d: rows_t < cols or ld_t < rows", __func__, i);
+        pb.d[i] = d;
+    }
+    hipLaunchKernelGGL(k_pack, dim3(64, n), dim3(256), 0, as_stream(stream), pb);
+    return check_launch(__func__);
+}
+
+extern "C" int nerf_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                              int64_t n, float lr, float beta1, float beta2, float eps,
+                              float weight_decay, int step, void* stream) {
+    NERF_CHECK_PTR(param); NERF_CHECK_PTR(grad); NERF_CHECK_PTR(exp_avg); NERF_CHECK_PTR(exp_avg_sq);
+    NERF_CHECK(n > 0 && step >= 1, "%s: n=%lld step=%d", __func__, (long long)n, step);
+    const double bc1 = 1.0 - std::pow((double)beta1, step);
+    const double bc2 = 1.0 - std::pow((double)beta2, step);
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), param, grad,
+                       exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay,
+                       (float)((double)lr / bc1), (float)std::sqrt(bc2));
+    return check_launch(__func__);
+}
+
+extern "C" int nerf_chamfer_nn(const float* x, int p, const float* y, int q, int64_t* idx, void* stream) {
+    NERF_CHECK_PTR(x); NERF_CHECK_PTR(y); NERF_CHECK_PTR(idx);
+    NERF_CHECK(p > 0 && q > 0, "%s: empty point cloud (p=%d q=%d)", __func__, p, q);
+    hipLaunchKernelGGL(k_chamfer_nn, dim3((p + 255) / 256), dim3(256), 0, as_stream(stream), x, p, y, q, idx);
+    return check_launch(__func__);
+}

@@ -1,0 +1,660 @@
+// Per-sample and per-ray kernels of the render path: stratified samples +
+// positional encoding, output heads, fused sigma->alpha->transmittance compositing
+// (forward/backward) and the gradient back to the ray inputs.
+//
+// Reference semantics: model/rendering.py:36-198, model/official_nerf.py:66-119.
+#include "common.hpp"
+
+namespace nerf {
+
+constexpr int ENC_P = 64;  // 63 used + 1 zero pad (L = 10)
+constexpr int ENC_D = 64;  // 27 used + 37 zero pad (L = 4); 64 wide so every GEMM K tile is whole
+
+// Sample positions are rounded exactly as eager torch rounds them (separate multiply and
+// add, never fused): HIP's __fmul_rn/__fadd_rn are plain operators that -ffp-contract=fast
+// would fuse into v_fma, so contraction is switched off explicitly in these helpers.
+
+// torch.linspace(0, 1, S) element i (CUDA kernel: halfway split, float step)
+__device__ __forceinline__ float linspace01(int i, int S) {
+#pragma clang fp contract(off)
+    if (S == 1) return 0.f;
+    const float step = __fdiv_rn(1.0f, (float)(S - 1));
+    return (i < S / 2) ? __fmul_rn(step, (float)i) : __fsub_rn(1.0f, __fmul_rn(step, (float)(S - 1 - i)));
+}
+// depth_range[0] * (1 - t) + depth_range[1] * t   (rendering.py:186), rounded like eager torch
+__device__ __forceinline__ float lerp_z(float t, float nz, float fz) {
+#pragma clang fp contract(off)
+    return __fadd_rn(__fmul_rn(nz, __fsub_rn(1.0f, t)), __fmul_rn(fz, t));
+}
+
+// Streams an encoding row to global memory 16 bytes at a time (keeps few values live).
+template <int W>
+struct RowWriter {
+    float4* dst;
+    float buf[4];
+    int n;
+    __device__ __forceinline__ void put(float v) {
+        buf[n & 3] = v;
+        ++n;
+        if ((n & 3) == 0) dst[(n >> 2) - 1] = make_float4(buf[0], buf[1], buf[2], buf[3]);
+    }
+    __device__ __forceinline__ void finish() {
+        while (n < W) put(0.f);
+    }
+};
+
+// encode_position (official_nerf.py:99-119): [x, sin(2^0 x), cos(2^0 x), ...], zero padded to W
+template <int L, int W>
+__device__ __forceinline__ void encode3(const float x[3], float* row) {
+    RowWriter<W> w{reinterpret_cast<float4*>(row), {0.f, 0.f, 0.f, 0.f}, 0};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) w.put(x[c]);
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        const float f = (float)(1 << i);
+        float s[3], co[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) sincosf(f * x[c], &s[c], &co[c]);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) w.put(s[c]);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) w.put(co[c]);
+    }
+    w.finish();
+}
+
+__global__ __launch_bounds__(256) void k_encode_samples(const float* __restrict__ po, const float* __restrict__ pd,
+                                 const float* __restrict__ view, const float* __restrict__ noise,
+                                 int R, int S, int n_pad, float nz, float fz,
+                                 float* __restrict__ z_out, float* __restrict__ enc_p,
+                                 float* __restrict__ enc_d) {
+#pragma clang fp contract(off)
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_pad) return;
+    const int total = R * S;
+    float* rp = enc_p + (size_t)s * ENC_P;
+    float* rd = enc_d + (size_t)s * ENC_D;
+    if (s < total) {
+        const int r = s / S, i = s - r * S;
+        float z = lerp_z(linspace01(i, S), nz, fz);
+        if (noise != nullptr) {  // rendering.py:187-191
+            const float zp = i > 0 ? lerp_z(linspace01(i - 1, S), nz, fz) : z;
+            const float zn = i < S - 1 ? lerp_z(linspace01(i + 1, S), nz, fz) : z;
+            const float lo = i > 0 ? __fmul_rn(0.5f, __fadd_rn(z, zp)) : z;
+            const float hi = i < S - 1 ? __fmul_rn(0.5f, __fadd_rn(zn, z)) : z;
+            z = __fadd_rn(lo, __fmul_rn(__fsub_rn(hi, lo), noise[s]));
+        }
+        float x[3], v[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            x[c] = __fadd_rn(po[3 * r + c], __fmul_rn(pd[3 * r + c], z));  // rendering.py:193-194
+            v[c] = view[3 * r + c];
+        }
+        encode3<10, ENC_P>(x, rp);
+        encode3<4, ENC_D>(v, rd);
+        z_out[s] = z;
+    } else {
+        const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < ENC_P / 4; ++q) reinterpret_cast<float4*>(rp)[q] = zero;
+#pragma unroll
+        for (int q = 0; q < ENC_D / 4; ++q) reinterpret_cast<float4*>(rd)[q] = zero;
+        z_out[s] = 0.f;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Output heads.  A wave processes 16 consecutive samples; lane l owns features
+// l, l+64, ...; the 16 per-sample partial dots are reduced across the wave by a
+// halving butterfly (17 shuffles for 16 samples) that leaves the total of sample
+// (lane >> 2) in every lane.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float reduce16(float (&v)[16]) {
+    const int lane = lane_id();
+    float w8[8], w4[4], w2[2];
+    {
+        const bool h = (lane >> 5) & 1;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float keep = h ? v[j + 8] : v[j];
+            const float send = h ? v[j] : v[j + 8];
+            w8[j] = keep + __shfl_xor(send, 32, 64);
+        }
+    }
+    {
+        const bool h = (lane >> 4) & 1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float keep = h ? w8[j + 4] : w8[j];
+            const float send = h ? w8[j] : w8[j + 4];
+            w4[j] = keep + __shfl_xor(send, 16, 64);
+        }
+    }
+    {
+        const bool h = (lane >> 3) & 1;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const float keep = h ? w4[j + 2] : w4[j];
+            const float send = h ? w4[j] : w4[j + 2];
+            w2[j] = keep + __shfl_xor(send, 8, 64);
+        }
+    }
+    const bool h = (lane >> 2) & 1;
+    float w = (h ? w2[1] : w2[0]) + __shfl_xor(h ? w2[0] : w2[1], 4, 64);
+    w += __shfl_xor(w, 2, 64);
+    w += __shfl_xor(w, 1, 64);
+    return w;
+}
+
+template <int NH, int NR>  // NH = hidden/64, NR = rgb-hidden/64
+__global__ __launch_bounds__(256) void k_heads_fwd(const float* __restrict__ h8, int ld8,
+                                                   const float* __restrict__ hr, int ldr,
+                                                   const float* __restrict__ wd, const float* __restrict__ bd,
+                                                   const float* __restrict__ wc, const float* __restrict__ bc,
+                                                   float* __restrict__ raw4, int n_pad) {
+    const int lane = lane_id();
+    const int gwave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int nwaves = (gridDim.x * blockDim.x) >> 6;
+    float wdr[NH], wcr[3][NR];
+#pragma unroll
+    for (int q = 0; q < NH; ++q) wdr[q] = wd[lane + 64 * q];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int q = 0; q < NR; ++q) wcr[c][q] = wc[c * NR * 64 + lane + 64 * q];
+    const float b_d = bd[0];
+    const float b_c[3] = {bc[0], bc[1], bc[2]};
+
+    for (int g = gwave; g * 16 < n_pad; g += nwaves) {
+        const size_t s0 = (size_t)g * 16;
+        float pd[16], pc0[16], pc1[16], pc2[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            float a = 0.f;
+#pragma unroll
+            for (int q = 0; q < NH; ++q) a += h8[(s0 + t) * ld8 + lane + 64 * q] * wdr[q];
+            pd[t] = a;
+            float c0 = 0.f, c1 = 0.f, c2 = 0.f;
+#pragma unroll
+            for (int q = 0; q < NR; ++q) {
+                const float x = hr[(s0 + t) * ldr + lane + 64 * q];
+                c0 += x * wcr[0][q];
+                c1 += x * wcr[1][q];
+                c2 += x * wcr[2][q];
+            }
+            pc0[t] = c0; pc1[t] = c1; pc2[t] = c2;
+        }
+        const float sd = reduce16(pd);
+        const float s0c = reduce16(pc0);
+        const float s1c = reduce16(pc1);
+        const float s2c = reduce16(pc2);
+        if ((lane & 3) == 0) {
+            const size_t s = s0 + (lane >> 2);
+            *reinterpret_cast<float4*>(raw4 + 4 * s) =
+                make_float4(sd + b_d, s0c + b_c[0], s1c + b_c[1], s2c + b_c[2]);
+        }
+    }
+}
+
+// part layout per block: [wd: 64*NH][wc: 3*64*NR][bd, bc0, bc1, bc2]
+template <int NH, int NR>
+__global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ graw4,
+                                                   const float* __restrict__ h8, int ld8,
+                                                   const float* __restrict__ hr, int ldr,
+                                                   const float* __restrict__ wc,
+                                                   float* __restrict__ dyr, int lddyr,
+                                                   float* __restrict__ part, int n_pad) {
+    constexpr int H = 64 * NH, HR = 64 * NR, PART = H + 3 * HR + 4;
+    __shared__ float red[4][PART];
+    const int lane = lane_id();
+    const int wave = threadIdx.x >> 6;
+    const int gwave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int nwaves = (gridDim.x * blockDim.x) >> 6;
+    float wcr[3][NR];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int q = 0; q < NR; ++q) wcr[c][q] = wc[c * HR + lane + 64 * q];
+    float awd[NH], awc[3][NR], abd = 0.f, abc[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NH; ++q) awd[q] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int q = 0; q < NR; ++q) awc[c][q] = 0.f;
+
+    for (int g = gwave; g * 16 < n_pad; g += nwaves) {
+        const size_t s0 = (size_t)g * 16;
+#pragma unroll 4
+        for (int t = 0; t < 16; ++t) {
+            const size_t s = s0 + t;
+            const float4 gr = *reinterpret_cast<const float4*>(graw4 + 4 * s);
+#pragma unroll
+            for (int q = 0; q < NH; ++q) awd[q] += gr.x * h8[s * ld8 + lane + 64 * q];
+#pragma unroll
+            for (int q = 0; q < NR; ++q) {
+                const float x = hr[s * ldr + lane + 64 * q];
+                float d = gr.y * wcr[0][q] + gr.z * wcr[1][q] + gr.w * wcr[2][q];
+                dyr[s * lddyr + lane + 64 * q] = x > 0.f ? d : 0.f;
+                awc[0][q] += gr.y * x;
+                awc[1][q] += gr.z * x;
+                awc[2][q] += gr.w * x;
+            }
+            abd += gr.x;
+            abc[0] += gr.y; abc[1] += gr.z; abc[2] += gr.w;
+        }
+    }
+    float* rw = red[wave];
+#pragma unroll
+    for (int q = 0; q < NH; ++q) rw[lane + 64 * q] = awd[q];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int q = 0; q < NR; ++q) rw[H + c * HR + lane + 64 * q] = awc[c][q];
+    if (lane == 0) {
+        rw[H + 3 * HR + 0] = abd;
+        rw[H + 3 * HR + 1] = abc[0];
+        rw[H + 3 * HR + 2] = abc[1];
+        rw[H + 3 * HR + 3] = abc[2];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < PART; e += blockDim.x)
+        part[(size_t)blockIdx.x * PART + e] = red[0][e] + red[1][e] + red[2][e] + red[3][e];
+}
+
+__global__ void k_heads_reduce(const float* __restrict__ part, int nblocks, int H, int HR,
+                               float* __restrict__ gwd, float* __restrict__ gbd,
+                               float* __restrict__ gwc, float* __restrict__ gbc, int accumulate) {
+    const int PART = H + 3 * HR + 4;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < PART; e += gridDim.x * blockDim.x) {
+        float acc = 0.f;
+        for (int b = 0; b < nblocks; ++b) acc += part[(size_t)b * PART + e];
+        float* dst;
+        if (e < H) dst = gwd + e;
+        else if (e < H + 3 * HR) dst = gwc + (e - H);
+        else if (e == H + 3 * HR) dst = gbd;
+        else dst = gbc + (e - H - 3 * HR - 1);
+        *dst = accumulate ? *dst + acc : acc;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Compositing: one wavefront per ray, lane l owns samples [l*J, l*J + J).
+// ---------------------------------------------------------------------------
+enum { F_DIST_ALPHA = 1, F_WHITE_BKGD = 2, F_RELU = 4 };
+constexpr float kEps = 1e-6f;  // rendering.py:9
+
+__device__ __forceinline__ float density_act(float raw, int flags) {
+    return (flags & F_RELU) ? fmaxf(raw, 0.f) : softplus_f(raw);
+}
+
+// inclusive multiplicative scan across the wave
+__device__ __forceinline__ float wave_scan_mul(float v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const float o = __shfl_up(v, off, 64);
+        if (lane >= off) v *= o;
+    }
+    return v;
+}
+// inclusive additive scan from the top lane down (suffix sums)
+__device__ __forceinline__ float wave_suffix_add(float v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const float o = __shfl_down(v, off, 64);
+        if (lane + off < 64) v += o;
+    }
+    return v;
+}
+
+template <int J>
+struct RaySamples {
+    float alpha[J], f[J], T[J], w[J], c[J][3], z[J];
+    bool valid[J];
+};
+
+// alpha_i (rendering.py:113-122 / official_nerf.py:77-83), colour sigmoid, transmittance
+template <int J>
+__device__ __forceinline__ void load_ray(const float* __restrict__ raw4, const float* __restrict__ zv,
+                                         int ray, int S, int flags, RaySamples<J>& rs) {
+    const int lane = lane_id();
+    const size_t base = (size_t)ray * S;
+    float pl = 1.f;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int i = lane * J + j;
+        rs.valid[j] = i < S;
+        float a = 0.f, zz = 0.f;
+        float c0 = 0.f, c1 = 0.f, c2 = 0.f;
+        if (rs.valid[j]) {
+            const float4 r = *reinterpret_cast<const float4*>(raw4 + 4 * (base + i));
+            zz = zv[base + i];
+            const float sig = density_act(r.x, flags);
+            if (flags & F_DIST_ALPHA) {
+                if (i == S - 1) {
+                    a = 1.f;  // rendering.py:121 (delta_last = 1e10 then alpha forced to 1)
+                } else {
+                    const float delta = zv[base + i + 1] - zz;
+                    a = 1.f - expf(-1.0f * sig * delta);
+                }
+            } else {
+                a = 1.f - expf(-1.0f * sig);
+            }
+            c0 = sigmoid_f(r.y); c1 = sigmoid_f(r.z); c2 = sigmoid_f(r.w);
+        }
+        rs.alpha[j] = a;
+        rs.z[j] = zz;
+        rs.c[j][0] = c0; rs.c[j][1] = c1; rs.c[j][2] = c2;
+        const float f = rs.valid[j] ? (1.f - a + kEps) : 1.f;
+        rs.f[j] = f;
+        rs.T[j] = pl;  // exclusive within the lane
+        pl *= f;
+    }
+    // exclusive prefix of the lane products
+    const float incl = wave_scan_mul(pl);
+    float excl = __shfl_up(incl, 1, 64);
+    if (lane == 0) excl = 1.f;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        rs.T[j] *= excl;
+        rs.w[j] = rs.alpha[j] * rs.T[j];
+    }
+}
+
+template <int J>
+__global__ __launch_bounds__(256) void k_composite_fwd(const float* __restrict__ raw4,
+                                                       const float* __restrict__ zv, int R, int S,
+                                                       int flags, float* __restrict__ rgb,
+                                                       float* __restrict__ dist,
+                                                       float* __restrict__ alpha_out) {
+    const int ray = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (ray >= R) return;
+    const int lane = lane_id();
+    RaySamples<J> rs;
+    load_ray<J>(raw4, zv, ray, S, flags, rs);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, sd = 0.f, sw = 0.f;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        if (!rs.valid[j]) continue;
+        s0 += rs.w[j] * rs.c[j][0];
+        s1 += rs.w[j] * rs.c[j][1];
+        s2 += rs.w[j] * rs.c[j][2];
+        sd += rs.w[j] * rs.z[j];
+        sw += rs.w[j];
+        alpha_out[(size_t)ray * S + lane * J + j] = rs.alpha[j];
+    }
+    s0 = wave_sum(s0); s1 = wave_sum(s1); s2 = wave_sum(s2); sd = wave_sum(sd);
+    if (flags & F_WHITE_BKGD) sw = wave_sum(sw);
+    if (lane == 0) {
+        if (flags & F_WHITE_BKGD) {  // rendering.py:139-141
+            const float bg = 1.f - sw;
+            s0 += bg; s1 += bg; s2 += bg;
+        }
+        rgb[3 * ray + 0] = s0;
+        rgb[3 * ray + 1] = s1;
+        rgb[3 * ray + 2] = s2;
+        dist[ray] = sd;
+    }
+}
+
+template <int J>
+__global__ __launch_bounds__(256) void k_composite_bwd(const float* __restrict__ raw4,
+                                                       const float* __restrict__ zv, int R, int S,
+                                                       int flags, const float* __restrict__ g_rgb,
+                                                       const float* __restrict__ g_dist,
+                                                       float* __restrict__ graw4, int n_pad) {
+    const int gtid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ray = gtid >> 6;
+    // zero the padded sample rows (grid-stride over the tail)
+    for (size_t s = (size_t)R * S + gtid; s < (size_t)n_pad; s += (size_t)gridDim.x * blockDim.x)
+        *reinterpret_cast<float4*>(graw4 + 4 * s) = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ray >= R) return;
+    const int lane = lane_id();
+    RaySamples<J> rs;
+    load_ray<J>(raw4, zv, ray, S, flags, rs);
+    const float gc0 = g_rgb[3 * ray], gc1 = g_rgb[3 * ray + 1], gc2 = g_rgb[3 * ray + 2];
+    const float gd = g_dist[ray];
+    const float gbg = (flags & F_WHITE_BKGD) ? -(gc0 + gc1 + gc2) : 0.f;
+    // g_w_i and the suffix sums S_i = sum_{k>i} g_w_k w_k
+    float gw[J], lsum = 0.f;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        gw[j] = rs.valid[j] ? (gc0 * rs.c[j][0] + gc1 * rs.c[j][1] + gc2 * rs.c[j][2] + gd * rs.z[j] + gbg) : 0.f;
+        lsum += gw[j] * rs.w[j];
+    }
+    const float incl = wave_suffix_add(lsum);
+    float after = __shfl_down(incl, 1, 64);  // sum over lanes > this one
+    if (lane == 63) after = 0.f;
+    float suffix = after;
+#pragma unroll
+    for (int j = J - 1; j >= 0; --j) {
+        if (!rs.valid[j]) continue;
+        const int i = lane * J + j;
+        const size_t s = (size_t)ray * S + i;
+        // d alpha_i = T_i g_w_i - S_i / (1 - alpha_i + eps)
+        const float ga = rs.T[j] * gw[j] - suffix / rs.f[j];
+        suffix += gw[j] * rs.w[j];
+        const float4 r = *reinterpret_cast<const float4*>(raw4 + 4 * s);
+        float graw;
+        const float sig = density_act(r.x, flags);
+        const float dact = (flags & F_RELU) ? (sig > 0.f ? 1.f : 0.f) : softplus_grad_f(r.x);
+        if (flags & F_DIST_ALPHA) {
+            if (i == S - 1) {
+                graw = 0.f;
+            } else {
+                const float delta = zv[s + 1] - rs.z[j];
+                graw = ga * expf(-1.0f * sig * delta) * delta * dact;
+            }
+        } else {
+            graw = ga * expf(-1.0f * sig) * dact;
+        }
+        const float gcw = rs.w[j];
+        float4 o;
+        o.x = graw;
+        o.y = gcw * gc0 * (1.f - rs.c[j][0]) * rs.c[j][0];
+        o.z = gcw * gc1 * (1.f - rs.c[j][1]) * rs.c[j][1];
+        o.w = gcw * gc2 * (1.f - rs.c[j][2]) * rs.c[j][2];
+        *reinterpret_cast<float4*>(graw4 + 4 * s) = o;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// gradient back to the ray inputs (pose / ray learning)
+// ---------------------------------------------------------------------------
+template <int L, int LD>
+__device__ __forceinline__ void encode3_bwd(const float x[3], const float* __restrict__ g, float out[3]) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) out[c] = g[c];
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        const float f = (float)(1 << i);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float s, co;
+            sincosf(f * x[c], &s, &co);
+            out[c] += f * (co * g[3 + 6 * i + c] - s * g[6 + 6 * i + c]);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_encode_bwd(const float* __restrict__ po, const float* __restrict__ pd,
+                                                    const float* __restrict__ view, const float* __restrict__ zv,
+                                                    const float* __restrict__ gp, const float* __restrict__ gd,
+                                                    int R, int S, float* __restrict__ g_po,
+                                                    float* __restrict__ g_pd, float* __restrict__ g_view) {
+    const int ray = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (ray >= R) return;
+    const int lane = lane_id();
+    float ao[3] = {0.f, 0.f, 0.f}, ad[3] = {0.f, 0.f, 0.f}, av[3] = {0.f, 0.f, 0.f};
+    const float o[3] = {po[3 * ray], po[3 * ray + 1], po[3 * ray + 2]};
+    const float d[3] = {pd[3 * ray], pd[3 * ray + 1], pd[3 * ray + 2]};
+    const float v[3] = {view[3 * ray], view[3 * ray + 1], view[3 * ray + 2]};
+    for (int i = lane; i < S; i += 64) {
+        const size_t s = (size_t)ray * S + i;
+        const float z = zv[s];
+        float x[3], gx[3], gv[3];
+        {
+#pragma clang fp contract(off)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) x[c] = o[c] + d[c] * z;
+        }
+        encode3_bwd<10, ENC_P>(x, gp + s * ENC_P, gx);
+        encode3_bwd<4, ENC_D>(v, gd + s * ENC_D, gv);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            ao[c] += gx[c];
+            ad[c] += gx[c] * z;
+            av[c] += gv[c];
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        ao[c] = wave_sum(ao[c]);
+        ad[c] = wave_sum(ad[c]);
+        av[c] = wave_sum(av[c]);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            g_po[3 * ray + c] = ao[c];
+            g_pd[3 * ray + c] = ad[c];
+            g_view[3 * ray + c] = av[c];
+        }
+    }
+}
+
+}  // namespace nerf
+
+using namespace nerf;
+
+extern "C" int nerf_encode_samples(const float* pts_o, const float* pts_d, const float* view,
+                                   const float* noise, int n_rays, int n_samples, int n_pad,
+                                   float near_z, float far_z, float* z, float* enc_p, float* enc_d,
+                                   void* stream) {
+    NERF_CHECK_PTR(pts_o); NERF_CHECK_PTR(pts_d); NERF_CHECK_PTR(view);
+    NERF_CHECK_PTR(z); NERF_CHECK_PTR(enc_p); NERF_CHECK_PTR(enc_d);
+    NERF_CHECK_ALIGN16(enc_p); NERF_CHECK_ALIGN16(enc_d);
+    NERF_CHECK(n_rays > 0 && n_samples > 0 && (int64_t)n_rays * n_samples <= n_pad,
+               "%s: n_pad=%d < R*S=%lld", __func__, n_pad, (long long)n_rays * n_samples);
+    const int blocks = (n_pad + 255) / 256;
+    hipLaunchKernelGGL(k_encode_samples, dim3(blocks), dim3(256), 0, as_stream(stream), pts_o, pts_d,
+                       view, noise, n_rays, n_samples, n_pad, near_z, far_z, z, enc_p, enc_d);
+    return check_launch(__func__);
+}
+
+static int heads_blocks(int n_pad) {
+    const int groups = n_pad / 16;
+    int b = (groups + 3) / 4;
+    return b > 1024 ? 1024 : (b < 1 ? 1 : b);
+}
+
+extern "C" int nerf_heads_fwd(const float* h8, int ld8, const float* hr, int ldr, int hidden,
+                              const float* wd, const float* bd, const float* wc, const float* bc,
+                              float* raw4, int n_pad, void* stream) {
+    NERF_CHECK_PTR(h8); NERF_CHECK_PTR(hr); NERF_CHECK_PTR(wd); NERF_CHECK_PTR(bd);
+    NERF_CHECK_PTR(wc); NERF_CHECK_PTR(bc); NERF_CHECK_PTR(raw4);
+    NERF_CHECK_ALIGN16(raw4);
+    NERF_CHECK(n_pad % 16 == 0, "%s: n_pad %% 16 != 0", __func__);
+    const int hrw = hidden / 2 < 64 ? 64 : hidden / 2;  // colour hidden is padded to >= 64
+    hipStream_t s = as_stream(stream);
+    dim3 g(heads_blocks(n_pad)), b(256);
+    if (hidden == 256 && hrw == 128)
+        hipLaunchKernelGGL((k_heads_fwd<4, 2>), g, b, 0, s, h8, ld8, hr, ldr, wd, bd, wc, bc, raw4, n_pad);
+    else if (hidden == 128 && hrw == 64)
+        hipLaunchKernelGGL((k_heads_fwd<2, 1>), g, b, 0, s, h8, ld8, hr, ldr, wd, bd, wc, bc, raw4, n_pad);
+    else if (hidden == 64 && hrw == 64)
+        hipLaunchKernelGGL((k_heads_fwd<1, 1>), g, b, 0, s, h8, ld8, hr, ldr, wd, bd, wc, bc, raw4, n_pad);
+    else if (hidden == 512 && hrw == 256)
+        hipLaunchKernelGGL((k_heads_fwd<8, 4>), g, b, 0, s, h8, ld8, hr, ldr, wd, bd, wc, bc, raw4, n_pad);
+    else
+        NERF_CHECK(false, "%s: unsupported hidden width %d (64/128/256/512)", __func__, hidden);
+    return check_launch(__func__);
+}
+
+extern "C" int nerf_heads_part_size(int hidden, int n_pad) {
+    const int hrw = hidden / 2 < 64 ? 64 : hidden / 2;
+    return heads_blocks(n_pad) * (hidden + 3 * hrw + 4);
+}
+
+extern "C" int nerf_heads_bwd(const float* graw4, const float* h8, int ld8, const float* hr, int ldr,
+                              int hidden, const float* wc, float* dyr, int lddyr, float* part,
+                              int n_pad, void* stream) {
+    NERF_CHECK_PTR(graw4); NERF_CHECK_PTR(h8); NERF_CHECK_PTR(hr); NERF_CHECK_PTR(wc);
+    NERF_CHECK_PTR(dyr); NERF_CHECK_PTR(part);
+    NERF_CHECK_ALIGN16(graw4);
+    NERF_CHECK(n_pad % 16 == 0, "%s: n_pad %% 16 != 0", __func__);
+    const int hrw = hidden / 2 < 64 ? 64 : hidden / 2;
+    hipStream_t s = as_stream(stream);
+    dim3 g(heads_blocks(n_pad)), b(256);
+    if (hidden == 256 && hrw == 128)
+        hipLaunchKernelGGL((k_heads_bwd<4, 2>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad);
+    else if (hidden == 128 && hrw == 64)
+        hipLaunchKernelGGL((k_heads_bwd<2, 1>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad);
+    else if (hidden == 64 && hrw == 64)
+        hipLaunchKernelGGL((k_heads_bwd<1, 1>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad);
+    else if (hidden == 512 && hrw == 256)
+        hipLaunchKernelGGL((k_heads_bwd<8, 4>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad);
+    else
+        NERF_CHECK(false, "%s: unsupported hidden width %d (64/128/256/512)", __func__, hidden);
+    return check_launch(__func__);
+}
+
+extern "C" int nerf_heads_reduce(const float* part, int hidden, int n_pad, float* gwd, float* gbd,
+                                 float* gwc, float* gbc, int accumulate, void* stream) {
+    NERF_CHECK_PTR(part); NERF_CHECK_PTR(gwd); NERF_CHECK_PTR(gbd); NERF_CHECK_PTR(gwc); NERF_CHECK_PTR(gbc);
+    const int hrw = hidden / 2 < 64 ? 64 : hidden / 2;
+    const int PART = hidden + 3 * hrw + 4;
+    hipLaunchKernelGGL(k_heads_reduce, dim3((PART + 255) / 256), dim3(256), 0, as_stream(stream), part,
+                       heads_blocks(n_pad), hidden, hrw, gwd, gbd, gwc, gbc, accumulate);
+    return check_launch(__func__);
+}
+
+#define NERF_J_DISPATCH(KERNEL, S, ...)                                            \
+    do {                                                                           \
+        const int J_ = ((S) + 63) / 64;                                            \
+        if (J_ <= 1) hipLaunchKernelGGL((KERNEL<1>), __VA_ARGS__);                 \
+        else if (J_ == 2) hipLaunchKernelGGL((KERNEL<2>), __VA_ARGS__);            \
+        else if (J_ <= 4) hipLaunchKernelGGL((KERNEL<4>), __VA_ARGS__);            \
+        else if (J_ <= 8) hipLaunchKernelGGL((KERNEL<8>), __VA_ARGS__);            \
+        else if (J_ <= 16) hipLaunchKernelGGL((KERNEL<16>), __VA_ARGS__);          \
+        else NERF_CHECK(false, "%s: n_samples=%d > 1024", __func__, (int)(S));     \
+    } while (0)
+
+extern "C" int nerf_composite_fwd(const float* raw4, const float* z, int n_rays, int n_samples, int flags,
+                                  float* rgb, float* dist, float* alpha, void* stream) {
+    NERF_CHECK_PTR(raw4); NERF_CHECK_PTR(z); NERF_CHECK_PTR(rgb); NERF_CHECK_PTR(dist); NERF_CHECK_PTR(alpha);
+    NERF_CHECK_ALIGN16(raw4);
+    NERF_CHECK(n_rays > 0 && n_samples > 0, "%s: empty input", __func__);
+    const int blocks = (n_rays + 3) / 4;
+    NERF_J_DISPATCH(k_composite_fwd, n_samples, dim3(blocks), dim3(256), 0, as_stream(stream), raw4, z,
+                    n_rays, n_samples, flags, rgb, dist, alpha);
+    return check_launch(__func__);
+}
+
+extern "C" int nerf_composite_bwd(const float* raw4, const float* z, int n_rays, int n_samples, int flags,
+                                  const float* grad_rgb, const float* grad_dist, float* graw4, int n_pad,
+                                  void* stream) {
+    NERF_CHECK_PTR(raw4); NERF_CHECK_PTR(z); NERF_CHECK_PTR(grad_rgb); NERF_CHECK_PTR(grad_dist);
+    NERF_CHECK_PTR(graw4);
+    NERF_CHECK_ALIGN16(raw4); NERF_CHECK_ALIGN16(graw4);
+    NERF_CHECK(n_rays > 0 && n_samples > 0 && (int64_t)n_rays * n_samples <= n_pad, "%s: bad sizes", __func__);
+    const int blocks = (n_rays + 3) / 4;
+    NERF_J_DISPATCH(k_composite_bwd, n_samples, dim3(blocks), dim3(256), 0, as_stream(stream), raw4, z,
+                    n_rays, n_samples, flags, grad_rgb, grad_dist, graw4, n_pad);
+    return check_launch(__func__);
+}
+
+extern "C" int nerf_encode_bwd(const float* pts_o, const float* pts_d, const float* view, const float* z,
+                               const float* genc_p, const float* genc_d, int n_rays, int n_samples,
+                               float* g_pts_o, float* g_pts_d, float* g_view, void* stream) {
+    NERF_CHECK_PTR(pts_o); NERF_CHECK_PTR(pts_d); NERF_CHECK_PTR(view); NERF_CHECK_PTR(z);
+    NERF_CHECK_PTR(genc_p); NERF_CHECK_PTR(genc_d);
+    NERF_CHECK_PTR(g_pts_o); NERF_CHECK_PTR(g_pts_d); NERF_CHECK_PTR(g_view);
+    NERF_CHECK(n_rays > 0 && n_samples > 0, "%s: empty input", __func__);
+    const int blocks = (n_rays + 3) / 4;
+    hipLaunchKernelGGL(k_encode_bwd, dim3(blocks), dim3(256), 0, as_stream(stream), pts_o, pts_d, view, z,
+                       genc_p, genc_d, n_rays, n_samples, g_pts_o, g_pts_d, g_view);
+    return check_launch(__func__);
+}

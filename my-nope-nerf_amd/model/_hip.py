@@ -1,0 +1,198 @@
+"""ctypes binding of the nerf_hip C-ABI (include/nerf_hip.h).
+
+This is the reference-side binding a maintainer adds to call the MI355X kernels:
+every function takes torch tensors, checks dtype/device/contiguity, passes raw
+device pointers plus the current HIP stream, and raises ``RuntimeError`` with the
+library's message on a non-zero return code (the reference's own ops raise
+``RuntimeError`` from ATen on bad shapes; same error behaviour here).
+
+There is deliberately no CPU fallback: importing this module on a machine without
+the built library, or calling into it without a GPU, fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NERF_HIP_LIB", os.path.join(_HERE, "..", "lib", "libnerf_hip.so"))
+
+ROW_TILE = 128
+ENC_P = 64
+ENC_D = 64
+
+_c_f = ctypes.c_float
+_c_i = ctypes.c_int
+_c_p = ctypes.c_void_p
+_c_i64 = ctypes.c_int64
+
+
+class PackDesc(ctypes.Structure):
+    _fields_ = [("src", _c_p), ("dst", _c_p), ("dst_t", _c_p), ("rows", _c_i), ("cols", _c_i),
+                ("ld_dst", _c_i), ("rows_t", _c_i), ("ld_t", _c_i)]
+
+
+_SIGS = {
+    "nerf_hip_abi_version": ([], _c_i),
+    "nerf_hip_last_error": ([], ctypes.c_char_p),
+    "nerf_encode_samples": ([_c_p, _c_p, _c_p, _c_p, _c_i, _c_i, _c_i, _c_f, _c_f, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_linear_fwd": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p], _c_i),
+    "nerf_linear_bwd_data": ([_c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_i, _c_i, _c_p], _c_i),
+    "nerf_linear_bwd_weight": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p], _c_i),
+    "nerf_slab_reduce": ([_c_p, _c_i, _c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
+    "nerf_heads_fwd": ([_c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
+    "nerf_heads_part_size": ([_c_i, _c_i], _c_i),
+    "nerf_heads_bwd": ([_c_p, _c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_p], _c_i),
+    "nerf_heads_reduce": ([_c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
+    "nerf_composite_fwd": ([_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_composite_bwd": ([_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
+    "nerf_encode_bwd": ([_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_pack_weights": ([ctypes.POINTER(PackDesc), _c_i, _c_p], _c_i),
+    "nerf_adam_step": ([_c_p, _c_p, _c_p, _c_p, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_f, _c_i, _c_p], _c_i),
+    "nerf_chamfer_nn": ([_c_p, _c_i, _c_p, _c_i, _c_p, _c_p], _c_i),
+    "nerf_prof_enable": ([_c_i], _c_i),
+    "nerf_prof_read": ([ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_i64),
+                        ctypes.POINTER(ctypes.c_double)], _c_i),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(
+            f"nerf_hip: HIP library not found at {path}; build it with `make -C my-nope-nerf_amd` "
+            "(or __graft_entry__.build()). There is no CPU fallback.")
+    lib = ctypes.CDLL(path)
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    return lib
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        _lib = load_library()
+    return _lib
+
+
+def _call(name: str, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().nerf_hip_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("nerf_hip: tensor must live on the GPU (no CPU fallback)")
+    if t.dtype not in (torch.float32, torch.int64):
+        raise RuntimeError(f"nerf_hip: unsupported dtype {t.dtype}")
+    return t.data_ptr()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ld(t: torch.Tensor) -> int:
+    """Row stride (elements) of a 2-D row-major view (columns contiguous)."""
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise RuntimeError("nerf_hip: expected a 2-D row-major view")
+    return t.stride(0)
+
+
+# --------------------------------------------------------------------------------------
+def encode_samples(pts_o, pts_d, view, noise, n_rays, n_samples, n_pad, near, far, z, enc_p, enc_d):
+    _call("nerf_encode_samples", _ptr(pts_o), _ptr(pts_d), _ptr(view), _ptr(noise), n_rays, n_samples,
+          n_pad, float(near), float(far), _ptr(z), _ptr(enc_p), _ptr(enc_d), _stream())
+
+
+def linear_fwd(x1, k1, x2, k2, w, bias, y, m, n, relu):
+    _call("nerf_linear_fwd", _ptr(x1), _ld(x1), k1, _ptr(x2), _ld(x2) if x2 is not None else 0, k2,
+          _ptr(w), _ptr(bias), _ptr(y), _ld(y), m, n, int(relu), _stream())
+
+
+def linear_bwd_data(dy, k, wt, dx, m, n, mask=None, u=None, ldu=1, v=None):
+    _call("nerf_linear_bwd_data", _ptr(dy), _ld(dy), k, _ptr(wt), _ptr(u), int(ldu), _ptr(v), _ptr(mask),
+          _ld(mask) if mask is not None else 0, _ptr(dx), _ld(dx), m, n, _stream())
+
+
+def linear_bwd_weight(dy, nout, x, kin, m, splits, slab, ldslab, col0, bslab):
+    _call("nerf_linear_bwd_weight", _ptr(dy), _ld(dy), nout, _ptr(x), _ld(x), kin, m, splits,
+          _ptr(slab), ldslab, col0, _ptr(bslab), _stream())
+
+
+def slab_reduce(slab, splits, nout, ldslab, nout_ref, kin_ref, bslab, gw, gb, accumulate=False):
+    _call("nerf_slab_reduce", _ptr(slab), splits, nout, ldslab, nout_ref, kin_ref, _ptr(bslab), _ptr(gw),
+          _ptr(gb), int(accumulate), _stream())
+
+
+def heads_fwd(h8, hr, hidden, wd, bd, wc, bc, raw4, n_pad):
+    _call("nerf_heads_fwd", _ptr(h8), _ld(h8), _ptr(hr), _ld(hr), hidden, _ptr(wd), _ptr(bd), _ptr(wc),
+          _ptr(bc), _ptr(raw4), n_pad, _stream())
+
+
+def heads_part_size(hidden, n_pad) -> int:
+    return int(lib().nerf_heads_part_size(hidden, n_pad))
+
+
+def heads_bwd(graw4, h8, hr, hidden, wc, dyr, part, n_pad):
+    _call("nerf_heads_bwd", _ptr(graw4), _ptr(h8), _ld(h8), _ptr(hr), _ld(hr), hidden, _ptr(wc), _ptr(dyr),
+          _ld(dyr), _ptr(part), n_pad, _stream())
+
+
+def heads_reduce(part, hidden, n_pad, gwd, gbd, gwc, gbc, accumulate=False):
+    _call("nerf_heads_reduce", _ptr(part), hidden, n_pad, _ptr(gwd), _ptr(gbd), _ptr(gwc), _ptr(gbc),
+          int(accumulate), _stream())
+
+
+def composite_fwd(raw4, z, n_rays, n_samples, flags, rgb, dist, alpha):
+    _call("nerf_composite_fwd", _ptr(raw4), _ptr(z), n_rays, n_samples, flags, _ptr(rgb), _ptr(dist),
+          _ptr(alpha), _stream())
+
+
+def composite_bwd(raw4, z, n_rays, n_samples, flags, g_rgb, g_dist, graw4, n_pad):
+    _call("nerf_composite_bwd", _ptr(raw4), _ptr(z), n_rays, n_samples, flags, _ptr(g_rgb), _ptr(g_dist),
+          _ptr(graw4), n_pad, _stream())
+
+
+def encode_bwd(pts_o, pts_d, view, z, genc_p, genc_d, n_rays, n_samples, g_po, g_pd, g_view):
+    _call("nerf_encode_bwd", _ptr(pts_o), _ptr(pts_d), _ptr(view), _ptr(z), _ptr(genc_p), _ptr(genc_d),
+          n_rays, n_samples, _ptr(g_po), _ptr(g_pd), _ptr(g_view), _stream())
+
+
+def pack_weights(descs: Sequence[PackDesc]):
+    arr = (PackDesc * len(descs))(*descs)
+    _call("nerf_pack_weights", arr, len(descs), _stream())
+
+
+def adam_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step):
+    _call("nerf_adam_step", _ptr(param), _ptr(grad), _ptr(exp_avg), _ptr(exp_avg_sq), param.numel(),
+          float(lr), float(beta1), float(beta2), float(eps), float(weight_decay), int(step), _stream())
+
+
+def chamfer_nn(x, y, idx):
+    _call("nerf_chamfer_nn", _ptr(x), x.shape[0], _ptr(y), y.shape[0], _ptr(idx), _stream())
+
+
+def prof_enable(on: bool):
+    _call("nerf_prof_enable", int(on))
+
+
+def prof_read():
+    ms = ctypes.c_double()
+    n = _c_i64()
+    fl = ctypes.c_double()
+    _call("nerf_prof_read", ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl))
+    return ms.value, n.value, fl.value

@@ -1,0 +1,148 @@
+"""Camera / pose helpers of the hot path (drop-in subset of model/common.py).
+
+Device-agnostic (the reference hard-codes ``device=cuda`` defaults, common.py:113); the
+three 4x4 inversions of every unprojection (common.py:139-141, 205-208) are composed
+once per call into a single camera-to-world matrix.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+
+def arange_pixels(resolution=(128, 128), batch_size=1, image_range=(-1.0, 1.0), device=torch.device("cpu")):
+    """common.py:13-40 -> (integer (x, y) locations [B, H*W, 2], scaled locations)."""
+    h, w = resolution
+    ys, xs = torch.meshgrid(torch.arange(h, device=device), torch.arange(w, device=device), indexing="ij")
+    loc = torch.stack([xs, ys], dim=-1).long().view(1, -1, 2).repeat(batch_size, 1, 1)
+    span = image_range[1] - image_range[0]
+    scaled = loc.float()
+    scaled[:, :, 0] = span * scaled[:, :, 0] / (w - 1) - span / 2
+    scaled[:, :, 1] = span * scaled[:, :, 1] / (h - 1) - span / 2
+    return loc, scaled
+
+
+def get_mask(t):
+    """common.py:60-72: finite entries."""
+    if isinstance(t, np.ndarray):
+        return np.isfinite(t)
+    return (t.abs() != math.inf) & ~torch.isnan(t)
+
+
+def unproject_matrix(camera_mat, world_mat, scale_mat):
+    """scale^-1 @ world^-1 @ K^-1 evaluated in the reference's association order."""
+    return (torch.inverse(scale_mat) @ torch.inverse(world_mat)) @ torch.inverse(camera_mat)
+
+
+def transform_to_world(pixels, depth, camera_mat, world_mat=None, scale_mat=None, invert=True, device=None):
+    """common.py:112-160: world points of pixels [B,N,2] at depth [B,N,1]."""
+    eye = torch.eye(4, dtype=camera_mat.dtype, device=camera_mat.device).unsqueeze(0)
+    world_mat = eye if world_mat is None else world_mat
+    scale_mat = eye if scale_mat is None else scale_mat
+    if invert:
+        M = unproject_matrix(camera_mat, world_mat, scale_mat)
+    else:
+        M = scale_mat @ world_mat @ camera_mat
+    hom = torch.cat([pixels * depth, depth, torch.ones_like(depth)], dim=-1).transpose(1, 2)
+    return (M @ hom)[:, :3].transpose(1, 2)
+
+
+def origin_to_world(n_points, camera_mat, world_mat, scale_mat, invert=True):
+    """common.py:186-215: camera centre repeated n_points times."""
+    M = unproject_matrix(camera_mat, world_mat, scale_mat) if invert else scale_mat @ world_mat @ camera_mat
+    B = camera_mat.shape[0]
+    p = torch.zeros(B, 4, n_points, device=camera_mat.device, dtype=camera_mat.dtype)
+    p[:, -1] = 1.0
+    return (M @ p)[:, :3].transpose(1, 2)
+
+
+def image_points_to_world(image_points, camera_mat, world_mat, scale_mat, invert=True):
+    """common.py:218-237: unprojection at depth 1."""
+    d = torch.ones(*image_points.shape[:2], 1, device=image_points.device, dtype=image_points.dtype)
+    return transform_to_world(image_points, d, camera_mat, world_mat, scale_mat, invert)
+
+
+def get_tensor_values(tensor, p, mode="nearest", scale=True, detach=True, detach_p=True, align_corners=False):
+    """common.py:75-109: grid_sample lookup of [B,C,H,W] at p [B,N,2]."""
+    _, _, h, w = tensor.shape
+    if detach_p:
+        p = p.detach()
+    if scale:
+        p = p.clone()
+        p[:, :, 0] = 2.0 * p[:, :, 0] / w - 1
+        p[:, :, 1] = 2.0 * p[:, :, 1] / h - 1
+    v = torch.nn.functional.grid_sample(tensor, p.unsqueeze(1), mode=mode, align_corners=align_corners)
+    v = v.squeeze(2)
+    if detach:
+        v = v.detach()
+    return v.permute(0, 2, 1)
+
+
+def project_to_cam(points, camera_mat, device=None):
+    """common.py:436-457: project [B,N,3] with K; returns xy [B,N,2] and |xy|<=1 mask."""
+    B, N, _ = points.shape
+    hom = torch.cat([points, torch.ones(B, N, 1, device=points.device, dtype=points.dtype)], -1).transpose(1, 2)
+    xyz = (camera_mat @ hom)[:, :3].transpose(1, 2)
+    xy = xyz[..., :2] / xyz[..., 2:]
+    valid = (xy.abs().max(dim=-1)[0] <= 1).unsqueeze(-1)
+    return xy, valid
+
+
+def vec2skew(v):
+    """common.py:277-287."""
+    z = torch.zeros_like(v[0:1])
+    return torch.stack([torch.cat([z, -v[2:3], v[1:2]]),
+                        torch.cat([v[2:3], z, -v[0:1]]),
+                        torch.cat([-v[1:2], v[0:1], z])], dim=0)
+
+
+def Exp(r):
+    """common.py:290-299: axis-angle -> SO(3), theta = |r| + 1e-15."""
+    K = vec2skew(r)
+    th = r.norm() + 1e-15
+    I = torch.eye(3, dtype=r.dtype, device=r.device)
+    return I + (torch.sin(th) / th) * K + ((1 - torch.cos(th)) / th ** 2) * (K @ K)
+
+
+def convert3x4_4x4(m):
+    """common.py:312-330."""
+    if torch.is_tensor(m):
+        if m.dim() == 3:
+            out = torch.cat([m, torch.zeros_like(m[:, 0:1])], dim=1)
+            out[:, 3, 3] = 1.0
+            return out
+        return torch.cat([m, torch.tensor([[0, 0, 0, 1]], dtype=m.dtype, device=m.device)], dim=0)
+    if m.ndim == 3:
+        out = np.concatenate([m, np.zeros_like(m[:, 0:1])], axis=1)
+        out[:, 3, 3] = 1.0
+        return out
+    out = np.concatenate([m, np.array([[0, 0, 0, 1]], dtype=m.dtype)], axis=0)
+    out[3, 3] = 1.0
+    return out
+
+
+def make_c2w(r, t):
+    """common.py:301-310: [Exp(r) | t] as 4x4."""
+    return convert3x4_4x4(torch.cat([Exp(r), t.unsqueeze(1)], dim=1))
+
+
+def get_ndc_rays_fxfy(fxfy, near, rays_o, rays_d):
+    """common.py:632-675: rays to NDC (LLFF configs)."""
+    t = -(near + rays_o[..., 2]) / rays_d[..., 2]
+    o = rays_o + t[..., None] * rays_d
+    ox, oy = o[..., 0] / o[..., 2], o[..., 1] / o[..., 2]
+    fx, fy = fxfy[0], fxfy[1]
+    o2 = 1.0 + 2.0 * near / o[..., 2]
+    o_ndc = torch.stack([-1.0 / (1 / fx) * ox, -1.0 / (1 / fy) * oy, o2], -1)
+    d_ndc = torch.stack([-1.0 / (1 / fx) * (rays_d[..., 0] / rays_d[..., 2] - ox),
+                         -1.0 / (1 / fy) * (rays_d[..., 1] / rays_d[..., 2] - oy),
+                         1 - o2], -1)
+    return o_ndc, d_ndc
+
+
+def mse2psnr(mse):
+    """common.py:623-630."""
+    mse = np.maximum(mse, 1e-10)
+    return (-10.0 * np.log10(mse)).astype(np.float32)

@@ -1,0 +1,351 @@
+"""Host orchestration of the MI355X per-sample hot path.
+
+One call renders R rays x S samples through
+  samples + encodings  (rendering.py:183-198, official_nerf.py:99-119)
+  -> 8-layer trunk with skip, feature, colour layer on FP32 MFMA (official_nerf.py:60-91)
+  -> density / colour heads (official_nerf.py:66, 91)
+  -> sigma->alpha + exclusive-product compositing (rendering.py:113-141)
+and its backward (training.py:92), entirely in the nerf_hip kernels.  Parameters stay the
+reference ``nn.Linear`` tensors (so state_dicts and ``torch.optim`` keep working); a pack
+kernel copies them into zero-padded MFMA-friendly layouts once per call.
+
+Data layout in HBM (N_pad = R*S rounded up to 128 rows, samples ray-major):
+  enc_p, enc_d : [N_pad][64] fp32        z, raw4 : [N_pad], [N_pad][4]
+  h1..h8, f    : [N_pad][D] fp32 (post-ReLU, saved for the backward)
+  hr           : [N_pad][HR] fp32 (HR = max(64, D/2))
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import torch
+
+from . import _hip
+
+F_DIST_ALPHA, F_WHITE_BKGD, F_RELU = 1, 2, 4
+
+
+def _pad_rows(n: int) -> int:
+    return (n + _hip.ROW_TILE - 1) // _hip.ROW_TILE * _hip.ROW_TILE
+
+
+def _dw_splits(m: int, tiles: int, target_blocks: int = 1024) -> int:
+    """Split-K factor for the weight-gradient GEMM: a power of two giving ~target blocks
+    with each split a whole number of 32-row K tiles."""
+    splits = 1
+    while (splits * 2 * tiles <= target_blocks and m % (splits * 2 * 32) == 0
+           and m // (splits * 2) >= 256):
+        splits *= 2
+    return splits
+
+
+@dataclass
+class LayerSpec:
+    name: str
+    linear: torch.nn.Linear
+    k1: int          # columns taken from the first input
+    seg2: Optional[str]  # 'enc_p' / 'enc_d' / None (second K segment, 64 wide)
+    out_p: int       # padded output rows
+    relu: bool
+
+    @property
+    def kp(self) -> int:
+        return self.k1 + (_hip.ENC_P if self.seg2 else 0)
+
+
+class FieldRunner:
+    """Owns the packed weights of one OfficialStaticNerf and launches the kernels."""
+
+    def __init__(self, module):
+        self.m = module
+        D = module.hidden_dim
+        if D % 64 != 0:
+            raise ValueError(f"nerf_hip: hidden_dim {D} must be a multiple of 64")
+        self.D = D
+        self.HR = max(64, D // 2)
+        m = module
+        L = [
+            LayerSpec("l0", m.layers0[0], _hip.ENC_P, None, D, True),
+            LayerSpec("l1", m.layers0[2], D, None, D, True),
+            LayerSpec("l2", m.layers0[4], D, None, D, True),
+            LayerSpec("l3", m.layers0[6], D, None, D, True),
+            LayerSpec("l4", m.layers1[0], D, "enc_p", D, True),
+            LayerSpec("l5", m.layers1[2], D, None, D, True),
+            LayerSpec("l6", m.layers1[4], D, None, D, True),
+            LayerSpec("l7", m.layers1[6], D, None, D, True),
+            LayerSpec("lf", m.fc_feature, D, None, D, False),
+            LayerSpec("lr", m.rgb_layers[0], D, "enc_d", self.HR, True),
+        ]
+        self.layers = L
+        self.device = None
+        self._bufs = None
+
+    # ------------------------------------------------------------------ packing
+    def _alloc(self, device):
+        D, HR = self.D, self.HR
+        z = lambda *s: torch.zeros(*s, device=device, dtype=torch.float32)
+        self.w = {l.name: z(l.out_p, l.kp) for l in self.layers}
+        self.wt = {l.name: z(l.kp, l.out_p) for l in self.layers}
+        self.b_r = z(HR)           # padded colour-layer bias
+        self.wc = z(3, HR)         # padded fc_rgb weight
+        self.device = device
+
+    def pack(self):
+        dev = self.m.layers0[0].weight.device
+        if dev.type != "cuda":
+            raise RuntimeError("nerf_hip: the field must live on the GPU (no CPU fallback)")
+        if self.device != dev:
+            self._alloc(dev)
+        descs = []
+        for l in self.layers:
+            W = l.linear.weight
+            assert W.is_contiguous() and W.dtype == torch.float32
+            descs.append(_hip.PackDesc(W.data_ptr(), self.w[l.name].data_ptr(), self.wt[l.name].data_ptr(),
+                                       W.shape[0], W.shape[1], l.kp, l.kp, l.out_p))
+        br = self.m.rgb_layers[0].bias
+        descs.append(_hip.PackDesc(br.data_ptr(), self.b_r.data_ptr(), None, 1, br.shape[0], self.HR, 0, 0))
+        wc = self.m.fc_rgb.weight
+        descs.append(_hip.PackDesc(wc.data_ptr(), self.wc.data_ptr(), None, 3, wc.shape[1], self.HR, 0, 0))
+        _hip.pack_weights(descs)
+
+    def bias(self, l: LayerSpec):
+        return self.b_r if l.name == "lr" else l.linear.bias
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, pts_o, pts_d, view, noise, near, far, S: int, flags: int, keep: bool,
+                composite: bool = True):
+        """Renders R = pts_o.shape[0] rays.  Returns rgb [R,3], dist [R], alpha [R,S], z [R,S]
+        and (if keep) the saved state for backward().  With composite=False the first
+        output is the raw head tensor raw4 [N_pad,4] (sigma_raw, rgb logits)."""
+        R = pts_o.shape[0]
+        N = R * S
+        Np = _pad_rows(N)
+        dev = pts_o.device
+        D, HR = self.D, self.HR
+        e = lambda *s: torch.empty(*s, device=dev, dtype=torch.float32)
+        self.pack()
+        z = e(Np)
+        enc_p = e(Np, _hip.ENC_P)
+        enc_d = e(Np, _hip.ENC_D)
+        _hip.encode_samples(pts_o, pts_d, view, noise, R, S, Np, near, far, z, enc_p, enc_d)
+        acts = []
+        if keep:
+            outs = [e(Np, D) for _ in range(9)] + [e(Np, HR)]
+        else:
+            ping = [e(Np, D), e(Np, D)]
+            outs = [ping[i % 2] for i in range(9)] + [e(Np, HR)]
+        x = enc_p
+        segs = {"enc_p": enc_p, "enc_d": enc_d}
+        for i, l in enumerate(self.layers):
+            y = outs[i]
+            x2 = segs[l.seg2] if l.seg2 else None
+            k1 = l.k1
+            _hip.linear_fwd(x, k1, x2, _hip.ENC_P if x2 is not None else 0, self.w[l.name], self.bias(l), y,
+                            Np, l.out_p, l.relu)
+            acts.append(y)
+            x = y
+            if l.name == "l7":
+                h8 = y
+        hr = acts[9]
+        raw4 = e(Np, 4)
+        m = self.m
+        _hip.heads_fwd(h8, hr, D, m.fc_density.weight, m.fc_density.bias, self.wc, m.fc_rgb.bias, raw4, Np)
+        if composite:
+            rgb = e(R, 3)
+            dist = e(R)
+            alpha = e(R, S)
+            _hip.composite_fwd(raw4, z, R, S, flags, rgb, dist, alpha)
+        else:
+            rgb, dist, alpha = raw4, None, None
+        state = None
+        if keep:
+            state = dict(R=R, S=S, Np=Np, flags=flags, z=z, enc_p=enc_p, enc_d=enc_d, acts=acts, raw4=raw4,
+                         pts_o=pts_o, pts_d=pts_d, view=view)
+        return rgb, dist, alpha, z[:N].view(R, S), state
+
+    # ------------------------------------------------------------------ backward
+    def param_list(self) -> List[torch.nn.Parameter]:
+        return list(self.m.parameters())
+
+    def backward(self, st, g_rgb, g_dist, want_ray_grad: bool, graw4=None):
+        """Returns (list of parameter gradients in self.param_list() order, ray grads or None).
+        Starts from the ray gradients (composite backward) or, when ``graw4`` is given,
+        directly from the gradient of the raw head outputs."""
+        R, S, Np, flags = st["R"], st["S"], st["Np"], st["flags"]
+        D, HR = self.D, self.HR
+        dev = st["z"].device
+        e = lambda *s: torch.empty(*s, device=dev, dtype=torch.float32)
+        acts = st["acts"]
+        h = {l.name: acts[i] for i, l in enumerate(self.layers)}
+        m = self.m
+        params = self.param_list()
+        flat = torch.empty(sum(p.numel() for p in params), device=dev, dtype=torch.float32)
+        grads, off = {}, 0
+        for p in params:
+            grads[id(p)] = flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        G = lambda p: grads[id(p)]
+
+        if graw4 is None:
+            graw4 = e(Np, 4)
+            _hip.composite_bwd(st["raw4"], st["z"], R, S, flags, g_rgb, g_dist, graw4, Np)
+        # heads: d(fc_density), d(fc_rgb), dY of the colour layer
+        dyr = e(Np, HR)
+        part = e(_hip.heads_part_size(D, Np))
+        _hip.heads_bwd(graw4, h["l7"], h["lr"], D, self.wc, dyr, part, Np)
+        gwc = G(m.fc_rgb.weight) if HR == D // 2 else e(3, HR)
+        _hip.heads_reduce(part, D, Np, G(m.fc_density.weight), G(m.fc_density.bias), gwc, G(m.fc_rgb.bias))
+        if HR != D // 2:
+            G(m.fc_rgb.weight).copy_(gwc[:, :D // 2])
+
+        genc_p = genc_d = None
+        if want_ray_grad:
+            genc_p = torch.zeros(Np, _hip.ENC_P, device=dev)
+            genc_d = torch.zeros(Np, _hip.ENC_D, device=dev)
+
+        # walk the layers backwards; dy = gradient w.r.t. the layer's pre-activation output
+        dy = dyr
+        prev_in = {"l0": st["enc_p"], "l1": h["l0"], "l2": h["l1"], "l3": h["l2"], "l4": h["l3"],
+                   "l5": h["l4"], "l6": h["l5"], "l7": h["l6"], "lf": h["l7"], "lr": h["lf"]}
+        order = ["lr", "lf", "l7", "l6", "l5", "l4", "l3", "l2", "l1", "l0"]
+        spec = {l.name: l for l in self.layers}
+        seg_buf = {"enc_p": st["enc_p"], "enc_d": st["enc_d"]}
+        pingpong = [e(Np, D), e(Np, D)]
+        for step, name in enumerate(order):
+            l = spec[name]
+            W = l.linear.weight
+            nout_ref, kin_ref = W.shape
+            x_in = prev_in[name]
+            k1 = l.k1
+            # --- weight / bias gradient: split-K slabs + reduce into the reference layout
+            tiles = (l.out_p // 64) * (l.kp // 64)
+            splits = _dw_splits(Np, max(1, tiles // 4))
+            slab = e(splits * l.out_p * l.kp)
+            bslab = e(splits * l.out_p)
+            _hip.linear_bwd_weight(dy, l.out_p, x_in, k1, Np, splits, slab, l.kp, 0, bslab)
+            if l.seg2:
+                _hip.linear_bwd_weight(dy, l.out_p, seg_buf[l.seg2], 64, Np, splits, slab, l.kp, k1, None)
+            gb = G(l.linear.bias) if l.out_p == nout_ref else e(l.out_p)
+            gw = G(W)
+            _hip.slab_reduce(slab, splits, l.out_p, l.kp, nout_ref, kin_ref, bslab, gw, gb)
+            if l.out_p != nout_ref:
+                G(l.linear.bias).copy_(gb[:nout_ref])
+            # --- input gradient
+            wt = self.wt[name]
+            if name == "l0":
+                if want_ray_grad:
+                    tmp = e(Np, _hip.ENC_P)
+                    _hip.linear_bwd_data(dy, l.out_p, wt, tmp, Np, _hip.ENC_P)
+                    genc_p.add_(tmp)
+                break
+            if l.seg2 and want_ray_grad:
+                tgt = genc_p if l.seg2 == "enc_p" else genc_d
+                tmp = e(Np, 64)
+                _hip.linear_bwd_data(dy, l.out_p, wt[k1:k1 + 64], tmp, Np, 64)
+                tgt.add_(tmp)
+            dx = pingpong[step % 2]
+            mask = None if name == "lr" else prev_in[name]   # f (input of lr) has no activation
+            if name == "lf":   # + density path: d sigma_raw (graw4[:,0]) x w_density
+                _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask, u=graw4, ldu=4,
+                                     v=m.fc_density.weight)
+            else:
+                _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask)
+            dy = dx
+
+        ray = None
+        if want_ray_grad:
+            g_po, g_pd, g_view = e(R, 3), e(R, 3), e(R, 3)
+            _hip.encode_bwd(st["pts_o"], st["pts_d"], st["view"], st["z"], genc_p, genc_d, R, S,
+                            g_po, g_pd, g_view)
+            ray = (g_po, g_pd, g_view)
+        return [G(p) for p in params], ray
+
+
+class FieldRenderFn(torch.autograd.Function):
+    """autograd boundary of the fused HIP render path.  Inputs: ray origins/directions
+    used for the sample points, the view direction fed to the colour branch, the
+    injected stratified noise, and the field parameters (so autograd routes their
+    gradients to ``param.grad`` exactly as nn.Linear would)."""
+
+    @staticmethod
+    def forward(ctx, runner: FieldRunner, pts_o, pts_d, view, noise, near, far, S, flags, *params):
+        need = torch.is_grad_enabled() and any(ctx.needs_input_grad)
+        rgb, dist, alpha, z, st = runner.forward(pts_o, pts_d, view, noise, near, far, S, flags, keep=True)
+        ctx.runner = runner
+        ctx.state = st
+        ctx.ray_grad = any(ctx.needs_input_grad[1:4])
+        ctx.mark_non_differentiable(alpha, z)
+        return rgb, dist, alpha, z
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_dist, g_alpha, g_z):
+        st = ctx.state
+        R = st["R"]
+        if g_rgb is None:
+            g_rgb = torch.zeros(R, 3, device=st["z"].device)
+        if g_dist is None:
+            g_dist = torch.zeros(R, device=st["z"].device)
+        grads, ray = ctx.runner.backward(st, g_rgb.contiguous(), g_dist.contiguous(), ctx.ray_grad)
+        ctx.state = None
+        g_po = g_pd = g_view = None
+        if ray is not None:
+            g_po, g_pd, g_view = ray
+        return (None, g_po, g_pd, g_view, None, None, None, None, None, *grads)
+
+
+def render_field(module, pts_o, pts_d, view, noise, near, far, S, flags):
+    """Differentiable render of R rays through the HIP path (training)."""
+    runner = module.hip_runner()
+    params = runner.param_list()
+    return FieldRenderFn.apply(runner, pts_o.contiguous(), pts_d.contiguous(), view.contiguous(),
+                               None if noise is None else noise.contiguous(), float(near), float(far),
+                               int(S), int(flags), *params)
+
+
+@torch.no_grad()
+def render_field_eval(module, pts_o, pts_d, view, near, far, S, flags, ray_chunk: int = 8192):
+    """Forward-only render in ray chunks (ping-pong activations, no saved state)."""
+    runner = module.hip_runner()
+    R = pts_o.shape[0]
+    outs = []
+    for r0 in range(0, R, ray_chunk):
+        r1 = min(R, r0 + ray_chunk)
+        rgb, dist, alpha, z, _ = runner.forward(pts_o[r0:r1].contiguous(), pts_d[r0:r1].contiguous(),
+                                                view[r0:r1].contiguous(), None, near, far, S, flags, keep=False)
+        outs.append((rgb, dist, alpha, z))
+    return tuple(torch.cat([o[i] for o in outs], 0) for i in range(4))
+
+
+class FieldRawFn(torch.autograd.Function):
+    """Per-point evaluation (OfficialStaticNerf.forward, official_nerf.py:69-96): points
+    p [n,3] and view directions [n,3] -> raw head outputs [n,4] (sigma_raw, rgb logits),
+    differentiable w.r.t. the points, the directions and the parameters."""
+
+    @staticmethod
+    def forward(ctx, runner: FieldRunner, p, d, *params):
+        n = p.shape[0]
+        zeros = torch.zeros_like(p)
+        raw4, _, _, _, st = runner.forward(p, zeros, d, None, 0.0, 0.0, 1, 0, keep=True, composite=False)
+        ctx.runner, ctx.state, ctx.n = runner, st, n
+        ctx.ray_grad = any(ctx.needs_input_grad[1:3])
+        return raw4[:n]
+
+    @staticmethod
+    def backward(ctx, g_raw):
+        st = ctx.state
+        Np = st["Np"]
+        graw4 = torch.zeros(Np, 4, device=g_raw.device)
+        graw4[:ctx.n] = g_raw
+        grads, ray = ctx.runner.backward(st, None, None, ctx.ray_grad, graw4=graw4)
+        ctx.state = None
+        g_p = g_d = None
+        if ray is not None:
+            g_p, _, g_d = ray
+        return (None, g_p, g_d, *grads)
+
+
+def eval_points(module, p, d):
+    """raw head outputs for arbitrary points (autograd-aware)."""
+    runner = module.hip_runner()
+    return FieldRawFn.apply(runner, p.contiguous(), d.contiguous(), *runner.param_list())

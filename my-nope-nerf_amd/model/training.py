@@ -1,0 +1,304 @@
+"""Trainer (drop-in for model/training.py:16-416).
+
+Same constructor, ``train_step`` / ``render_visdata`` / ``compute_loss`` signatures and
+loss-dict keys.  The step itself is the reference algorithm; what changes is where it
+runs and what it waits for:
+  * the render + its backward are the fused nerf_hip path (rendering.Renderer);
+  * the step is free of device->host syncs: the depth-loss mask stays a dense weight,
+    the distortion clamp is a ``torch.where``, the "any valid depth among the sampled
+    rays" resampling loop (training.py:280-283) only runs when the image's valid-pixel
+    count (known on the host from the data dict) does not already guarantee it;
+  * with torch.distributed initialised (one process per GPU, RCCL), every rank renders
+    its own rays and the NeRF / pose / distortion gradients are averaged by ONE
+    all-reduce over a flat bucket before the optimiser steps.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+from torch.nn import functional as F
+
+from .common import arange_pixels, get_tensor_values, project_to_cam, transform_to_world
+from .losses import Loss
+
+
+class Trainer(object):
+    def __init__(self, model, optimizer, cfg, device=None, optimizer_pose=None, pose_param_net=None,
+                 optimizer_focal=None, focal_net=None, optimizer_distortion=None, distortion_net=None, **kwargs):
+        self.model = model
+        self.optimizer = optimizer
+        self.device = device
+        self.optimizer_pose = optimizer_pose
+        self.pose_param_net = pose_param_net
+        self.focal_net = focal_net
+        self.optimizer_focal = optimizer_focal
+        self.distortion_net = distortion_net
+        self.optimizer_distortion = optimizer_distortion
+
+        self.n_training_points = cfg["n_training_points"]
+        self.rendering_technique = cfg["type"]
+        self.vis_geo = cfg.get("vis_geo", False)
+        self.detach_gt_depth = cfg["detach_gt_depth"]
+        self.pc_ratio = cfg["pc_ratio"]
+        self.match_method = cfg["match_method"]
+        self.shift_first = cfg["shift_first"]
+        self.detach_ref_img = cfg["detach_ref_img"]
+        self.scale_pcs = cfg["scale_pcs"]
+        self.detach_rgbs_scale = cfg["detach_rgbs_scale"]
+        self.vis_reprojection_every = cfg["vis_reprojection_every"]
+        self.nearest_limit = cfg["nearest_limit"]
+        self.annealing_epochs = cfg["annealing_epochs"]
+        for w in ("pc_weight", "rgb_s_weight", "rgb_weight", "depth_weight", "weight_dist_2nd_loss",
+                  "weight_dist_1st_loss", "depth_consistency_weight", "t_cycle_weight"):
+            setattr(self, w, cfg[w])
+        self.loss = Loss(cfg)
+        self._pix_cache = {}
+        self.world_size = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+    # ------------------------------------------------------------------ step
+    def _modules_and_optims(self):
+        mods = [(self.model, self.optimizer), (self.pose_param_net, self.optimizer_pose),
+                (self.focal_net, self.optimizer_focal), (self.distortion_net, self.optimizer_distortion)]
+        return [(m, o) for m, o in mods if m is not None]
+
+    def train_step(self, data, it=None, epoch=None, scheduling_start=None, render_path=None):
+        """training.py:70-100."""
+        for m, o in self._modules_and_optims():
+            m.train()
+            if o is not None:
+                o.zero_grad()
+        loss_dict = self.compute_loss(data, it=it, epoch=epoch, scheduling_start=scheduling_start,
+                                      out_render_path=render_path)
+        loss_dict["loss"].backward()
+        if self.world_size > 1:
+            self.allreduce_grads()
+        for _, o in self._modules_and_optims():
+            if o is not None:
+                o.step()
+        return loss_dict
+
+    def allreduce_grads(self):
+        """Average every gradient over the ranks with one flat RCCL all-reduce."""
+        grads = []
+        for m, _ in self._modules_and_optims():
+            grads += [p.grad for p in m.parameters() if p.grad is not None]
+        if not grads:
+            return
+        flat = torch._utils._flatten_dense_tensors(grads)
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+        flat.mul_(1.0 / self.world_size)
+        for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+            g.copy_(f)
+
+    # ------------------------------------------------------------------ data
+    def process_data_dict(self, data):
+        """training.py:166-183."""
+        dev = self.device
+        img = data.get("img").to(dev, non_blocking=True)
+        img_idx = data.get("img.idx")
+        depth = data.get("img.dpt")
+        if depth is None:
+            depth = data.get("img.depth")
+        depth = depth.to(dev, non_blocking=True).unsqueeze(1)
+        depth_mask = data.get("img.depth_mask")
+        camera_mat = data.get("img.camera_mat").to(dev, non_blocking=True)
+        scale_mat = data.get("img.scale_mat").to(dev, non_blocking=True)
+        pose_gt = data.get("img.pose_gt").to(dev, non_blocking=True)
+        return (img, depth, camera_mat, scale_mat, img_idx, pose_gt, depth_mask)
+
+    def process_data_reference(self, data):
+        dev = self.device
+        ref_imgs = data.get("img.ref_imgs").to(dev, non_blocking=True)
+        ref_depths = data.get("img.ref_dpts")
+        if ref_depths is None:
+            ref_depths = data.get("img.ref_depths")
+        ref_depths = ref_depths.to(dev, non_blocking=True).unsqueeze(1)
+        ref_pose_gt = data.get("img.ref_pose_gt").to(dev, non_blocking=True)
+        return (ref_imgs, ref_depths, data.get("img.ref_idxs"), ref_pose_gt)
+
+    def anneal(self, start_weight, end_weight, anneal_start_epoch, anneal_epoches, current):
+        """training.py:204-212."""
+        if current <= anneal_start_epoch:
+            return start_weight
+        if current >= anneal_start_epoch + anneal_epoches:
+            return end_weight
+        return start_weight + (end_weight - start_weight) * (current - anneal_start_epoch) / anneal_epoches
+
+    def _pixels(self, h, w, device):
+        key = (h, w, str(device))
+        if key not in self._pix_cache:
+            self._pix_cache[key] = arange_pixels((h, w), 1, device=device)[1]
+        return self._pix_cache[key]
+
+    def sample_rays(self, n_pix, depth_mask, need_valid):
+        """training.py:277-283: a random subset of pixels; resample while none has a valid
+        depth, which is only possible when fewer than n_pix - n_points + 1 are valid."""
+        dev = self.device
+        ray_idx = torch.randperm(n_pix, device=dev)[:self.n_training_points]
+        if need_valid and depth_mask is not None:
+            n_valid = int(depth_mask.sum()) if not depth_mask.is_cuda else None
+            if n_valid is None or n_valid <= n_pix - self.n_training_points:
+                m = depth_mask.flatten().to(dev)
+                while not m[ray_idx].any():
+                    ray_idx = torch.randperm(n_pix, device=dev)[:self.n_training_points]
+        return ray_idx
+
+    # ------------------------------------------------------------------ loss
+    def compute_loss(self, data, eval_mode=False, it=None, epoch=None, scheduling_start=None,
+                     out_render_path=None):
+        """training.py:214-416."""
+        names = ["rgb_weight", "depth_weight", "pc_weight", "rgb_s_weight", "depth_consistency_weight",
+                 "weight_dist_2nd_loss", "weight_dist_1st_loss", "t_cycle_weight"]
+        weights = {n: self.anneal(getattr(self, n)[0], getattr(self, n)[1], scheduling_start,
+                                  self.annealing_epochs, epoch) for n in names}
+        rgb_loss_type = "l1" if epoch < self.annealing_epochs + scheduling_start else "l2"
+        render_model = weights["rgb_weight"] != 0.0 or weights["depth_weight"] != 0.0
+        use_ref_imgs = (weights["pc_weight"] != 0.0 or weights["rgb_s_weight"] != 0.0
+                        or weights["t_cycle_weight"] != 0.0)
+        nl = self.nearest_limit
+        img, depth_input, camera_mat_gt, scale_mat, img_idx, pose_gt, depth_mask = self.process_data_dict(data)
+        if use_ref_imgs:
+            ref_img, depth_ref, ref_idx, ref_pose_gt = self.process_data_reference(data)
+        dev = self.device
+        B, _, h, w = img.shape
+        _, _, h_depth, w_depth = depth_input.shape
+        kwargs = {"weights": weights, "rgb_loss_type": rgb_loss_type}
+        if self.pose_param_net is not None:
+            kwargs["t_list"] = self.pose_param_net.get_t()
+        world_mat_gt = torch.inverse(pose_gt).unsqueeze(0)
+        num_cams = self.pose_param_net.num_cams if self.pose_param_net is not None else None
+        c2w = self.pose_param_net(img_idx) if self.pose_param_net is not None else pose_gt.reshape(4, 4)
+        world_mat = torch.inverse(c2w).unsqueeze(0)
+        scale_input = shift_input = None
+        if self.distortion_net is not None:
+            scale_input, shift_input = self.distortion_net(img_idx)
+            if self.shift_first:
+                depth_input = (depth_input + shift_input) * scale_input
+            else:
+                depth_input = depth_input * scale_input + shift_input
+        if self.optimizer_focal:
+            fxfy = self.focal_net(0)
+            pad = torch.zeros(4, device=dev)
+            one = torch.ones(1, device=dev)
+            camera_mat = torch.cat([fxfy[0:1], pad, -fxfy[1:2], pad, -one, pad, one]).view(1, 4, 4)
+        else:
+            camera_mat = camera_mat_gt
+
+        ray_idx = self.sample_rays(h * w, depth_mask, data.get("img.dpt") is None)
+        rgb_gt = img.view(B, 3, h * w).permute(0, 2, 1)[:, ray_idx]
+        p = self._pixels(h, w, dev)[:, ray_idx]
+
+        rendered_rgb = rendered_depth = gt_depth = dmask = None
+        if render_model:
+            out = self.model(p, ray_idx, camera_mat, world_mat, scale_mat, self.rendering_technique, it=it,
+                             eval_mode=eval_mode, depth_img=depth_input, img_size=(h, w),
+                             dense_depth=not eval_mode)
+            rendered_rgb, rendered_depth, gt_depth = out["rgb"], out["depth_pred"], out["depth_gt"]
+            dmask = out.get("depth_mask")
+
+        if use_ref_imgs:
+            kwargs.update(self._reference_terms(weights, img, ref_img, depth_input, depth_ref, img_idx, ref_idx,
+                                                ref_pose_gt, world_mat, world_mat_gt, camera_mat, scale_input,
+                                                num_cams, h_depth, w_depth, nl, it, out_render_path))
+        if render_model and self.detach_gt_depth:
+            gt_depth = gt_depth.detach()
+        loss_dict = self.loss(rendered_rgb, rgb_gt, rendered_depth, gt_depth, depth_mask=dmask, **kwargs)
+        if self.optimizer_focal:
+            loss_dict["focalx"] = fxfy[0] / camera_mat_gt[0, 0, 0]
+            loss_dict["focaly"] = fxfy[1] / camera_mat_gt[0, 1, 1]
+        loss_dict["scale"] = scale_input
+        loss_dict["shift"] = shift_input
+        return loss_dict
+
+    def _reference_terms(self, weights, img, ref_img, depth_input, depth_ref, img_idx, ref_idx, ref_pose_gt,
+                         world_mat, world_mat_gt, camera_mat, scale_input, num_cams, h_depth, w_depth, nl, it,
+                         out_render_path):
+        """training.py:305-405: point clouds of the image pair, relative pose, reprojection."""
+        B = img.shape[0]
+        ref_Rt_gt = torch.inverse(ref_pose_gt).unsqueeze(0)
+        c2w_ref = self.pose_param_net(ref_idx)
+        scale_ref = shift_ref = None
+        if self.distortion_net is not None:
+            scale_ref, shift_ref = self.distortion_net(ref_idx)
+            if self.shift_first:
+                depth_ref = scale_ref * (depth_ref + shift_ref)
+            else:
+                depth_ref = scale_ref * depth_ref + shift_ref
+        if self.detach_ref_img:
+            c2w_ref = c2w_ref.detach()
+            scale_ref = scale_ref.detach() if scale_ref is not None else None
+            depth_ref = depth_ref.detach()
+        ref_Rt = torch.inverse(c2w_ref).unsqueeze(0)
+        if int(img_idx) < num_cams - 1:
+            d1, d2, img1, img2 = depth_input, depth_ref, img, ref_img
+            Rt_rel_12 = ref_Rt @ torch.inverse(world_mat)
+            Rt_rel_12_gt = ref_Rt_gt @ torch.inverse(world_mat_gt)
+            scale1 = scale_input
+        else:
+            d1, d2, img1, img2 = depth_ref, depth_input, ref_img, img
+            Rt_rel_12 = world_mat @ torch.inverse(ref_Rt)
+            Rt_rel_12_gt = world_mat_gt @ torch.inverse(ref_Rt_gt)
+            scale1 = scale_ref
+        R_rel_12, t_rel_12 = Rt_rel_12[:, :3, :3], Rt_rel_12[:, :3, 3]
+        res = (int(h_depth / self.pc_ratio), int(w_depth / self.pc_ratio))
+        pixel_locations, p_pc = arange_pixels(resolution=res, device=img.device)
+        d1 = F.interpolate(d1, res, mode="nearest").clamp_min(nl)       # d[d < nl] = nl
+        d2 = F.interpolate(d2, res, mode="nearest").clamp_min(nl)
+        pc1 = transform_to_world(p_pc, d1.view(1, -1, 1), camera_mat)
+        pc2 = transform_to_world(p_pc, d2.view(1, -1, 1), camera_mat)
+        out = {}
+        if weights["rgb_s_weight"] != 0.0:
+            i1 = F.interpolate(img1, res, mode="bilinear")
+            i2 = F.interpolate(img2, res, mode="bilinear")
+            rgb_pc1 = get_tensor_values(i1, p_pc, mode="bilinear", scale=False, detach=False, detach_p=False,
+                                        align_corners=True)
+            src = pc1.detach().clone() if self.detach_rgbs_scale else pc1
+            pc1_rot = src @ R_rel_12.transpose(1, 2) + t_rel_12
+            bad = (-pc1_rot[:, :, 2:] < nl).expand_as(pc1_rot)
+            pc1_rot = torch.where(bad, torch.full_like(pc1_rot, nl), pc1_rot)
+            p_reproj, valid = project_to_cam(pc1_rot, camera_mat)
+            rgb_proj = get_tensor_values(i2, p_reproj, mode="bilinear", scale=False, detach=False,
+                                         detach_p=False, align_corners=True)
+            out["rgb_pc1"] = rgb_pc1.view(B, res[0], res[1], 3)
+            out["rgb_pc1_proj"] = rgb_proj.view(B, res[0], res[1], 3)
+            out["valid_points"] = valid.view(B, res[0], res[1], 1)
+        if self.scale_pcs and scale1 is not None:
+            pc1 = pc1 / scale1
+            pc2 = pc2 / scale1
+        out["X"] = pc1 @ R_rel_12.transpose(1, 2) + t_rel_12
+        out["Y"] = pc2
+        out["sample_resolution"] = res
+        out["p_2d"] = pixel_locations
+        out["rt_12"] = Rt_rel_12
+        out["rt_12_gt"] = Rt_rel_12_gt
+        return out
+
+    # ------------------------------------------------------------------ render
+    def render_visdata(self, data, resolution, it, out_render_path):
+        """training.py:103-165 (colour + depth PNGs at ``resolution``; the phong geometry
+        visualisation is outside the MI355X path)."""
+        from PIL import Image
+        img, depth_input, camera_mat, scale_mat, img_idx, *_ = self.process_data_dict(data)
+        h, w = resolution
+        c2w = self.pose_param_net(img_idx)
+        world_mat = torch.inverse(c2w).unsqueeze(0)
+        if self.optimizer_focal:
+            fxfy = self.focal_net(0)
+            camera_mat = torch.tensor([[[fxfy[0], 0, 0, 0], [0, -fxfy[1], 0, 0], [0, 0, -1, 0], [0, 0, 0, 1]]],
+                                      device=self.device)
+        pixels = self._pixels(h, w, self.device)
+        p_idx = torch.arange(h * w, device=self.device)
+        with torch.no_grad():
+            out = self.model(pixels, p_idx, camera_mat, world_mat, scale_mat, self.rendering_technique,
+                             add_noise=False, eval_mode=True, it=it, depth_img=depth_input, img_size=(h, w))
+            rgb = out["rgb"].view(h, w, 3).cpu().numpy()
+            depth = out["depth_pred"].view(h, w).cpu().numpy()
+        img_out = (rgb * 255).astype(np.uint8)
+        if out_render_path:
+            dimg = np.clip(255.0 / depth.max() * (depth - depth.min()), 0, 255).astype(np.uint8)
+            Image.fromarray(dimg).save(os.path.join(out_render_path, "%04d_depth.png" % int(img_idx)))
+            Image.fromarray(img_out).convert("RGB").save(os.path.join(out_render_path, "%04d_img.png" % int(img_idx)))
+        return img_out
