@@ -1,0 +1,222 @@
+"""Benchmark: training rays/s of the NoPe-NeRF render path at 1024 rays x 128 samples.
+
+Workload (BASELINE.json configs[1], config 2 of SURVEY.md section 8(d)): a V_KITTI-shaped
+synthetic scene (188x621 image, fx = fy = 362.5, depth prior U[1,8] with ~5 % holes, a
+fixed camera pose), hidden width 256, 1024 rays per GPU per step, 128 stratified samples
+per ray.  One step = Trainer.train_step: ray sampling (randperm on device), ray
+generation, fused HIP render forward, rgb-L2 + depth-L1 loss, fused HIP backward,
+gradient all-reduce over RCCL (N > 1), Adam.  Inputs are resident in HBM.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+
+Rank 0 prints ONE JSON line.  Extra objects: "roofline" (FP32-MFMA GEMM family, timed
+live with hipEvents around every GEMM launch of the timed steps) and "cpu_baseline"
+(the oracle CPU restatement of the same step on this host's cores, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "my-nope-nerf_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "training rays/sec at 1024 rays×128 samples; PSNR parity (±0.1 dB) vs ref"
+H, W, FOCAL = 188, 621, 362.5
+RAYS, SAMPLES, HIDDEN = 1024, 128, 256
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_cfg():
+    from tests.helpers import make_cfg as mk
+    cfg = mk(hidden=HIDDEN, S=SAMPLES)
+    t = cfg["training"]
+    t["n_training_points"] = RAYS
+    t["pc_weight"] = [0.0, 0.0]        # config 2: pure render path (rgb l2 + depth l1)
+    t["rgb_s_weight"] = [0.0, 0.0]
+    return cfg
+
+
+def synthetic_scene(dev, seed=0):
+    """V_KITTI-shaped data dict (dataset.py:281-364 keys), resident on the GPU."""
+    from tests.helpers import camera_K, rigid_c2w
+    g = torch.Generator().manual_seed(seed)
+    yy, xx = torch.meshgrid(torch.linspace(0, 1, H), torch.linspace(0, 1, W), indexing="ij")
+    img = torch.stack([0.5 + 0.4 * torch.sin(6 * xx + 2 * yy), 0.5 + 0.4 * torch.cos(5 * yy),
+                       0.3 + 0.3 * xx * yy], 0).unsqueeze(0)
+    img = (img + 0.02 * torch.rand(img.shape, generator=g)).clamp(0, 1)
+    depth = 1.0 + 7.0 * torch.rand(1, H, W, generator=g)
+    holes = torch.rand(1, H, W, generator=g) < 0.05
+    depth[holes] = 0.0
+    c2w = rigid_c2w(seed)
+    data = {"img": img, "img.idx": torch.tensor([0]), "img.depth": depth, "img.depth_mask": ~holes,
+            "img.camera_mat": camera_K(H, W, FOCAL, FOCAL), "img.scale_mat": torch.eye(4).unsqueeze(0),
+            "img.pose_gt": c2w.unsqueeze(0)}
+    for k, v in list(data.items()):
+        if k not in ("img.idx", "img.depth_mask"):
+            data[k] = v.to(dev)
+    return data, c2w
+
+
+def build_trainer(dev, c2w, cfg):
+    import model as mdl
+    from model.optim import HipAdam
+    torch.manual_seed(42)                                   # train.py:23-24
+    net = mdl.OfficialStaticNerf(cfg)
+    renderer = mdl.Renderer(net, cfg["rendering"], device=dev)
+    nn_model = mdl.get_model(renderer, cfg, device=dev)
+    opt = HipAdam(nn_model.parameters(), lr=cfg["training"]["learning_rate"])
+    pose = mdl.LearnPose(1, False, False, cfg, init_c2w=c2w.unsqueeze(0).to(dev)).to(dev)
+    trainer = mdl.Trainer(nn_model, opt, cfg["training"], device=dev, pose_param_net=pose)
+    return trainer, net
+
+
+def algorithmic_gemm_flops(net, n_samples):
+    """FP32 FLOPs of the field GEMMs one train step needs (reference shapes, no padding):
+    forward and weight-gradient of every Linear, input-gradient of every Linear except
+    the first and except the encoding columns (poses fixed)."""
+    D = net.hidden_dim
+    layers = [net.layers0[0], net.layers0[2], net.layers0[4], net.layers0[6], net.layers1[0], net.layers1[2],
+              net.layers1[4], net.layers1[6], net.fc_feature, net.rgb_layers[0]]
+    fl = 0
+    for i, lin in enumerate(layers):
+        out_f, in_f = lin.weight.shape
+        fl += 2 * n_samples * out_f * in_f * 2          # forward + dW
+        if i > 0:
+            in_x = D if lin in (net.layers1[0], net.rgb_layers[0]) else in_f
+            fl += 2 * n_samples * out_f * in_x           # dX
+    return fl
+
+
+def cpu_baseline(budget_s=20.0):
+    """The oracle (CPU restatement of the reference step) on this host's cores."""
+    from oracle import nerf_oracle as orc
+    from tests.helpers import synthetic_rays
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():      # the box's CPU share
+        threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
+    threads = max(1, threads)
+    torch.set_num_threads(threads)
+    torch.manual_seed(42)
+    net = orc.OracleNerf(hidden_dim=HIDDEN)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    b = synthetic_rays(R=RAYS, S=SAMPLES, seed=3)
+    img = torch.rand(1, 3, H, W)
+    depth_img = 1.0 + 7.0 * torch.rand(1, 1, H, W)
+    ray_idx = torch.randperm(H * W)[:RAYS]
+
+    def step():
+        orc.train_step_render(net, opt, img, depth_img, b["K"], b["c2w"], b["scale"], ray_idx,
+                              b["noise"], {"num_points": SAMPLES})
+
+    step()                                                  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step()
+        n += 1
+        el = time.perf_counter() - t0
+        if el > budget_s or n >= 20:
+            break
+    return {"value": RAYS * n / el, "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"oracle train step (torch CPU fp32), {RAYS} rays x {SAMPLES} samples, D={HIDDEN}, "
+                      f"{n} timed steps after 1 warm-up ({el:.1f} s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    from model import _hip
+    _hip.load_library()
+
+    cfg = make_cfg()
+    data, c2w = synthetic_scene(dev)
+    trainer, net = build_trainer(dev, c2w, cfg)
+    torch.cuda.manual_seed(1000 + rank)                     # each rank samples its own rays
+
+    def one(it):
+        return trainer.train_step(data, it=it, epoch=0, scheduling_start=0)
+
+    for i in range(args.warmup):
+        one(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    _hip.prof_enable(True)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ld = one(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    gemm_ms, gemm_launches, _ = _hip.prof_read()
+    _hip.prof_enable(False)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    loss = ld["loss"].detach().item()
+    psnr = -10.0 * math.log10(max(ld["l2_mean"].detach().item(), 1e-10))
+    if not math.isfinite(loss):
+        raise RuntimeError(f"non-finite loss {loss}")
+
+    if rank == 0:
+        ms = 1e3 * elapsed / args.steps
+        alg = algorithmic_gemm_flops(net, RAYS * SAMPLES) * args.steps
+        achieved = alg / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else None
+        roof = {"bound": "mfma", "kernel": "k_gemm_nt/k_gemm_tn (FP32 MFMA 32x32x2, field MLP)",
+                "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None, "traffic": None,
+                "launches_per_step": gemm_launches / args.steps,
+                "avg_launch_us": 1e3 * gemm_ms / max(1, gemm_launches),
+                "gemm_ms_per_step": gemm_ms / args.steps}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            log("timing the CPU baseline (oracle) ...")
+            cpu = cpu_baseline(args.cpu_budget)
+        out = {"metric": METRIC, "value": world * RAYS / (elapsed / args.steps), "unit": "rays/s",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+               "data": "synthetic (V_KITTI-shaped scene, random-init NeRF D=256; no dataset offline)",
+               "config": {"workload": "config 2: V_KITTI scene-1 shape 188x621, 1024 rays x 128 samples per GPU, "
+                                      "poses fixed, full train_step (render fwd+bwd, rgb-l2+depth-l1, Adam)",
+                          "global_batch": world * RAYS, "seq_len": SAMPLES, "hidden_dim": HIDDEN,
+                          "parallelism": f"dp{world}"},
+               "final_loss": loss, "train_psnr_last_step": psnr,
+               "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -152,30 +152,52 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(NTArgs p) {
         __syncthreads();
     }
 
-    // epilogue
+    // epilogue.  The backward's mask / rank-1 operands are loaded as whole batches before
+    // any store: p.c may alias them as far as the compiler knows, so interleaved
+    // load/store pairs would serialise one memory round trip per element.
     const int lane = lane_id();
     const int l32 = lane & 31, hi = lane >> 5;
+    if (EPI == EPI_FWD) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wn0 + 32 * j + l32;
-        float bcol = 0.f, vcol = 0.f;
-        if (EPI == EPI_FWD) bcol = p.bias ? p.bias[col] : 0.f;
-        if (EPI == EPI_BWD) vcol = p.u ? p.v[col] : 0.f;
+        for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn0 + 32 * j + l32;
+            const float bcol = p.bias ? p.bias[col] : 0.f;
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = m0 + wm0 + 32 * i + acc_row(r, hi);
-                float x = acc[i][j][r];
-                if (EPI == EPI_FWD) {
-                    x = x + bcol;
+                for (int r = 0; r < 16; ++r) {
+                    const int row = m0 + wm0 + 32 * i + acc_row(r, hi);
+                    float x = acc[i][j][r] + bcol;
                     if (p.relu) x = fmaxf(x, 0.f);
-                } else {
-                    if (p.u) x = x + p.u[(size_t)row * p.ldu] * vcol;
-                    if (p.mask) x = (p.mask[(size_t)row * p.ldmask + col] > 0.f) ? x : 0.f;
+                    p.c[(size_t)row * p.ldc + col] = x;
                 }
-                p.c[(size_t)row * p.ldc + col] = x;
-            }
+        }
+    } else {
+        float uv[TM][16];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                uv[i][r] = p.u ? p.u[(size_t)(m0 + wm0 + 32 * i + acc_row(r, hi)) * p.ldu] : 0.f;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn0 + 32 * j + l32;
+            const float vcol = p.u ? p.v[col] : 0.f;
+            float mv[TM][16];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    mv[i][r] = p.mask ? p.mask[(size_t)(m0 + wm0 + 32 * i + acc_row(r, hi)) * p.ldmask + col] : 1.f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = m0 + wm0 + 32 * i + acc_row(r, hi);
+                    float x = acc[i][j][r] + uv[i][r] * vcol;
+                    x = mv[i][r] > 0.f ? x : 0.f;
+                    p.c[(size_t)row * p.ldc + col] = x;
+                }
         }
     }
 }
@@ -287,25 +309,38 @@ __global__ __launch_bounds__(kThreads) void k_gemm_tn(TNArgs p) {
     if (do_bias && tid < BM) p.bslab[(size_t)split * p.nout + o0 + tid] = bsum;
 }
 
-// sum split-K slabs into the reference-layout gradient
-__global__ void k_slab_reduce(const float* __restrict__ slab, int splits, int nout, int ldslab,
-                              int nout_ref, int kin_ref, const float* __restrict__ bslab,
-                              float* __restrict__ gw, float* __restrict__ gb, int accumulate) {
+// sum split-K slabs into the reference-layout gradient: one thread per output element,
+// 4 independent partial sums so the split loop keeps several loads in flight
+__global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ slab, int splits, int nout,
+                                                     int ldslab, int nout_ref, int kin_ref,
+                                                     const float* __restrict__ bslab, float* __restrict__ gw,
+                                                     float* __restrict__ gb, int accumulate) {
     const size_t stride = (size_t)nout * ldslab;
     const int total = nout_ref * kin_ref;
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total + nout_ref; e += gridDim.x * blockDim.x) {
+        const float* src;
+        size_t st;
         if (e < total) {
             const int o = e / kin_ref, j = e % kin_ref;
-            const float* s = slab + (size_t)o * ldslab + j;
-            float acc = 0.f;
-            for (int q = 0; q < splits; ++q) acc += s[q * stride];
-            gw[e] = accumulate ? gw[e] + acc : acc;
-        } else if (bslab != nullptr && gb != nullptr) {
-            const int o = e - total;
-            float acc = 0.f;
-            for (int q = 0; q < splits; ++q) acc += bslab[(size_t)q * nout + o];
-            gb[o] = accumulate ? gb[o] + acc : acc;
+            src = slab + (size_t)o * ldslab + j;
+            st = stride;
+        } else {
+            if (bslab == nullptr || gb == nullptr) continue;
+            src = bslab + (e - total);
+            st = nout;
         }
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        int q = 0;
+        for (; q + 4 <= splits; q += 4) {
+            a0 += src[(size_t)q * st];
+            a1 += src[(size_t)(q + 1) * st];
+            a2 += src[(size_t)(q + 2) * st];
+            a3 += src[(size_t)(q + 3) * st];
+        }
+        for (; q < splits; ++q) a0 += src[(size_t)q * st];
+        const float acc = (a0 + a1) + (a2 + a3);
+        float* dst = e < total ? gw + e : gb + (e - total);
+        *dst = accumulate ? *dst + acc : acc;
     }
 }
 
@@ -418,7 +453,7 @@ extern "C" int nerf_slab_reduce(const float* slab, int splits, int nout, int lds
     NERF_CHECK(splits > 0 && nout > 0 && kin_ref > 0 && ldslab >= kin_ref && nout_ref <= nout,
                "%s: bad sizes", __func__);
     const int total = nout_ref * kin_ref + nout_ref;
-    const int blocks = (total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048;
+    const int blocks = (total + 255) / 256;
     hipLaunchKernelGGL(k_slab_reduce, dim3(blocks), dim3(256), 0, as_stream(stream), slab, splits,
                        nout, ldslab, nout_ref, kin_ref, bslab, gw, gb, accumulate);
     return check_launch(__func__);

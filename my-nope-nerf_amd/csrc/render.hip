@@ -11,20 +11,32 @@ constexpr int ENC_P = 64;  // 63 used + 1 zero pad (L = 10)
 constexpr int ENC_D = 64;  // 27 used + 37 zero pad (L = 4); 64 wide so every GEMM K tile is whole
 
 // Sample positions are rounded exactly as eager torch rounds them (separate multiply and
-// add, never fused): HIP's __fmul_rn/__fadd_rn are plain operators that -ffp-contract=fast
-// would fuse into v_fma, so contraction is switched off explicitly in these helpers.
+// add, never fused).  HIP's __fmul_rn/__fadd_rn are plain operators inside the header, where
+// -ffp-contract=fast still fuses them, so these helpers use plain operators under
+// `#pragma clang fp contract(off)` instead.
 
 // torch.linspace(0, 1, S) element i (CUDA kernel: halfway split, float step)
 __device__ __forceinline__ float linspace01(int i, int S) {
 #pragma clang fp contract(off)
     if (S == 1) return 0.f;
-    const float step = __fdiv_rn(1.0f, (float)(S - 1));
-    return (i < S / 2) ? __fmul_rn(step, (float)i) : __fsub_rn(1.0f, __fmul_rn(step, (float)(S - 1 - i)));
+    const float step = 1.0f / (float)(S - 1);
+    return (i < S / 2) ? step * (float)i : 1.0f - step * (float)(S - 1 - i);
 }
-// depth_range[0] * (1 - t) + depth_range[1] * t   (rendering.py:186), rounded like eager torch
+// depth_range[0] * (1 - t) + depth_range[1] * t   (rendering.py:186)
 __device__ __forceinline__ float lerp_z(float t, float nz, float fz) {
 #pragma clang fp contract(off)
-    return __fadd_rn(__fmul_rn(nz, __fsub_rn(1.0f, t)), __fmul_rn(fz, t));
+    return nz * (1.0f - t) + fz * t;
+}
+// stratified jitter inside the bin (rendering.py:187-191)
+__device__ __forceinline__ float jitter_z(float z, float zp, float zn, bool first, bool last, float u) {
+#pragma clang fp contract(off)
+    const float lo = first ? z : 0.5f * (z + zp);
+    const float hi = last ? z : 0.5f * (zn + z);
+    return lo + (hi - lo) * u;
+}
+__device__ __forceinline__ float ray_point(float o, float d, float z) {
+#pragma clang fp contract(off)
+    return o + d * z;
 }
 
 // Streams an encoding row to global memory 16 bytes at a time (keeps few values live).
@@ -68,7 +80,6 @@ __global__ __launch_bounds__(256) void k_encode_samples(const float* __restrict_
                                  int R, int S, int n_pad, float nz, float fz,
                                  float* __restrict__ z_out, float* __restrict__ enc_p,
                                  float* __restrict__ enc_d) {
-#pragma clang fp contract(off)
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_pad) return;
     const int total = R * S;
@@ -80,14 +91,12 @@ __global__ __launch_bounds__(256) void k_encode_samples(const float* __restrict_
         if (noise != nullptr) {  // rendering.py:187-191
             const float zp = i > 0 ? lerp_z(linspace01(i - 1, S), nz, fz) : z;
             const float zn = i < S - 1 ? lerp_z(linspace01(i + 1, S), nz, fz) : z;
-            const float lo = i > 0 ? __fmul_rn(0.5f, __fadd_rn(z, zp)) : z;
-            const float hi = i < S - 1 ? __fmul_rn(0.5f, __fadd_rn(zn, z)) : z;
-            z = __fadd_rn(lo, __fmul_rn(__fsub_rn(hi, lo), noise[s]));
+            z = jitter_z(z, zp, zn, i == 0, i == S - 1, noise[s]);
         }
         float x[3], v[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            x[c] = __fadd_rn(po[3 * r + c], __fmul_rn(pd[3 * r + c], z));  // rendering.py:193-194
+            x[c] = ray_point(po[3 * r + c], pd[3 * r + c], z);  // rendering.py:193-194
             v[c] = view[3 * r + c];
         }
         encode3<10, ENC_P>(x, rp);
@@ -262,13 +271,29 @@ __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ gra
         part[(size_t)blockIdx.x * PART + e] = red[0][e] + red[1][e] + red[2][e] + red[3][e];
 }
 
-__global__ void k_heads_reduce(const float* __restrict__ part, int nblocks, int H, int HR,
-                               float* __restrict__ gwd, float* __restrict__ gbd,
-                               float* __restrict__ gwc, float* __restrict__ gbc, int accumulate) {
+// sum the per-block partials: a block per 64 partial elements, its 4 waves split the block
+// range and combine through LDS
+__global__ __launch_bounds__(256) void k_heads_reduce(const float* __restrict__ part, int nblocks, int H, int HR,
+                                                      float* __restrict__ gwd, float* __restrict__ gbd,
+                                                      float* __restrict__ gwc, float* __restrict__ gbc,
+                                                      int accumulate) {
+    __shared__ float red[4][64];
     const int PART = H + 3 * HR + 4;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < PART; e += gridDim.x * blockDim.x) {
-        float acc = 0.f;
-        for (int b = 0; b < nblocks; ++b) acc += part[(size_t)b * PART + e];
+    const int e = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int w = threadIdx.x >> 6;
+    float a0 = 0.f, a1 = 0.f;
+    if (e < PART) {
+        int b = w;
+        for (; b + 4 < nblocks; b += 8) {
+            a0 += part[(size_t)b * PART + e];
+            a1 += part[(size_t)(b + 4) * PART + e];
+        }
+        for (; b < nblocks; b += 4) a0 += part[(size_t)b * PART + e];
+    }
+    red[w][threadIdx.x & 63] = a0 + a1;
+    __syncthreads();
+    if (w == 0 && e < PART) {
+        const float acc = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
         float* dst;
         if (e < H) dst = gwd + e;
         else if (e < H + 3 * HR) dst = gwc + (e - H);
@@ -495,11 +520,8 @@ __global__ __launch_bounds__(256) void k_encode_bwd(const float* __restrict__ po
         const size_t s = (size_t)ray * S + i;
         const float z = zv[s];
         float x[3], gx[3], gv[3];
-        {
-#pragma clang fp contract(off)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) x[c] = o[c] + d[c] * z;
-        }
+        for (int c = 0; c < 3; ++c) x[c] = ray_point(o[c], d[c], z);
         encode3_bwd<10, ENC_P>(x, gp + s * ENC_P, gx);
         encode3_bwd<4, ENC_D>(v, gd + s * ENC_D, gv);
 #pragma unroll
@@ -547,7 +569,7 @@ extern "C" int nerf_encode_samples(const float* pts_o, const float* pts_d, const
 static int heads_blocks(int n_pad) {
     const int groups = n_pad / 16;
     int b = (groups + 3) / 4;
-    return b > 1024 ? 1024 : (b < 1 ? 1 : b);
+    return b > 256 ? 256 : (b < 1 ? 1 : b);
 }
 
 extern "C" int nerf_heads_fwd(const float* h8, int ld8, const float* hr, int ldr, int hidden,
@@ -606,7 +628,7 @@ extern "C" int nerf_heads_reduce(const float* part, int hidden, int n_pad, float
     NERF_CHECK_PTR(part); NERF_CHECK_PTR(gwd); NERF_CHECK_PTR(gbd); NERF_CHECK_PTR(gwc); NERF_CHECK_PTR(gbc);
     const int hrw = hidden / 2 < 64 ? 64 : hidden / 2;
     const int PART = hidden + 3 * hrw + 4;
-    hipLaunchKernelGGL(k_heads_reduce, dim3((PART + 255) / 256), dim3(256), 0, as_stream(stream), part,
+    hipLaunchKernelGGL(k_heads_reduce, dim3((PART + 63) / 64), dim3(256), 0, as_stream(stream), part,
                        heads_blocks(n_pad), hidden, hrw, gwd, gbd, gwc, gbc, accumulate);
     return check_launch(__func__);
 }

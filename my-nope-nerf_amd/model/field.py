@@ -30,7 +30,7 @@ def _pad_rows(n: int) -> int:
     return (n + _hip.ROW_TILE - 1) // _hip.ROW_TILE * _hip.ROW_TILE
 
 
-def _dw_splits(m: int, tiles: int, target_blocks: int = 1024) -> int:
+def _dw_splits(m: int, tiles: int, target_blocks: int = 512) -> int:
     """Split-K factor for the weight-gradient GEMM: a power of two giving ~target blocks
     with each split a whole number of 32-row K tiles."""
     splits = 1

@@ -1,0 +1,64 @@
+"""Adam on one flat fp32 buffer with a single nerf_adam_step launch per step.
+
+Same update as torch.optim.Adam (amsgrad=False, train.py:59 / :100 / :118 use the
+defaults betas=(0.9, 0.999), eps=1e-8).  At construction the parameters' storage is
+moved into one contiguous buffer (each ``p.data`` becomes a view of it) so the update
+is one launch; the FieldRunner backward already produces the NeRF gradients as views of
+one flat buffer in parameter order, in which case no gather copy is made either.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _hip
+
+
+class HipAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        if len(self.param_groups) != 1:
+            raise ValueError("HipAdam supports one parameter group")
+        ps = [p for p in self.param_groups[0]["params"] if p.requires_grad]
+        if not ps:
+            raise ValueError("no trainable parameters")
+        dev = ps[0].device
+        n = sum(p.numel() for p in ps)
+        self._flat = torch.empty(n, device=dev, dtype=torch.float32)
+        off = 0
+        for p in ps:
+            k = p.numel()
+            self._flat[off:off + k].copy_(p.data.reshape(-1))
+            p.data = self._flat[off:off + k].view_as(p)
+            off += k
+        self._params = ps
+        self._m = torch.zeros_like(self._flat)
+        self._v = torch.zeros_like(self._flat)
+        self._step = 0
+
+    def _flat_grad(self):
+        gs = [p.grad for p in self._params]
+        if any(g is None for g in gs):
+            gs = [torch.zeros_like(p) if p.grad is None else p.grad for p in self._params]
+        g0 = gs[0]
+        base = g0.untyped_storage().data_ptr() if g0.is_contiguous() else None
+        if base is not None:
+            ptr = g0.data_ptr()
+            ok = True
+            for g, p in zip(gs, self._params):
+                if not g.is_contiguous() or g.data_ptr() != ptr:
+                    ok = False
+                    break
+                ptr += p.numel() * 4
+            if ok:
+                return torch.as_strided(g0, (self._flat.numel(),), (1,))
+        return torch.cat([g.reshape(-1) for g in gs])
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        g = self.param_groups[0]
+        self._step += 1
+        b1, b2 = g["betas"]
+        _hip.adam_step(self._flat, self._flat_grad().contiguous(), self._m, self._v, g["lr"], b1, b2, g["eps"],
+                       g["weight_decay"], self._step)
+        return loss
