@@ -1,0 +1,130 @@
+"""Host-side logic of the drop-in package, checked against the oracle on the CPU
+(no compute call reaches the HIP library here)."""
+import pytest
+import torch
+
+import model as mdl
+from model import field
+from model.losses import Loss
+from model.rendering import camera_rays
+from oracle import nerf_oracle as orc
+from tests.helpers import make_cfg, synthetic_rays
+
+
+def test_state_dict_interop_with_reference_layout():
+    cfg = make_cfg(hidden=256)
+    torch.manual_seed(42)
+    net = mdl.OfficialStaticNerf(cfg)
+    torch.manual_seed(42)
+    ref = orc.OracleNerf(256)
+    sd, sr = net.state_dict(), ref.state_dict()
+    assert list(sd) == list(sr)                      # reference key names, same order
+    for k in sd:
+        assert torch.equal(sd[k], sr[k]), k          # same init under the same seed (train.py:23-24)
+
+
+def test_encoding_levels_are_hard_wired():
+    cfg = make_cfg()
+    cfg["model"]["pos_enc_levels"] = 6
+    with pytest.raises(ValueError, match="hard-codes"):
+        mdl.OfficialStaticNerf(cfg)
+
+
+def test_no_cpu_fallback():
+    net = mdl.OfficialStaticNerf(make_cfg(hidden=64))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        net(torch.rand(4, 3), torch.rand(4, 3))
+
+
+def test_camera_rays_match_oracle():
+    b = synthetic_rays(R=300, S=8, seed=1)
+    cam, ray, rn, d_src, mask = camera_rays(b["pixels"], b["depth"], b["K"], b["w2c"], b["scale"])
+    oc, orr, od, orn, om = orc.rays_from_cameras(b["pixels"], b["depth"], b["K"], b["w2c"], b["scale"])
+    assert torch.allclose(cam, oc, atol=1e-6) and torch.allclose(ray, orr, atol=1e-6)
+    assert torch.allclose(d_src, od, rtol=1e-6) and torch.allclose(rn, orn, rtol=1e-6)
+    assert torch.equal(mask, om) and (~mask).any()
+
+
+def test_dense_depth_loss_equals_masked_loss():
+    """the sync-free dense form gives the reference's masked l1 value (losses.py:60-66)."""
+    L = Loss(make_cfg()["training"])
+    dp = torch.rand(50)
+    dg = torch.rand(50)
+    dg[::7] = float("inf")
+    mask = torch.isfinite(dg)
+    dense = L.get_depth_loss(dp, dg, mask)
+    masked = orc.depth_l1_loss(dp[mask], dg[mask])
+    assert torch.allclose(dense, masked)
+
+
+def test_loss_dict_keys_and_values():
+    cfg = make_cfg()["training"]
+    L = Loss(cfg)
+    w = {"rgb_weight": 1.0, "depth_weight": 0.04, "pc_weight": 0.0, "rgb_s_weight": 0.0,
+         "depth_consistency_weight": 0.0, "weight_dist_2nd_loss": 0.0, "weight_dist_1st_loss": 0.0,
+         "t_cycle_weight": 0.0}
+    rgb, gt = torch.rand(1, 64, 3), torch.rand(1, 64, 3)
+    dp, dg = torch.rand(60), torch.rand(60)
+    out = L(rgb, gt, dp, dg, weights=w, rgb_loss_type="l2", t_list=torch.zeros(3, 3))
+    ref = orc.total_loss(rgb, gt, dp, dg, w, "l2")
+    assert set(out) == {"loss", "loss_rgb", "loss_depth", "l2_mean", "loss_dist_1st", "loss_dist_2nd",
+                        "loss_pc", "loss_rgb_s", "loss_depth_consistency", "loss_t_cycle"}
+    for k in ("loss", "loss_rgb", "loss_depth", "l2_mean"):
+        assert torch.allclose(out[k], ref[k])
+
+
+def test_rgb_s_mask_mean_and_empty_mask():
+    L = Loss(make_cfg()["training"])
+    a, b = torch.rand(1, 5, 6, 3), torch.rand(1, 5, 6, 3)
+    v = torch.rand(1, 5, 6, 1) > 0.5
+    assert torch.allclose(L.get_rgb_s_loss(a, b, v), orc.rgb_s_loss(a, b, v))
+    assert L.get_rgb_s_loss(a, b, torch.zeros_like(v)).item() == 0.0
+
+
+def test_pose_and_distortion_modules_match_oracle():
+    cfg = make_cfg()
+    init = torch.stack([torch.eye(4), torch.eye(4)])
+    init[1, :3, 3] = torch.tensor([0.1, 0.2, 0.3])
+    lp = mdl.LearnPose(2, True, True, cfg, init_c2w=init)
+    with torch.no_grad():
+        lp.r.copy_(torch.tensor([[0.01, 0.02, -0.03], [0.2, -0.1, 0.05]]))
+        lp.t.copy_(torch.tensor([[0.5, 0.0, 0.1], [0.0, -0.4, 0.2]]))
+    for cam in (0, 1):
+        assert torch.allclose(lp(torch.tensor(cam)), orc.learn_pose_forward(lp.r, lp.t, init, cam), atol=1e-7)
+    ld = mdl.Learn_Distortion(3, True, True, cfg)
+    with torch.no_grad():
+        ld.global_scales.copy_(torch.tensor([[0.001], [2.0], [3.0]]))
+    for cam in range(3):
+        s, sh = ld(cam)
+        so, sho = orc.learn_distortion_forward(ld.global_scales, ld.global_shifts, cam)
+        assert torch.allclose(s.reshape(()), so.reshape(()).float()) and torch.allclose(sh, sho)
+
+
+def test_dw_split_policy():
+    assert field._dw_splits(131072, 4) == 128
+    assert field._dw_splits(16384, 4) % 2 == 0 or field._dw_splits(16384, 4) == 1
+    for m in (128, 1024, 16384, 131072, 131072 + 128):
+        for t in (1, 4, 10):
+            s = field._dw_splits(m, t)
+            assert m % s == 0 and (m // s) % 32 == 0
+    assert field._pad_rows(1) == 128 and field._pad_rows(131072) == 131072
+
+
+def test_trainer_anneal_and_pixel_cache():
+    cfg = make_cfg()
+    tr = mdl.Trainer(None, None, cfg["training"], device=torch.device("cpu"))
+    assert tr.anneal(0.04, 0.0, 0, 0, 0) == 0.04 and tr.anneal(0.04, 0.0, 0, 0, 1) == 0.0
+    p = tr._pixels(4, 6, torch.device("cpu"))
+    assert torch.equal(p, orc.arange_pixels(4, 6)[1])
+
+
+def test_ray_resampling_guarantee():
+    """training.py:280-283 resampling only triggers when the valid count can't guarantee a hit."""
+    cfg = make_cfg()
+    cfg["training"]["n_training_points"] = 4
+    tr = mdl.Trainer(None, None, cfg["training"], device=torch.device("cpu"))
+    mask = torch.zeros(1, 10, 10, dtype=torch.bool)
+    mask[0, 9, 9] = True                  # one valid pixel: must resample until it is drawn
+    torch.manual_seed(0)
+    idx = tr.sample_rays(100, mask, True)
+    assert mask.flatten()[idx].any()
