@@ -60,19 +60,21 @@ int nerf_encode_samples(const float* pts_o, const float* pts_d, const float* vie
  *   y[m, n] = act( sum_k x1[m,k] w[n,k] + sum_k x2[m,k] w[n,k1+k] + bias[n] )
  * x1: [m][ldx1] (k1 cols used), x2: [m][ldx2] (k2 cols, may be NULL with k2 = 0),
  * w : [n][k1+k2] (padded packed weight), y: [m][ldy]. m % 128 == 0, n % 64 == 0,
- * k1 % 32 == 0, k2 % 32 == 0. relu: 0/1.
+ * k1 % 32 == 0, k2 % 32 == 0. relu: 0/1.  mask_out (optional): ReLU mask bits of y,
+ * word [m][n/32] (row stride ldmo words), bit b of word w = y[m][32w+b] > 0.
  */
 int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2, int k2,
                     const float* w, const float* bias, float* y, int ldy, int m, int n,
-                    int relu, void* stream);
+                    int relu, uint32_t* mask_out, int ldmo, void* stream);
 
 /* Backward w.r.t. the layer input (autograd of official_nerf.py:62-91).
- *   dx[m, j] = ( sum_o dy[m,o] wt[j,o]  + (u ? u[m*ldu] * v[j] : 0) ) * (mask ? (mask[m,j] > 0) : 1)
+ *   dx[m, j] = ( sum_o dy[m,o] wt[j,o]  + (u ? u[m*ldu] * v[j] : 0) ) * (mask ? bit(m,j) : 1)
  * wt: [n][k] = transpose of the packed weight restricted to the wanted input columns
- * (n = number of input columns produced, k = layer outputs), mask: post-ReLU
- * activation of the previous layer ([m][ldmask]) or NULL.  m%128==0, n%64==0, k%32==0. */
+ * (n = number of input columns produced, k = layer outputs), mask: ReLU mask bits of
+ * the previous layer's output as written by nerf_linear_fwd (ldmask words per row) or
+ * NULL.  m%128==0, n%64==0, k%32==0. */
 int nerf_linear_bwd_data(const float* dy, int lddy, int k, const float* wt,
-                         const float* u, int ldu, const float* v, const float* mask, int ldmask,
+                         const float* u, int ldu, const float* v, const uint32_t* mask, int ldmask,
                          float* dx, int lddx, int m, int n, void* stream);
 
 /* Backward w.r.t. weight and bias, split over sample rows:
@@ -85,12 +87,20 @@ int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const float* x, 
                            int kin, int m, int splits, float* slab, int ldslab, int col0,
                            float* bslab, void* stream);
 
+/* Recommended `splits` for nerf_linear_bwd_weight at this shape and tile policy. */
+int nerf_linear_bwd_weight_splits(int nout, int kin, int m);
+
 /* Sum the split-K slabs (slab[split][nout][ldslab], bslab[split][nout]) into a
  * parameter gradient in the reference layout (unpadded gw[nout_ref][kin_ref],
  * gb[nout_ref]); accumulate != 0 adds into gw/gb. */
 int nerf_slab_reduce(const float* slab, int splits, int nout, int ldslab, int nout_ref,
                      int kin_ref, const float* bslab, float* gw, float* gb, int accumulate,
                      void* stream);
+
+/* GEMM tile policy (tuning knob; 0 = built-in default).  nt: 1 = 128x128 / 4 waves,
+ * 2 = 128x256 / 8 waves, 3 = 256x256 / 8 waves;  tn (weight gradient): 1 = 128x128,
+ * 3 = 256x256 / 8 waves. */
+int nerf_gemm_set_policy(int nt_policy, int tn_policy);
 
 /* ---------------------------------------------------------------------------
  * Output heads (density + colour logits), forward and backward.

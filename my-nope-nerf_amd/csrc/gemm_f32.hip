@@ -24,7 +24,6 @@ namespace nerf {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int BK = 32;
-constexpr int kThreads = 256;
 
 // ---------------------------------------------------------------------------
 // shared MFMA block: acc[TM][TN] += As[k][wm0..] x Bs[k][wn0..] over BK
@@ -54,8 +53,19 @@ __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const fl
 // accumulator register r of a 32x32 tile -> row offset inside the tile (gfx950 C/D map)
 __device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
 
+template <int TM, int TN>
+__device__ __forceinline__ void zero_acc(f32x16 (&acc)[TM][TN]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+}
+
 // ---------------------------------------------------------------------------
 // NT GEMM: C[m][n] = epi( sum_k A[m][k] B[n][k] ), A from up to two K segments.
+// WM x WN waves; each wave owns a (BM/WM) x (BN/WN) output tile of 32x32 MFMA blocks.
 // ---------------------------------------------------------------------------
 struct NTArgs {
     const float* a1; int lda1; int k1;
@@ -64,7 +74,8 @@ struct NTArgs {
     const float* bias;                  // fwd
     const float* u;  const float* v;    // bwd-data rank-1 term u[m*ldu] v[n]
     int ldu;
-    const float* mask; int ldmask;      // bwd-data ReLU mask (x > 0)
+    const uint32_t* mask; int ldmask;   // bwd-data ReLU mask bits [m][n/32] (bit = x > 0)
+    uint32_t* mask_out; int ldmo;       // fwd: write the ReLU mask bits of the output
     float* c; int ldc;
     int m, n;
     int relu;
@@ -72,15 +83,17 @@ struct NTArgs {
 
 enum { EPI_FWD = 0, EPI_BWD = 1 };
 
-template <int BM, int BN, int WAVES_M, int EPI>
-__global__ __launch_bounds__(kThreads) void k_gemm_nt(NTArgs p) {
-    constexpr int WAVES_N = 4 / WAVES_M;
-    constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+template <int BM, int BN, int WM, int WN, int EPI>
+__global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(NTArgs p) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
-    constexpr int LDA = BM + 1, LDB = BN + 1;
-    constexpr int A_F4 = BM * BK / 4 / kThreads;  // float4 per thread
-    constexpr int B_F4 = BN * BK / 4 / kThreads;
-    static_assert(A_F4 >= 1 && B_F4 >= 1, "tile too small");
+    constexpr int LDA = BM + 1, LDB = BN + 1;     // odd strides: conflict-free transposing stores
+    constexpr int A_F4 = BM * BK / 4 / NT;
+    constexpr int B_F4 = BN * BK / 4 / NT;
+    constexpr int MW = BN / 32;                   // mask words per row of the tile
+    constexpr int M_PF = (BM * MW + NT - 1) / NT; // mask words prefetched per thread
+    static_assert(A_F4 >= 1 && B_F4 >= 1 && TM >= 1 && TN >= 1, "bad tile");
 
     __shared__ __attribute__((aligned(16))) float smem[2 * BK * (LDA + LDB)];
     auto As = [&](int buf) { return smem + buf * BK * LDA; };
@@ -88,15 +101,13 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(NTArgs p) {
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
-    const int wm0 = (wave / WAVES_N) * WTM;
-    const int wn0 = (wave % WAVES_N) * WTN;
+    const int wm0 = (wave / WN) * WTM;
+    const int wn0 = (wave % WN) * WTN;
     const int m0 = blockIdx.x * BM;
     const int n0 = blockIdx.y * BN;
-    const int ktot = p.k1 + p.k2;
-    const int nkt = ktot / BK;
+    const int nkt = (p.k1 + p.k2) / BK;
 
     float4 ra[A_F4], rb[B_F4];
-
     auto load_tile = [&](int kt) {
         const int kk = kt * BK;
         const float* abase;
@@ -105,13 +116,13 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(NTArgs p) {
         else           { abase = p.a2; lda = p.lda2; kc0 = kk - p.k1; }
 #pragma unroll
         for (int i = 0; i < A_F4; ++i) {
-            const int idx = tid + kThreads * i;
+            const int idx = tid + NT * i;
             const int row = idx >> 3, kc = idx & 7;
             ra[i] = *reinterpret_cast<const float4*>(abase + (size_t)(m0 + row) * lda + kc0 + 4 * kc);
         }
 #pragma unroll
         for (int i = 0; i < B_F4; ++i) {
-            const int idx = tid + kThreads * i;
+            const int idx = tid + NT * i;
             const int row = idx >> 3, kc = idx & 7;
             rb[i] = *reinterpret_cast<const float4*>(p.b + (size_t)(n0 + row) * p.ldb + kk + 4 * kc);
         }
@@ -119,14 +130,14 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(NTArgs p) {
     auto store_tile = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < A_F4; ++i) {
-            const int idx = tid + kThreads * i;
+            const int idx = tid + NT * i;
             const int row = idx >> 3, kc = idx & 7;
             float* d = As(buf) + (4 * kc) * LDA + row;
             d[0] = ra[i].x; d[LDA] = ra[i].y; d[2 * LDA] = ra[i].z; d[3 * LDA] = ra[i].w;
         }
 #pragma unroll
         for (int i = 0; i < B_F4; ++i) {
-            const int idx = tid + kThreads * i;
+            const int idx = tid + NT * i;
             const int row = idx >> 3, kc = idx & 7;
             float* d = Bs(buf) + (4 * kc) * LDB + row;
             d[0] = rb[i].x; d[LDB] = rb[i].y; d[2 * LDB] = rb[i].z; d[3 * LDB] = rb[i].w;
@@ -134,12 +145,22 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(NTArgs p) {
     };
 
     f32x16 acc[TM][TN];
+    zero_acc(acc);
+
+    // backward epilogue operands (ReLU bits, rank-1 column) are prefetched with coalesced
+    // loads while the last K tile computes, then parked in LDS
+    uint32_t mpf[M_PF];
+    float upf = 0.f;
+    auto prefetch_epi = [&]() {
+        if (EPI != EPI_BWD) return;
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        for (int q = 0; q < M_PF; ++q) {
+            const int e = tid + NT * q;
+            mpf[q] = (p.mask && e < BM * MW) ? p.mask[(size_t)(m0 + e / MW) * p.ldmask + (n0 >> 5) + e % MW]
+                                             : 0xffffffffu;
+        }
+        if (tid < BM) upf = p.u ? p.u[(size_t)(m0 + tid) * p.ldu] : 0.f;
+    };
 
     load_tile(0);
     store_tile(0);
@@ -147,20 +168,19 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(NTArgs p) {
     for (int kt = 0; kt < nkt; ++kt) {
         const int cur = kt & 1;
         if (kt + 1 < nkt) load_tile(kt + 1);
+        else prefetch_epi();
         mfma_tile<TM, TN, LDA, LDB>(As(cur), Bs(cur), wm0, wn0, acc);
         if (kt + 1 < nkt) store_tile(cur ^ 1);
         __syncthreads();
     }
 
-    // epilogue.  The backward's mask / rank-1 operands are loaded as whole batches before
-    // any store: p.c may alias them as far as the compiler knows, so interleaved
-    // load/store pairs would serialise one memory round trip per element.
     const int lane = lane_id();
     const int l32 = lane & 31, hi = lane >> 5;
     if (EPI == EPI_FWD) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int col = n0 + wn0 + 32 * j + l32;
+            const int cword = (n0 + wn0 + 32 * j) >> 5;
             const float bcol = p.bias ? p.bias[col] : 0.f;
 #pragma unroll
             for (int i = 0; i < TM; ++i)
@@ -170,33 +190,39 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(NTArgs p) {
                     float x = acc[i][j][r] + bcol;
                     if (p.relu) x = fmaxf(x, 0.f);
                     p.c[(size_t)row * p.ldc + col] = x;
+                    if (p.mask_out) {
+                        // bits 0-31: the 32 columns of this register's row held by lanes 0-31,
+                        // bits 32-63: the row held by lanes 32-63
+                        const uint64_t bits = __ballot(x > 0.f);
+                        if (l32 == 0)
+                            p.mask_out[(size_t)row * p.ldmo + cword] = (uint32_t)(hi ? (bits >> 32) : bits);
+                    }
                 }
         }
     } else {
-        float uv[TM][16];
+        // park the prefetched operands in LDS (the staging buffers are free now)
+        uint32_t* lmask = reinterpret_cast<uint32_t*>(smem);
+        float* lu = smem + BM * MW;
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                uv[i][r] = p.u ? p.u[(size_t)(m0 + wm0 + 32 * i + acc_row(r, hi)) * p.ldu] : 0.f;
+        for (int q = 0; q < M_PF; ++q) {
+            const int e = tid + NT * q;
+            if (e < BM * MW) lmask[e] = mpf[q];
+        }
+        if (tid < BM) lu[tid] = upf;
+        __syncthreads();
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int col = n0 + wn0 + 32 * j + l32;
+            const int cw = (wn0 + 32 * j) >> 5;
             const float vcol = p.u ? p.v[col] : 0.f;
-            float mv[TM][16];
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    mv[i][r] = p.mask ? p.mask[(size_t)(m0 + wm0 + 32 * i + acc_row(r, hi)) * p.ldmask + col] : 1.f;
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int row = m0 + wm0 + 32 * i + acc_row(r, hi);
-                    float x = acc[i][j][r] + uv[i][r] * vcol;
-                    x = mv[i][r] > 0.f ? x : 0.f;
-                    p.c[(size_t)row * p.ldc + col] = x;
+                    const int lr = wm0 + 32 * i + acc_row(r, hi);
+                    float x = acc[i][j][r] + lu[lr] * vcol;
+                    x = ((lmask[lr * MW + cw] >> l32) & 1u) ? x : 0.f;
+                    p.c[(size_t)(m0 + lr) * p.ldc + col] = x;
                 }
         }
     }
@@ -213,15 +239,16 @@ struct TNArgs {
     float* bslab; int nout;
 };
 
-template <int BM, int BN, int WAVES_M>
-__global__ __launch_bounds__(kThreads) void k_gemm_tn(TNArgs p) {
-    constexpr int WAVES_N = 4 / WAVES_M;
-    constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void k_gemm_tn(TNArgs p) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
-    constexpr int LDA = BM + 4, LDB = BN + 4;
-    constexpr int A_F4 = BM * BK / 4 / kThreads;
-    constexpr int B_F4 = BN * BK / 4 / kThreads;
-    constexpr int A_C4 = BM / 4, B_C4 = BN / 4;  // float4 per k-row
+    constexpr int LDA = BM + 4, LDB = BN + 4;   // 16-B aligned rows for ds_write_b128
+    constexpr int A_F4 = BM * BK / 4 / NT;
+    constexpr int B_F4 = BN * BK / 4 / NT;
+    constexpr int A_C4 = BM / 4, B_C4 = BN / 4;
+    static_assert(A_F4 >= 1 && B_F4 >= 1, "bad tile");
 
     __shared__ __attribute__((aligned(16))) float smem[2 * BK * (LDA + LDB)];
     auto As = [&](int buf) { return smem + buf * BK * LDA; };
@@ -229,8 +256,8 @@ __global__ __launch_bounds__(kThreads) void k_gemm_tn(TNArgs p) {
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
-    const int wm0 = (wave / WAVES_N) * WTM;
-    const int wn0 = (wave % WAVES_N) * WTN;
+    const int wm0 = (wave / WN) * WTM;
+    const int wn0 = (wave % WN) * WTN;
     const int o0 = blockIdx.x * BM;
     const int j0 = blockIdx.y * BN;
     const int split = blockIdx.z;
@@ -243,13 +270,13 @@ __global__ __launch_bounds__(kThreads) void k_gemm_tn(TNArgs p) {
         const size_t sb = s0 + (size_t)kt * BK;
 #pragma unroll
         for (int i = 0; i < A_F4; ++i) {
-            const int idx = tid + kThreads * i;
+            const int idx = tid + NT * i;
             const int row = idx / A_C4, c4 = idx % A_C4;
             ra[i] = *reinterpret_cast<const float4*>(p.dy + (sb + row) * p.lddy + o0 + 4 * c4);
         }
 #pragma unroll
         for (int i = 0; i < B_F4; ++i) {
-            const int idx = tid + kThreads * i;
+            const int idx = tid + NT * i;
             const int row = idx / B_C4, c4 = idx % B_C4;
             rb[i] = *reinterpret_cast<const float4*>(p.x + (sb + row) * p.ldx + j0 + 4 * c4);
         }
@@ -257,25 +284,20 @@ __global__ __launch_bounds__(kThreads) void k_gemm_tn(TNArgs p) {
     auto store_tile = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < A_F4; ++i) {
-            const int idx = tid + kThreads * i;
+            const int idx = tid + NT * i;
             const int row = idx / A_C4, c4 = idx % A_C4;
             *reinterpret_cast<float4*>(As(buf) + row * LDA + 4 * c4) = ra[i];
         }
 #pragma unroll
         for (int i = 0; i < B_F4; ++i) {
-            const int idx = tid + kThreads * i;
+            const int idx = tid + NT * i;
             const int row = idx / B_C4, c4 = idx % B_C4;
             *reinterpret_cast<float4*>(Bs(buf) + row * LDB + 4 * c4) = rb[i];
         }
     };
 
     f32x16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    zero_acc(acc);
     float bsum = 0.f;
 
     load_tile(0);
@@ -348,13 +370,27 @@ __global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ s
 
 using namespace nerf;
 
-template <int BM, int BN, int WM, int EPI>
+template <int BM, int BN, int WM, int WN, int EPI>
 static int launch_nt(const NTArgs& a, hipStream_t s, double flops) {
     dim3 grid(a.m / BM, a.n / BN);
     prof_begin(s);
-    hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, EPI>), grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, EPI>), grid, dim3(64 * WM * WN), 0, s, a);
     prof_end(s, flops);
     return check_launch("k_gemm_nt");
+}
+
+// tile policy (nerf_gemm_set_policy): 0 = default, 1 = 128x128/4 waves, 2 = 128x256/8 waves,
+// 3 = 256x256/8 waves
+static int g_nt_policy = 0;
+static int g_tn_policy = 0;
+
+template <int EPI>
+static int dispatch_nt(const NTArgs& a, hipStream_t s, double flops) {
+    const int pol = g_nt_policy ? g_nt_policy : 3;
+    if (pol == 3 && a.m % 256 == 0 && a.n % 256 == 0) return launch_nt<256, 256, 2, 4, EPI>(a, s, flops);
+    if (pol >= 2 && a.n % 256 == 0) return launch_nt<128, 256, 2, 4, EPI>(a, s, flops);
+    if (a.n % 128 == 0) return launch_nt<128, 128, 2, 2, EPI>(a, s, flops);
+    return launch_nt<128, 64, 4, 1, EPI>(a, s, flops);
 }
 
 static int check_nt(const NTArgs& a, const char* fn) {
@@ -375,22 +411,22 @@ static int check_nt(const NTArgs& a, const char* fn) {
 
 extern "C" int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2, int k2,
                                const float* w, const float* bias, float* y, int ldy, int m, int n,
-                               int relu, void* stream) {
+                               int relu, uint32_t* mask_out, int ldmo, void* stream) {
     NTArgs a{};
     a.a1 = x1; a.lda1 = ldx1; a.k1 = k1;
     a.a2 = x2; a.lda2 = x2 ? ldx2 : 0; a.k2 = x2 ? k2 : 0;
     a.b = w; a.ldb = k1 + a.k2;
     a.bias = bias; a.c = y; a.ldc = ldy; a.m = m; a.n = n; a.relu = relu;
+    a.mask_out = mask_out; a.ldmo = ldmo;
     int rc = check_nt(a, __func__);
     if (rc) return rc;
+    NERF_CHECK(mask_out == nullptr || ldmo >= n / 32, "%s: ldmo=%d < n/32", __func__, ldmo);
     const double fl = 2.0 * m * n * (double)(k1 + a.k2);
-    hipStream_t s = as_stream(stream);
-    if (n % 128 == 0) return launch_nt<128, 128, 2, EPI_FWD>(a, s, fl);
-    return launch_nt<128, 64, 4, EPI_FWD>(a, s, fl);
+    return dispatch_nt<EPI_FWD>(a, as_stream(stream), fl);
 }
 
 extern "C" int nerf_linear_bwd_data(const float* dy, int lddy, int k, const float* wt,
-                                    const float* u, int ldu, const float* v, const float* mask,
+                                    const float* u, int ldu, const float* v, const uint32_t* mask,
                                     int ldmask, float* dx, int lddx, int m, int n, void* stream) {
     NTArgs a{};
     a.a1 = dy; a.lda1 = lddy; a.k1 = k;
@@ -401,10 +437,9 @@ extern "C" int nerf_linear_bwd_data(const float* dy, int lddy, int k, const floa
     int rc = check_nt(a, __func__);
     if (rc) return rc;
     NERF_CHECK(u == nullptr || v != nullptr, "%s: u without v", __func__);
+    NERF_CHECK(mask == nullptr || ldmask >= n / 32, "%s: ldmask=%d < n/32 words", __func__, ldmask);
     const double fl = 2.0 * m * n * (double)k;
-    hipStream_t s = as_stream(stream);
-    if (n % 128 == 0) return launch_nt<128, 128, 2, EPI_BWD>(a, s, fl);
-    return launch_nt<128, 64, 4, EPI_BWD>(a, s, fl);
+    return dispatch_nt<EPI_BWD>(a, as_stream(stream), fl);
 }
 
 extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const float* x, int ldx,
@@ -428,18 +463,22 @@ extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const
     hipStream_t s = as_stream(stream);
     const double fl = 2.0 * m * nout * (double)kin;
     prof_begin(s);
-    if (nout % 128 == 0 && kin % 128 == 0) {
+    const int pol = g_tn_policy ? g_tn_policy : 3;
+    if (pol == 3 && nout % 256 == 0 && kin % 256 == 0) {
+        dim3 grid(nout / 256, kin / 256, splits);
+        hipLaunchKernelGGL((k_gemm_tn<256, 256, 2, 4>), grid, dim3(512), 0, s, a);
+    } else if (nout % 128 == 0 && kin % 128 == 0) {
         dim3 grid(nout / 128, kin / 128, splits);
-        hipLaunchKernelGGL((k_gemm_tn<128, 128, 2>), grid, dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((k_gemm_tn<128, 128, 2, 2>), grid, dim3(256), 0, s, a);
     } else if (nout % 128 == 0) {
         dim3 grid(nout / 128, kin / 64, splits);
-        hipLaunchKernelGGL((k_gemm_tn<128, 64, 4>), grid, dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((k_gemm_tn<128, 64, 4, 1>), grid, dim3(256), 0, s, a);
     } else if (kin % 128 == 0) {
         dim3 grid(nout / 64, kin / 128, splits);
-        hipLaunchKernelGGL((k_gemm_tn<64, 128, 2>), grid, dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((k_gemm_tn<64, 128, 2, 2>), grid, dim3(256), 0, s, a);
     } else {
         dim3 grid(nout / 64, kin / 64, splits);
-        hipLaunchKernelGGL((k_gemm_tn<64, 64, 2>), grid, dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((k_gemm_tn<64, 64, 2, 2>), grid, dim3(256), 0, s, a);
     }
     prof_end(s, fl);
     return check_launch(__func__);
@@ -457,4 +496,25 @@ extern "C" int nerf_slab_reduce(const float* slab, int splits, int nout, int lds
     hipLaunchKernelGGL(k_slab_reduce, dim3(blocks), dim3(256), 0, as_stream(stream), slab, splits,
                        nout, ldslab, nout_ref, kin_ref, bslab, gw, gb, accumulate);
     return check_launch(__func__);
+}
+
+extern "C" int nerf_gemm_set_policy(int nt_policy, int tn_policy) {
+    NERF_CHECK(nt_policy >= 0 && nt_policy <= 3 && tn_policy >= 0 && tn_policy <= 3,
+               "%s: policies are 0..3", __func__);
+    g_nt_policy = nt_policy;
+    g_tn_policy = tn_policy;
+    return NERF_OK;
+}
+
+// split-K factor for nerf_linear_bwd_weight under the current tile policy: about one
+// resident wave of blocks (256-tiles: 1 block per CU, 128-tiles: 2), each split a whole
+// number of 32-row K tiles and at least 256 rows
+extern "C" int nerf_linear_bwd_weight_splits(int nout, int kin, int m) {
+    const int pol = g_tn_policy ? g_tn_policy : 3;
+    int tiles, target;
+    if (pol == 3 && nout % 256 == 0 && kin % 256 == 0) { tiles = (nout / 256) * (kin / 256); target = 256; }
+    else { tiles = ((nout + 127) / 128) * ((kin + 127) / 128); target = 512; }
+    int splits = 1;
+    while (splits * 2 * tiles <= target && m % (splits * 2 * BK) == 0 && m / (splits * 2) >= 256) splits *= 2;
+    return splits;
 }

@@ -39,9 +39,11 @@ _SIGS = {
     "nerf_hip_abi_version": ([], _c_i),
     "nerf_hip_last_error": ([], ctypes.c_char_p),
     "nerf_encode_samples": ([_c_p, _c_p, _c_p, _c_p, _c_i, _c_i, _c_i, _c_f, _c_f, _c_p, _c_p, _c_p, _c_p], _c_i),
-    "nerf_linear_fwd": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p], _c_i),
+    "nerf_linear_fwd": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p, _c_i,
+                         _c_p], _c_i),
     "nerf_linear_bwd_data": ([_c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_i, _c_i, _c_p], _c_i),
     "nerf_linear_bwd_weight": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p], _c_i),
+    "nerf_linear_bwd_weight_splits": ([_c_i, _c_i, _c_i], _c_i),
     "nerf_slab_reduce": ([_c_p, _c_i, _c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_heads_fwd": ([_c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_heads_part_size": ([_c_i, _c_i], _c_i),
@@ -53,6 +55,7 @@ _SIGS = {
     "nerf_pack_weights": ([ctypes.POINTER(PackDesc), _c_i, _c_p], _c_i),
     "nerf_adam_step": ([_c_p, _c_p, _c_p, _c_p, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_f, _c_i, _c_p], _c_i),
     "nerf_chamfer_nn": ([_c_p, _c_i, _c_p, _c_i, _c_p, _c_p], _c_i),
+    "nerf_gemm_set_policy": ([_c_i, _c_i], _c_i),
     "nerf_prof_enable": ([_c_i], _c_i),
     "nerf_prof_read": ([ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_i64),
                         ctypes.POINTER(ctypes.c_double)], _c_i),
@@ -96,7 +99,7 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
         return None
     if not t.is_cuda:
         raise RuntimeError("nerf_hip: tensor must live on the GPU (no CPU fallback)")
-    if t.dtype not in (torch.float32, torch.int64):
+    if t.dtype not in (torch.float32, torch.int64, torch.int32):
         raise RuntimeError(f"nerf_hip: unsupported dtype {t.dtype}")
     return t.data_ptr()
 
@@ -118,12 +121,15 @@ def encode_samples(pts_o, pts_d, view, noise, n_rays, n_samples, n_pad, near, fa
           n_pad, float(near), float(far), _ptr(z), _ptr(enc_p), _ptr(enc_d), _stream())
 
 
-def linear_fwd(x1, k1, x2, k2, w, bias, y, m, n, relu):
+def linear_fwd(x1, k1, x2, k2, w, bias, y, m, n, relu, mask_out=None):
+    """mask_out: int32 [m][n/32] ReLU mask bits of y (optional)."""
     _call("nerf_linear_fwd", _ptr(x1), _ld(x1), k1, _ptr(x2), _ld(x2) if x2 is not None else 0, k2,
-          _ptr(w), _ptr(bias), _ptr(y), _ld(y), m, n, int(relu), _stream())
+          _ptr(w), _ptr(bias), _ptr(y), _ld(y), m, n, int(relu), _ptr(mask_out),
+          _ld(mask_out) if mask_out is not None else 0, _stream())
 
 
 def linear_bwd_data(dy, k, wt, dx, m, n, mask=None, u=None, ldu=1, v=None):
+    """mask: int32 ReLU mask bits [m][words] from linear_fwd(mask_out=...)."""
     _call("nerf_linear_bwd_data", _ptr(dy), _ld(dy), k, _ptr(wt), _ptr(u), int(ldu), _ptr(v), _ptr(mask),
           _ld(mask) if mask is not None else 0, _ptr(dx), _ld(dx), m, n, _stream())
 
@@ -131,6 +137,10 @@ def linear_bwd_data(dy, k, wt, dx, m, n, mask=None, u=None, ldu=1, v=None):
 def linear_bwd_weight(dy, nout, x, kin, m, splits, slab, ldslab, col0, bslab):
     _call("nerf_linear_bwd_weight", _ptr(dy), _ld(dy), nout, _ptr(x), _ld(x), kin, m, splits,
           _ptr(slab), ldslab, col0, _ptr(bslab), _stream())
+
+
+def bwd_weight_splits(nout, kin, m) -> int:
+    return int(lib().nerf_linear_bwd_weight_splits(nout, kin, m))
 
 
 def slab_reduce(slab, splits, nout, ldslab, nout_ref, kin_ref, bslab, gw, gb, accumulate=False):
@@ -184,6 +194,10 @@ def adam_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_de
 
 def chamfer_nn(x, y, idx):
     _call("nerf_chamfer_nn", _ptr(x), x.shape[0], _ptr(y), y.shape[0], _ptr(idx), _stream())
+
+
+def gemm_set_policy(nt: int = 0, tn: int = 0):
+    _call("nerf_gemm_set_policy", int(nt), int(tn))
 
 
 def prof_enable(on: bool):

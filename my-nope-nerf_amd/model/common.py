@@ -31,9 +31,16 @@ def get_mask(t):
     return (t.abs() != math.inf) & ~torch.isnan(t)
 
 
+def inv(m):
+    """torch.inverse without its host-side singularity check: ``torch.inverse`` reads the
+    LAPACK info back to the host (a device sync every call, 5+ per step); inv_ex runs the
+    same factorisation and leaves ``info`` on the device."""
+    return torch.linalg.inv_ex(m)[0]
+
+
 def unproject_matrix(camera_mat, world_mat, scale_mat):
     """scale^-1 @ world^-1 @ K^-1 evaluated in the reference's association order."""
-    return (torch.inverse(scale_mat) @ torch.inverse(world_mat)) @ torch.inverse(camera_mat)
+    return (inv(scale_mat) @ inv(world_mat)) @ inv(camera_mat)
 
 
 def transform_to_world(pixels, depth, camera_mat, world_mat=None, scale_mat=None, invert=True, device=None):

@@ -137,12 +137,17 @@ class FieldRunner:
             outs = [ping[i % 2] for i in range(9)] + [e(Np, HR)]
         x = enc_p
         segs = {"enc_p": enc_p, "enc_d": enc_d}
+        masks = {}
         for i, l in enumerate(self.layers):
             y = outs[i]
             x2 = segs[l.seg2] if l.seg2 else None
             k1 = l.k1
+            mo = None
+            if keep and l.relu and l.name != "lr":   # ReLU bits for the backward's input masks
+                mo = torch.empty(Np, l.out_p // 32, device=dev, dtype=torch.int32)
+                masks[l.name] = mo
             _hip.linear_fwd(x, k1, x2, _hip.ENC_P if x2 is not None else 0, self.w[l.name], self.bias(l), y,
-                            Np, l.out_p, l.relu)
+                            Np, l.out_p, l.relu, mask_out=mo)
             acts.append(y)
             x = y
             if l.name == "l7":
@@ -161,7 +166,7 @@ class FieldRunner:
         state = None
         if keep:
             state = dict(R=R, S=S, Np=Np, flags=flags, z=z, enc_p=enc_p, enc_d=enc_d, acts=acts, raw4=raw4,
-                         pts_o=pts_o, pts_d=pts_d, view=view)
+                         masks=masks, pts_o=pts_o, pts_d=pts_d, view=view)
         return rgb, dist, alpha, z[:N].view(R, S), state
 
     # ------------------------------------------------------------------ backward
@@ -209,6 +214,8 @@ class FieldRunner:
         prev_in = {"l0": st["enc_p"], "l1": h["l0"], "l2": h["l1"], "l3": h["l2"], "l4": h["l3"],
                    "l5": h["l4"], "l6": h["l5"], "l7": h["l6"], "lf": h["l7"], "lr": h["lf"]}
         order = ["lr", "lf", "l7", "l6", "l5", "l4", "l3", "l2", "l1", "l0"]
+        prev_name = {"l1": "l0", "l2": "l1", "l3": "l2", "l4": "l3", "l5": "l4", "l6": "l5", "l7": "l6",
+                     "lf": "l7", "lr": "lf"}
         spec = {l.name: l for l in self.layers}
         seg_buf = {"enc_p": st["enc_p"], "enc_d": st["enc_d"]}
         pingpong = [e(Np, D), e(Np, D)]
@@ -219,8 +226,7 @@ class FieldRunner:
             x_in = prev_in[name]
             k1 = l.k1
             # --- weight / bias gradient: split-K slabs + reduce into the reference layout
-            tiles = (l.out_p // 64) * (l.kp // 64)
-            splits = _dw_splits(Np, max(1, tiles // 4))
+            splits = _hip.bwd_weight_splits(l.out_p, k1, Np)
             slab = e(splits * l.out_p * l.kp)
             bslab = e(splits * l.out_p)
             _hip.linear_bwd_weight(dy, l.out_p, x_in, k1, Np, splits, slab, l.kp, 0, bslab)
@@ -245,7 +251,8 @@ class FieldRunner:
                 _hip.linear_bwd_data(dy, l.out_p, wt[k1:k1 + 64], tmp, Np, 64)
                 tgt.add_(tmp)
             dx = pingpong[step % 2]
-            mask = None if name == "lr" else prev_in[name]   # f (input of lr) has no activation
+            # ReLU bits of this layer's input (f, the input of lr, has no activation)
+            mask = None if name == "lr" else st["masks"][prev_name[name]]
             if name == "lf":   # + density path: d sigma_raw (graw4[:,0]) x w_density
                 _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask, u=graw4, ldu=4,
                                      v=m.fc_density.weight)

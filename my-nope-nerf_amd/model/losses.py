@@ -15,6 +15,7 @@ from torch import nn
 from torch.nn import functional as F
 
 from . import _hip
+from .common import inv
 
 
 class Loss_Eval(nn.Module):
@@ -164,7 +165,7 @@ class Loss(nn.Module):
 
     def get_t_cycle_loss(self, rt_pred, rt_gt):
         eye = torch.eye(4, device=rt_gt.device, dtype=rt_gt.dtype)
-        return torch.norm(eye - torch.inverse(rt_gt) @ rt_pred)
+        return torch.norm(eye - inv(rt_gt) @ rt_pred)
 
     # ---- total ----------------------------------------------------------------------
     def forward(self, rgb_pred, rgb_gt, depth_pred=None, depth_gt=None, t_list=None, X=None, Y=None,

@@ -21,7 +21,7 @@ import torch
 import torch.distributed as dist
 from torch.nn import functional as F
 
-from .common import arange_pixels, get_tensor_values, project_to_cam, transform_to_world
+from .common import arange_pixels, get_tensor_values, inv, project_to_cam, transform_to_world
 from .losses import Loss
 
 
@@ -168,10 +168,10 @@ class Trainer(object):
         kwargs = {"weights": weights, "rgb_loss_type": rgb_loss_type}
         if self.pose_param_net is not None:
             kwargs["t_list"] = self.pose_param_net.get_t()
-        world_mat_gt = torch.inverse(pose_gt).unsqueeze(0)
+        world_mat_gt = inv(pose_gt).unsqueeze(0)
         num_cams = self.pose_param_net.num_cams if self.pose_param_net is not None else None
         c2w = self.pose_param_net(img_idx) if self.pose_param_net is not None else pose_gt.reshape(4, 4)
-        world_mat = torch.inverse(c2w).unsqueeze(0)
+        world_mat = inv(c2w).unsqueeze(0)
         scale_input = shift_input = None
         if self.distortion_net is not None:
             scale_input, shift_input = self.distortion_net(img_idx)
@@ -218,7 +218,7 @@ class Trainer(object):
                          out_render_path):
         """training.py:305-405: point clouds of the image pair, relative pose, reprojection."""
         B = img.shape[0]
-        ref_Rt_gt = torch.inverse(ref_pose_gt).unsqueeze(0)
+        ref_Rt_gt = inv(ref_pose_gt).unsqueeze(0)
         c2w_ref = self.pose_param_net(ref_idx)
         scale_ref = shift_ref = None
         if self.distortion_net is not None:
@@ -231,16 +231,16 @@ class Trainer(object):
             c2w_ref = c2w_ref.detach()
             scale_ref = scale_ref.detach() if scale_ref is not None else None
             depth_ref = depth_ref.detach()
-        ref_Rt = torch.inverse(c2w_ref).unsqueeze(0)
+        ref_Rt = inv(c2w_ref).unsqueeze(0)
         if int(img_idx) < num_cams - 1:
             d1, d2, img1, img2 = depth_input, depth_ref, img, ref_img
-            Rt_rel_12 = ref_Rt @ torch.inverse(world_mat)
-            Rt_rel_12_gt = ref_Rt_gt @ torch.inverse(world_mat_gt)
+            Rt_rel_12 = ref_Rt @ inv(world_mat)
+            Rt_rel_12_gt = ref_Rt_gt @ inv(world_mat_gt)
             scale1 = scale_input
         else:
             d1, d2, img1, img2 = depth_ref, depth_input, ref_img, img
-            Rt_rel_12 = world_mat @ torch.inverse(ref_Rt)
-            Rt_rel_12_gt = world_mat_gt @ torch.inverse(ref_Rt_gt)
+            Rt_rel_12 = world_mat @ inv(ref_Rt)
+            Rt_rel_12_gt = world_mat_gt @ inv(ref_Rt_gt)
             scale1 = scale_ref
         R_rel_12, t_rel_12 = Rt_rel_12[:, :3, :3], Rt_rel_12[:, :3, 3]
         res = (int(h_depth / self.pc_ratio), int(w_depth / self.pc_ratio))
@@ -284,7 +284,7 @@ class Trainer(object):
         img, depth_input, camera_mat, scale_mat, img_idx, *_ = self.process_data_dict(data)
         h, w = resolution
         c2w = self.pose_param_net(img_idx)
-        world_mat = torch.inverse(c2w).unsqueeze(0)
+        world_mat = inv(c2w).unsqueeze(0)
         if self.optimizer_focal:
             fxfy = self.focal_net(0)
             camera_mat = torch.tensor([[[fxfy[0], 0, 0, 0], [0, -fxfy[1], 0, 0], [0, 0, -1, 0], [0, 0, 0, 1]]],

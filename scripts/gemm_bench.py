@@ -1,0 +1,66 @@
+"""GEMM tile-policy A/B at the production shapes (one process, interleaved rounds).
+
+    python scripts/gemm_bench.py
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "my-nope-nerf_amd"))
+
+import torch  # noqa: E402
+
+from model import _hip  # noqa: E402
+
+
+def timeit(fn, iters=20):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3   # us
+
+
+def main():
+    dev = torch.device("cuda")
+    M, D = 131072, 256
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.rand(M, D, device=dev, generator=g) - 0.5
+    enc = torch.rand(M, 64, device=dev, generator=g) - 0.5
+    W = (torch.rand(D, D, device=dev, generator=g) - 0.5) * 0.1
+    W4 = (torch.rand(D, D + 64, device=dev, generator=g) - 0.5) * 0.1
+    b = torch.rand(D, device=dev, generator=g)
+    y = torch.empty(M, D, device=dev)
+    mask = torch.empty(M, D // 32, device=dev, dtype=torch.int32)
+    dy = torch.rand(M, D, device=dev, generator=g) - 0.5
+    u = torch.rand(M, 4, device=dev, generator=g)
+    cases = {}
+    cases["fwd 256x256"] = (lambda: _hip.linear_fwd(x, D, None, 0, W, b, y, M, D, 1, mask_out=mask), 2 * M * D * D)
+    cases["fwd skip 320"] = (lambda: _hip.linear_fwd(x, D, enc, 64, W4, b, y, M, D, 1), 2 * M * D * (D + 64))
+    cases["bwd-data mask+u"] = (lambda: _hip.linear_bwd_data(dy, D, W, y, M, D, mask=mask, u=u, ldu=4, v=b),
+                                2 * M * D * D)
+    for sp in (64, 128, 256):
+        slab = torch.empty(sp * D * D, device=dev)
+        bslab = torch.empty(sp * D, device=dev)
+        cases[f"dW splits={sp}"] = ((lambda sp=sp, slab=slab, bslab=bslab:
+                                     _hip.linear_bwd_weight(dy, D, x, D, M, sp, slab, D, 0, bslab)), 2 * M * D * D)
+    res = {}
+    for rnd in range(3):
+        for pol in (1, 2, 3):
+            _hip.gemm_set_policy(pol, pol)
+            for name, (fn, fl) in cases.items():
+                us = timeit(fn)
+                res.setdefault((name, pol), []).append(us)
+    for (name, pol), v in sorted(res.items()):
+        fl = cases[name][1]
+        best = min(v)
+        print(f"{name:22s} policy {pol}: {best:8.1f} us  {fl / best / 1e6:6.1f} TF/s  (rounds {['%.0f' % t for t in v]})")
+    _hip.gemm_set_policy(0, 0)
+
+
+if __name__ == "__main__":
+    main()

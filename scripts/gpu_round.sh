@@ -1,0 +1,14 @@
+# one GPU box call: parity tests, GEMM tile A/B, bench, rocprofv3 kernel stats
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R
+OUT=$R/gpurun_out
+mkdir -p $OUT
+timeout -k 10 600 python -m pytest tests -q -m gpu -p no:cacheprovider > $OUT/t_all.log 2>&1
+echo "tests rc=$?"
+timeout -k 10 300 python scripts/gemm_bench.py > $OUT/gemm_bench.txt 2>&1 && echo "gemm bench ok" && \
+timeout -k 10 600 python bench.py --steps ${STEPS:-30} --warmup 5 > $OUT/bench.json 2> $OUT/bench.err && \
+echo "bench ok" && \
+cd /tmp && export TMPDIR=/tmp && \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err && \
+echo "prof ok"

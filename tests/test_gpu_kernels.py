@@ -24,13 +24,17 @@ def test_linear_fwd(dev, m, n, k1, k2, relu):
     W = _rand(n, k1 + k2, g=g) * 0.1
     b = _rand(n, g=g)
     y = torch.empty(m, n, device=dev)
-    _hip.linear_fwd(x1.to(dev), k1, x2.to(dev) if x2 is not None else None, k2, W.to(dev), b.to(dev), y, m, n, relu)
+    mo = torch.empty(m, n // 32, device=dev, dtype=torch.int32)
+    _hip.linear_fwd(x1.to(dev), k1, x2.to(dev) if x2 is not None else None, k2, W.to(dev), b.to(dev), y, m, n, relu,
+                    mask_out=mo)
     xc = torch.cat([x1, x2], 1) if x2 is not None else x1
     ref = xc.double() @ W.double().t() + b.double()
     if relu:
         ref = ref.clamp_min(0)
     torch.cuda.synchronize()
     assert (y.cpu().double() - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
+    bits = ((mo.cpu().long() & 0xffffffff).unsqueeze(-1) >> torch.arange(32)) & 1
+    assert torch.equal(bits.view(m, n).bool(), y.cpu() > 0)          # ReLU bits agree with y
 
 
 def test_linear_fwd_asymmetric_identity(dev):
@@ -52,7 +56,10 @@ def test_linear_bwd_data(dev):
     u = _rand(m, 4, g=g)
     v = _rand(n, g=g)
     dx = torch.empty(m, n, device=dev)
-    _hip.linear_bwd_data(dy.to(dev), k, Wt.to(dev), dx, m, n, mask=mask.to(dev), u=u.to(dev), ldu=4, v=v.to(dev))
+    bits = (mask > 0).view(m, n // 32, 32).long() << torch.arange(32)
+    words = bits.sum(-1)
+    words = torch.where(words >= 2 ** 31, words - 2 ** 32, words).to(torch.int32)
+    _hip.linear_bwd_data(dy.to(dev), k, Wt.to(dev), dx, m, n, mask=words.to(dev), u=u.to(dev), ldu=4, v=v.to(dev))
     ref = dy.double() @ Wt.double().t() + u[:, 0:1].double() * v.double()
     ref = torch.where(mask > 0, ref, torch.zeros_like(ref))
     torch.cuda.synchronize()

@@ -101,12 +101,14 @@ def test_pose_and_distortion_modules_match_oracle():
 
 
 def test_dw_split_policy():
-    assert field._dw_splits(131072, 4) == 128
-    assert field._dw_splits(16384, 4) % 2 == 0 or field._dw_splits(16384, 4) == 1
+    from model import _hip
+    _hip.load_library()
+    assert _hip.bwd_weight_splits(256, 256, 131072) == 256
+    assert _hip.bwd_weight_splits(128, 256, 131072) == 256
     for m in (128, 1024, 16384, 131072, 131072 + 128):
-        for t in (1, 4, 10):
-            s = field._dw_splits(m, t)
-            assert m % s == 0 and (m // s) % 32 == 0
+        for nout, kin in ((256, 256), (128, 256), (256, 64), (64, 64)):
+            s = _hip.bwd_weight_splits(nout, kin, m)
+            assert s >= 1 and m % s == 0 and (m // s) % 32 == 0
     assert field._pad_rows(1) == 128 and field._pad_rows(131072) == 131072
 
 
