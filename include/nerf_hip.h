@@ -160,10 +160,11 @@ int nerf_pack_weights(const nerf_pack_desc* descs, int n, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Adam (torch.optim.Adam semantics, amsgrad False) over one flat fp32 buffer.
- * Replaces optimizer.step() (training.py:93-99). */
+ * Replaces optimizer.step() (training.py:93-99).  hyper (device, 6 floats) =
+ * {step, lr, beta1, beta2, eps, weight_decay}; the call increments step on the device
+ * first, so a captured graph replays the correct bias corrections. */
 int nerf_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
-                   int64_t n, float lr, float beta1, float beta2, float eps,
-                   float weight_decay, int step, void* stream);
+                   int64_t n, float* hyper, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Brute-force nearest neighbour for the dense point-cloud loss

@@ -30,9 +30,16 @@ __global__ void k_pack(PackBatch pb) {
 // torch.optim.Adam (amsgrad=False, maximize=False), single-tensor formulation:
 //   g += wd*p; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2
 //   denom = sqrt(v)/sqrt(bc2) + eps;  p -= (lr/bc1) * m / denom
+// Hyper-parameters and the step count live in device memory (hyper = {step, lr, b1, b2,
+// eps, wd}) so a captured hipGraph replays correct bias corrections and picks up lr changes.
+__global__ void k_adam_tick(float* hyper) { hyper[0] += 1.f; }
+
 __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                       float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
-                       float wd, float step_size, float sbc2) {
+                       float* __restrict__ v, int64_t n, const float* __restrict__ hyper) {
+    const float step = hyper[0], lr = hyper[1], b1 = hyper[2], b2 = hyper[3], eps = hyper[4], wd = hyper[5];
+    const float bc1 = 1.f - powf(b1, step);
+    const float sbc2 = sqrtf(1.f - powf(b2, step));
+    const float step_size = lr / bc1;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         float gi = g[i];
         if (wd != 0.f) gi = gi + wd * p[i];
@@ -94,17 +101,16 @@ extern "C" int nerf_pack_weights(const nerf_pack_desc* descs, int n, void* strea
 }
 
 extern "C" int nerf_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
-                              int64_t n, float lr, float beta1, float beta2, float eps,
-                              float weight_decay, int step, void* stream) {
+                              int64_t n, float* hyper, void* stream) {
     NERF_CHECK_PTR(param); NERF_CHECK_PTR(grad); NERF_CHECK_PTR(exp_avg); NERF_CHECK_PTR(exp_avg_sq);
-    NERF_CHECK(n > 0 && step >= 1, "%s: n=%lld step=%d", __func__, (long long)n, step);
-    const double bc1 = 1.0 - std::pow((double)beta1, step);
-    const double bc2 = 1.0 - std::pow((double)beta2, step);
+    NERF_CHECK_PTR(hyper);
+    NERF_CHECK(n > 0, "%s: n=%lld", __func__, (long long)n);
     int64_t blocks = (n + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), param, grad,
-                       exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay,
-                       (float)((double)lr / bc1), (float)std::sqrt(bc2));
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(k_adam_tick, dim3(1), dim3(1), 0, s, hyper);
+    hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, s, param, grad, exp_avg, exp_avg_sq, n,
+                       (const float*)hyper);
     return check_launch(__func__);
 }
 

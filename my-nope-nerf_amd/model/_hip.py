@@ -53,7 +53,7 @@ _SIGS = {
     "nerf_composite_bwd": ([_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_encode_bwd": ([_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_pack_weights": ([ctypes.POINTER(PackDesc), _c_i, _c_p], _c_i),
-    "nerf_adam_step": ([_c_p, _c_p, _c_p, _c_p, _c_i64, _c_f, _c_f, _c_f, _c_f, _c_f, _c_i, _c_p], _c_i),
+    "nerf_adam_step": ([_c_p, _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p], _c_i),
     "nerf_chamfer_nn": ([_c_p, _c_i, _c_p, _c_i, _c_p, _c_p], _c_i),
     "nerf_gemm_set_policy": ([_c_i, _c_i], _c_i),
     "nerf_prof_enable": ([_c_i], _c_i),
@@ -187,9 +187,11 @@ def pack_weights(descs: Sequence[PackDesc]):
     _call("nerf_pack_weights", arr, len(descs), _stream())
 
 
-def adam_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step):
+def adam_step(param, grad, exp_avg, exp_avg_sq, hyper):
+    """hyper: device float32 [6] = (step, lr, beta1, beta2, eps, weight_decay); step is
+    incremented on the device before the update."""
     _call("nerf_adam_step", _ptr(param), _ptr(grad), _ptr(exp_avg), _ptr(exp_avg_sq), param.numel(),
-          float(lr), float(beta1), float(beta2), float(eps), float(weight_decay), int(step), _stream())
+          _ptr(hyper), _stream())
 
 
 def chamfer_nn(x, y, idx):

@@ -120,7 +120,9 @@ def convert3x4_4x4(m):
             out = torch.cat([m, torch.zeros_like(m[:, 0:1])], dim=1)
             out[:, 3, 3] = 1.0
             return out
-        return torch.cat([m, torch.tensor([[0, 0, 0, 1]], dtype=m.dtype, device=m.device)], dim=0)
+        # [0, 0, 0, 1] built on the device (a host->device copy breaks hipGraph capture)
+        bottom = torch.eye(4, dtype=m.dtype, device=m.device)[3:]
+        return torch.cat([m, bottom], dim=0)
     if m.ndim == 3:
         out = np.concatenate([m, np.zeros_like(m[:, 0:1])], axis=1)
         out[:, 3, 3] = 1.0

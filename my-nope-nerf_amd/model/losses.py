@@ -93,7 +93,7 @@ class Loss(nn.Module):
             if depth_mask is None:
                 return (depth_pred - depth_gt).abs().sum() / float(depth_pred.shape[0])
             err = torch.where(depth_mask, (depth_pred - depth_gt).abs(), torch.zeros_like(depth_pred))
-            return err.sum() / depth_mask.sum()
+            return err.sum() / depth_mask.sum().clamp_min(1)   # 0 (not 0/0) if no ray is valid
         if depth_mask is not None:
             depth_pred, depth_gt = depth_pred[depth_mask], depth_gt[depth_mask]
         return self.depth_loss_dpt(depth_pred, depth_gt)

@@ -33,7 +33,17 @@ class HipAdam(torch.optim.Optimizer):
         self._params = ps
         self._m = torch.zeros_like(self._flat)
         self._v = torch.zeros_like(self._flat)
-        self._step = 0
+        # {step, lr, beta1, beta2, eps, weight_decay} on the device (graph-replay safe)
+        self._hyper = torch.zeros(6, device=dev, dtype=torch.float32)
+        self._hyper_host = None
+        self._sync_hyper()
+
+    def _sync_hyper(self):
+        g = self.param_groups[0]
+        h = (float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]), float(g["weight_decay"]))
+        if h != self._hyper_host:      # lr schedulers edit param_groups; push the change
+            self._hyper[1:].copy_(torch.tensor(h, dtype=torch.float32), non_blocking=False)
+            self._hyper_host = h
 
     def _flat_grad(self):
         gs = [p.grad for p in self._params]
@@ -56,9 +66,7 @@ class HipAdam(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
-        g = self.param_groups[0]
-        self._step += 1
-        b1, b2 = g["betas"]
-        _hip.adam_step(self._flat, self._flat_grad().contiguous(), self._m, self._v, g["lr"], b1, b2, g["eps"],
-                       g["weight_decay"], self._step)
+        if not torch.cuda.is_current_stream_capturing():
+            self._sync_hyper()
+        _hip.adam_step(self._flat, self._flat_grad().contiguous(), self._m, self._v, self._hyper)
         return loss

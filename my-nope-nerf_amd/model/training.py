@@ -134,16 +134,24 @@ class Trainer(object):
         return self._pix_cache[key]
 
     def sample_rays(self, n_pix, depth_mask, need_valid):
-        """training.py:277-283: a random subset of pixels; resample while none has a valid
-        depth, which is only possible when fewer than n_pix - n_points + 1 are valid."""
+        """training.py:277-283: a random subset of pixels, resampled while none of them has a
+        valid depth.  The check is a device->host sync per step in the reference; here it
+        runs only when an all-invalid draw is plausible: with n_invalid of n_pix pixels
+        invalid that probability is <= (n_invalid / n_pix) ** n_points, computed on the host
+        from the data dict's CPU mask (5 % holes at 1024 rays: 1e-1332)."""
         dev = self.device
-        ray_idx = torch.randperm(n_pix, device=dev)[:self.n_training_points]
+        R = self.n_training_points
+        ray_idx = torch.randperm(n_pix, device=dev)[:R]
         if need_valid and depth_mask is not None:
-            n_valid = int(depth_mask.sum()) if not depth_mask.is_cuda else None
-            if n_valid is None or n_valid <= n_pix - self.n_training_points:
+            if depth_mask.is_cuda:
+                risky = True
+            else:
+                n_invalid = n_pix - int(depth_mask.sum())
+                risky = n_invalid > 0 and (n_invalid / n_pix) ** R > 1e-9
+            if risky:
                 m = depth_mask.flatten().to(dev)
                 while not m[ray_idx].any():
-                    ray_idx = torch.randperm(n_pix, device=dev)[:self.n_training_points]
+                    ray_idx = torch.randperm(n_pix, device=dev)[:R]
         return ray_idx
 
     # ------------------------------------------------------------------ loss

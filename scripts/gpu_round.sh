@@ -1,4 +1,4 @@
-# one GPU box call: parity tests, GEMM tile A/B, bench, rocprofv3 kernel stats
+# one GPU box call: parity tests, smoke, micro-benchmarks, bench, rocprofv3 kernel stats
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
@@ -6,7 +6,9 @@ OUT=$R/gpurun_out
 mkdir -p $OUT
 timeout -k 10 600 python -m pytest tests -q -m gpu -p no:cacheprovider > $OUT/t_all.log 2>&1
 echo "tests rc=$?"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && echo "smoke ok" && \
 timeout -k 10 300 python scripts/gemm_bench.py > $OUT/gemm_bench.txt 2>&1 && echo "gemm bench ok" && \
+timeout -k 10 300 python scripts/composite_bench.py > $OUT/composite_bench.txt 2>&1 && echo "composite bench ok" && \
 timeout -k 10 600 python bench.py --steps ${STEPS:-30} --warmup 5 > $OUT/bench.json 2> $OUT/bench.err && \
 echo "bench ok" && \
 cd /tmp && export TMPDIR=/tmp && \

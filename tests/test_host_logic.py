@@ -130,3 +130,9 @@ def test_ray_resampling_guarantee():
     torch.manual_seed(0)
     idx = tr.sample_rays(100, mask, True)
     assert mask.flatten()[idx].any()
+    # a mostly valid mask skips the (sync) check: the all-invalid draw is impossible
+    cfg["training"]["n_training_points"] = 64
+    tr2 = mdl.Trainer(None, None, cfg["training"], device=torch.device("cpu"))
+    mask2 = torch.ones(1, 100, 100, dtype=torch.bool)
+    mask2[0, :5] = False
+    assert tr2.sample_rays(10000, mask2, True).shape == (64,)
