@@ -101,6 +101,10 @@ int nerf_slab_reduce(const float* slab, int splits, int nout, int ldslab, int no
  * 2 = 128x256 / 8 waves, 3 = 256x256 / 8 waves;  tn (weight gradient): 1 = 128x128,
  * 3 = 256x256 / 8 waves. */
 int nerf_gemm_set_policy(int nt_policy, int tn_policy);
+/* Diagnostics only (results are wrong while non-zero): bits 0-3 NT GEMM (1 = skip the
+ * epilogue stores, 2 = skip the K-loop loads), bits 4-7 TN GEMM (16 = skip the slab stores,
+ * 32 = skip the K-loop loads, 64 = skip the bias column sums). */
+int nerf_gemm_debug_ablate(int mask);
 
 /* ---------------------------------------------------------------------------
  * Output heads (density + colour logits), forward and backward.

@@ -31,22 +31,38 @@ constexpr int BK = 32;
 template <int TM, int TN, int LDA, int LDB>
 __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const float* __restrict__ Bs,
                                           int wm0, int wn0, f32x16 (&acc)[TM][TN]) {
+    // operands of k-pair kp+1 are read from LDS before the MFMAs of kp issue, so the
+    // ds_read latency hides behind 64-cycle MFMAs instead of stalling every group
     const int lane = lane_id();
     const int l32 = lane & 31;
     const int hi = lane >> 5;
-#pragma unroll
-    for (int kp = 0; kp < BK / 2; ++kp) {
+    // two NAMED operand sets (a runtime-indexed a[cur] would live in scratch, guide rule 20)
+    float a0[TM], b0[TN], a1[TM], b1[TN];
+    auto rd = [&](int kp, float (&ra)[TM], float (&rb)[TN]) {
         const int k = 2 * kp + hi;
-        float a[TM], b[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = As[k * LDA + wm0 + 32 * i + l32];
+        for (int i = 0; i < TM; ++i) ra[i] = As[k * LDA + wm0 + 32 * i + l32];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = Bs[k * LDB + wn0 + 32 * j + l32];
+        for (int j = 0; j < TN; ++j) rb[j] = Bs[k * LDB + wn0 + 32 * j + l32];
+    };
+    auto mm = [&](const float (&ra)[TM], const float (&rb)[TN]) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[i], rb[j], acc[i][j], 0, 0, 0);
+    };
+    rd(0, a0, b0);
+#pragma unroll
+    for (int kp = 0; kp < BK / 2; kp += 2) {
+        rd(kp + 1, a1, b1);
+        // pin the order: hipcc otherwise sinks the reads below the MFMAs and reuses one
+        // operand register set, exposing the LDS latency before every MFMA group
+        __builtin_amdgcn_sched_barrier(0);
+        mm(a0, b0);
+        if (kp + 2 < BK / 2) rd(kp + 2, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(a1, b1);
     }
 }
 
@@ -79,6 +95,7 @@ struct NTArgs {
     float* c; int ldc;
     int m, n;
     int relu;
+    int ablate;   // diagnostics only (nerf_gemm_debug_ablate): 1 = no epilogue stores, 2 = no K-loop loads
 };
 
 enum { EPI_FWD = 0, EPI_BWD = 1 };
@@ -107,25 +124,27 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(NTArgs p) {
     const int n0 = blockIdx.y * BN;
     const int nkt = (p.k1 + p.k2) / BK;
 
+    // staging addresses: a wave-uniform base (SGPRs) + a 32-bit per-thread offset that is
+    // the same for every K tile (keeps VGPR use and 64-bit address math out of the loop)
+    const float* __restrict__ a1b = p.a1 + (size_t)m0 * p.lda1;
+    const float* __restrict__ a2b = p.a2 ? p.a2 + (size_t)m0 * p.lda2 : nullptr;
+    const float* __restrict__ bb = p.b + (size_t)n0 * p.ldb;
+    const int r0 = tid >> 3, kc4 = 4 * (tid & 7);
+    const int ao1 = r0 * p.lda1 + kc4, ao2 = r0 * p.lda2 + kc4, bo = r0 * p.ldb + kc4;
+    constexpr int RSTEP = NT / 8;   // rows covered by one pass of the block
     float4 ra[A_F4], rb[B_F4];
     auto load_tile = [&](int kt) {
         const int kk = kt * BK;
-        const float* abase;
-        int lda, kc0;
-        if (kk < p.k1) { abase = p.a1; lda = p.lda1; kc0 = kk; }
-        else           { abase = p.a2; lda = p.lda2; kc0 = kk - p.k1; }
+        const bool seg1 = kk < p.k1;
+        const float* abase = seg1 ? a1b + kk : a2b + (kk - p.k1);
+        const int lda = seg1 ? p.lda1 : p.lda2;
+        const int ao = seg1 ? ao1 : ao2;
 #pragma unroll
-        for (int i = 0; i < A_F4; ++i) {
-            const int idx = tid + NT * i;
-            const int row = idx >> 3, kc = idx & 7;
-            ra[i] = *reinterpret_cast<const float4*>(abase + (size_t)(m0 + row) * lda + kc0 + 4 * kc);
-        }
+        for (int i = 0; i < A_F4; ++i)
+            ra[i] = *reinterpret_cast<const float4*>(abase + ao + i * RSTEP * lda);
 #pragma unroll
-        for (int i = 0; i < B_F4; ++i) {
-            const int idx = tid + NT * i;
-            const int row = idx >> 3, kc = idx & 7;
-            rb[i] = *reinterpret_cast<const float4*>(p.b + (size_t)(n0 + row) * p.ldb + kk + 4 * kc);
-        }
+        for (int i = 0; i < B_F4; ++i)
+            rb[i] = *reinterpret_cast<const float4*>(bb + kk + bo + i * RSTEP * p.ldb);
     };
     auto store_tile = [&](int buf) {
 #pragma unroll
@@ -167,7 +186,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(NTArgs p) {
     __syncthreads();
     for (int kt = 0; kt < nkt; ++kt) {
         const int cur = kt & 1;
-        if (kt + 1 < nkt) load_tile(kt + 1);
+        if (kt + 1 < nkt) { if (!(p.ablate & 2)) load_tile(kt + 1); }
         else prefetch_epi();
         mfma_tile<TM, TN, LDA, LDB>(As(cur), Bs(cur), wm0, wn0, acc);
         if (kt + 1 < nkt) store_tile(cur ^ 1);
@@ -176,6 +195,17 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(NTArgs p) {
 
     const int lane = lane_id();
     const int l32 = lane & 31, hi = lane >> 5;
+    if (p.ablate & 1) {   // keep the accumulators live, store one value per thread
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+        p.c[(size_t)(m0 + (tid & 127)) * p.ldc + n0 + (tid >> 7)] = t;
+        return;
+    }
     if (EPI == EPI_FWD) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -237,6 +267,7 @@ struct TNArgs {
     int rows_per_split;
     float* slab; int ldslab; int col0; size_t slab_stride;
     float* bslab; int nout;
+    int ablate;   // diagnostics: 1 = no slab stores, 2 = no K-loop loads, 4 = no bias column sums
 };
 
 template <int BM, int BN, int WM, int WN>
@@ -263,36 +294,39 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_tn(TNArgs p) {
     const int split = blockIdx.z;
     const size_t s0 = (size_t)split * p.rows_per_split;
     const int nkt = p.rows_per_split / BK;
-    const bool do_bias = (p.bslab != nullptr) && (blockIdx.y == 0);
+    const bool do_bias = (p.bslab != nullptr) && (blockIdx.y == 0) && !(p.ablate & 4);
 
+    // wave-uniform bases + constant 32-bit per-thread offsets (see k_gemm_nt)
+    const float* __restrict__ dyb = p.dy + s0 * p.lddy + o0;
+    const float* __restrict__ xb = p.x + s0 * p.ldx + j0;
+    const int ao = (tid / A_C4) * p.lddy + 4 * (tid % A_C4);
+    const int bo = (tid / B_C4) * p.ldx + 4 * (tid % B_C4);
+    constexpr int ARSTEP = NT / A_C4, BRSTEP = NT / B_C4;
     float4 ra[A_F4], rb[B_F4];
     auto load_tile = [&](int kt) {
-        const size_t sb = s0 + (size_t)kt * BK;
+        const float* da = dyb + (size_t)kt * BK * p.lddy;
+        const float* db = xb + (size_t)kt * BK * p.ldx;
 #pragma unroll
-        for (int i = 0; i < A_F4; ++i) {
-            const int idx = tid + NT * i;
-            const int row = idx / A_C4, c4 = idx % A_C4;
-            ra[i] = *reinterpret_cast<const float4*>(p.dy + (sb + row) * p.lddy + o0 + 4 * c4);
-        }
+        for (int i = 0; i < A_F4; ++i)
+            ra[i] = *reinterpret_cast<const float4*>(da + ao + i * ARSTEP * p.lddy);
 #pragma unroll
-        for (int i = 0; i < B_F4; ++i) {
-            const int idx = tid + NT * i;
-            const int row = idx / B_C4, c4 = idx % B_C4;
-            rb[i] = *reinterpret_cast<const float4*>(p.x + (sb + row) * p.ldx + j0 + 4 * c4);
-        }
+        for (int i = 0; i < B_F4; ++i)
+            rb[i] = *reinterpret_cast<const float4*>(db + bo + i * BRSTEP * p.ldx);
     };
     auto store_tile = [&](int buf) {
+        // component-wise copies: a whole-float4 aggregate store made hipcc keep ra/rb in
+        // a scratch (stack) array instead of registers
 #pragma unroll
         for (int i = 0; i < A_F4; ++i) {
             const int idx = tid + NT * i;
             const int row = idx / A_C4, c4 = idx % A_C4;
-            *reinterpret_cast<float4*>(As(buf) + row * LDA + 4 * c4) = ra[i];
+            *reinterpret_cast<float4*>(As(buf) + row * LDA + 4 * c4) = make_float4(ra[i].x, ra[i].y, ra[i].z, ra[i].w);
         }
 #pragma unroll
         for (int i = 0; i < B_F4; ++i) {
             const int idx = tid + NT * i;
             const int row = idx / B_C4, c4 = idx % B_C4;
-            *reinterpret_cast<float4*>(Bs(buf) + row * LDB + 4 * c4) = rb[i];
+            *reinterpret_cast<float4*>(Bs(buf) + row * LDB + 4 * c4) = make_float4(rb[i].x, rb[i].y, rb[i].z, rb[i].w);
         }
     };
 
@@ -305,7 +339,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_tn(TNArgs p) {
     __syncthreads();
     for (int kt = 0; kt < nkt; ++kt) {
         const int cur = kt & 1;
-        if (kt + 1 < nkt) load_tile(kt + 1);
+        if (kt + 1 < nkt && !(p.ablate & 2)) load_tile(kt + 1);
         mfma_tile<TM, TN, LDA, LDB>(As(cur), Bs(cur), wm0, wn0, acc);
         if (do_bias && tid < BM) {
 #pragma unroll 8
@@ -318,6 +352,17 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_tn(TNArgs p) {
     float* slab = p.slab + (size_t)split * p.slab_stride;
     const int lane = lane_id();
     const int l32 = lane & 31, hi = lane >> 5;
+    if (p.ablate & 1) {
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+        slab[tid] = t;
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -370,11 +415,15 @@ __global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ s
 
 using namespace nerf;
 
+static int g_ablate = 0;   // nerf_gemm_debug_ablate
+
 template <int BM, int BN, int WM, int WN, int EPI>
 static int launch_nt(const NTArgs& a, hipStream_t s, double flops) {
     dim3 grid(a.m / BM, a.n / BN);
+    NTArgs b = a;
+    b.ablate = g_ablate;
     prof_begin(s);
-    hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, EPI>), grid, dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, EPI>), grid, dim3(64 * WM * WN), 0, s, b);
     prof_end(s, flops);
     return check_launch("k_gemm_nt");
 }
@@ -460,6 +509,7 @@ extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const
     a.rows_per_split = m / splits;
     a.slab = slab; a.ldslab = ldslab; a.col0 = col0; a.slab_stride = (size_t)nout * ldslab;
     a.bslab = bslab; a.nout = nout;
+    a.ablate = g_ablate >> 4;
     hipStream_t s = as_stream(stream);
     const double fl = 2.0 * m * nout * (double)kin;
     prof_begin(s);
@@ -517,4 +567,10 @@ extern "C" int nerf_linear_bwd_weight_splits(int nout, int kin, int m) {
     int splits = 1;
     while (splits * 2 * tiles <= target && m % (splits * 2 * BK) == 0 && m / (splits * 2) >= 256) splits *= 2;
     return splits;
+}
+
+// diagnostics: ablate parts of the NT GEMM (results are wrong while set); not for production
+extern "C" int nerf_gemm_debug_ablate(int mask) {
+    g_ablate = mask;
+    return NERF_OK;
 }

@@ -56,6 +56,7 @@ _SIGS = {
     "nerf_adam_step": ([_c_p, _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p], _c_i),
     "nerf_chamfer_nn": ([_c_p, _c_i, _c_p, _c_i, _c_p, _c_p], _c_i),
     "nerf_gemm_set_policy": ([_c_i, _c_i], _c_i),
+    "nerf_gemm_debug_ablate": ([_c_i], _c_i),
     "nerf_prof_enable": ([_c_i], _c_i),
     "nerf_prof_read": ([ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_i64),
                         ctypes.POINTER(ctypes.c_double)], _c_i),

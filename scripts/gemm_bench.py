@@ -48,6 +48,29 @@ def main():
         bslab = torch.empty(sp * D, device=dev)
         cases[f"dW splits={sp}"] = ((lambda sp=sp, slab=slab, bslab=bslab:
                                      _hip.linear_bwd_weight(dy, D, x, D, M, sp, slab, D, 0, bslab)), 2 * M * D * D)
+    quick = "--quick" in sys.argv
+    if quick:   # one launch per case at the default policy (for PMC collection)
+        for name, (fn, fl) in cases.items():
+            fn()
+        torch.cuda.synchronize()
+        return
+    if "--ablate" in sys.argv:
+        for pol in (2, 3):
+            _hip.gemm_set_policy(pol, 3)
+            for ab in (0, 1, 2, 3):
+                _hip.lib().nerf_gemm_debug_ablate(ab)
+                for name in ("fwd 256x256", "bwd-data mask+u"):
+                    fn, fl = cases[name]
+                    us = min(timeit(fn) for _ in range(3))
+                    print(f"ablate={ab} policy {pol} {name:18s}: {us:8.1f} us {fl / us / 1e6:6.1f} TF/s")
+        _hip.gemm_set_policy(0, 0)
+        for ab in (0, 16, 32, 64, 16 + 32 + 64):
+            _hip.lib().nerf_gemm_debug_ablate(ab)
+            fn, fl = cases["dW splits=256"]
+            us = min(timeit(fn) for _ in range(3))
+            print(f"ablate={ab} dW splits=256: {us:8.1f} us {fl / us / 1e6:6.1f} TF/s")
+        _hip.lib().nerf_gemm_debug_ablate(0)
+        return
     res = {}
     for rnd in range(3):
         for pol in (1, 2, 3):
