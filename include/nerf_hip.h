@@ -178,10 +178,12 @@ int nerf_chamfer_nn(const float* x, int p, const float* y, int q, int64_t* idx, 
 
 /* ---------------------------------------------------------------------------
  * Timing hooks for bench.py: when enabled, every GEMM launch is bracketed by
- * hipEvents on its stream; nerf_prof_read returns the summed milliseconds and
- * launch count of the GEMM family since the last reset (synchronises events). */
+ * hipEvents on its stream; nerf_prof_read returns, for the GEMM family since the last
+ * reset, the summed launch durations, the launch count, the padded FLOPs issued and the
+ * union of the launch intervals (launches overlapping on two streams count once);
+ * synchronises the events. */
 int nerf_prof_enable(int on);
-int nerf_prof_read(double* gemm_ms, int64_t* gemm_launches, double* gemm_flops);
+int nerf_prof_read(double* gemm_ms, int64_t* gemm_launches, double* gemm_flops, double* union_ms);
 
 #ifdef __cplusplus
 }

@@ -1,6 +1,7 @@
 // Error reporting and GEMM timing hooks of the nerf_hip C-ABI.
 #include "common.hpp"
 
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -61,22 +62,42 @@ int nerf_prof_enable(int on) {
     return NERF_OK;
 }
 
-int nerf_prof_read(double* gemm_ms, int64_t* gemm_launches, double* gemm_flops) {
+int nerf_prof_read(double* gemm_ms, int64_t* gemm_launches, double* gemm_flops, double* union_ms) {
     NERF_CHECK_PTR(gemm_ms);
     NERF_CHECK_PTR(gemm_launches);
     NERF_CHECK_PTR(gemm_flops);
     std::lock_guard<std::mutex> lk(nerf::g_prof_mu);
     double ms = 0, fl = 0;
+    // launch intervals relative to the first start event: summed durations (per-launch
+    // average) and the union of the intervals (GEMM family running concurrently on two
+    // streams counts once)
+    std::vector<std::pair<double, double>> iv;
     for (size_t i = 0; i < nerf::g_used; ++i) {
         (void)hipEventSynchronize(nerf::g_pool[i].b);
-        float t = 0;
+        float t = 0, a = 0, b = 0;
         (void)hipEventElapsedTime(&t, nerf::g_pool[i].a, nerf::g_pool[i].b);
+        (void)hipEventElapsedTime(&a, nerf::g_pool[0].a, nerf::g_pool[i].a);
+        (void)hipEventElapsedTime(&b, nerf::g_pool[0].a, nerf::g_pool[i].b);
+        iv.emplace_back(a, b);
         ms += t;
         fl += nerf::g_pool[i].flops;
     }
+    std::sort(iv.begin(), iv.end());
+    double un = 0, cs = -1e30, ce = -1e30;
+    for (auto& x : iv) {
+        if (x.first > ce) {
+            if (ce > cs) un += ce - cs;
+            cs = x.first;
+            ce = x.second;
+        } else if (x.second > ce) {
+            ce = x.second;
+        }
+    }
+    if (ce > cs) un += ce - cs;
     *gemm_ms = ms;
     *gemm_launches = (int64_t)nerf::g_used;
     *gemm_flops = fl;
+    if (union_ms) *union_ms = un;
     nerf::g_used = 0;
     return NERF_OK;
 }

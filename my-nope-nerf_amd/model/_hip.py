@@ -59,7 +59,7 @@ _SIGS = {
     "nerf_gemm_debug_ablate": ([_c_i], _c_i),
     "nerf_prof_enable": ([_c_i], _c_i),
     "nerf_prof_read": ([ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_i64),
-                        ctypes.POINTER(ctypes.c_double)], _c_i),
+                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], _c_i),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
@@ -208,8 +208,10 @@ def prof_enable(on: bool):
 
 
 def prof_read():
+    """-> (summed GEMM launch ms, launches, padded FLOPs, union-of-intervals ms)."""
     ms = ctypes.c_double()
     n = _c_i64()
     fl = ctypes.c_double()
-    _call("nerf_prof_read", ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl))
-    return ms.value, n.value, fl.value
+    un = ctypes.c_double()
+    _call("nerf_prof_read", ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl), ctypes.byref(un))
+    return ms.value, n.value, fl.value, un.value

@@ -79,7 +79,7 @@ class FieldRunner:
         ]
         self.layers = L
         self.device = None
-        self._bufs = None
+        self._side = None
 
     # ------------------------------------------------------------------ packing
     def _alloc(self, device):
@@ -209,7 +209,14 @@ class FieldRunner:
             genc_p = torch.zeros(Np, _hip.ENC_P, device=dev)
             genc_d = torch.zeros(Np, _hip.ENC_D, device=dev)
 
-        # walk the layers backwards; dy = gradient w.r.t. the layer's pre-activation output
+        # walk the layers backwards; dy = gradient w.r.t. the layer's pre-activation output.
+        # The weight gradients (split-K GEMM + slab reduce) of layer l depend only on dy_l and
+        # the saved input, so they run on a side stream beside the dX chain: compute-bound
+        # GEMM phases overlap the memory-bound reductions and each other's prologue/epilogue.
+        main = torch.cuda.current_stream(dev)
+        if self._side is None or self._side.device != dev:
+            self._side = torch.cuda.Stream(dev)
+        side = self._side
         dy = dyr
         prev_in = {"l0": st["enc_p"], "l1": h["l0"], "l2": h["l1"], "l3": h["l2"], "l4": h["l3"],
                    "l5": h["l4"], "l6": h["l5"], "l7": h["l6"], "lf": h["l7"], "lr": h["lf"]}
@@ -218,25 +225,29 @@ class FieldRunner:
                      "lf": "l7", "lr": "lf"}
         spec = {l.name: l for l in self.layers}
         seg_buf = {"enc_p": st["enc_p"], "enc_d": st["enc_d"]}
-        pingpong = [e(Np, D), e(Np, D)]
         for step, name in enumerate(order):
             l = spec[name]
             W = l.linear.weight
             nout_ref, kin_ref = W.shape
             x_in = prev_in[name]
             k1 = l.k1
-            # --- weight / bias gradient: split-K slabs + reduce into the reference layout
-            splits = _hip.bwd_weight_splits(l.out_p, k1, Np)
-            slab = e(splits * l.out_p * l.kp)
-            bslab = e(splits * l.out_p)
-            _hip.linear_bwd_weight(dy, l.out_p, x_in, k1, Np, splits, slab, l.kp, 0, bslab)
-            if l.seg2:
-                _hip.linear_bwd_weight(dy, l.out_p, seg_buf[l.seg2], 64, Np, splits, slab, l.kp, k1, None)
-            gb = G(l.linear.bias) if l.out_p == nout_ref else e(l.out_p)
-            gw = G(W)
-            _hip.slab_reduce(slab, splits, l.out_p, l.kp, nout_ref, kin_ref, bslab, gw, gb)
-            if l.out_p != nout_ref:
-                G(l.linear.bias).copy_(gb[:nout_ref])
+            # --- weight / bias gradient on the side stream: split-K slabs + reduce
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            dy.record_stream(side)          # dy_l is freed by the main loop while side reads it
+            with torch.cuda.stream(side):
+                splits = _hip.bwd_weight_splits(l.out_p, k1, Np)
+                slab = e(splits * l.out_p * l.kp)
+                bslab = e(splits * l.out_p)
+                _hip.linear_bwd_weight(dy, l.out_p, x_in, k1, Np, splits, slab, l.kp, 0, bslab)
+                if l.seg2:
+                    _hip.linear_bwd_weight(dy, l.out_p, seg_buf[l.seg2], 64, Np, splits, slab, l.kp, k1, None)
+                gb = G(l.linear.bias) if l.out_p == nout_ref else e(l.out_p)
+                gw = G(W)
+                _hip.slab_reduce(slab, splits, l.out_p, l.kp, nout_ref, kin_ref, bslab, gw, gb)
+                if l.out_p != nout_ref:
+                    G(l.linear.bias).copy_(gb[:nout_ref])
             # --- input gradient
             wt = self.wt[name]
             if name == "l0":
@@ -250,7 +261,7 @@ class FieldRunner:
                 tmp = e(Np, 64)
                 _hip.linear_bwd_data(dy, l.out_p, wt[k1:k1 + 64], tmp, Np, 64)
                 tgt.add_(tmp)
-            dx = pingpong[step % 2]
+            dx = e(Np, k1)
             # ReLU bits of this layer's input (f, the input of lr, has no activation)
             mask = None if name == "lr" else st["masks"][prev_name[name]]
             if name == "lf":   # + density path: d sigma_raw (graw4[:,0]) x w_density
@@ -260,6 +271,9 @@ class FieldRunner:
                 _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask)
             dy = dx
 
+        done = torch.cuda.Event()
+        done.record(side)
+        main.wait_event(done)               # gradients complete before autograd hands them on
         ray = None
         if want_ray_grad:
             g_po, g_pd, g_view = e(R, 3), e(R, 3), e(R, 3)
