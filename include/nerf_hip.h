@@ -62,20 +62,26 @@ int nerf_encode_samples(const float* pts_o, const float* pts_d, const float* vie
  * w : [n][k1+k2] (padded packed weight), y: [m][ldy]. m % 128 == 0, n % 64 == 0,
  * k1 % 32 == 0, k2 % 32 == 0. relu: 0/1.  mask_out (optional): ReLU mask bits of y,
  * word [m][n/32] (row stride ldmo words), bit b of word w = y[m][32w+b] > 0.
+ * w_split (optional, used by GEMM precision mode 1): the same weight as a bf16x3 split
+ * image (nerf_pack_weights dst_s): element (plane p, row r, col c) at
+ * w_split[((p*(K/8) + c/8)*w_split_rows + r)*8 + c%8], K = k1+k2; w_split may point at
+ * a row offset inside a larger image whose row count is w_split_rows.  NULL: this call
+ * runs on the exact-f32 kernel even in mode 1.
  */
 int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2, int k2,
-                    const float* w, const float* bias, float* y, int ldy, int m, int n,
-                    int relu, uint32_t* mask_out, int ldmo, void* stream);
+                    const float* w, const uint16_t* w_split, int w_split_rows, const float* bias, float* y,
+                    int ldy, int m, int n, int relu, uint32_t* mask_out, int ldmo, void* stream);
 
 /* Backward w.r.t. the layer input (autograd of official_nerf.py:62-91).
  *   dx[m, j] = ( sum_o dy[m,o] wt[j,o]  + (u ? u[m*ldu] * v[j] : 0) ) * (mask ? bit(m,j) : 1)
  * wt: [n][k] = transpose of the packed weight restricted to the wanted input columns
  * (n = number of input columns produced, k = layer outputs), mask: ReLU mask bits of
  * the previous layer's output as written by nerf_linear_fwd (ldmask words per row) or
- * NULL.  m%128==0, n%64==0, k%32==0. */
-int nerf_linear_bwd_data(const float* dy, int lddy, int k, const float* wt,
-                         const float* u, int ldu, const float* v, const uint32_t* mask, int ldmask,
-                         float* dx, int lddx, int m, int n, void* stream);
+ * NULL.  m%128==0, n%64==0, k%32==0.  wt_split / wt_split_rows: optional bf16x3 image of
+ * wt as for nerf_linear_fwd (K = k). */
+int nerf_linear_bwd_data(const float* dy, int lddy, int k, const float* wt, const uint16_t* wt_split,
+                         int wt_split_rows, const float* u, int ldu, const float* v, const uint32_t* mask,
+                         int ldmask, float* dx, int lddx, int m, int n, void* stream);
 
 /* Backward w.r.t. weight and bias, split over sample rows:
  *   slab[split][o][col0 + j] = sum_{rows of split} dy[row, o] * x[row, j]   (j < kin)
@@ -101,9 +107,20 @@ int nerf_slab_reduce(const float* slab, int splits, int nout, int ldslab, int no
  * 2 = 128x256 / 8 waves, 3 = 256x256 / 8 waves;  tn (weight gradient): 1 = 128x128,
  * 3 = 256x256 / 8 waves. */
 int nerf_gemm_set_policy(int nt_policy, int tn_policy);
+
+/* f32 arithmetic of the GEMM family (process-wide; default 0):
+ *   0  exact-f32 v_mfma_f32_32x32x2_f32 (a k-ordered f32 fma chain);
+ *   1  f32 emulated on v_mfma_f32_32x32x16_bf16: operands split into three bf16
+ *      words (exact), the six cross products >= 2^-16 |a||b| accumulated in f32.
+ *      nerf_linear_fwd / nerf_linear_bwd_data use it when given the weight's split
+ *      image (w_split / wt_split), nerf_linear_bwd_weight always.
+ * Returns NERF_EINVAL for other modes. */
+int nerf_gemm_set_precision(int mode);
+int nerf_gemm_get_precision(void);
 /* Diagnostics only (results are wrong while non-zero): bits 0-3 NT GEMM (1 = skip the
  * epilogue stores, 2 = skip the K-loop loads), bits 4-7 TN GEMM (16 = skip the slab stores,
  * 32 = skip the K-loop loads, 64 = skip the bias column sums). */
+int nerf_gemm_debug_stamps(void* buf);
 int nerf_gemm_debug_ablate(int mask);
 
 /* ---------------------------------------------------------------------------
@@ -152,13 +169,18 @@ int nerf_encode_bwd(const float* pts_o, const float* pts_d, const float* view, c
  * Weight packing: src [rows][cols] (reference nn.Linear layout) -> dst [rows][ld_dst]
  * zero padded, and (if dst_t != NULL) its transpose dst_t[c][r] (row stride ld_t,
  * rows c >= cols zero).  Padding rows/cols outside the written ranges keep their
- * previous contents (callers zero the buffers once).  Up to NERF_MAX_PACK descriptors. */
+ * previous contents (callers zero the buffers once).  Up to NERF_MAX_PACK descriptors.
+ * dst_s / dst_ts (optional): the whole padded dst / dst_t as bf16x3 split images, the B
+ * operand format of GEMM precision mode 1 (hi, mid, lo planes; ld_dst, ld_t % 8 == 0). */
 #define NERF_MAX_PACK 16
 typedef struct {
     const float* src;
     float* dst;    /* [rows][ld_dst] */
     float* dst_t;  /* [rows_t][ld_t] or NULL */
     int rows, cols, ld_dst, rows_t, ld_t;
+    uint16_t* dst_s;   /* optional bf16x3 split image of dst:   [3][ld_dst/8][rows_s][8] */
+    uint16_t* dst_ts;  /* optional bf16x3 split image of dst_t: [3][ld_t/8][rows_t][8]  */
+    int rows_s;        /* image rows of dst_s (>= rows, rows past `rows` zero; 0 = rows) */
 } nerf_pack_desc;
 int nerf_pack_weights(const nerf_pack_desc* descs, int n, void* stream);
 

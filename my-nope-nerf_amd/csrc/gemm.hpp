@@ -1,0 +1,348 @@
+// Shared pieces of the field-MLP GEMMs: launch arguments, the gfx950 32x32 MFMA C/D map
+// and the fused epilogues.  Two K-loop bodies use them:
+//   gemm_f32.hip  exact-f32 v_mfma_f32_32x32x2_f32 (64 FLOP/clk/SIMD);
+//   gemm_x6.hip   f32 emulated on v_mfma_f32_32x32x16_bf16: every f32 operand is split
+//                 into three bf16 words and the six significant cross products are
+//                 accumulated in f32 (1024 FLOP/clk/SIMD / 6).
+// The 32x32 C/D layout is dtype-independent on gfx950, so the epilogues are shared.
+#pragma once
+#include "common.hpp"
+
+namespace nerf {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// accumulator register r of a 32x32 tile -> row offset inside the tile (gfx950 C/D map)
+__device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
+
+template <int TM, int TN>
+__device__ __forceinline__ void zero_acc(f32x16 (&acc)[TM][TN]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+}
+
+// NT GEMM: C[m][n] = epi( sum_k A[m][k] B[n][k] ), A from up to two K segments.
+struct NTArgs {
+    const float* a1; int lda1; int k1;
+    const float* a2; int lda2; int k2;
+    const float* b;  int ldb;           // [n][k1+k2]
+    const uint16_t* bs; int bs_rows;    // optional bf16x3 image of b (split-bf16 kernels only)
+    const float* bias;                  // fwd
+    const float* u;  const float* v;    // bwd-data rank-1 term u[m*ldu] v[n]
+    int ldu;
+    const uint32_t* mask; int ldmask;   // bwd-data ReLU mask bits [m][n/32] (bit = x > 0)
+    uint32_t* mask_out; int ldmo;       // fwd: write the ReLU mask bits of the output
+    float* c; int ldc;
+    int m, n;
+    int relu;
+    unsigned long long* stamps;   // diagnostics (nerf_gemm_debug_stamps): per-block phase clocks or NULL
+    int ablate;   // diagnostics only (nerf_gemm_debug_ablate): 1 = no epilogue stores, 2 = no K-loop loads
+                  // (f32 kernels; the split-bf16 kernels honour 1 only)
+};
+
+enum { EPI_FWD = 0, EPI_BWD = 1 };
+
+// TN GEMM (weight gradient): slab[split][o][col0+j] = sum_s dy[s][o] x[s][j]
+struct TNArgs {
+    const float* dy; int lddy;   // A[m=o][k=s] = dy[s][o]
+    const float* x;  int ldx;    // B[k=s][n=j] = x[s][j]
+    int rows_per_split;
+    float* slab; int ldslab; int col0; size_t slab_stride;
+    float* bslab; int nout;
+    int ablate;   // diagnostics: 1 = no slab stores, 2 = no K-loop loads, 4 = no bias column sums
+};
+
+// Backward-data epilogue operands (ReLU bits, rank-1 column), prefetched into registers
+// with coalesced loads while the last K tile computes, parked in LDS by nt_epilogue.
+template <int BM, int BN, int NT, int EPI>
+struct NTEpiPrefetch {
+    static constexpr int MW = BN / 32;                    // mask words per row of the tile
+    static constexpr int M_PF = (BM * MW + NT - 1) / NT;  // mask words prefetched per thread
+    uint32_t mpf[M_PF];
+    float upf = 0.f;
+    __device__ __forceinline__ void load(const NTArgs& p, int m0, int n0) {
+        if (EPI != EPI_BWD) return;
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int q = 0; q < M_PF; ++q) {
+            const int e = tid + NT * q;
+            mpf[q] = (p.mask && e < BM * MW) ? p.mask[(size_t)(m0 + e / MW) * p.ldmask + (n0 >> 5) + e % MW]
+                                             : 0xffffffffu;
+        }
+        if (tid < BM) upf = p.u ? p.u[(size_t)(m0 + tid) * p.ldu] : 0.f;
+    }
+};
+
+// Fused NT epilogue.  smem: at least BM*(BN/32) words + BM floats, free (after the last
+// K-loop barrier).  FWD: +bias, ReLU, ReLU bit mask via ballot.  BWD: + u[m] v[n], masked.
+template <int BM, int BN, int NT, int TM, int TN, int EPI>
+__device__ __forceinline__ void nt_epilogue(const NTArgs& p, f32x16 (&acc)[TM][TN], float* smem, int m0, int n0,
+                                            int wm0, int wn0, const NTEpiPrefetch<BM, BN, NT, EPI>& pf) {
+    constexpr int MW = BN / 32;
+    const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const int l32 = lane & 31, hi = lane >> 5;
+    if (p.ablate & 1) {   // keep the accumulators live, store one value per thread
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+        p.c[(size_t)(m0 + (tid & 127)) * p.ldc + n0 + (tid >> 7)] = t;
+        return;
+    }
+    if (EPI == EPI_FWD) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn0 + 32 * j + l32;
+            const int cword = (n0 + wn0 + 32 * j) >> 5;
+            const float bcol = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = m0 + wm0 + 32 * i + acc_row(r, hi);
+                    float x = acc[i][j][r] + bcol;
+                    if (p.relu) x = fmaxf(x, 0.f);
+                    p.c[(size_t)row * p.ldc + col] = x;
+                    if (p.mask_out) {
+                        // bits 0-31: the 32 columns of this register's row held by lanes 0-31,
+                        // bits 32-63: the row held by lanes 32-63
+                        const uint64_t bits = __ballot(x > 0.f);
+                        if (l32 == 0)
+                            p.mask_out[(size_t)row * p.ldmo + cword] = (uint32_t)(hi ? (bits >> 32) : bits);
+                    }
+                }
+        }
+    } else {
+        uint32_t* lmask = reinterpret_cast<uint32_t*>(smem);
+        float* lu = smem + BM * MW;
+#pragma unroll
+        for (int q = 0; q < NTEpiPrefetch<BM, BN, NT, EPI>::M_PF; ++q) {
+            const int e = tid + NT * q;
+            if (e < BM * MW) lmask[e] = pf.mpf[q];
+        }
+        if (tid < BM) lu[tid] = pf.upf;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn0 + 32 * j + l32;
+            const int cw = (wn0 + 32 * j) >> 5;
+            const float vcol = p.u ? p.v[col] : 0.f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int lr = wm0 + 32 * i + acc_row(r, hi);
+                    float x = acc[i][j][r] + lu[lr] * vcol;
+                    x = ((lmask[lr * MW + cw] >> l32) & 1u) ? x : 0.f;
+                    p.c[(size_t)(m0 + lr) * p.ldc + col] = x;
+                }
+        }
+    }
+}
+
+// TN epilogue: this split's partial weight gradient tile into its slab
+template <int TM, int TN>
+__device__ __forceinline__ void tn_store(const TNArgs& p, f32x16 (&acc)[TM][TN], int split, int o0, int j0,
+                                         int wm0, int wn0) {
+    float* slab = p.slab + (size_t)split * p.slab_stride;
+    const int lane = lane_id();
+    const int l32 = lane & 31, hi = lane >> 5;
+    if (p.ablate & 1) {
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+        slab[threadIdx.x] = t;
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int o = o0 + wm0 + 32 * i + acc_row(r, hi);
+                const int c = p.col0 + j0 + wn0 + 32 * j + l32;
+                slab[(size_t)o * p.ldslab + c] = acc[i][j][r];
+            }
+}
+
+// diagnostics: wave 0 of each block records (s_memtime, s_memrealtime) at phase
+// boundaries into stamps[block][phase][2]
+constexpr int kStampPhases = 4;
+__device__ __forceinline__ void stamp(unsigned long long* st, int phase) {
+    if (st == nullptr) return;
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    const unsigned long long r = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        const size_t b = (size_t)blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
+        st[(b * kStampPhases + phase) * 2] = t;
+        st[(b * kStampPhases + phase) * 2 + 1] = r;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// LDS-transposed tile writer (split-bf16 kernels).  The 32x32 C/D layout gives each
+// lane one column of 16 rows, so storing from registers takes one 4-byte store per
+// element (256 per wave at a 128x128 wave tile) and the store issue dominates the
+// epilogue.  Instead each wave writes its tile, 64 rows per pass, into a private LDS
+// region (rows padded to WTN + 8 floats: the column writes of lanes 0-31 and 32-63
+// land on disjoint banks) and reads it back as row-contiguous float4s: emit(row, col,
+// v) is called for WTN/4 lanes per row, 64*4/WTN rows per wave-instruction.
+// ---------------------------------------------------------------------------
+template <int TN>
+struct TileLds {
+    static constexpr int WTN = 32 * TN;
+    static constexpr int LD = WTN + 8;              // floats per LDS row
+    static constexpr int BYTES = 64 * LD * 4;       // per wave
+    static constexpr int LPR = WTN / 4;             // lanes per row (read phase)
+    static constexpr int RPI = 64 / LPR;            // rows per read instruction
+};
+
+template <int TM, int TN, typename Emit>
+__device__ __forceinline__ void write_tile_lds(f32x16 (&acc)[TM][TN], float* wlds, Emit&& emit) {
+    using T = TileLds<TN>;
+    const int lane = lane_id();
+    const int l32 = lane & 31, hi = lane >> 5;
+#pragma unroll
+    for (int h = 0; h < TM; h += 2) {
+        constexpr int NT2 = TM >= 2 ? 2 : 1;
+#pragma unroll
+        for (int ii = 0; ii < NT2; ++ii)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    wlds[(32 * ii + acc_row(r, hi)) * T::LD + 32 * j + l32] = acc[h + ii][j][r];
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < 32 * NT2 / T::RPI; ++q) {
+            const int rl = q * T::RPI + lane / T::LPR;
+            const int c4 = (lane % T::LPR) * 4;
+            const float4 v = *reinterpret_cast<const float4*>(wlds + rl * T::LD + c4);
+            emit(32 * h + rl, c4, v);
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+}
+
+// ReLU mask word of 32 columns from 8 lanes holding 4 consecutive columns each (lane
+// groups of 8 aligned to the word): valid in the lane with (lane & 7) == 0.  The OR over
+// the 8 lanes runs on DPP (quad_perm xor 1, xor 2, then row_half_mirror), not on
+// ds_bpermute round trips.
+__device__ __forceinline__ uint32_t mask_word8(float4 v) {
+    const uint32_t nib = (v.x > 0.f ? 1u : 0u) | (v.y > 0.f ? 2u : 0u) | (v.z > 0.f ? 4u : 0u) | (v.w > 0.f ? 8u : 0u);
+    int w = (int)(nib << (4 * (lane_id() & 7)));
+    w |= __builtin_amdgcn_mov_dpp(w, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+    w |= __builtin_amdgcn_mov_dpp(w, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+    w |= __builtin_amdgcn_mov_dpp(w, 0x141, 0xF, 0xF, false);   // row_half_mirror
+    return (uint32_t)w;
+}
+
+// Fused NT epilogue through the LDS writer.  smem layout: [4 waves][TileLds::BYTES],
+// then (BWD) the parked mask words and u column.
+template <int BM, int BN, int NT, int TM, int TN, int EPI>
+__device__ __forceinline__ void nt_epilogue_lds(const NTArgs& p, f32x16 (&acc)[TM][TN], char* smem, int m0,
+                                                int n0, int wm0, int wn0,
+                                                const NTEpiPrefetch<BM, BN, NT, EPI>& pf) {
+    using T = TileLds<TN>;
+    constexpr int MW = BN / 32;
+    constexpr int NW = NT / 64;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    if (p.ablate & 1) {
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+        p.c[(size_t)(m0 + (tid & 127)) * p.ldc + n0 + (tid >> 7)] = t;
+        return;
+    }
+    float* wlds = reinterpret_cast<float*>(smem + wave * T::BYTES);
+    const int c4l = (lane_id() % T::LPR) * 4;          // this lane's 4 columns (read phase)
+    const int col = n0 + wn0 + c4l;
+    if (EPI == EPI_FWD) {
+        // ReLU mask words are gathered in LDS and written as the block's contiguous rows
+        // at the end (per-wave 16-byte pieces at a 32-byte row stride are partial-line
+        // HBM writes)
+        uint32_t* lmask = reinterpret_cast<uint32_t*>(smem + NW * T::BYTES);
+        const float4 b4 = p.bias ? *reinterpret_cast<const float4*>(p.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int cw = (wn0 + c4l) >> 5;
+        write_tile_lds<TM, TN>(acc, wlds, [&](int rl, int c4, float4 v) {
+            const int row = m0 + wm0 + rl;
+            float4 x = make_float4(v.x + b4.x, v.y + b4.y, v.z + b4.z, v.w + b4.w);
+            if (p.relu) x = make_float4(fmaxf(x.x, 0.f), fmaxf(x.y, 0.f), fmaxf(x.z, 0.f), fmaxf(x.w, 0.f));
+            *reinterpret_cast<float4*>(p.c + (size_t)row * p.ldc + col) = x;
+            if (p.mask_out) {
+                const uint32_t w = mask_word8(x);
+                if ((lane_id() & 7) == 0) lmask[(wm0 + rl) * MW + cw] = w;
+            }
+        });
+        if (p.mask_out) {
+            __syncthreads();
+            for (int e = tid; e < BM * MW; e += NT)
+                p.mask_out[(size_t)(m0 + e / MW) * p.ldmo + (n0 >> 5) + e % MW] = lmask[e];
+        }
+    } else {
+        uint32_t* lmask = reinterpret_cast<uint32_t*>(smem + NW * T::BYTES);
+        float* lu = reinterpret_cast<float*>(lmask + BM * MW);
+#pragma unroll
+        for (int q = 0; q < NTEpiPrefetch<BM, BN, NT, EPI>::M_PF; ++q) {
+            const int e = tid + NT * q;
+            if (e < BM * MW) lmask[e] = pf.mpf[q];
+        }
+        if (tid < BM) lu[tid] = pf.upf;
+        __syncthreads();
+        const float4 v4 = p.u ? *reinterpret_cast<const float4*>(p.v + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int cw = (wn0 + c4l) >> 5, sh = (wn0 + c4l) & 31;
+        write_tile_lds<TM, TN>(acc, wlds, [&](int rl, int c4, float4 v) {
+            const int lr = wm0 + rl;
+            const float u = lu[lr];
+            const uint32_t bits = lmask[lr * MW + cw] >> sh;
+            float4 x = make_float4(v.x + u * v4.x, v.y + u * v4.y, v.z + u * v4.z, v.w + u * v4.w);
+            x.x = (bits & 1u) ? x.x : 0.f;
+            x.y = (bits & 2u) ? x.y : 0.f;
+            x.z = (bits & 4u) ? x.z : 0.f;
+            x.w = (bits & 8u) ? x.w : 0.f;
+            *reinterpret_cast<float4*>(p.c + (size_t)(m0 + lr) * p.ldc + col) = x;
+        });
+    }
+}
+
+// TN epilogue through the LDS writer: float4 slab stores
+template <int TM, int TN>
+__device__ __forceinline__ void tn_store_lds(const TNArgs& p, f32x16 (&acc)[TM][TN], char* smem, int split, int o0,
+                                             int j0, int wm0, int wn0) {
+    using T = TileLds<TN>;
+    if (p.ablate & 1) {
+        tn_store(p, acc, split, o0, j0, wm0, wn0);
+        return;
+    }
+    float* slab = p.slab + (size_t)split * p.slab_stride;
+    float* wlds = reinterpret_cast<float*>(smem + (threadIdx.x >> 6) * T::BYTES);
+    write_tile_lds<TM, TN>(acc, wlds, [&](int rl, int c4, float4 v) {
+        *reinterpret_cast<float4*>(slab + (size_t)(o0 + wm0 + rl) * p.ldslab + p.col0 + j0 + wn0 + c4) = v;
+    });
+}
+
+// split-bf16 launchers (gemm_x6.hip); policy as nerf_gemm_set_policy
+int dispatch_nt_x6(const NTArgs& a, int epi, int policy, hipStream_t s, double flops);
+int dispatch_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, hipStream_t s, double flops);
+
+}  // namespace nerf

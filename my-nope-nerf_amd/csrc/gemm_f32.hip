@@ -17,11 +17,9 @@
 //    k-major: 16-B loads and ds_write_b128 into rows padded to BM+4 floats;
 //  * fused epilogues: +bias/ReLU (forward), rank-1 add + ReLU-mask (backward-data),
 //    split-K slab + bias-gradient column sums (backward-weight).
-#include "common.hpp"
+#include "gemm.hpp"
 
 namespace nerf {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int BK = 32;
 
@@ -66,40 +64,10 @@ __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const fl
     }
 }
 
-// accumulator register r of a 32x32 tile -> row offset inside the tile (gfx950 C/D map)
-__device__ __forceinline__ int acc_row(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
-
-template <int TM, int TN>
-__device__ __forceinline__ void zero_acc(f32x16 (&acc)[TM][TN]) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-}
-
 // ---------------------------------------------------------------------------
 // NT GEMM: C[m][n] = epi( sum_k A[m][k] B[n][k] ), A from up to two K segments.
 // WM x WN waves; each wave owns a (BM/WM) x (BN/WN) output tile of 32x32 MFMA blocks.
 // ---------------------------------------------------------------------------
-struct NTArgs {
-    const float* a1; int lda1; int k1;
-    const float* a2; int lda2; int k2;
-    const float* b;  int ldb;           // [n][k1+k2]
-    const float* bias;                  // fwd
-    const float* u;  const float* v;    // bwd-data rank-1 term u[m*ldu] v[n]
-    int ldu;
-    const uint32_t* mask; int ldmask;   // bwd-data ReLU mask bits [m][n/32] (bit = x > 0)
-    uint32_t* mask_out; int ldmo;       // fwd: write the ReLU mask bits of the output
-    float* c; int ldc;
-    int m, n;
-    int relu;
-    int ablate;   // diagnostics only (nerf_gemm_debug_ablate): 1 = no epilogue stores, 2 = no K-loop loads
-};
-
-enum { EPI_FWD = 0, EPI_BWD = 1 };
-
 template <int BM, int BN, int WM, int WN, int EPI>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(NTArgs p) {
     constexpr int NT = 64 * WM * WN;
@@ -108,8 +76,6 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(NTArgs p) {
     constexpr int LDA = BM + 1, LDB = BN + 1;     // odd strides: conflict-free transposing stores
     constexpr int A_F4 = BM * BK / 4 / NT;
     constexpr int B_F4 = BN * BK / 4 / NT;
-    constexpr int MW = BN / 32;                   // mask words per row of the tile
-    constexpr int M_PF = (BM * MW + NT - 1) / NT; // mask words prefetched per thread
     static_assert(A_F4 >= 1 && B_F4 >= 1 && TM >= 1 && TN >= 1, "bad tile");
 
     __shared__ __attribute__((aligned(16))) float smem[2 * BK * (LDA + LDB)];
@@ -166,20 +132,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(NTArgs p) {
     f32x16 acc[TM][TN];
     zero_acc(acc);
 
-    // backward epilogue operands (ReLU bits, rank-1 column) are prefetched with coalesced
-    // loads while the last K tile computes, then parked in LDS
-    uint32_t mpf[M_PF];
-    float upf = 0.f;
-    auto prefetch_epi = [&]() {
-        if (EPI != EPI_BWD) return;
-#pragma unroll
-        for (int q = 0; q < M_PF; ++q) {
-            const int e = tid + NT * q;
-            mpf[q] = (p.mask && e < BM * MW) ? p.mask[(size_t)(m0 + e / MW) * p.ldmask + (n0 >> 5) + e % MW]
-                                             : 0xffffffffu;
-        }
-        if (tid < BM) upf = p.u ? p.u[(size_t)(m0 + tid) * p.ldu] : 0.f;
-    };
+    NTEpiPrefetch<BM, BN, NT, EPI> pf;
 
     load_tile(0);
     store_tile(0);
@@ -187,89 +140,18 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(NTArgs p) {
     for (int kt = 0; kt < nkt; ++kt) {
         const int cur = kt & 1;
         if (kt + 1 < nkt) { if (!(p.ablate & 2)) load_tile(kt + 1); }
-        else prefetch_epi();
+        else pf.load(p, m0, n0);
         mfma_tile<TM, TN, LDA, LDB>(As(cur), Bs(cur), wm0, wn0, acc);
         if (kt + 1 < nkt) store_tile(cur ^ 1);
         __syncthreads();
     }
 
-    const int lane = lane_id();
-    const int l32 = lane & 31, hi = lane >> 5;
-    if (p.ablate & 1) {   // keep the accumulators live, store one value per thread
-        float t = 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) t += acc[i][j][r];
-        p.c[(size_t)(m0 + (tid & 127)) * p.ldc + n0 + (tid >> 7)] = t;
-        return;
-    }
-    if (EPI == EPI_FWD) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int col = n0 + wn0 + 32 * j + l32;
-            const int cword = (n0 + wn0 + 32 * j) >> 5;
-            const float bcol = p.bias ? p.bias[col] : 0.f;
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = m0 + wm0 + 32 * i + acc_row(r, hi);
-                    float x = acc[i][j][r] + bcol;
-                    if (p.relu) x = fmaxf(x, 0.f);
-                    p.c[(size_t)row * p.ldc + col] = x;
-                    if (p.mask_out) {
-                        // bits 0-31: the 32 columns of this register's row held by lanes 0-31,
-                        // bits 32-63: the row held by lanes 32-63
-                        const uint64_t bits = __ballot(x > 0.f);
-                        if (l32 == 0)
-                            p.mask_out[(size_t)row * p.ldmo + cword] = (uint32_t)(hi ? (bits >> 32) : bits);
-                    }
-                }
-        }
-    } else {
-        // park the prefetched operands in LDS (the staging buffers are free now)
-        uint32_t* lmask = reinterpret_cast<uint32_t*>(smem);
-        float* lu = smem + BM * MW;
-#pragma unroll
-        for (int q = 0; q < M_PF; ++q) {
-            const int e = tid + NT * q;
-            if (e < BM * MW) lmask[e] = mpf[q];
-        }
-        if (tid < BM) lu[tid] = upf;
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int col = n0 + wn0 + 32 * j + l32;
-            const int cw = (wn0 + 32 * j) >> 5;
-            const float vcol = p.u ? p.v[col] : 0.f;
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int lr = wm0 + 32 * i + acc_row(r, hi);
-                    float x = acc[i][j][r] + lu[lr] * vcol;
-                    x = ((lmask[lr * MW + cw] >> l32) & 1u) ? x : 0.f;
-                    p.c[(size_t)(m0 + lr) * p.ldc + col] = x;
-                }
-        }
-    }
+    nt_epilogue<BM, BN, NT, TM, TN, EPI>(p, acc, smem, m0, n0, wm0, wn0, pf);
 }
 
 // ---------------------------------------------------------------------------
 // TN GEMM (weight gradient): slab[split][o][col0+j] = sum_s dy[s][o] x[s][j]
 // ---------------------------------------------------------------------------
-struct TNArgs {
-    const float* dy; int lddy;   // A[m=o][k=s] = dy[s][o]
-    const float* x;  int ldx;    // B[k=s][n=j] = x[s][j]
-    int rows_per_split;
-    float* slab; int ldslab; int col0; size_t slab_stride;
-    float* bslab; int nout;
-    int ablate;   // diagnostics: 1 = no slab stores, 2 = no K-loop loads, 4 = no bias column sums
-};
-
 template <int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_tn(TNArgs p) {
     constexpr int NT = 64 * WM * WN;
@@ -349,31 +231,8 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_tn(TNArgs p) {
         __syncthreads();
     }
 
-    float* slab = p.slab + (size_t)split * p.slab_stride;
-    const int lane = lane_id();
-    const int l32 = lane & 31, hi = lane >> 5;
-    if (p.ablate & 1) {
-        float t = 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) t += acc[i][j][r];
-        slab[tid] = t;
-        return;
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int o = o0 + wm0 + 32 * i + acc_row(r, hi);
-                const int c = p.col0 + j0 + wn0 + 32 * j + l32;
-                slab[(size_t)o * p.ldslab + c] = acc[i][j][r];
-            }
-    if (do_bias && tid < BM) p.bslab[(size_t)split * p.nout + o0 + tid] = bsum;
+    tn_store(p, acc, split, o0, j0, wm0, wn0);
+    if (do_bias && tid < BM && !(p.ablate & 1)) p.bslab[(size_t)split * p.nout + o0 + tid] = bsum;
 }
 
 // sum split-K slabs into the reference-layout gradient: one thread per output element,
@@ -416,6 +275,7 @@ __global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ s
 using namespace nerf;
 
 static int g_ablate = 0;   // nerf_gemm_debug_ablate
+static unsigned long long* g_stamps = nullptr;   // nerf_gemm_debug_stamps
 
 template <int BM, int BN, int WM, int WN, int EPI>
 static int launch_nt(const NTArgs& a, hipStream_t s, double flops) {
@@ -433,9 +293,18 @@ static int launch_nt(const NTArgs& a, hipStream_t s, double flops) {
 static int g_nt_policy = 0;
 static int g_tn_policy = 0;
 
+// f32 arithmetic (nerf_gemm_set_precision): 0 = exact-f32 MFMA, 1 = split-bf16 emulation
+static int g_precision = 0;
+
 template <int EPI>
 static int dispatch_nt(const NTArgs& a, hipStream_t s, double flops) {
     const int pol = g_nt_policy ? g_nt_policy : 3;
+    if (g_precision == 1 && a.bs != nullptr) {   // the split path needs the weight image
+        NTArgs b = a;
+        b.ablate = g_ablate;
+        b.stamps = g_stamps;
+        return dispatch_nt_x6(b, EPI, pol, s, flops);
+    }
     if (pol == 3 && a.m % 256 == 0 && a.n % 256 == 0) return launch_nt<256, 256, 2, 4, EPI>(a, s, flops);
     if (pol >= 2 && a.n % 256 == 0) return launch_nt<128, 256, 2, 4, EPI>(a, s, flops);
     if (a.n % 128 == 0) return launch_nt<128, 128, 2, 2, EPI>(a, s, flops);
@@ -455,16 +324,20 @@ static int check_nt(const NTArgs& a, const char* fn) {
                "%s: leading dimension smaller than K", fn);
     NERF_CHECK((((uintptr_t)a.a1 | (uintptr_t)a.b | (uintptr_t)(a.a2 ? a.a2 : a.a1)) & 15u) == 0,
                "%s: operands must be 16-byte aligned", fn);
+    NERF_CHECK(a.bs == nullptr || ((((uintptr_t)a.bs) & 15u) == 0 && a.bs_rows >= a.n),
+               "%s: split weight image must be 16-byte aligned with at least n rows", fn);
     return NERF_OK;
 }
 
 extern "C" int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2, int k2,
-                               const float* w, const float* bias, float* y, int ldy, int m, int n,
-                               int relu, uint32_t* mask_out, int ldmo, void* stream) {
+                               const float* w, const uint16_t* w_split, int w_split_rows, const float* bias,
+                               float* y, int ldy, int m, int n, int relu, uint32_t* mask_out, int ldmo,
+                               void* stream) {
     NTArgs a{};
     a.a1 = x1; a.lda1 = ldx1; a.k1 = k1;
     a.a2 = x2; a.lda2 = x2 ? ldx2 : 0; a.k2 = x2 ? k2 : 0;
     a.b = w; a.ldb = k1 + a.k2;
+    a.bs = w_split; a.bs_rows = w_split_rows;
     a.bias = bias; a.c = y; a.ldc = ldy; a.m = m; a.n = n; a.relu = relu;
     a.mask_out = mask_out; a.ldmo = ldmo;
     int rc = check_nt(a, __func__);
@@ -475,12 +348,14 @@ extern "C" int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x
 }
 
 extern "C" int nerf_linear_bwd_data(const float* dy, int lddy, int k, const float* wt,
-                                    const float* u, int ldu, const float* v, const uint32_t* mask,
-                                    int ldmask, float* dx, int lddx, int m, int n, void* stream) {
+                                    const uint16_t* wt_split, int wt_split_rows, const float* u, int ldu,
+                                    const float* v, const uint32_t* mask, int ldmask, float* dx, int lddx,
+                                    int m, int n, void* stream) {
     NTArgs a{};
     a.a1 = dy; a.lda1 = lddy; a.k1 = k;
     a.a2 = nullptr; a.lda2 = 0; a.k2 = 0;
     a.b = wt; a.ldb = k;
+    a.bs = wt_split; a.bs_rows = wt_split_rows;
     a.u = u; a.ldu = ldu; a.v = v; a.mask = mask; a.ldmask = ldmask;
     a.c = dx; a.ldc = lddx; a.m = m; a.n = n;
     int rc = check_nt(a, __func__);
@@ -512,8 +387,9 @@ extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const
     a.ablate = g_ablate >> 4;
     hipStream_t s = as_stream(stream);
     const double fl = 2.0 * m * nout * (double)kin;
-    prof_begin(s);
     const int pol = g_tn_policy ? g_tn_policy : 3;
+    if (g_precision == 1) return dispatch_tn_x6(a, nout, kin, splits, pol, s, fl);
+    prof_begin(s);
     if (pol == 3 && nout % 256 == 0 && kin % 256 == 0) {
         dim3 grid(nout / 256, kin / 256, splits);
         hipLaunchKernelGGL((k_gemm_tn<256, 256, 2, 4>), grid, dim3(512), 0, s, a);
@@ -567,6 +443,21 @@ extern "C" int nerf_linear_bwd_weight_splits(int nout, int kin, int m) {
     int splits = 1;
     while (splits * 2 * tiles <= target && m % (splits * 2 * BK) == 0 && m / (splits * 2) >= 256) splits *= 2;
     return splits;
+}
+
+extern "C" int nerf_gemm_set_precision(int mode) {
+    NERF_CHECK(mode == 0 || mode == 1, "%s: mode must be 0 (f32 MFMA) or 1 (split-bf16)", __func__);
+    g_precision = mode;
+    return NERF_OK;
+}
+
+extern "C" int nerf_gemm_get_precision(void) { return g_precision; }
+
+// diagnostics: per-block phase clocks of the split-bf16 NT kernel into a device buffer
+// of grid * 4 * 2 uint64 (NULL switches it off); not for production
+extern "C" int nerf_gemm_debug_stamps(void* buf) {
+    g_stamps = reinterpret_cast<unsigned long long*>(buf);
+    return NERF_OK;
 }
 
 // diagnostics: ablate parts of the NT GEMM (results are wrong while set); not for production

@@ -1,0 +1,570 @@
+// f32 GEMMs of the field MLP emulated on the bf16 matrix cores (gfx950).
+//
+// Same launches, arguments and epilogues as gemm_f32.hip (forward, backward-data,
+// backward-weight of OfficialStaticNerf's linears, official_nerf.py:60-96), different
+// K loop:
+//  * every f32 operand x is split while it is staged into LDS into three bf16 words,
+//    x = hi + mid + lo, each the round-to-nearest-even bf16 of what the previous words
+//    leave (8 + 8 + 8 significand bits: exact for normal f32 x);
+//  * a.b = sum over the six cross products whose magnitude is >= 2^-16 |a||b| (hi.hi,
+//    hi.mid, mid.hi, hi.lo, mid.mid, lo.hi), issued smallest first into ONE f32
+//    accumulator with v_mfma_f32_32x32x16_bf16; the dropped ones (mid.lo, lo.mid, lo.lo)
+//    are <= 2^-26 |a||b| each, below the f32 rounding of the sum.  Per product this is
+//    within ~2^-24 of the exact-f32 v_mfma_f32_32x32x2_f32 result, at 6/16 of its cost:
+//    1024 FLOP/clk/SIMD bf16 vs 64 FLOP/clk/SIMD f32.
+//  * LDS images per operand and buffer: 3 planes (hi/mid/lo) x 2 k-halves of
+//    [row][8 bf16]; a lane's MFMA fragment (row r, k = 8h..8h+7) is one ds_read_b128,
+//    and the half images are offset by 128 B so a wave's staging ds_write_b64 covers
+//    all 64 banks.  K tile = 16 (one MFMA K step), double-buffered: ~99 KB at 256x256.
+//  * K-contiguous operands ([m][k], [n][k]) load as float4 along k; sample-major ones
+//    (dy[s][o], x[s][j]) load as 8-row column strips so each thread owns 8 consecutive
+//    k of one column and writes its fragment chunk with one ds_write_b128 per plane.
+#include "gemm.hpp"
+
+namespace nerf {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int XK = 16;   // K per LDS tile
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+    f32x2 v = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));   // v_cvt_pk_bf16_f32 (RNE)
+}
+
+// (a, b) -> packed bf16 pairs hi, mid, lo with a = hi.x + mid.x + lo.x (same for b)
+__device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
+    h = pk_bf16(a, b);
+    const float ra = a - __uint_as_float(h << 16);
+    const float rb = b - __uint_as_float(h & 0xffff0000u);
+    m = pk_bf16(ra, rb);
+    l = pk_bf16(ra - __uint_as_float(m << 16), rb - __uint_as_float(m & 0xffff0000u));
+}
+
+// bytes of one k-half image of ROWS rows (+128 B bank offset between the halves)
+template <int ROWS>
+struct XImg {
+    static constexpr int HALF = ROWS * 16 + 128;
+    static constexpr int PLANE = 2 * HALF;
+    static constexpr int BYTES = 3 * PLANE;
+};
+
+__device__ __forceinline__ f32x16 mfma_bf16(const uint4& a, const uint4& b, const f32x16& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+}
+
+// float4 along k at (row, k = 4q) -> the three planes' 8-byte pieces of that row's chunk
+template <int ROWS>
+__device__ __forceinline__ void put_row4(char* img, int row, int q, float4 v) {
+    using I = XImg<ROWS>;
+    uint32_t h0, m0, l0, h1, m1, l1;
+    split2(v.x, v.y, h0, m0, l0);
+    split2(v.z, v.w, h1, m1, l1);
+    char* d = img + (q >> 1) * I::HALF + row * 16 + (q & 1) * 8;
+    *reinterpret_cast<uint2*>(d) = make_uint2(h0, h1);
+    *reinterpret_cast<uint2*>(d + I::PLANE) = make_uint2(m0, m1);
+    *reinterpret_cast<uint2*>(d + 2 * I::PLANE) = make_uint2(l0, l1);
+}
+
+// 8 consecutive k of column c (k-half g) -> one 16-byte chunk per plane
+template <int ROWS>
+__device__ __forceinline__ void put_col8(char* img, int c, int g, const float (&v)[8]) {
+    using I = XImg<ROWS>;
+    uint32_t h[4], m[4], l[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) split2(v[2 * t], v[2 * t + 1], h[t], m[t], l[t]);
+    char* d = img + g * I::HALF + c * 16;
+    *reinterpret_cast<uint4*>(d) = make_uint4(h[0], h[1], h[2], h[3]);
+    *reinterpret_cast<uint4*>(d + I::PLANE) = make_uint4(m[0], m[1], m[2], m[3]);
+    *reinterpret_cast<uint4*>(d + 2 * I::PLANE) = make_uint4(l[0], l[1], l[2], l[3]);
+}
+
+// ---------------------------------------------------------------------------
+// Main loop shared by the NT and TN kernels (one wave per SIMD, accumulators in AGPRs).
+//
+// 16-deep K tiles alternate between two split-image LDS buffers.  Iteration kt reads
+// the B fragments of tile kt (all TN) and its A fragments one 32-row tile ahead from
+// buffer kt&1 and issues the MFMAs; beside them the stager
+//   issue_early(kt)  starts asynchronous copies at the top of the iteration;
+//   split(kt)        puts tile kt+1 into buffer (kt+1)&1 -- interleaved with row tile
+//                    0's MFMAs (<= 3 VALU per 32-cycle MFMA gap);
+//   issue(kt)        starts the register loads its later iterations need;
+//   before_barrier() waits for whatever the barrier publishes;
+// then one barrier.  Stager::prologue leaves tile 0 in buffer 0.
+// ---------------------------------------------------------------------------
+template <int TM, int TN, int BM, int BN, typename Stager>
+__device__ __forceinline__ void x6_mainloop(char* smem, int nkt, int wm0, int wn0, f32x16 (&acc)[TM][TN],
+                                            Stager& st, unsigned long long* stamps = nullptr) {
+    using IA = XImg<BM>;
+    using IB = XImg<BN>;
+    constexpr int BUF = IA::BYTES + IB::BYTES;
+    const int lane = lane_id();
+    const int l32 = lane & 31, hi = lane >> 5;
+    const int aoff = hi * IA::HALF + (wm0 + l32) * 16;
+    const int boff = IA::BYTES + hi * IB::HALF + (wn0 + l32) * 16;
+    auto rd = [&](const char* q, int plane, uint4 (&f)[3]) {
+        f[0] = *reinterpret_cast<const uint4*>(q);
+        f[1] = *reinterpret_cast<const uint4*>(q + plane);
+        f[2] = *reinterpret_cast<const uint4*>(q + 2 * plane);
+    };
+    auto mm = [&](int i, const uint4 (&a)[3], const uint4 (&b)[TN][3]) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            f32x16 c = acc[i][j];
+            c = mfma_bf16(a[1], b[j][1], c);   // mid.mid
+            c = mfma_bf16(a[0], b[j][2], c);   // hi.lo
+            c = mfma_bf16(a[2], b[j][0], c);   // lo.hi
+            c = mfma_bf16(a[0], b[j][1], c);   // hi.mid
+            c = mfma_bf16(a[1], b[j][0], c);   // mid.hi
+            c = mfma_bf16(a[0], b[j][0], c);   // hi.hi
+            acc[i][j] = c;
+        }
+    };
+
+    st.prologue(smem, nkt);
+    stamp(stamps, 1);
+    for (int kt = 0; kt < nkt; ++kt) {
+        const char* cur = smem + (kt & 1) * BUF;
+        char* wimg = smem + ((kt + 1) & 1) * BUF;
+        uint4 b[TN][3], a0[3], a1[3];
+        st.issue_early(kt, nkt, wimg + IA::BYTES);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) rd(cur + boff + 32 * 16 * j, IB::PLANE, b[j]);
+        rd(cur + aoff, IA::PLANE, a0);
+        if (TM > 1) rd(cur + aoff + 32 * 16, IA::PLANE, a1);
+        st.split(kt, nkt, wimg, wimg + IA::BYTES);
+        mm(0, a0, b);
+#pragma unroll
+        for (int q = 0; q < 6 * TN; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        st.issue(kt, nkt, wimg + IA::BYTES);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 1; i < TM; ++i) {
+            uint4 (&ac)[3] = (i & 1) ? a1 : a0;
+            uint4 (&an)[3] = (i & 1) ? a0 : a1;
+            if (i + 1 < TM) rd(cur + aoff + 32 * 16 * (i + 1), IA::PLANE, an);
+            mm(i, ac, b);
+        }
+        st.before_barrier();
+        __syncthreads();
+    }
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// 16 bytes per lane global -> LDS (global_load_lds_dwordx4): lane l lands at
+// lds_wave_base + 16 l; the base must be wave-uniform.  Issued from inline asm so the
+// compiler does not treat the in-flight DMA as a pending write of every later ds_read
+// (it would drain it with vmcnt(0) at the next fragment read); the stager waits for
+// its DMAs itself (dma_wait) before the barrier that publishes them.
+__device__ __forceinline__ void dma16(const void* gsrc, char* lds_wave_base) {
+    const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t*)lds_wave_base);
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(l) : "memory", "m0");
+}
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// ---------------------------------------------------------------------------
+// Main loop of the NT kernel, with every fragment double-buffered in registers.
+//
+// Iteration kt: the fragments of tile kt are in registers (set `fc`); the MFMAs run on
+// them while the fragments of tile kt+1 are read from image buffer (kt+1)&1 (set `fn`),
+// so no wave waits on LDS after a barrier.  Image buffer kt&1 -- whose fragments were
+// read into registers during iteration kt-1 -- receives tile kt+2: its B part by
+// LDS-DMA, its A part split from the raw ring, interleaved with the first MFMAs.  The
+// raw ring slot freed by that split (its tile went through iteration kt-1's split)
+// is refilled with raw A of tile kt+3.  Every DMA lands before the iteration's barrier.
+// ---------------------------------------------------------------------------
+template <int TM, int TN, int BM, int BN, typename Stager>
+__device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int wn0, f32x16 (&acc)[TM][TN],
+                                               Stager& st, unsigned long long* stamps = nullptr) {
+    using IA = XImg<BM>;
+    using IB = XImg<BN>;
+    constexpr int BUF = IA::BYTES + IB::BYTES;
+    const int lane = lane_id();
+    const int l32 = lane & 31, hi = lane >> 5;
+    const int aoff = hi * IA::HALF + (wm0 + l32) * 16;
+    const int boff = IA::BYTES + hi * IB::HALF + (wn0 + l32) * 16;
+    auto rd = [&](const char* q, int plane, uint4 (&f)[3]) {
+        f[0] = *reinterpret_cast<const uint4*>(q);
+        f[1] = *reinterpret_cast<const uint4*>(q + plane);
+        f[2] = *reinterpret_cast<const uint4*>(q + 2 * plane);
+    };
+    auto rd_all = [&](const char* buf, uint4 (&a)[TM][3], uint4 (&b)[TN][3]) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) rd(buf + boff + 32 * 16 * j, IB::PLANE, b[j]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) rd(buf + aoff + 32 * 16 * i, IA::PLANE, a[i]);
+    };
+    auto mm = [&](int i, const uint4 (&a)[3], const uint4 (&b)[TN][3]) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            f32x16 c = acc[i][j];
+            c = mfma_bf16(a[1], b[j][1], c);   // mid.mid
+            c = mfma_bf16(a[0], b[j][2], c);   // hi.lo
+            c = mfma_bf16(a[2], b[j][0], c);   // lo.hi
+            c = mfma_bf16(a[0], b[j][1], c);   // hi.mid
+            c = mfma_bf16(a[1], b[j][0], c);   // mid.hi
+            c = mfma_bf16(a[0], b[j][0], c);   // hi.hi
+            acc[i][j] = c;
+        }
+    };
+    uint4 aX[TM][3], bX[TN][3], aY[TM][3], bY[TN][3];
+
+    st.prologue2(smem, nkt);        // tiles 0, 1 in image buffers 0, 1; raw tile 2 in slot 0
+    rd_all(smem, aX, bX);
+    __syncthreads();                // buffer 0 is restaged in iteration 0
+    stamp(stamps, 1);
+
+    auto iter = [&](int kt, uint4 (&ac)[TM][3], uint4 (&bc)[TN][3], uint4 (&an)[TM][3], uint4 (&bn)[TN][3]) {
+        char* wimg = smem + (kt & 1) * BUF;
+        const char* nbuf = smem + ((kt + 1) & 1) * BUF;
+        constexpr int H = (TM + 1) / 2;
+        st.issue2(kt, nkt, wimg + IA::BYTES);
+        // next tile's B fragments and first half of its A fragments now; the second half
+        // after the first half of this tile's MFMAs retired their A registers
+#pragma unroll
+        for (int j = 0; j < TN; ++j) rd(nbuf + boff + 32 * 16 * j, IB::PLANE, bn[j]);
+#pragma unroll
+        for (int i = 0; i < H; ++i) rd(nbuf + aoff + 32 * 16 * i, IA::PLANE, an[i]);
+        st.split2(kt, nkt, wimg);
+        mm(0, ac[0], bc);
+#pragma unroll
+        for (int q = 0; q < 6 * TN; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 1; i < H; ++i) mm(i, ac[i], bc);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = H; i < TM; ++i) rd(nbuf + aoff + 32 * 16 * i, IA::PLANE, an[i]);
+#pragma unroll
+        for (int i = H; i < TM; ++i) mm(i, ac[i], bc);
+        st.before_barrier();
+        __syncthreads();
+    };
+    for (int kt = 0; kt < nkt; kt += 2) {
+        iter(kt, aX, bX, aY, bY);
+        iter(kt + 1, aY, bY, aX, bX);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// NT: C[m][n] = epi( sum_k A[m][k] B[n][k] ).
+// A (activations, f32 [m][k]): LDS-DMA into a 2-slot raw ring, 16-B per lane (a wave
+// moves 16 rows x 64 B), split from there.  B: the pre-split weight image (p.bs),
+// LDS-DMA'd straight into the image buffer.  No staging registers.
+// ---------------------------------------------------------------------------
+template <int BM, int BN, int NT>
+struct NTStager {
+    static constexpr int A_F4 = BM * XK / 4 / NT;   // raw A float4 per thread and tile
+    static constexpr int RSTEP = NT / 4;            // rows per pass of the block
+    static constexpr int B_CH = 6 * BN;             // 16-B chunks of a tile's B image
+    static constexpr int B_C = (B_CH + NT - 1) / NT;
+    static constexpr int RAW = BM * XK * 4;         // bytes of one raw A slot
+    static_assert(A_F4 >= 1 && BN % 64 == 0, "bad tile");
+    const float* a1b; const float* a2b; const uint16_t* bsb;
+    int lda1, lda2, k1, bs_rows;
+    int r0, q0;
+    char* raw;
+
+    __device__ __forceinline__ void init(const NTArgs& p, int m0, int n0, char* raw_ring) {
+        lda1 = p.lda1; lda2 = p.lda2; k1 = p.k1; bs_rows = p.bs_rows;
+        a1b = p.a1 + (size_t)m0 * lda1;
+        a2b = p.a2 ? p.a2 + (size_t)m0 * lda2 : p.a1;
+        bsb = p.bs + (size_t)n0 * 8;
+        r0 = threadIdx.x >> 2; q0 = threadIdx.x & 3;
+        raw = raw_ring;
+    }
+    __device__ __forceinline__ void dma_a(int kt, int slot) {
+        const int kk = kt * XK;
+        const bool seg1 = kk < k1;
+        const float* abase = seg1 ? a1b + kk : a2b + (kk - k1);
+        const int lda = seg1 ? lda1 : lda2;
+        const int wrow = (threadIdx.x >> 6) * 16;   // first row of this wave's lanes
+#pragma unroll
+        for (int i = 0; i < A_F4; ++i)
+            dma16(abase + (size_t)(r0 + i * RSTEP) * lda + 4 * q0, raw + slot * RAW + (wrow + i * RSTEP) * 64);
+    }
+    __device__ __forceinline__ void dma_b(int kt, char* Bimg) {
+        const uint16_t* bt = bsb + (size_t)kt * 16 * bs_rows;
+        const int lane = threadIdx.x & 63;
+#pragma unroll
+        for (int i = 0; i < B_C; ++i) {
+            const int idx = threadIdx.x + NT * i;
+            if (B_C * NT != B_CH && (int)(threadIdx.x & ~63) + NT * i >= B_CH) break;   // wave-uniform
+            const int n = idx % BN, pk = idx / BN;
+            dma16(bt + (((size_t)(pk >> 1) * Kc + (pk & 1)) * bs_rows + n) * 8,
+                  Bimg + (pk >> 1) * XImg<BN>::PLANE + (pk & 1) * XImg<BN>::HALF + (n - lane) * 16);
+        }
+    }
+    int Kc = 0;   // K / 8: 8-k chunks per plane of the B image
+    __device__ __forceinline__ void split_slot(int slot, char* Aimg) {
+#pragma unroll
+        for (int i = 0; i < A_F4; ++i) {
+            const int row = r0 + i * RSTEP;
+            const float4 v = *reinterpret_cast<const float4*>(raw + slot * RAW + row * 64 + q0 * 16);
+            put_row4<BM>(Aimg, row, q0, v);
+        }
+    }
+    // tile 0 in image buffer 0 (A split, B DMA), raw tile 1 in slot 1
+    __device__ __forceinline__ void prologue(char* smem, int nkt) {
+        dma_a(0, 0);
+        dma_b(0, smem + XImg<BM>::BYTES);
+        dma_a(nkt > 1 ? 1 : 0, 1);
+        dma_wait();
+        __syncthreads();
+        split_slot(0, smem);
+        __syncthreads();
+    }
+    // iteration kt: split raw tile kt+1 (slot (kt+1)&1) into the other image buffer
+    __device__ __forceinline__ void split(int kt, int nkt, char* Aimg, char*) {
+        split_slot((kt + 1) & 1, Aimg);
+    }
+    // iteration kt: B image of tile kt+1 into the other buffer, raw A of tile kt+2 into
+    // slot kt&1 (split in iteration kt+1); both land before this iteration's barrier
+    __device__ __forceinline__ void issue_early(int kt, int nkt, char* Bimg) {
+        dma_b(kt + 1 < nkt ? kt + 1 : nkt - 1, Bimg);
+        dma_a(kt + 2 < nkt ? kt + 2 : nkt - 1, kt & 1);
+    }
+    __device__ __forceinline__ void issue(int, int, char*) {}
+    __device__ __forceinline__ void before_barrier() { dma_wait(); }
+
+    // --- x6_mainloop_pf protocol
+    __device__ __forceinline__ void prologue2(char* smem, int nkt) {
+        constexpr int BUF = XImg<BM>::BYTES + XImg<BN>::BYTES;
+        const int t1 = nkt > 1 ? 1 : 0, t2 = nkt > 2 ? 2 : nkt - 1;
+        dma_a(0, 0);
+        dma_b(0, smem + XImg<BM>::BYTES);
+        dma_a(t1, 1);
+        dma_b(t1, smem + BUF + XImg<BM>::BYTES);
+        dma_wait();
+        __syncthreads();
+        split_slot(0, smem);
+        split_slot(1, smem + BUF);
+        __syncthreads();            // raw slot 0 is refilled below
+        dma_a(t2, 0);
+        dma_wait();
+        __syncthreads();
+    }
+    // iteration kt: B image of tile kt+2 into buffer kt&1, raw A of tile kt+3 into slot (kt+1)&1
+    __device__ __forceinline__ void issue2(int kt, int nkt, char* Bimg) {
+        dma_b(kt + 2 < nkt ? kt + 2 : nkt - 1, Bimg);
+        dma_a(kt + 3 < nkt ? kt + 3 : nkt - 1, (kt + 1) & 1);
+    }
+    // iteration kt: raw A of tile kt+2 (slot kt&1) into buffer kt&1
+    __device__ __forceinline__ void split2(int kt, int, char* Aimg) { split_slot(kt & 1, Aimg); }
+};
+
+template <int BM, int BN, int WM, int WN, int EPI>
+__global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt_x6(NTArgs p) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int WTM = BM / WM, WTN = BN / WN;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int BUF = XImg<BM>::BYTES + XImg<BN>::BYTES;
+    using St = NTStager<BM, BN, NT>;
+    static_assert(TM >= 1 && TN >= 1, "bad tile");
+
+    constexpr int LOOP_BYTES = 2 * BUF + 2 * St::RAW;
+    constexpr int EPI_BYTES = (NT / 64) * TileLds<TN>::BYTES + (BM * (BN / 32) + BM) * 4;
+    __shared__ __attribute__((aligned(16))) char smem[LOOP_BYTES > EPI_BYTES ? LOOP_BYTES : EPI_BYTES];
+    const int wave = threadIdx.x >> 6;
+    const int wm0 = (wave / WN) * WTM;
+    const int wn0 = (wave % WN) * WTN;
+    const int m0 = blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const int K = p.k1 + p.k2;
+
+    stamp(p.stamps, 0);
+    St st;
+    st.init(p, m0, n0, smem + 2 * BUF);
+    st.Kc = K / 8;
+    NTEpiPrefetch<BM, BN, NT, EPI> pf;
+    pf.load(p, m0, n0);
+    f32x16 acc[TM][TN];
+    zero_acc(acc);
+    x6_mainloop_pf<TM, TN, BM, BN>(smem, K / XK, wm0, wn0, acc, st, p.stamps);
+    stamp(p.stamps, 2);
+    nt_epilogue_lds<BM, BN, NT, TM, TN, EPI>(p, acc, smem, m0, n0, wm0, wn0, pf);
+    if (p.stamps) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stamp(p.stamps, 3);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// TN (weight gradient): slab[split][o][col0+j] = sum_s dy[s][o] x[s][j].  Both operands
+// are sample-major: 8-row column strips, split in the kernel; the bias gradient (column
+// sums of dy) is accumulated from the same registers.
+// ---------------------------------------------------------------------------
+template <int BM, int BN, int NT>
+struct TNStager {
+    static constexpr int SA = (2 * BM + NT - 1) / NT;
+    static constexpr int SB = (2 * BN + NT - 1) / NT;
+    const float* dyb; const float* xb;
+    int lddy, ldx;
+    int offa[SA], offb[SB];
+    float va[SA][8], vb[SB][8];
+    float bsum[SA];
+    bool do_bias;
+    __device__ __forceinline__ bool a_ok(int i) const { return SA * NT == 2 * BM || (int)threadIdx.x + NT * i < 2 * BM; }
+    __device__ __forceinline__ bool b_ok(int i) const { return SB * NT == 2 * BN || (int)threadIdx.x + NT * i < 2 * BN; }
+
+    __device__ __forceinline__ void init(const TNArgs& p, size_t s0, int o0, int j0, bool bias) {
+        lddy = p.lddy; ldx = p.ldx;
+        dyb = p.dy + s0 * lddy + o0;
+        xb = p.x + s0 * ldx + j0;
+#pragma unroll
+        for (int i = 0; i < SA; ++i) {
+            const int idx = threadIdx.x + NT * i;
+            offa[i] = 8 * (idx / BM) * lddy + idx % BM;
+            bsum[i] = 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < SB; ++i) {
+            const int idx = threadIdx.x + NT * i;
+            offb[i] = 8 * (idx / BN) * ldx + idx % BN;
+        }
+        do_bias = bias;
+    }
+    __device__ __forceinline__ void load(int kt) {
+        const float* da = dyb + (size_t)kt * XK * lddy;
+        const float* db = xb + (size_t)kt * XK * ldx;
+#pragma unroll
+        for (int i = 0; i < SA; ++i)
+            if (a_ok(i)) {
+#pragma unroll
+                for (int t = 0; t < 8; ++t) va[i][t] = da[offa[i] + t * lddy];
+            }
+#pragma unroll
+        for (int i = 0; i < SB; ++i)
+            if (b_ok(i)) {
+#pragma unroll
+                for (int t = 0; t < 8; ++t) vb[i][t] = db[offb[i] + t * ldx];
+            }
+    }
+    // bias sums are taken here, once per real tile (`count` false for the clamped
+    // re-stage of the last tile at the end of the main loop)
+    __device__ __forceinline__ void put(char* Aimg, char* Bimg, bool count) {
+#pragma unroll
+        for (int i = 0; i < SA; ++i)
+            if (a_ok(i)) {
+                const int idx = threadIdx.x + NT * i;
+                put_col8<BM>(Aimg, idx % BM, idx / BM, va[i]);
+                if (do_bias && count) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) s += va[i][t];
+                    bsum[i] += s;
+                }
+            }
+#pragma unroll
+        for (int i = 0; i < SB; ++i)
+            if (b_ok(i)) {
+                const int idx = threadIdx.x + NT * i;
+                put_col8<BN>(Bimg, idx % BN, idx / BN, vb[i]);
+            }
+    }
+    // register pipeline: tile 0 in image buffer 0, raw tile 1 in registers
+    __device__ __forceinline__ void prologue(char* smem, int nkt) {
+        load(0);
+        put(smem, smem + XImg<BM>::BYTES, true);
+        load(nkt > 1 ? 1 : 0);
+        __syncthreads();
+    }
+    __device__ __forceinline__ void split(int kt, int nkt, char* Aimg, char* Bimg) {
+        put(Aimg, Bimg, kt + 1 < nkt);
+    }
+    __device__ __forceinline__ void issue_early(int, int, char*) {}
+    __device__ __forceinline__ void issue(int kt, int nkt, char*) { load(kt + 2 < nkt ? kt + 2 : nkt - 1); }
+    __device__ __forceinline__ void before_barrier() {}
+};
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void k_gemm_tn_x6(TNArgs p) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int WTM = BM / WM, WTN = BN / WN;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int BUF = XImg<BM>::BYTES + XImg<BN>::BYTES;
+    static_assert(TM >= 1 && TN >= 1, "bad tile");
+    static_assert(2 * BUF >= 2 * BM * 4, "bias scratch");
+
+    constexpr int LOOP_BYTES = 2 * BUF;
+    constexpr int EPI_BYTES = (NT / 64) * TileLds<TN>::BYTES;
+    __shared__ __attribute__((aligned(16))) char smem[LOOP_BYTES > EPI_BYTES ? LOOP_BYTES : EPI_BYTES];
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int wm0 = (wave / WN) * WTM;
+    const int wn0 = (wave % WN) * WTN;
+    const int o0 = blockIdx.x * BM;
+    const int j0 = blockIdx.y * BN;
+    const int split = blockIdx.z;
+    const size_t s0 = (size_t)split * p.rows_per_split;
+    const int nkt = p.rows_per_split / XK;
+    const bool do_bias = (p.bslab != nullptr) && (blockIdx.y == 0) && !(p.ablate & 4);
+
+    TNStager<BM, BN, NT> st;
+    st.init(p, s0, o0, j0, do_bias);
+    f32x16 acc[TM][TN];
+    zero_acc(acc);
+    x6_mainloop<TM, TN, BM, BN>(smem, nkt, wm0, wn0, acc, st);
+
+    tn_store_lds(p, acc, smem, split, o0, j0, wm0, wn0);
+    if (do_bias && !(p.ablate & 1)) {
+        // strip (c, g) partial sums -> column sums, added in g order (deterministic)
+        __syncthreads();
+        float* lb = reinterpret_cast<float*>(smem);
+#pragma unroll
+        for (int i = 0; i < TNStager<BM, BN, NT>::SA; ++i)
+            if (st.a_ok(i)) lb[tid + NT * i] = st.bsum[i];
+        __syncthreads();
+        for (int c = tid; c < BM; c += NT) p.bslab[(size_t)split * p.nout + o0 + c] = lb[c] + lb[BM + c];
+    }
+}
+
+template <int BM, int BN, int WM, int WN, int EPI>
+static void launch_nt_x6(const NTArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL((k_gemm_nt_x6<BM, BN, WM, WN, EPI>), dim3(a.m / BM, a.n / BN), dim3(64 * WM * WN), 0, s, a);
+}
+
+template <int EPI>
+static void pick_nt_x6(const NTArgs& a, int pol, hipStream_t s) {
+    if (pol == 3 && a.m % 256 == 0 && a.n % 256 == 0) launch_nt_x6<256, 256, 2, 2, EPI>(a, s);
+    else if (pol >= 2 && a.n % 256 == 0) launch_nt_x6<128, 256, 2, 2, EPI>(a, s);
+    else if (a.n % 128 == 0) launch_nt_x6<128, 128, 2, 2, EPI>(a, s);
+    else launch_nt_x6<128, 64, 2, 2, EPI>(a, s);
+}
+
+int dispatch_nt_x6(const NTArgs& a, int epi, int policy, hipStream_t s, double flops) {
+    prof_begin(s);
+    if (epi == EPI_FWD) pick_nt_x6<EPI_FWD>(a, policy, s);
+    else pick_nt_x6<EPI_BWD>(a, policy, s);
+    prof_end(s, flops);
+    return check_launch("k_gemm_nt_x6");
+}
+
+int dispatch_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, hipStream_t s, double flops) {
+    prof_begin(s);
+    if (policy == 3 && nout % 256 == 0 && kin % 256 == 0)
+        hipLaunchKernelGGL((k_gemm_tn_x6<256, 256, 2, 2>), dim3(nout / 256, kin / 256, splits), dim3(256), 0, s, a);
+    else if (nout % 128 == 0 && kin % 128 == 0)
+        hipLaunchKernelGGL((k_gemm_tn_x6<128, 128, 2, 2>), dim3(nout / 128, kin / 128, splits), dim3(256), 0, s, a);
+    else if (nout % 128 == 0)
+        hipLaunchKernelGGL((k_gemm_tn_x6<128, 64, 2, 2>), dim3(nout / 128, kin / 64, splits), dim3(256), 0, s, a);
+    else if (kin % 128 == 0)
+        hipLaunchKernelGGL((k_gemm_tn_x6<64, 128, 1, 4>), dim3(nout / 64, kin / 128, splits), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_gemm_tn_x6<64, 64, 1, 2>), dim3(nout / 64, kin / 64, splits), dim3(128), 0, s, a);
+    prof_end(s, flops);
+    return check_launch("k_gemm_tn_x6");
+}
+
+}  // namespace nerf

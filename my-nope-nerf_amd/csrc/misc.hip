@@ -10,19 +10,53 @@ struct PackBatch {
     int n;
 };
 
+// x -> three bf16 words (RNE each) with x = hi + mid + lo (same split as gemm_x6.hip)
+__device__ __forceinline__ void split3(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
+    const __bf16 bh = (__bf16)x;
+    const float r = x - (float)bh;
+    const __bf16 bm = (__bf16)r;
+    const __bf16 bl = (__bf16)(r - (float)bm);
+    h = __builtin_bit_cast(uint16_t, bh);
+    m = __builtin_bit_cast(uint16_t, bm);
+    l = __builtin_bit_cast(uint16_t, bl);
+}
+
+// element (r, c) of a [N][K] operand into its bf16x3 image [3][K/8][N][8]
+__device__ __forceinline__ void put_split(uint16_t* img, int N, int K, int r, int c, float x) {
+    uint16_t h, m, l;
+    split3(x, h, m, l);
+    const size_t plane = (size_t)K * N;
+    const size_t o = ((size_t)(c >> 3) * N + r) * 8 + (c & 7);
+    img[o] = h;
+    img[o + plane] = m;
+    img[o + 2 * plane] = l;
+}
+
 // blockIdx.y selects the descriptor; grid-stride over the padded destination
 __global__ void k_pack(PackBatch pb) {
+#pragma clang fp contract(off)
     const nerf_pack_desc& d = pb.d[blockIdx.y];
-    const int total = d.rows * d.ld_dst;
+    const int rows_s = d.rows_s > d.rows ? d.rows_s : d.rows;
+    const int total = (d.dst_s != nullptr ? rows_s : d.rows) * d.ld_dst;
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
         const int r = e / d.ld_dst, c = e % d.ld_dst;
-        d.dst[e] = c < d.cols ? d.src[(size_t)r * d.cols + c] : 0.f;
+        const float x = (c < d.cols && r < d.rows) ? d.src[(size_t)r * d.cols + c] : 0.f;
+        if (r < d.rows) d.dst[e] = x;
+        if (d.dst_s != nullptr) put_split(d.dst_s, rows_s, d.ld_dst, r, c, x);
     }
     if (d.dst_t != nullptr) {
         const int tt = d.rows_t * d.rows;  // dst_t[c][r], c < rows_t, r < rows
         for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < tt; e += gridDim.x * blockDim.x) {
             const int c = e / d.rows, r = e % d.rows;
             d.dst_t[(size_t)c * d.ld_t + r] = c < d.cols ? d.src[(size_t)r * d.cols + c] : 0.f;
+        }
+    }
+    if (d.dst_ts != nullptr) {
+        const int tt = d.rows_t * d.ld_t;  // whole image of dst_t, zero past the source
+        for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < tt; e += gridDim.x * blockDim.x) {
+            const int c = e / d.ld_t, r = e % d.ld_t;   // dst_t row c, column r
+            const float x = (c < d.cols && r < d.rows) ? d.src[(size_t)r * d.cols + c] : 0.f;
+            put_split(d.dst_ts, d.rows_t, d.ld_t, c, r, x);
         }
     }
 }
@@ -94,6 +128,11 @@ extern "C" int nerf_pack_weights(const nerf_pack_desc* descs, int n, void* strea
                    "%s: bad descriptor %d", __func__, i);
         NERF_CHECK(d.dst_t == nullptr || (d.rows_t >= d.cols && d.ld_t >= d.rows),
                    "%s: descriptor %d: rows_t < cols or ld_t < rows", __func__, i);
+        NERF_CHECK(d.dst_s == nullptr || d.ld_dst % 8 == 0, "%s: descriptor %d: split image needs ld_dst %% 8 == 0",
+                   __func__, i);
+        NERF_CHECK(d.dst_ts == nullptr || (d.rows_t >= d.cols && d.ld_t >= d.rows && d.ld_t % 8 == 0),
+                   "%s: descriptor %d: transposed split image needs rows_t >= cols, ld_t >= rows, ld_t %% 8 == 0",
+                   __func__, i);
         pb.d[i] = d;
     }
     hipLaunchKernelGGL(k_pack, dim3(64, n), dim3(256), 0, as_stream(stream), pb);

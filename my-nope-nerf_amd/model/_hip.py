@@ -32,16 +32,18 @@ _c_i64 = ctypes.c_int64
 
 class PackDesc(ctypes.Structure):
     _fields_ = [("src", _c_p), ("dst", _c_p), ("dst_t", _c_p), ("rows", _c_i), ("cols", _c_i),
-                ("ld_dst", _c_i), ("rows_t", _c_i), ("ld_t", _c_i)]
+                ("ld_dst", _c_i), ("rows_t", _c_i), ("ld_t", _c_i), ("dst_s", _c_p), ("dst_ts", _c_p),
+                ("rows_s", _c_i)]
 
 
 _SIGS = {
     "nerf_hip_abi_version": ([], _c_i),
     "nerf_hip_last_error": ([], ctypes.c_char_p),
     "nerf_encode_samples": ([_c_p, _c_p, _c_p, _c_p, _c_i, _c_i, _c_i, _c_f, _c_f, _c_p, _c_p, _c_p, _c_p], _c_i),
-    "nerf_linear_fwd": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p, _c_i,
-                         _c_p], _c_i),
-    "nerf_linear_bwd_data": ([_c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_i, _c_i, _c_p], _c_i),
+    "nerf_linear_fwd": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_p, _c_i, _c_i, _c_i, _c_i,
+                         _c_p, _c_i, _c_p], _c_i),
+    "nerf_linear_bwd_data": ([_c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_i,
+                              _c_i, _c_p], _c_i),
     "nerf_linear_bwd_weight": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p], _c_i),
     "nerf_linear_bwd_weight_splits": ([_c_i, _c_i, _c_i], _c_i),
     "nerf_slab_reduce": ([_c_p, _c_i, _c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
@@ -56,7 +58,10 @@ _SIGS = {
     "nerf_adam_step": ([_c_p, _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p], _c_i),
     "nerf_chamfer_nn": ([_c_p, _c_i, _c_p, _c_i, _c_p, _c_p], _c_i),
     "nerf_gemm_set_policy": ([_c_i, _c_i], _c_i),
+    "nerf_gemm_set_precision": ([_c_i], _c_i),
+    "nerf_gemm_get_precision": ([], _c_i),
     "nerf_gemm_debug_ablate": ([_c_i], _c_i),
+    "nerf_gemm_debug_stamps": ([_c_p], _c_i),
     "nerf_prof_enable": ([_c_i], _c_i),
     "nerf_prof_read": ([ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_i64),
                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], _c_i),
@@ -100,7 +105,7 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
         return None
     if not t.is_cuda:
         raise RuntimeError("nerf_hip: tensor must live on the GPU (no CPU fallback)")
-    if t.dtype not in (torch.float32, torch.int64, torch.int32):
+    if t.dtype not in (torch.float32, torch.int64, torch.int32, torch.int16):
         raise RuntimeError(f"nerf_hip: unsupported dtype {t.dtype}")
     return t.data_ptr()
 
@@ -122,16 +127,33 @@ def encode_samples(pts_o, pts_d, view, noise, n_rays, n_samples, n_pad, near, fa
           n_pad, float(near), float(far), _ptr(z), _ptr(enc_p), _ptr(enc_d), _stream())
 
 
-def linear_fwd(x1, k1, x2, k2, w, bias, y, m, n, relu, mask_out=None):
-    """mask_out: int32 [m][n/32] ReLU mask bits of y (optional)."""
+def _split_args(ws):
+    """bf16x3 image view [3][K/8][rows][8] (int16, rows may be a slice) -> (ptr, image rows)."""
+    if ws is None:
+        return None, 0
+    if ws.dim() != 4 or ws.shape[0] != 3 or ws.shape[3] != 8 or ws.stride(2) != 8 or ws.stride(3) != 1:
+        raise ValueError("split weight image must be a [3][K/8][rows][8] view with contiguous rows")
+    return _ptr(ws), ws.stride(1) // 8
+
+
+def split_image(rows: int, k: int, device) -> "torch.Tensor":
+    """Zeroed bf16x3 image buffer for a [rows][k] operand (nerf_pack_desc.dst_s layout)."""
+    return torch.zeros(3, k // 8, rows, 8, dtype=torch.int16, device=device)
+
+
+def linear_fwd(x1, k1, x2, k2, w, bias, y, m, n, relu, mask_out=None, w_split=None):
+    """mask_out: int32 [m][n/32] ReLU mask bits of y (optional).  w_split: optional bf16x3
+    image of w (used by GEMM precision mode 1)."""
+    wsp, wsr = _split_args(w_split)
     _call("nerf_linear_fwd", _ptr(x1), _ld(x1), k1, _ptr(x2), _ld(x2) if x2 is not None else 0, k2,
-          _ptr(w), _ptr(bias), _ptr(y), _ld(y), m, n, int(relu), _ptr(mask_out),
+          _ptr(w), wsp, wsr, _ptr(bias), _ptr(y), _ld(y), m, n, int(relu), _ptr(mask_out),
           _ld(mask_out) if mask_out is not None else 0, _stream())
 
 
-def linear_bwd_data(dy, k, wt, dx, m, n, mask=None, u=None, ldu=1, v=None):
+def linear_bwd_data(dy, k, wt, dx, m, n, mask=None, u=None, ldu=1, v=None, wt_split=None):
     """mask: int32 ReLU mask bits [m][words] from linear_fwd(mask_out=...)."""
-    _call("nerf_linear_bwd_data", _ptr(dy), _ld(dy), k, _ptr(wt), _ptr(u), int(ldu), _ptr(v), _ptr(mask),
+    wsp, wsr = _split_args(wt_split)
+    _call("nerf_linear_bwd_data", _ptr(dy), _ld(dy), k, _ptr(wt), wsp, wsr, _ptr(u), int(ldu), _ptr(v), _ptr(mask),
           _ld(mask) if mask is not None else 0, _ptr(dx), _ld(dx), m, n, _stream())
 
 
@@ -201,6 +223,15 @@ def chamfer_nn(x, y, idx):
 
 def gemm_set_policy(nt: int = 0, tn: int = 0):
     _call("nerf_gemm_set_policy", int(nt), int(tn))
+
+
+def gemm_set_precision(mode):
+    """0 = exact-f32 MFMA, 1 = f32 emulated on bf16 MFMA (3-word split, 6 products)."""
+    _call("nerf_gemm_set_precision", int(mode))
+
+
+def gemm_get_precision():
+    return int(lib().nerf_gemm_get_precision())
 
 
 def prof_enable(on: bool):

@@ -87,6 +87,9 @@ class FieldRunner:
         z = lambda *s: torch.zeros(*s, device=device, dtype=torch.float32)
         self.w = {l.name: z(l.out_p, l.kp) for l in self.layers}
         self.wt = {l.name: z(l.kp, l.out_p) for l in self.layers}
+        # bf16x3 split images of w / wt: the B operands of GEMM precision mode 1
+        self.ws = {l.name: _hip.split_image(l.out_p, l.kp, device) for l in self.layers}
+        self.wts = {l.name: _hip.split_image(l.kp, l.out_p, device) for l in self.layers}
         self.b_r = z(HR)           # padded colour-layer bias
         self.wc = z(3, HR)         # padded fc_rgb weight
         self.device = device
@@ -97,12 +100,16 @@ class FieldRunner:
             raise RuntimeError("nerf_hip: the field must live on the GPU (no CPU fallback)")
         if self.device != dev:
             self._alloc(dev)
+        # split images only when the GEMMs run in the split-bf16 mode
+        self.split = _hip.gemm_get_precision() == 1
         descs = []
         for l in self.layers:
             W = l.linear.weight
             assert W.is_contiguous() and W.dtype == torch.float32
+            ws = self.ws[l.name].data_ptr() if self.split else None
+            wts = self.wts[l.name].data_ptr() if self.split else None
             descs.append(_hip.PackDesc(W.data_ptr(), self.w[l.name].data_ptr(), self.wt[l.name].data_ptr(),
-                                       W.shape[0], W.shape[1], l.kp, l.kp, l.out_p))
+                                       W.shape[0], W.shape[1], l.kp, l.kp, l.out_p, ws, wts, l.out_p))
         br = self.m.rgb_layers[0].bias
         descs.append(_hip.PackDesc(br.data_ptr(), self.b_r.data_ptr(), None, 1, br.shape[0], self.HR, 0, 0))
         wc = self.m.fc_rgb.weight
@@ -147,7 +154,7 @@ class FieldRunner:
                 mo = torch.empty(Np, l.out_p // 32, device=dev, dtype=torch.int32)
                 masks[l.name] = mo
             _hip.linear_fwd(x, k1, x2, _hip.ENC_P if x2 is not None else 0, self.w[l.name], self.bias(l), y,
-                            Np, l.out_p, l.relu, mask_out=mo)
+                            Np, l.out_p, l.relu, mask_out=mo, w_split=self.ws[l.name] if self.split else None)
             acts.append(y)
             x = y
             if l.name == "l7":
@@ -250,25 +257,27 @@ class FieldRunner:
                     G(l.linear.bias).copy_(gb[:nout_ref])
             # --- input gradient
             wt = self.wt[name]
+            wts = self.wts[name] if self.split else None
+            rows = (lambda a, b: wts[:, :, a:b]) if self.split else (lambda a, b: None)
             if name == "l0":
                 if want_ray_grad:
                     tmp = e(Np, _hip.ENC_P)
-                    _hip.linear_bwd_data(dy, l.out_p, wt, tmp, Np, _hip.ENC_P)
+                    _hip.linear_bwd_data(dy, l.out_p, wt, tmp, Np, _hip.ENC_P, wt_split=wts)
                     genc_p.add_(tmp)
                 break
             if l.seg2 and want_ray_grad:
                 tgt = genc_p if l.seg2 == "enc_p" else genc_d
                 tmp = e(Np, 64)
-                _hip.linear_bwd_data(dy, l.out_p, wt[k1:k1 + 64], tmp, Np, 64)
+                _hip.linear_bwd_data(dy, l.out_p, wt[k1:k1 + 64], tmp, Np, 64, wt_split=rows(k1, k1 + 64))
                 tgt.add_(tmp)
             dx = e(Np, k1)
             # ReLU bits of this layer's input (f, the input of lr, has no activation)
             mask = None if name == "lr" else st["masks"][prev_name[name]]
             if name == "lf":   # + density path: d sigma_raw (graw4[:,0]) x w_density
                 _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask, u=graw4, ldu=4,
-                                     v=m.fc_density.weight)
+                                     v=m.fc_density.weight, wt_split=rows(0, k1))
             else:
-                _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask)
+                _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask, wt_split=rows(0, k1))
             dy = dx
 
         done = torch.cuda.Event()

@@ -2,6 +2,7 @@
 
     python scripts/gemm_bench.py
 """
+import ctypes
 import os
 import sys
 
@@ -38,16 +39,52 @@ def main():
     mask = torch.empty(M, D // 32, device=dev, dtype=torch.int32)
     dy = torch.rand(M, D, device=dev, generator=g) - 0.5
     u = torch.rand(M, 4, device=dev, generator=g)
+    # bf16x3 images of W (forward B operand) and of W as the transposed backward operand
+    ws, wts = _hip.split_image(D, D, dev), _hip.split_image(D, D, dev)
+    Wp, Wt = torch.zeros(D, D, device=dev), torch.zeros(D, D, device=dev)
+    _hip.pack_weights([_hip.PackDesc(W.data_ptr(), Wp.data_ptr(), Wt.data_ptr(), D, D, D, D, D, ws.data_ptr(),
+                                     wts.data_ptr())])
     cases = {}
-    cases["fwd 256x256"] = (lambda: _hip.linear_fwd(x, D, None, 0, W, b, y, M, D, 1, mask_out=mask), 2 * M * D * D)
-    cases["fwd skip 320"] = (lambda: _hip.linear_fwd(x, D, enc, 64, W4, b, y, M, D, 1), 2 * M * D * (D + 64))
-    cases["bwd-data mask+u"] = (lambda: _hip.linear_bwd_data(dy, D, W, y, M, D, mask=mask, u=u, ldu=4, v=b),
-                                2 * M * D * D)
+    ws4 = _hip.split_image(D, D + 64, dev)
+    W4p, W4t = torch.zeros(D, D + 64, device=dev), torch.zeros(D + 64, D, device=dev)
+    _hip.pack_weights([_hip.PackDesc(W4.data_ptr(), W4p.data_ptr(), W4t.data_ptr(), D, D + 64, D + 64, D + 64, D,
+                                     ws4.data_ptr(), None)])
+    # split images are passed everywhere; the exact-f32 mode ignores them
+    cases["fwd 256x256"] = (lambda: _hip.linear_fwd(x, D, None, 0, W, b, y, M, D, 1, mask_out=mask, w_split=ws),
+                            2 * M * D * D)
+    cases["fwd skip 320"] = (lambda: _hip.linear_fwd(x, D, enc, 64, W4, b, y, M, D, 1, w_split=ws4),
+                             2 * M * D * (D + 64))
+    cases["bwd-data mask+u"] = (lambda: _hip.linear_bwd_data(dy, D, W, y, M, D, mask=mask, u=u, ldu=4, v=b,
+                                                             wt_split=wts), 2 * M * D * D)
     for sp in (64, 128, 256):
         slab = torch.empty(sp * D * D, device=dev)
         bslab = torch.empty(sp * D, device=dev)
         cases[f"dW splits={sp}"] = ((lambda sp=sp, slab=slab, bslab=bslab:
                                      _hip.linear_bwd_weight(dy, D, x, D, M, sp, slab, D, 0, bslab)), 2 * M * D * D)
+    if "--x6" in sys.argv:
+        _hip.gemm_set_precision(1)
+    if "--stamps" in sys.argv:   # per-block phase clocks of the split-bf16 NT kernel
+        import numpy as np
+        for name in ("fwd 256x256", "bwd-data mask+u"):
+            fn, fl = cases[name]
+            for _ in range(20):
+                fn()
+            buf = torch.zeros((M // 256) * 4 * 2, dtype=torch.int64, device=dev)
+            _hip.lib().nerf_gemm_debug_stamps(ctypes.c_void_p(buf.data_ptr()))
+            fn()
+            torch.cuda.synchronize()
+            _hip.lib().nerf_gemm_debug_stamps(None)
+            st = buf.cpu().numpy().reshape(-1, 4, 2).astype(np.float64)
+            clk = (st[:, 3, 0] - st[:, 0, 0]) / ((st[:, 3, 1] - st[:, 0, 1]) / 100e6)
+            ph = np.diff(st[:, :, 0], axis=1)
+            t0 = st[:, 0, 1].min()
+            start = (st[:, 0, 1] - t0) / 100.0
+            end = (st[:, 3, 1] - t0) / 100.0
+            print(f"{name}: blocks {len(st)}  clock median {np.median(clk) / 1e9:.2f} GHz  "
+                  f"cycles median prologue {np.median(ph[:, 0]):.0f} mainloop {np.median(ph[:, 1]):.0f} "
+                  f"epilogue {np.median(ph[:, 2]):.0f}  block us median {np.median(end - start):.1f} "
+                  f"span {end.max():.1f} us  start quartiles {np.percentile(start, [25, 50, 75, 100]).round(1)}")
+        return
     quick = "--quick" in sys.argv
     if quick:   # one launch per case at the default policy (for PMC collection)
         for name, (fn, fl) in cases.items():
@@ -57,19 +94,32 @@ def main():
     if "--ablate" in sys.argv:
         for pol in (2, 3):
             _hip.gemm_set_policy(pol, 3)
-            for ab in (0, 1, 2, 3):
+            for ab in (0, 1, 2, 3, 4, 7):
                 _hip.lib().nerf_gemm_debug_ablate(ab)
                 for name in ("fwd 256x256", "bwd-data mask+u"):
                     fn, fl = cases[name]
                     us = min(timeit(fn) for _ in range(3))
                     print(f"ablate={ab} policy {pol} {name:18s}: {us:8.1f} us {fl / us / 1e6:6.1f} TF/s")
         _hip.gemm_set_policy(0, 0)
-        for ab in (0, 16, 32, 64, 16 + 32 + 64):
+        for ab in (0, 16, 32, 64, 128, 16 + 32 + 64, 16 + 32 + 64 + 128):
             _hip.lib().nerf_gemm_debug_ablate(ab)
             fn, fl = cases["dW splits=256"]
             us = min(timeit(fn) for _ in range(3))
             print(f"ablate={ab} dW splits=256: {us:8.1f} us {fl / us / 1e6:6.1f} TF/s")
         _hip.lib().nerf_gemm_debug_ablate(0)
+        return
+    if "--prec" in sys.argv:   # exact-f32 MFMA vs split-bf16, default tile policy
+        res = {}
+        for rnd in range(3):
+            for prec in (0, 1):
+                _hip.gemm_set_precision(prec)
+                for name, (fn, fl) in cases.items():
+                    res.setdefault((name, prec), []).append(timeit(fn))
+        _hip.gemm_set_precision(0)
+        for (name, prec), v in sorted(res.items()):
+            fl = cases[name][1]
+            best = min(v)
+            print(f"{name:22s} precision {prec}: {best:8.1f} us  {fl / best / 1e6:6.1f} TF/s (f32-equivalent)")
         return
     res = {}
     for rnd in range(3):

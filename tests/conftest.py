@@ -19,3 +19,13 @@ def dev():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(params=[0, 1], ids=["f32mfma", "bf16x6"])
+def gemm_precision(request, dev):
+    """Run a GPU test under both GEMM arithmetic modes (nerf_gemm_set_precision)."""
+    from model import _hip
+    old = _hip.gemm_get_precision()
+    _hip.gemm_set_precision(request.param)
+    yield request.param
+    _hip.gemm_set_precision(old)

@@ -1,7 +1,9 @@
 """Per-kernel parity of the nerf_hip C-ABI against fp64 CPU references (GPU only).
 
 Tolerances: FP32 MFMA GEMMs are exact-f32 fma chains, so against an fp64 reference the
-error is ~1e-7 * sqrt(K) * |a||b|; we require max |err| <= 2e-5 * scale (rel 2e-5)."""
+error is ~1e-7 * sqrt(K) * |a||b|; we require max |err| <= 2e-5 * scale (rel 2e-5).  The
+GEMM tests run under both arithmetic modes (conftest.gemm_precision); the split-bf16
+emulation must also be no less accurate than the exact-f32 MFMA (test_split_bf16_accuracy)."""
 import pytest
 import torch
 
@@ -15,9 +17,19 @@ def _rand(*s, g=None):
     return torch.rand(*s, generator=g) * 2 - 1
 
 
+def _images(W, dev):
+    """W [n][k] (device) -> (bf16x3 image of W, image of W^T) via nerf_pack_weights."""
+    n, k = W.shape
+    Wp, Wt = torch.zeros(n, k, device=dev), torch.zeros(k, n, device=dev)
+    ws, wts = _hip.split_image(n, k, dev), _hip.split_image(k, n, dev)
+    _hip.pack_weights([_hip.PackDesc(W.data_ptr(), Wp.data_ptr(), Wt.data_ptr(), n, k, k, k, n, ws.data_ptr(),
+                                     wts.data_ptr())])
+    return ws, wts
+
+
 @pytest.mark.parametrize("m,n,k1,k2,relu", [(256, 256, 256, 0, 1), (384, 256, 64, 0, 1), (128, 256, 256, 64, 1),
                                             (256, 128, 256, 64, 1), (128, 64, 64, 0, 0), (512, 256, 256, 0, 0)])
-def test_linear_fwd(dev, m, n, k1, k2, relu):
+def test_linear_fwd(dev, gemm_precision, m, n, k1, k2, relu):
     g = torch.Generator().manual_seed(m + n + k1 + k2)
     x1 = _rand(m, k1, g=g)
     x2 = _rand(m, k2, g=g) if k2 else None
@@ -25,8 +37,10 @@ def test_linear_fwd(dev, m, n, k1, k2, relu):
     b = _rand(n, g=g)
     y = torch.empty(m, n, device=dev)
     mo = torch.empty(m, n // 32, device=dev, dtype=torch.int32)
-    _hip.linear_fwd(x1.to(dev), k1, x2.to(dev) if x2 is not None else None, k2, W.to(dev), b.to(dev), y, m, n, relu,
-                    mask_out=mo)
+    Wd = W.to(dev)
+    ws = _images(Wd, dev)[0] if gemm_precision == 1 else None
+    _hip.linear_fwd(x1.to(dev), k1, x2.to(dev) if x2 is not None else None, k2, Wd, b.to(dev), y, m, n, relu,
+                    mask_out=mo, w_split=ws)
     xc = torch.cat([x1, x2], 1) if x2 is not None else x1
     ref = xc.double() @ W.double().t() + b.double()
     if relu:
@@ -37,17 +51,19 @@ def test_linear_fwd(dev, m, n, k1, k2, relu):
     assert torch.equal(bits.view(m, n).bool(), y.cpu() > 0)          # ReLU bits agree with y
 
 
-def test_linear_fwd_asymmetric_identity(dev):
+def test_linear_fwd_asymmetric_identity(dev, gemm_precision):
     """A = I against an asymmetric B catches a transposed C write (guide section 3)."""
     m = n = k = 128
     x = torch.eye(m, k)
     W = torch.arange(n * k, dtype=torch.float32).view(n, k) / (n * k)
     y = torch.empty(m, n, device=dev)
-    _hip.linear_fwd(x.to(dev), k, None, 0, W.to(dev), None, y, m, n, 0)
+    Wd = W.to(dev)
+    ws = _images(Wd, dev)[0] if gemm_precision == 1 else None
+    _hip.linear_fwd(x.to(dev), k, None, 0, Wd, None, y, m, n, 0, w_split=ws)
     assert torch.equal(y.cpu(), W.t().contiguous())
 
 
-def test_linear_bwd_data(dev):
+def test_linear_bwd_data(dev, gemm_precision):
     g = torch.Generator().manual_seed(3)
     m, k, n = 256, 256, 128
     dy = _rand(m, k, g=g)
@@ -59,7 +75,10 @@ def test_linear_bwd_data(dev):
     bits = (mask > 0).view(m, n // 32, 32).long() << torch.arange(32)
     words = bits.sum(-1)
     words = torch.where(words >= 2 ** 31, words - 2 ** 32, words).to(torch.int32)
-    _hip.linear_bwd_data(dy.to(dev), k, Wt.to(dev), dx, m, n, mask=words.to(dev), u=u.to(dev), ldu=4, v=v.to(dev))
+    Wtd = Wt.to(dev)
+    ws = _images(Wtd, dev)[0] if gemm_precision == 1 else None     # image of wt itself ([n][k])
+    _hip.linear_bwd_data(dy.to(dev), k, Wtd, dx, m, n, mask=words.to(dev), u=u.to(dev), ldu=4, v=v.to(dev),
+                         wt_split=ws)
     ref = dy.double() @ Wt.double().t() + u[:, 0:1].double() * v.double()
     ref = torch.where(mask > 0, ref, torch.zeros_like(ref))
     torch.cuda.synchronize()
@@ -68,7 +87,7 @@ def test_linear_bwd_data(dev):
 
 @pytest.mark.parametrize("nout,kin,m,splits", [(256, 256, 4096, 8), (128, 320, 2048, 4), (256, 64, 1024, 1),
                                                (64, 128, 2048, 2)])
-def test_linear_bwd_weight_and_reduce(dev, nout, kin, m, splits):
+def test_linear_bwd_weight_and_reduce(dev, gemm_precision, nout, kin, m, splits):
     g = torch.Generator().manual_seed(nout + kin)
     dy = _rand(m, nout, g=g)
     x = _rand(m, kin, g=g)
@@ -88,6 +107,96 @@ def test_linear_bwd_weight_and_reduce(dev, nout, kin, m, splits):
     scale = ref.abs().max().item()
     assert (gw.cpu().double() - ref[:, :kin_ref]).abs().max().item() < 2e-5 * scale
     assert (gb.cpu().double() - dy.double().sum(0)).abs().max().item() < 1e-4 * max(1, dy.abs().sum(0).max().item())
+
+
+@pytest.mark.parametrize("scale_a,scale_b", [(1.0, 0.1), (1e-3, 1e3), (1e-20, 1.0)])
+def test_split_bf16_accuracy(dev, scale_a, scale_b):
+    """The split-bf16 GEMM (mode 1) against fp64: its error must stay within 1.5x (+ a
+    few ulps) of the exact-f32 MFMA's on the same operands, over K = 320 (two segments),
+    including operands far from 1 (the three bf16 words share f32's exponent range)."""
+    g = torch.Generator().manual_seed(11)
+    m, n, k1, k2 = 512, 256, 256, 64
+    x1, x2 = _rand(m, k1, g=g) * scale_a, _rand(m, k2, g=g) * scale_a
+    W = _rand(n, k1 + k2, g=g) * scale_b
+    ref = torch.cat([x1, x2], 1).double() @ W.double().t()
+    errs = []
+    Wd = W.to(dev)
+    ws = _images(Wd, dev)[0]
+    for mode in (0, 1):
+        _hip.gemm_set_precision(mode)
+        try:
+            y = torch.empty(m, n, device=dev)
+            _hip.linear_fwd(x1.to(dev), k1, x2.to(dev), k2, Wd, None, y, m, n, 0, w_split=ws)
+            torch.cuda.synchronize()
+        finally:
+            _hip.gemm_set_precision(0)
+        errs.append((y.cpu().double() - ref).abs().max().item())
+    tiny = 4 * 2.0 ** -24 * ref.abs().max().item()
+    assert errs[1] <= 1.5 * errs[0] + tiny, errs
+
+
+def _split3_ref(x):
+    """x -> (hi, mid, lo) bf16 words, each round-to-nearest-even (torch .bfloat16())."""
+    h = x.bfloat16()
+    r = x - h.float()
+    m = r.bfloat16()
+    lo = (r - m.float()).bfloat16()
+    return [t.view(torch.int16) for t in (h, m, lo)]
+
+
+def _image_ref(mat):
+    """[N][K] f32 -> bf16x3 image [3][K/8][N][8] (nerf_pack_desc.dst_s layout)."""
+    N, K = mat.shape
+    return torch.stack([p.view(N, K // 8, 8).permute(1, 0, 2) for p in _split3_ref(mat)])
+
+
+def test_pack_split_images(dev):
+    """nerf_pack_weights dst_s / dst_ts are the exact bf16x3 images of the padded packed
+    weight and its transpose; hi + mid + lo reconstructs every f32 exactly."""
+    g = torch.Generator().manual_seed(5)
+    rows, cols, ld, rows_t, ld_t, rows_s = 200, 300, 320, 320, 256, 256   # rows padded 200 -> 256 in the image
+    W = (_rand(rows, cols, g=g) * torch.logspace(-6, 2, cols)).to(dev)
+    dst = torch.zeros(rows, ld, device=dev)
+    dst_t = torch.zeros(rows_t, ld_t, device=dev)
+    ws = _hip.split_image(rows_s, ld, dev) - 1        # poisoned: every element must be written
+    wts = _hip.split_image(rows_t, ld_t, dev) - 1
+    _hip.pack_weights([_hip.PackDesc(W.data_ptr(), dst.data_ptr(), dst_t.data_ptr(), rows, cols, ld, rows_t, ld_t,
+                                     ws.data_ptr(), wts.data_ptr(), rows_s)])
+    torch.cuda.synchronize()
+    assert torch.equal(ws.cpu(), _image_ref(torch.cat([dst.cpu(), torch.zeros(rows_s - rows, ld)])))
+    assert torch.equal(wts.cpu(), _image_ref(dst_t.cpu()))
+    h, m, lo = (ws.cpu()[p].permute(1, 0, 2).reshape(rows_s, ld)[:rows].view(torch.bfloat16).double()
+                for p in range(3))
+    assert torch.equal((h + m + lo).float(), dst.cpu())
+
+
+@pytest.mark.parametrize("m,n,k1,k2", [(256, 256, 256, 64), (128, 64, 64, 0), (384, 128, 256, 0), (512, 256, 64, 64)])
+def test_split_weight_operand(dev, m, n, k1, k2):
+    """Mode 1 with the pre-split weight images: forward (two K segments) and
+    backward-data through a row slice of the transposed image, against fp64."""
+    g = torch.Generator().manual_seed(m + k2)
+    x1 = _rand(m, k1, g=g).to(dev)
+    x2 = _rand(m, k2, g=g).to(dev) if k2 else None
+    W = (_rand(n, k1 + k2, g=g) * 0.1).to(dev)
+    b = _rand(n, g=g).to(dev)
+    ws, wts = _images(W, dev)
+    Wt = W.t().contiguous()
+    dy = torch.rand(m, n, device=dev) - 0.5
+    lo, hi = (k1, k1 + k2) if k2 else (0, k1)
+    _hip.gemm_set_precision(1)
+    try:
+        y = torch.empty(m, n, device=dev)
+        _hip.linear_fwd(x1, k1, x2, k2, W, b, y, m, n, 1, w_split=ws)
+        d = torch.empty(m, hi - lo, device=dev)
+        _hip.linear_bwd_data(dy, n, Wt[lo:hi], d, m, hi - lo, wt_split=wts[:, :, lo:hi])
+        torch.cuda.synchronize()
+    finally:
+        _hip.gemm_set_precision(0)
+    xc = torch.cat([x1, x2], 1) if x2 is not None else x1
+    ref = (xc.double() @ W.double().t() + b.double()).clamp_min(0)
+    assert (y.double() - ref).abs().max().item() < 2e-5 * ref.abs().max().item()
+    refd = dy.double() @ Wt[lo:hi].double().t()
+    assert (d.double() - refd).abs().max().item() < 2e-5 * refd.abs().max().item()
 
 
 @pytest.mark.parametrize("S,flags", [(128, 0), (64, 0), (128, 1), (100, 0), (128, 2), (128, 4), (200, 1)])

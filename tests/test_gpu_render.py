@@ -34,7 +34,7 @@ def _rel(a, b):
     (256, 128, 200, {"white_background": True}),
     (128, 96, 300, {"dist_alpha": True}),
 ])
-def test_render_forward_matches_oracle(dev, hidden, S, R, opts):
+def test_render_forward_matches_oracle(dev, gemm_precision, hidden, S, R, opts):
     cfg = make_cfg(hidden=hidden, S=S, **opts)
     net, ref = _pair(cfg)
     b = synthetic_rays(R=R, S=S, seed=hidden + S)
@@ -51,7 +51,7 @@ def test_render_forward_matches_oracle(dev, hidden, S, R, opts):
     assert _rel(out["z_vals"].cpu(), o["z_vals"]) < 1e-6
 
 
-def test_render_eval_mode_full_frame_tile(dev):
+def test_render_eval_mode_full_frame_tile(dev, gemm_precision):
     """eval_=True (render/extraction path): no noise, depth normalised to z-depth."""
     cfg = make_cfg(hidden=256, S=128)
     net, ref = _pair(cfg, 3)
@@ -66,7 +66,7 @@ def test_render_eval_mode_full_frame_tile(dev):
     assert _rel(out["depth_pred"].cpu(), o["depth_pred"]) < RTOL
 
 
-def test_render_backward_matches_oracle(dev):
+def test_render_backward_matches_oracle(dev, gemm_precision):
     """parameter gradients of rgb-L2 + depth-L1 through the fused backward."""
     cfg = make_cfg(hidden=256, S=128)
     net, ref = _pair(cfg, 1)
@@ -90,7 +90,7 @@ def test_render_backward_matches_oracle(dev):
         assert err.item() < 2e-3, f"{n}: rel grad err {err.item():.2e}"
 
 
-def test_render_ray_gradients(dev):
+def test_render_ray_gradients(dev, gemm_precision):
     """pose learning: gradients w.r.t. the camera pose flow through the encodings."""
     cfg = make_cfg(hidden=64, S=64)
     net, ref = _pair(cfg, 2)
@@ -113,7 +113,7 @@ def test_render_ray_gradients(dev):
         assert ((a - bb).norm() / bb.norm()).item() < 5e-3
 
 
-def test_points_forward_api(dev):
+def test_points_forward_api(dev, gemm_precision):
     """OfficialStaticNerf.forward(p, ray_d, return_addocc=True) on arbitrary points."""
     cfg = make_cfg(hidden=256)
     net, ref = _pair(cfg, 4)
