@@ -10,9 +10,12 @@ gradient all-reduce over RCCL (N > 1), Adam.  Inputs are resident in HBM.
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
 
-Rank 0 prints ONE JSON line.  Extra objects: "roofline" (FP32-MFMA GEMM family, timed
-live with hipEvents around every GEMM launch of the timed steps) and "cpu_baseline"
-(the oracle CPU restatement of the same step on this host's cores, bounded sample).
+Rank 0 prints ONE JSON line.  Extra objects: "roofline" (the field-MLP GEMM family,
+timed live with hipEvents around every GEMM launch of the timed steps), "cpu_baseline"
+(the oracle CPU restatement of the same step on this host's cores, bounded sample) and
+"alt_gemm" (the same workload with the other GEMM arithmetic).  The GEMMs compute f32
+products either on the exact-f32 MFMA or, by default, as a 3-word bf16 split with six
+MFMA products accumulated in f32 (f32-accurate: DESIGN.md section 4).
 """
 from __future__ import annotations
 
@@ -143,8 +146,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--gemm-precision", choices=["f32", "bf16x6"], default="f32",
-                    help="GEMM arithmetic: exact-f32 MFMA or f32 emulated by a 3-word bf16 split (6 products)")
+    ap.add_argument("--gemm-precision", choices=["f32", "bf16x6"], default="bf16x6",
+                    help="GEMM arithmetic: f32 emulated by a 3-word bf16 split (6 products, f32-accurate; "
+                         "default) or the exact-f32 MFMA")
+    ap.add_argument("--no-alt", dest="alt", action="store_false",
+                    help="skip timing the other GEMM arithmetic (reported as alt_gemm)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -157,36 +163,52 @@ def main():
     dev = torch.device("cuda", local)
     from model import _hip
     _hip.load_library()
-    _hip.gemm_set_precision(1 if args.gemm_precision == "bf16x6" else 0)
 
     cfg = make_cfg()
     data, c2w = synthetic_scene(dev)
-    trainer, net = build_trainer(dev, c2w, cfg)
-    torch.cuda.manual_seed(1000 + rank)                     # each rank samples its own rays
 
-    def one(it):
-        return trainer.train_step(data, it=it, epoch=0, scheduling_start=0)
+    def measure(precision):
+        """W warm-up + K timed train steps with the GEMMs in `precision` (0 exact-f32 MFMA,
+        1 split-bf16); returns (max-over-ranks seconds, last loss dict, GEMM hook stats)."""
+        _hip.gemm_set_precision(precision)
+        trainer, net = build_trainer(dev, c2w, cfg)
+        torch.cuda.manual_seed(1000 + rank)                 # each rank samples its own rays
 
-    for i in range(args.warmup):
-        one(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    _hip.prof_enable(True)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ld = one(args.warmup + i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    gemm_ms, gemm_launches, _, gemm_union_ms = _hip.prof_read()
-    _hip.prof_enable(False)
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        def one(it):
+            return trainer.train_step(data, it=it, epoch=0, scheduling_start=0)
+
+        for i in range(args.warmup):
+            one(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        _hip.prof_enable(True)
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            ld = one(args.warmup + i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        stats = _hip.prof_read()
+        _hip.prof_enable(False)
+        el = t1 - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = t.item()
+        return el, ld, stats, net
+
+    main_prec = 1 if args.gemm_precision == "bf16x6" else 0
+    elapsed, ld, (gemm_ms, gemm_launches, _, gemm_union_ms), net = measure(main_prec)
+    alt = None
+    if args.alt:
+        # the other GEMM arithmetic on the same workload, reported beside the headline
+        el2, ld2, _, _ = measure(1 - main_prec)
+        alt = {"gemm_arithmetic": "f32" if main_prec == 1 else "bf16x6",
+               "value": world * RAYS / (el2 / args.steps), "ms_per_step": 1e3 * el2 / args.steps,
+               "final_loss": ld2["loss"].detach().item()}
+        _hip.gemm_set_precision(main_prec)
     loss = ld["loss"].detach().item()
     psnr = -10.0 * math.log10(max(ld["l2_mean"].detach().item(), 1e-10))
     if not math.isfinite(loss):
@@ -231,7 +253,7 @@ def main():
                           "global_batch": world * RAYS, "seq_len": SAMPLES, "hidden_dim": HIDDEN,
                           "parallelism": f"dp{world}"},
                "final_loss": loss, "train_psnr_last_step": psnr,
-               "roofline": roof, "cpu_baseline": cpu}
+               "roofline": roof, "cpu_baseline": cpu, "alt_gemm": alt}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -180,9 +180,10 @@ __device__ __forceinline__ void tn_store(const TNArgs& p, f32x16 (&acc)[TM][TN],
 
 // diagnostics: wave 0 of each block records (s_memtime, s_memrealtime) at phase
 // boundaries into stamps[block][phase][2]
-constexpr int kStampPhases = 4;
+constexpr int kStampPhases = 10;
 __device__ __forceinline__ void stamp(unsigned long long* st, int phase) {
     if (st == nullptr) return;
+    __builtin_amdgcn_sched_barrier(0);
     const unsigned long long t = __builtin_amdgcn_s_memtime();
     const unsigned long long r = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) {
@@ -190,6 +191,7 @@ __device__ __forceinline__ void stamp(unsigned long long* st, int phase) {
         st[(b * kStampPhases + phase) * 2] = t;
         st[(b * kStampPhases + phase) * 2 + 1] = r;
     }
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // ---------------------------------------------------------------------------

@@ -235,39 +235,68 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_tn(TNArgs p) {
     if (do_bias && tid < BM && !(p.ablate & 1)) p.bslab[(size_t)split * p.nout + o0 + tid] = bsum;
 }
 
-// sum split-K slabs into the reference-layout gradient: one thread per output element,
-// 4 independent partial sums so the split loop keeps several loads in flight
+// sum split-K slabs into the reference-layout gradient.  A block owns 256 consecutive
+// slab columns of one output row (64 lanes x float4); its 4 waves sum interleaved
+// quarters of the splits (8 float4 loads in flight per lane), then combine through LDS
+// in wave order (deterministic).  Bias partials (bslab) ride along in the last row
+// of blocks.
+constexpr int SR_COLS = 256;
 __global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ slab, int splits, int nout,
                                                      int ldslab, int nout_ref, int kin_ref,
                                                      const float* __restrict__ bslab, float* __restrict__ gw,
                                                      float* __restrict__ gb, int accumulate) {
-    const size_t stride = (size_t)nout * ldslab;
-    const int total = nout_ref * kin_ref;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total + nout_ref; e += gridDim.x * blockDim.x) {
-        const float* src;
-        size_t st;
-        if (e < total) {
-            const int o = e / kin_ref, j = e % kin_ref;
-            src = slab + (size_t)o * ldslab + j;
-            st = stride;
+    __shared__ float4 part[4][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int cblocks = (kin_ref + SR_COLS - 1) / SR_COLS;
+    const int o = blockIdx.x / cblocks;              // output row (o == nout_ref: the bias row)
+    const int c0 = (blockIdx.x % cblocks) * SR_COLS + 4 * lane;
+    const bool bias_row = o == nout_ref;
+    if (bias_row && (bslab == nullptr || gb == nullptr)) return;
+    const float* src;
+    size_t st;
+    int ncol;
+    if (!bias_row) { src = slab + (size_t)o * ldslab; st = (size_t)nout * ldslab; ncol = kin_ref; }
+    else { src = bslab; st = nout; ncol = nout_ref; }
+    const bool vec = (c0 + 4 <= ncol) && ((st & 3) == 0) && ((((uintptr_t)(src + c0)) & 15) == 0);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c0 < ncol) {
+        if (vec) {
+            int q = wv;
+            for (; q + 28 < splits; q += 32) {      // 8 loads in flight per lane
+                float4 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(src + (size_t)(q + 4 * u) * st + c0);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+                }
+            }
+            for (; q < splits; q += 4) {
+                const float4 v = *reinterpret_cast<const float4*>(src + (size_t)q * st + c0);
+                acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+            }
         } else {
-            if (bslab == nullptr || gb == nullptr) continue;
-            src = bslab + (e - total);
-            st = nout;
+            float a[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int q = wv; q < splits; q += 4)
+                for (int t = 0; t < 4; ++t)
+                    if (c0 + t < ncol) a[t] += src[(size_t)q * st + c0 + t];
+            acc = make_float4(a[0], a[1], a[2], a[3]);
         }
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-        int q = 0;
-        for (; q + 4 <= splits; q += 4) {
-            a0 += src[(size_t)q * st];
-            a1 += src[(size_t)(q + 1) * st];
-            a2 += src[(size_t)(q + 2) * st];
-            a3 += src[(size_t)(q + 3) * st];
-        }
-        for (; q < splits; ++q) a0 += src[(size_t)q * st];
-        const float acc = (a0 + a1) + (a2 + a3);
-        float* dst = e < total ? gw + e : gb + (e - total);
-        *dst = accumulate ? *dst + acc : acc;
     }
+    part[wv][lane] = acc;
+    __syncthreads();
+    if (wv != 0 || c0 >= ncol) return;
+    float4 r = part[0][lane];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+        const float4 v = part[w][lane];
+        r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+    }
+    float* dst = bias_row ? gb + c0 : gw + (size_t)o * kin_ref + c0;
+    const float rv[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        if (c0 + t < ncol) dst[t] = accumulate ? dst[t] + rv[t] : rv[t];
 }
 
 }  // namespace nerf
@@ -417,8 +446,12 @@ extern "C" int nerf_slab_reduce(const float* slab, int splits, int nout, int lds
     NERF_CHECK_PTR(gw);
     NERF_CHECK(splits > 0 && nout > 0 && kin_ref > 0 && ldslab >= kin_ref && nout_ref <= nout,
                "%s: bad sizes", __func__);
-    const int total = nout_ref * kin_ref + nout_ref;
-    const int blocks = (total + 255) / 256;
+    // one block per (output row, 256 columns); one extra row of blocks for the bias
+    const int cblocks = (kin_ref + SR_COLS - 1) / SR_COLS;
+    const int bias_blocks = (bslab && gb) ? cblocks : 0;
+    NERF_CHECK(nout_ref <= cblocks * SR_COLS || bias_blocks == 0,
+               "%s: bias row wider than the column blocks (nout_ref %d > %d)", __func__, nout_ref, cblocks * SR_COLS);
+    const int blocks = nout_ref * cblocks + bias_blocks;
     hipLaunchKernelGGL(k_slab_reduce, dim3(blocks), dim3(256), 0, as_stream(stream), slab, splits,
                        nout, ldslab, nout_ref, kin_ref, bslab, gw, gb, accumulate);
     return check_launch(__func__);

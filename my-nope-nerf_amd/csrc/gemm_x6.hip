@@ -157,6 +157,8 @@ __device__ __forceinline__ void x6_mainloop(char* smem, int nkt, int wm0, int wn
     }
 }
 
+
+
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 // 16 bytes per lane global -> LDS (global_load_lds_dwordx4): lane l lands at
@@ -171,15 +173,17 @@ __device__ __forceinline__ void dma16(const void* gsrc, char* lds_wave_base) {
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // ---------------------------------------------------------------------------
-// Main loop of the NT kernel, with every fragment double-buffered in registers.
+// Main loop of the NT kernel: every fragment double-buffered in registers, every
+// global operand moved by LDS-DMA (invisible to the compiler's wait counting, so no
+// hidden vmcnt drains; the waits are counted here).
 //
-// Iteration kt: the fragments of tile kt are in registers (set `fc`); the MFMAs run on
-// them while the fragments of tile kt+1 are read from image buffer (kt+1)&1 (set `fn`),
-// so no wave waits on LDS after a barrier.  Image buffer kt&1 -- whose fragments were
-// read into registers during iteration kt-1 -- receives tile kt+2: its B part by
-// LDS-DMA, its A part split from the raw ring, interleaved with the first MFMAs.  The
-// raw ring slot freed by that split (its tile went through iteration kt-1's split)
-// is refilled with raw A of tile kt+3.  Every DMA lands before the iteration's barrier.
+// Iteration kt: the fragments of tile kt are in registers (set `c`); its MFMAs run
+// while the fragments of tile kt+1 are read from image buffer (kt+1)&1 (set `n`).
+// Image buffer kt&1 -- read into registers during iteration kt-1 -- receives tile
+// kt+2: its B part by DMA from the pre-split weight image, its A part split from the
+// raw ring (VALU spread over row tile 0's MFMAs).  Raw A of tile kt+4 is DMA'd into
+// the ring slot freed by iteration kt-1's split.  At the end `vmcnt(A_F4)` retires
+// every DMA but this iteration's raw A, which gets a second iteration to land.
 // ---------------------------------------------------------------------------
 template <int TM, int TN, int BM, int BN, typename Stager>
 __device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int wn0, f32x16 (&acc)[TM][TN],
@@ -196,11 +200,13 @@ __device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int
         f[1] = *reinterpret_cast<const uint4*>(q + plane);
         f[2] = *reinterpret_cast<const uint4*>(q + 2 * plane);
     };
-    auto rd_all = [&](const char* buf, uint4 (&a)[TM][3], uint4 (&b)[TN][3]) {
+    auto rdA = [&](const char* buf, uint4 (&a)[TM][3], int i0, int i1) {
+#pragma unroll
+        for (int i = i0; i < i1; ++i) rd(buf + aoff + 32 * 16 * i, IA::PLANE, a[i]);
+    };
+    auto rdB = [&](const char* buf, uint4 (&b)[TN][3]) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) rd(buf + boff + 32 * 16 * j, IB::PLANE, b[j]);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) rd(buf + aoff + 32 * 16 * i, IA::PLANE, a[i]);
     };
     auto mm = [&](int i, const uint4 (&a)[3], const uint4 (&b)[TN][3]) {
 #pragma unroll
@@ -217,8 +223,9 @@ __device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int
     };
     uint4 aX[TM][3], bX[TN][3], aY[TM][3], bY[TN][3];
 
-    st.prologue2(smem, nkt);        // tiles 0, 1 in image buffers 0, 1; raw tile 2 in slot 0
-    rd_all(smem, aX, bX);
+    st.prologue3(smem, nkt);        // tiles 0, 1 in image buffers 0, 1; raw tiles 2, 3 in the ring
+    rdA(smem, aX, 0, TM);
+    rdB(smem, bX);
     __syncthreads();                // buffer 0 is restaged in iteration 0
     stamp(stamps, 1);
 
@@ -226,14 +233,12 @@ __device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int
         char* wimg = smem + (kt & 1) * BUF;
         const char* nbuf = smem + ((kt + 1) & 1) * BUF;
         constexpr int H = (TM + 1) / 2;
-        st.issue2(kt, nkt, wimg + IA::BYTES);
-        // next tile's B fragments and first half of its A fragments now; the second half
-        // after the first half of this tile's MFMAs retired their A registers
-#pragma unroll
-        for (int j = 0; j < TN; ++j) rd(nbuf + boff + 32 * 16 * j, IB::PLANE, bn[j]);
-#pragma unroll
-        for (int i = 0; i < H; ++i) rd(nbuf + aoff + 32 * 16 * i, IA::PLANE, an[i]);
-        st.split2(kt, nkt, wimg);
+        st.dma3(kt, nkt, wimg + IA::BYTES);   // B image of tile kt+2, then raw A of tile kt+4
+        float4 raw[Stager::A_F4];
+        st.read_raw3(kt, raw);                 // raw A of tile kt+2
+        rdB(nbuf, bn);
+        rdA(nbuf, an, 0, H);
+        st.split_raw(raw, wimg);
         mm(0, ac[0], bc);
 #pragma unroll
         for (int q = 0; q < 6 * TN; ++q) {
@@ -244,12 +249,14 @@ __device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int
 #pragma unroll
         for (int i = 1; i < H; ++i) mm(i, ac[i], bc);
         __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = H; i < TM; ++i) rd(nbuf + aoff + 32 * 16 * i, IA::PLANE, an[i]);
+        rdA(nbuf, an, H, TM);
 #pragma unroll
         for (int i = H; i < TM; ++i) mm(i, ac[i], bc);
-        st.before_barrier();
+        if (kt == 5) stamp(stamps, 6);
+        st.wait3();
+        if (kt == 5) stamp(stamps, 7);
         __syncthreads();
+        if (kt == 5) stamp(stamps, 8);
     };
     for (int kt = 0; kt < nkt; kt += 2) {
         iter(kt, aX, bX, aY, bY);
@@ -259,25 +266,26 @@ __device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int
 
 // ---------------------------------------------------------------------------
 // NT: C[m][n] = epi( sum_k A[m][k] B[n][k] ).
-// A (activations, f32 [m][k]): LDS-DMA into a 2-slot raw ring, 16-B per lane (a wave
-// moves 16 rows x 64 B), split from there.  B: the pre-split weight image (p.bs),
-// LDS-DMA'd straight into the image buffer.  No staging registers.
+// A (activations, f32 [m][k]): LDS-DMA into a 2-slot raw ring, 16 B per lane (a wave
+// moves 16 rows x 64 B), split from there into the A image.  B: fragments loaded
+// straight from the pre-split weight image (p.bs, L2-resident).  No staging registers.
 // ---------------------------------------------------------------------------
 template <int BM, int BN, int NT>
 struct NTStager {
-    static constexpr int A_F4 = BM * XK / 4 / NT;   // raw A float4 per thread and tile
+    static constexpr int A_F4 = BM * XK / 4 / NT;   // raw A float4 (= DMA instructions) per thread and tile
     static constexpr int RSTEP = NT / 4;            // rows per pass of the block
+    static constexpr int RAW = BM * XK * 4;         // bytes of one raw A slot
+    static constexpr int NSLOT = 3;
     static constexpr int B_CH = 6 * BN;             // 16-B chunks of a tile's B image
     static constexpr int B_C = (B_CH + NT - 1) / NT;
-    static constexpr int RAW = BM * XK * 4;         // bytes of one raw A slot
     static_assert(A_F4 >= 1 && BN % 64 == 0, "bad tile");
     const float* a1b; const float* a2b; const uint16_t* bsb;
-    int lda1, lda2, k1, bs_rows;
+    int lda1, lda2, k1, bs_rows, Kc;
     int r0, q0;
     char* raw;
 
-    __device__ __forceinline__ void init(const NTArgs& p, int m0, int n0, char* raw_ring) {
-        lda1 = p.lda1; lda2 = p.lda2; k1 = p.k1; bs_rows = p.bs_rows;
+    __device__ __forceinline__ void init(const NTArgs& p, int m0, int n0, int K, char* raw_ring) {
+        lda1 = p.lda1; lda2 = p.lda2; k1 = p.k1; bs_rows = p.bs_rows; Kc = K / 8;
         a1b = p.a1 + (size_t)m0 * lda1;
         a2b = p.a2 ? p.a2 + (size_t)m0 * lda2 : p.a1;
         bsb = p.bs + (size_t)n0 * 8;
@@ -299,69 +307,55 @@ struct NTStager {
         const int lane = threadIdx.x & 63;
 #pragma unroll
         for (int i = 0; i < B_C; ++i) {
-            const int idx = threadIdx.x + NT * i;
             if (B_C * NT != B_CH && (int)(threadIdx.x & ~63) + NT * i >= B_CH) break;   // wave-uniform
+            const int idx = threadIdx.x + NT * i;
             const int n = idx % BN, pk = idx / BN;
             dma16(bt + (((size_t)(pk >> 1) * Kc + (pk & 1)) * bs_rows + n) * 8,
                   Bimg + (pk >> 1) * XImg<BN>::PLANE + (pk & 1) * XImg<BN>::HALF + (n - lane) * 16);
         }
     }
-    int Kc = 0;   // K / 8: 8-k chunks per plane of the B image
-    __device__ __forceinline__ void split_slot(int slot, char* Aimg) {
+    __device__ __forceinline__ void read_slot(int slot, float4 (&v)[A_F4]) {
 #pragma unroll
-        for (int i = 0; i < A_F4; ++i) {
-            const int row = r0 + i * RSTEP;
-            const float4 v = *reinterpret_cast<const float4*>(raw + slot * RAW + row * 64 + q0 * 16);
-            put_row4<BM>(Aimg, row, q0, v);
-        }
+        for (int i = 0; i < A_F4; ++i)
+            v[i] = *reinterpret_cast<const float4*>(raw + slot * RAW + (r0 + i * RSTEP) * 64 + q0 * 16);
     }
-    // tile 0 in image buffer 0 (A split, B DMA), raw tile 1 in slot 1
-    __device__ __forceinline__ void prologue(char* smem, int nkt) {
-        dma_a(0, 0);
-        dma_b(0, smem + XImg<BM>::BYTES);
-        dma_a(nkt > 1 ? 1 : 0, 1);
-        dma_wait();
-        __syncthreads();
-        split_slot(0, smem);
-        __syncthreads();
+    __device__ __forceinline__ void put(const float4 (&v)[A_F4], char* Aimg) {
+#pragma unroll
+        for (int i = 0; i < A_F4; ++i) put_row4<BM>(Aimg, r0 + i * RSTEP, q0, v[i]);
     }
-    // iteration kt: split raw tile kt+1 (slot (kt+1)&1) into the other image buffer
-    __device__ __forceinline__ void split(int kt, int nkt, char* Aimg, char*) {
-        split_slot((kt + 1) & 1, Aimg);
-    }
-    // iteration kt: B image of tile kt+1 into the other buffer, raw A of tile kt+2 into
-    // slot kt&1 (split in iteration kt+1); both land before this iteration's barrier
-    __device__ __forceinline__ void issue_early(int kt, int nkt, char* Bimg) {
-        dma_b(kt + 1 < nkt ? kt + 1 : nkt - 1, Bimg);
-        dma_a(kt + 2 < nkt ? kt + 2 : nkt - 1, kt & 1);
-    }
-    __device__ __forceinline__ void issue(int, int, char*) {}
-    __device__ __forceinline__ void before_barrier() { dma_wait(); }
-
-    // --- x6_mainloop_pf protocol
-    __device__ __forceinline__ void prologue2(char* smem, int nkt) {
+    __device__ __forceinline__ int clamp(int t, int nkt) const { return t < nkt ? t : nkt - 1; }
+    // tiles 0, 1 in image buffers 0, 1 (raw tile t lives in slot t % 3); raw tiles 2 (landed)
+    // and 3 (in flight) in the ring
+    __device__ __forceinline__ void prologue3(char* smem, int nkt) {
         constexpr int BUF = XImg<BM>::BYTES + XImg<BN>::BYTES;
-        const int t1 = nkt > 1 ? 1 : 0, t2 = nkt > 2 ? 2 : nkt - 1;
         dma_a(0, 0);
+        dma_a(clamp(1, nkt), 1);
+        dma_a(clamp(2, nkt), 2);
         dma_b(0, smem + XImg<BM>::BYTES);
-        dma_a(t1, 1);
-        dma_b(t1, smem + BUF + XImg<BM>::BYTES);
+        dma_b(clamp(1, nkt), smem + BUF + XImg<BM>::BYTES);
         dma_wait();
         __syncthreads();
-        split_slot(0, smem);
-        split_slot(1, smem + BUF);
-        __syncthreads();            // raw slot 0 is refilled below
-        dma_a(t2, 0);
-        dma_wait();
-        __syncthreads();
+        float4 v[A_F4];
+        read_slot(0, v);
+        put(v, smem);
+        read_slot(1, v);
+        put(v, smem + BUF);
+        __syncthreads();            // slot 0 is refilled below (tile 3)
+        dma_a(clamp(3, nkt), 0);
     }
-    // iteration kt: B image of tile kt+2 into buffer kt&1, raw A of tile kt+3 into slot (kt+1)&1
-    __device__ __forceinline__ void issue2(int kt, int nkt, char* Bimg) {
-        dma_b(kt + 2 < nkt ? kt + 2 : nkt - 1, Bimg);
-        dma_a(kt + 3 < nkt ? kt + 3 : nkt - 1, (kt + 1) & 1);
+    // iteration kt: B image of tile kt+2 into buffer kt&1 (lands this iteration), then raw A
+    // of tile kt+4 into slot (kt+4)%3 = (kt+1)%3 (lands next iteration)
+    __device__ __forceinline__ void dma3(int kt, int nkt, char* Bimg) {
+        dma_b(clamp(kt + 2, nkt), Bimg);
+        dma_a(clamp(kt + 4, nkt), (kt + 1) % NSLOT);
     }
-    // iteration kt: raw A of tile kt+2 (slot kt&1) into buffer kt&1
-    __device__ __forceinline__ void split2(int kt, int, char* Aimg) { split_slot(kt & 1, Aimg); }
+    __device__ __forceinline__ void read_raw3(int kt, float4 (&v)[A_F4]) { read_slot((kt + 2) % NSLOT, v); }
+    __device__ __forceinline__ void split_raw(const float4 (&v)[A_F4], char* Aimg) { put(v, Aimg); }
+    // everything but this iteration's raw-A DMA (the last A_F4 VM instructions) has landed
+    __device__ __forceinline__ void wait3() {
+        static_assert(A_F4 <= 63, "vmcnt field");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_F4) : "memory");
+    }
 };
 
 template <int BM, int BN, int WM, int WN, int EPI>
@@ -369,11 +363,9 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt_x6(NTArgs p) {
     constexpr int NT = 64 * WM * WN;
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
-    constexpr int BUF = XImg<BM>::BYTES + XImg<BN>::BYTES;
     using St = NTStager<BM, BN, NT>;
     static_assert(TM >= 1 && TN >= 1, "bad tile");
-
-    constexpr int LOOP_BYTES = 2 * BUF + 2 * St::RAW;
+    constexpr int LOOP_BYTES = 2 * (XImg<BM>::BYTES + XImg<BN>::BYTES) + St::NSLOT * St::RAW;
     constexpr int EPI_BYTES = (NT / 64) * TileLds<TN>::BYTES + (BM * (BN / 32) + BM) * 4;
     __shared__ __attribute__((aligned(16))) char smem[LOOP_BYTES > EPI_BYTES ? LOOP_BYTES : EPI_BYTES];
     const int wave = threadIdx.x >> 6;
@@ -385,13 +377,14 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt_x6(NTArgs p) {
 
     stamp(p.stamps, 0);
     St st;
-    st.init(p, m0, n0, smem + 2 * BUF);
-    st.Kc = K / 8;
+    st.init(p, m0, n0, K, smem + 2 * (XImg<BM>::BYTES + XImg<BN>::BYTES));
     NTEpiPrefetch<BM, BN, NT, EPI> pf;
     pf.load(p, m0, n0);
     f32x16 acc[TM][TN];
     zero_acc(acc);
     x6_mainloop_pf<TM, TN, BM, BN>(smem, K / XK, wm0, wn0, acc, st, p.stamps);
+    dma_wait();          // the last (clamped) raw-A DMA must land before the epilogue reuses LDS
+    __syncthreads();
     stamp(p.stamps, 2);
     nt_epilogue_lds<BM, BN, NT, TM, TN, EPI>(p, acc, smem, m0, n0, wm0, wn0, pf);
     if (p.stamps) {

@@ -69,14 +69,18 @@ def main():
             fn, fl = cases[name]
             for _ in range(20):
                 fn()
-            buf = torch.zeros((M // 256) * 4 * 2, dtype=torch.int64, device=dev)
+            buf = torch.zeros((M // 256) * 10 * 2, dtype=torch.int64, device=dev)
             _hip.lib().nerf_gemm_debug_stamps(ctypes.c_void_p(buf.data_ptr()))
             fn()
             torch.cuda.synchronize()
             _hip.lib().nerf_gemm_debug_stamps(None)
-            st = buf.cpu().numpy().reshape(-1, 4, 2).astype(np.float64)
+            st = buf.cpu().numpy().reshape(-1, 10, 2).astype(np.float64)
+            sub = st[:, [9, 4, 5, 6, 7, 8], 0]
+            d = np.median(np.diff(sub, axis=1), axis=0)
+            print(f"  iteration 5 (cycles): issue+frag reads {d[0]:.0f}  split+row0 {d[1]:.0f}  rest MFMA issue "
+                  f"{d[2]:.0f}  dma wait {d[3]:.0f}  barrier {d[4]:.0f}")
             clk = (st[:, 3, 0] - st[:, 0, 0]) / ((st[:, 3, 1] - st[:, 0, 1]) / 100e6)
-            ph = np.diff(st[:, :, 0], axis=1)
+            ph = np.diff(st[:, :4, 0], axis=1)
             t0 = st[:, 0, 1].min()
             start = (st[:, 0, 1] - t0) / 100.0
             end = (st[:, 3, 1] - t0) / 100.0

@@ -1,16 +1,23 @@
-# one GPU box call: parity tests, smoke, micro-benchmarks, bench, rocprofv3 kernel stats
+# one GPU box call: parity tests, smoke, micro-benchmarks, bench, rocprofv3 kernel stats,
+# HBM traffic counters (FETCH_SIZE / WRITE_SIZE in separate passes) of single GEMM launches
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
 OUT=$R/gpurun_out
 mkdir -p $OUT
-timeout -k 10 600 python -m pytest tests -q -m gpu -p no:cacheprovider > $OUT/t_all.log 2>&1
-echo "tests rc=$?"
+timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider > $OUT/t_all.log 2>&1
+rc=$?
+echo "tests rc=$rc"; tail -2 $OUT/t_all.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && echo "smoke ok" && \
-timeout -k 10 300 python scripts/gemm_bench.py > $OUT/gemm_bench.txt 2>&1 && echo "gemm bench ok" && \
+timeout -k 10 300 python scripts/gemm_bench.py --prec > $OUT/gemm_prec.txt 2>&1 && echo "gemm bench ok" && \
 timeout -k 10 300 python scripts/composite_bench.py > $OUT/composite_bench.txt 2>&1 && echo "composite bench ok" && \
 timeout -k 10 600 python bench.py --steps ${STEPS:-30} --warmup 5 > $OUT/bench.json 2> $OUT/bench.err && \
 echo "bench ok" && \
 cd /tmp && export TMPDIR=/tmp && \
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err && \
-echo "prof ok"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-alt > $OUT/prof_bench.json 2> $OUT/prof.err && \
+echo "prof ok" && \
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run -- python $R/scripts/gemm_bench.py --quick --x6 > $OUT/pmc_fetch.log 2>&1 && \
+echo "pmc fetch ok" && \
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE -d $OUT/pmc_write -o run -- python $R/scripts/gemm_bench.py --quick --x6 > $OUT/pmc_write.log 2>&1 && \
+echo "pmc write ok"

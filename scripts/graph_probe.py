@@ -17,6 +17,7 @@ def main():
     dev = torch.device("cuda")
     from model import _hip
     _hip.load_library()
+    _hip.gemm_set_precision(1 if "--x6" in sys.argv else 0)
     cfg = bench.make_cfg()
     data, c2w = bench.synthetic_scene(dev)
     trainer, net = bench.build_trainer(dev, c2w, cfg)

@@ -86,6 +86,7 @@ def test_linear_bwd_data(dev, gemm_precision):
 
 
 @pytest.mark.parametrize("nout,kin,m,splits", [(256, 256, 4096, 8), (128, 320, 2048, 4), (256, 64, 1024, 1),
+                                               (256, 320, 32768, 64), (128, 256, 12288, 48),
                                                (64, 128, 2048, 2)])
 def test_linear_bwd_weight_and_reduce(dev, gemm_precision, nout, kin, m, splits):
     g = torch.Generator().manual_seed(nout + kin)
@@ -107,6 +108,28 @@ def test_linear_bwd_weight_and_reduce(dev, gemm_precision, nout, kin, m, splits)
     scale = ref.abs().max().item()
     assert (gw.cpu().double() - ref[:, :kin_ref]).abs().max().item() < 2e-5 * scale
     assert (gb.cpu().double() - dy.double().sum(0)).abs().max().item() < 1e-4 * max(1, dy.abs().sum(0).max().item())
+
+
+def test_slab_reduce_accumulate(dev):
+    """nerf_slab_reduce with accumulate=1 adds onto the existing gradient (train.py's
+    gradient accumulation across render calls); split sums in a fixed order."""
+    g = torch.Generator().manual_seed(9)
+    splits, nout, ld, kin_ref = 37, 64, 136, 130
+    slab = _rand(splits * nout * ld, g=g).to(dev)
+    bslab = _rand(splits * nout, g=g).to(dev)
+    gw0 = _rand(nout, kin_ref, g=g).to(dev)
+    gb0 = _rand(nout, g=g).to(dev)
+    gw, gb = gw0.clone(), gb0.clone()
+    _hip.slab_reduce(slab, splits, nout, ld, nout, kin_ref, bslab, gw, gb, accumulate=True)
+    gw2, gb2 = torch.empty_like(gw), torch.empty_like(gb)
+    _hip.slab_reduce(slab, splits, nout, ld, nout, kin_ref, bslab, gw2, gb2)
+    _hip.slab_reduce(slab, splits, nout, ld, nout, kin_ref, bslab, gw2, gb2, accumulate=True)
+    torch.cuda.synchronize()
+    ref = slab.view(splits, nout, ld)[:, :, :kin_ref].double().sum(0)
+    assert (gw.double() - gw0.double() - ref).abs().max().item() < 1e-4
+    assert (gb.double() - gb0.double() - bslab.view(splits, nout).double().sum(0)).abs().max().item() < 1e-4
+    assert torch.equal(gw2, 2 * (gw2 / 2))      # finite
+    assert torch.allclose(gw2, 2 * (gw - gw0), atol=1e-4)
 
 
 @pytest.mark.parametrize("scale_a,scale_b", [(1.0, 0.1), (1e-3, 1e3), (1e-20, 1.0)])
