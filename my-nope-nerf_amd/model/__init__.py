@@ -2,10 +2,11 @@
 
 ``sys.path.insert(0, '<repo>/my-nope-nerf_amd'); import model as mdl`` exposes the
 names the reference's train.py uses (mdl.OfficialStaticNerf, mdl.Renderer,
-mdl.get_model, mdl.LearnPose, mdl.Learn_Distortion, mdl.Trainer), backed by the
-nerf_hip kernels.  Out of scope: LearnFocal, CheckpointIO,
+mdl.get_model, mdl.LearnPose, mdl.Learn_Distortion, mdl.Trainer, mdl.CheckpointIO),
+backed by the nerf_hip kernels.  Out of scope: LearnFocal,
 Trainer_pose, DPT.
 """
+from .checkpoints import CheckpointIO
 from .config import get_model
 from .distortions import Learn_Distortion
 from .network import nope_nerf
@@ -14,5 +15,5 @@ from .poses import LearnPose
 from .rendering import Renderer
 from .training import Trainer
 
-__all__ = ["get_model", "Learn_Distortion", "nope_nerf", "OfficialStaticNerf", "LearnPose", "Renderer",
+__all__ = ["CheckpointIO", "get_model", "Learn_Distortion", "nope_nerf", "OfficialStaticNerf", "LearnPose", "Renderer",
            "Trainer"]

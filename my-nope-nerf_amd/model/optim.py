@@ -1,7 +1,9 @@
 """Adam on one flat fp32 buffer with a single nerf_adam_step launch per step.
 
 Same update as torch.optim.Adam (amsgrad=False, train.py:59 / :100 / :118 use the
-defaults betas=(0.9, 0.999), eps=1e-8).  At construction the parameters' storage is
+defaults betas=(0.9, 0.999), eps=1e-8), and the same state_dict format (per-parameter
+``step`` / ``exp_avg`` / ``exp_avg_sq``), so optimizer states in reference checkpoints
+(checkpoints.py:29-41, key ``optimizer``) load here and vice versa.  At construction the parameters' storage is
 moved into one contiguous buffer (each ``p.data`` becomes a view of it) so the update
 is one launch; the FieldRunner backward already produces the NeRF gradients as views of
 one flat buffer in parameter order, in which case no gather copy is made either.
@@ -25,10 +27,12 @@ class HipAdam(torch.optim.Optimizer):
         n = sum(p.numel() for p in ps)
         self._flat = torch.empty(n, device=dev, dtype=torch.float32)
         off = 0
+        self._slices = {}
         for p in ps:
             k = p.numel()
             self._flat[off:off + k].copy_(p.data.reshape(-1))
             p.data = self._flat[off:off + k].view_as(p)
+            self._slices[id(p)] = (off, k)
             off += k
         self._params = ps
         self._m = torch.zeros_like(self._flat)
@@ -62,6 +66,53 @@ class HipAdam(torch.optim.Optimizer):
             if ok:
                 return torch.as_strided(g0, (self._flat.numel(),), (1,))
         return torch.cat([g.reshape(-1) for g in gs])
+
+    # ---- torch.optim.Adam-compatible state_dict --------------------------------------
+    _ADAM_DEFAULTS = {"amsgrad": False, "maximize": False, "foreach": None, "capturable": False,
+                      "differentiable": False, "fused": None}
+
+    def state_dict(self):
+        sd = super().state_dict()
+        g = sd["param_groups"][0]
+        for k, v in self._ADAM_DEFAULTS.items():
+            g.setdefault(k, v)
+        step = float(self._hyper[0].item())
+        if step > 0:
+            for idx, p in enumerate(self.param_groups[0]["params"]):
+                if id(p) not in self._slices:
+                    continue
+                off, k = self._slices[id(p)]
+                sd["state"][idx] = {"step": torch.tensor(step, dtype=torch.float32),
+                                    "exp_avg": self._m[off:off + k].view_as(p).clone(),
+                                    "exp_avg_sq": self._v[off:off + k].view_as(p).clone()}
+        return sd
+
+    @torch.no_grad()
+    def load_state_dict(self, state_dict):
+        groups = state_dict["param_groups"]
+        if len(groups) != 1 or len(groups[0]["params"]) != len(self.param_groups[0]["params"]):
+            raise ValueError("HipAdam.load_state_dict: parameter groups do not match")
+        g = self.param_groups[0]
+        for k in ("lr", "betas", "eps", "weight_decay"):
+            if k in groups[0]:
+                g[k] = groups[0][k]
+        if groups[0].get("amsgrad", False):
+            raise ValueError("HipAdam: amsgrad states are not supported")
+        self._m.zero_()
+        self._v.zero_()
+        step = 0.0
+        pos = {pid: i for i, pid in enumerate(groups[0]["params"])}
+        for pid, st in state_dict["state"].items():
+            p = g["params"][pos[pid]]
+            if id(p) not in self._slices:
+                continue
+            off, k = self._slices[id(p)]
+            self._m[off:off + k].copy_(st["exp_avg"].reshape(-1))
+            self._v[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+            step = float(st["step"])
+        self._hyper_host = None
+        self._sync_hyper()
+        self._hyper[0].fill_(step)
 
     @torch.no_grad()
     def step(self, closure=None):

@@ -69,3 +69,57 @@ def test_ray_sharded_gradients_equal_full_batch():
         g0, g1 = torch.from_numpy(g0), torch.from_numpy(g1)
         assert torch.allclose(g0, g1)                       # every rank holds the same average
         assert torch.allclose(g0, p.grad, atol=1e-6, rtol=1e-4)
+
+
+def _render_worker(rank, world, port, q, n_rays):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from model.render_dist import render_frame_sharded, tile_bounds
+    torch.manual_seed(0)
+    net = orc.OracleNerf(hidden_dim=16)
+    b = synthetic_rays(R=n_rays, S=8, H=30, W=40, seed=11)
+    seen = []
+
+    def tile(start, end):                   # the CPU restatement stands in for the HIP renderer
+        seen.append((start, end))
+        with torch.no_grad():
+            o = orc.render_nope_nerf(net, b["pixels"][:, start:end], b["depth"][:, start:end], b["K"], b["w2c"],
+                                     b["scale"], {"num_points": 8}, noise=None, eval_=True)
+        return o["rgb"].reshape(-1, 3), o["depth_pred"].reshape(-1)
+
+    rgb, depth = render_frame_sharded(tile, n_rays, torch.device("cpu"))
+    assert seen == [tile_bounds(n_rays, rank, world)[:2]]     # one contiguous tile per rank
+    q.put((rank, rgb.numpy(), depth.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_full_frame_render_sharded_all_gather():
+    """config 4: contiguous ray tiles per rank (last one padded) + one all-gather give
+    every rank the frame the single-process render produces (uneven split: 3 ranks)."""
+    world, n_rays = 3, 1000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_render_worker, args=(r, world, port, q, n_rays)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, rgb, depth = q.get(timeout=120)
+        res[r] = (torch.from_numpy(rgb), torch.from_numpy(depth))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    net = orc.OracleNerf(hidden_dim=16)
+    b = synthetic_rays(R=n_rays, S=8, H=30, W=40, seed=11)
+    with torch.no_grad():
+        o = orc.render_nope_nerf(net, b["pixels"], b["depth"], b["K"], b["w2c"], b["scale"], {"num_points": 8},
+                                 noise=None, eval_=True)
+    for r in range(world):
+        assert res[r][0].shape == (n_rays, 3)
+        assert torch.allclose(res[r][0], o["rgb"].reshape(-1, 3), atol=1e-6)
+        assert torch.allclose(res[r][1], o["depth_pred"].reshape(-1), atol=1e-5)
+        assert torch.equal(res[r][0], res[0][0])

@@ -125,3 +125,25 @@ def test_points_forward_api(dev, gemm_precision):
     rgb_r, dens_r = ref(p, d)
     assert _rel(rgb.cpu(), rgb_r) < RTOL
     assert _rel(dens.cpu(), dens_r) < RTOL
+
+
+def test_render_image_full_frame(dev, gemm_precision):
+    """model.render_dist.render_image (the config-4 render caller, single rank): every
+    pixel of a small frame in eval mode (depth prior ones, z-depth output) vs the oracle."""
+    from model.render_dist import render_image
+    from tests.helpers import camera_K, rigid_c2w
+    H, W = 24, 40
+    cfg = make_cfg(hidden=64, S=32)
+    net, ref = _pair(cfg, 4)
+    rnd = Renderer(net.to(dev), cfg["rendering"], device=dev)
+    K = camera_K(H, W, 30.0, 30.0)
+    w2c = torch.inverse(rigid_c2w(2)).unsqueeze(0)
+    scale = torch.eye(4).unsqueeze(0)
+    pix = orc.arange_pixels(H, W)[1]
+    rgb, depth = render_image(rnd, pix.to(dev), K.to(dev), w2c.to(dev), scale.to(dev))
+    with torch.no_grad():
+        o = orc.render_nope_nerf(ref, pix, torch.ones(1, H * W, 1), K, w2c, scale, cfg["rendering"], noise=None,
+                                 eval_=True)
+    assert rgb.shape == (H * W, 3) and depth.shape == (H * W,)
+    assert _rel(rgb.cpu(), o["rgb"].reshape(-1, 3)) < RTOL
+    assert _rel(depth.cpu(), o["depth_pred"].reshape(-1)) < RTOL
