@@ -229,9 +229,21 @@ def main():
         else:
             peak = FP32_MFMA_PEAK_TFLOPS
             kname = "k_gemm_nt/k_gemm_tn (FP32 MFMA 32x32x2, field MLP)"
+        traffic, traffic_note = None, None
+        tpath = os.path.join(ROOT, "profiles", "r01", "gemm_traffic.json")
+        if args.gemm_precision == "bf16x6" and os.path.exists(tpath):
+            # HBM bytes of one 256x256-tile forward launch (131072 x 256 x 256, mask out) from
+            # the committed rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE); algorithmic:
+            # x 134.2 MB + y 134.2 MB + ReLU bits 4.2 MB + weight image 0.4 MB = 273 MB
+            t = json.load(open(tpath))
+            fwd = [x for x in t["launches"] if "k_gemm_nt_x6<256, 256, 2, 2, 0>" in x["kernel"]]
+            if fwd:
+                traffic = fwd[0]["bytes"]
+                traffic_note = ("k_gemm_nt_x6<256,256> forward, one launch, bytes from profiles/r01/gemm_traffic.json "
+                                "(algorithmic 2.73e8)")
         roof = {"bound": "mfma", "kernel": kname,
                 "achieved": achieved, "peak": peak, "unit": "TFLOP/s (f32-equivalent)",
-                "frac": (achieved / peak) if achieved else None, "traffic": None,
+                "frac": (achieved / peak) if achieved else None, "traffic": traffic, "traffic_note": traffic_note,
                 "achieved_union": achieved_union,
                 "frac_union": (achieved_union / peak) if achieved_union else None,
                 "algorithmic_gflop_per_step": alg / args.steps / 1e9,
