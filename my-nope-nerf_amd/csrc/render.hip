@@ -486,6 +486,262 @@ __global__ __launch_bounds__(256) void k_composite_bwd(const float* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// Compositing, 16 lanes per ray (4 rays per wave), lane l owns samples [l*J, l*J + J)
+// (S <= 256).  Scans and sums over a ray are 4-step DPP row operations (a DPP row is
+// exactly one ray), amortised over J samples per lane, and the activations use the
+// hardware transcendentals (v_exp_f32 / v_log_f32 / v_rcp_f32, a few ulp): with the
+// wave-per-ray kernels above the kernel was VALU-bound (~40 % of the HBM roofline at
+// 2^20 rays); these keep it on HBM.
+// ---------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float old, float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
+                                                                  CTRL, 0xF, 0xF, false));
+}
+// inclusive product scan over each 16-lane row (row_shr n; lanes without a source keep 1)
+__device__ __forceinline__ float row_scan_mul(float v) {
+    v *= dpp_f<0x111>(1.f, v);
+    v *= dpp_f<0x112>(1.f, v);
+    v *= dpp_f<0x114>(1.f, v);
+    v *= dpp_f<0x118>(1.f, v);
+    return v;
+}
+// inclusive suffix sum over each 16-lane row (row_shl n)
+__device__ __forceinline__ float row_suffix_add(float v) {
+    v += dpp_f<0x101>(0.f, v);
+    v += dpp_f<0x102>(0.f, v);
+    v += dpp_f<0x104>(0.f, v);
+    v += dpp_f<0x108>(0.f, v);
+    return v;
+}
+// sum over each 16-lane row, in every lane (quad_perm [1,0,3,2], [2,3,0,1], half-mirror, mirror)
+__device__ __forceinline__ float row_sum(float v) {
+    v += dpp_f<0xB1>(0.f, v);
+    v += dpp_f<0x4E>(0.f, v);
+    v += dpp_f<0x141>(0.f, v);
+    v += dpp_f<0x140>(0.f, v);
+    return v;
+}
+
+__device__ __forceinline__ float f_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float f_sigmoid(float x) { return f_rcp(1.f + __expf(-x)); }
+// torch softplus(beta=1, threshold=20) and its derivative z / (z + 1)
+__device__ __forceinline__ float f_softplus(float x) { return x > 20.f ? x : __logf(1.f + __expf(x)); }
+__device__ __forceinline__ float f_softplus_grad(float x) {
+    if (x > 20.f) return 1.f;
+    const float z = __expf(x);
+    return z * f_rcp(z + 1.f);
+}
+__device__ __forceinline__ float f_density(float raw, int flags) {
+    return (flags & F_RELU) ? fmaxf(raw, 0.f) : f_softplus(raw);
+}
+
+template <int J>
+struct Ray16 {
+    float alpha[J], f[J], T[J], w[J], c[J][3], z[J], sig[J], raw[J];
+    bool valid[J];
+};
+
+// alpha, colour sigmoid, exclusive transmittance of this lane's J samples
+// The block's raw4 rows (16 rays) staged in LDS with one 16-byte pad after every lane's
+// J samples: global loads stay fully coalesced and a lane's J consecutive samples sit at
+// a 16(J+1)-byte lane stride, conflict-free for ds_read_b128.
+template <int J>
+__device__ __forceinline__ int stage_slot(int r_local, int i) { return (r_local * 16 + i / J) * (J + 1) + i % J; }
+
+// ray-local (row, sample) of the c-th staged element; shifts when S is a power of two
+__device__ __forceinline__ void split_rs(int c, int S, int lgS, int& r, int& i) {
+    if (lgS >= 0) { r = c >> lgS; i = c & (S - 1); }
+    else { r = c / S; i = c - r * S; }
+}
+
+template <int J>
+__device__ __forceinline__ void stage_raw(const float* __restrict__ raw4, float4* lds, int ray0, int R, int S,
+                                          int lgS) {
+    const int nr = min(16, R - ray0);
+    if (nr <= 0) return;
+    const float4* src = reinterpret_cast<const float4*>(raw4) + (size_t)ray0 * S;
+    for (int c = threadIdx.x; c < nr * S; c += blockDim.x) {
+        int r, i;
+        split_rs(c, S, lgS, r, i);
+        lds[stage_slot<J>(r, i)] = src[c];
+    }
+}
+
+template <int J>
+__device__ __forceinline__ void load_ray16(const float4* __restrict__ lraw, const float* __restrict__ zv, int ray,
+                                           bool active, int S, int flags, Ray16<J>& rs) {
+    const int l16 = threadIdx.x & 15;
+    const size_t base = (size_t)ray * S;
+    const int i0 = l16 * J;
+    // z of this lane's samples (float4 when aligned), and of the next lane's first sample
+    if (J % 4 == 0 && (S & 3) == 0 && active && i0 + J <= S) {
+#pragma unroll
+        for (int q = 0; q < J / 4; ++q) {
+            const float4 v = *reinterpret_cast<const float4*>(zv + base + i0 + 4 * q);
+            rs.z[4 * q] = v.x; rs.z[4 * q + 1] = v.y; rs.z[4 * q + 2] = v.z; rs.z[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < J; ++j) rs.z[j] = (active && i0 + j < S) ? zv[base + i0 + j] : 0.f;
+    }
+    const float z_next = dpp_f<0x101>(0.f, rs.z[0]);   // lane l+1's first sample (row_shl 1)
+    float pl = 1.f;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int i = i0 + j;
+        rs.valid[j] = active && i < S;
+        float a = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f, sg = 0.f, r0 = 0.f;
+        if (rs.valid[j]) {
+            const float4 r = lraw[((threadIdx.x >> 4) * 16 + l16) * (J + 1) + j];
+            r0 = r.x;
+            sg = f_density(r.x, flags);
+            if (flags & F_DIST_ALPHA) {
+                if (i == S - 1) {
+                    a = 1.f;   // rendering.py:121
+                } else {
+                    const float zn = (j + 1 < J) ? rs.z[j + 1 < J ? j + 1 : 0] : z_next;
+                    a = 1.f - __expf(-1.0f * sg * (zn - rs.z[j]));
+                }
+            } else {
+                a = 1.f - __expf(-1.0f * sg);
+            }
+            c0 = f_sigmoid(r.y); c1 = f_sigmoid(r.z); c2 = f_sigmoid(r.w);
+        }
+        rs.sig[j] = sg;
+        rs.raw[j] = r0;
+        rs.alpha[j] = a;
+        rs.c[j][0] = c0; rs.c[j][1] = c1; rs.c[j][2] = c2;
+        const float f = rs.valid[j] ? (1.f - a + kEps) : 1.f;
+        rs.f[j] = f;
+        rs.T[j] = pl;
+        pl *= f;
+    }
+    const float excl = dpp_f<0x111>(1.f, row_scan_mul(pl));   // product over the lanes before this one
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        rs.T[j] *= excl;
+        rs.w[j] = rs.alpha[j] * rs.T[j];
+    }
+}
+
+template <int J>
+__global__ __launch_bounds__(256) void k_composite16_fwd(const float* __restrict__ raw4, const float* __restrict__ zv,
+                                                         int R, int S, int flags, float* __restrict__ rgb,
+                                                         float* __restrict__ dist, float* __restrict__ alpha_out) {
+    __shared__ float4 lraw[256 * (J + 1)];
+    const int ray = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const bool active = ray < R;       // a 16-lane DPP row is one ray: whole rows are (in)active
+    const int l16 = threadIdx.x & 15;
+    const int lgS = (S & (S - 1)) == 0 ? __builtin_ctz(S) : -1;
+    stage_raw<J>(raw4, lraw, blockIdx.x * 16, R, S, lgS);
+    __syncthreads();
+    Ray16<J> rs;
+    load_ray16<J>(lraw, zv, ray, active, S, flags, rs);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, sd = 0.f, sw = 0.f;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        s0 += rs.w[j] * rs.c[j][0];
+        s1 += rs.w[j] * rs.c[j][1];
+        s2 += rs.w[j] * rs.c[j][2];
+        sd += rs.w[j] * rs.z[j];
+        sw += rs.w[j];
+    }
+    const size_t a0 = (size_t)ray * S + l16 * J;
+    if (J % 4 == 0 && (S & 3) == 0 && active && l16 * J + J <= S) {
+#pragma unroll
+        for (int q = 0; q < J / 4; ++q)
+            *reinterpret_cast<float4*>(alpha_out + a0 + 4 * q) =
+                make_float4(rs.alpha[4 * q], rs.alpha[4 * q + 1], rs.alpha[4 * q + 2], rs.alpha[4 * q + 3]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+            if (rs.valid[j]) alpha_out[a0 + j] = rs.alpha[j];
+    }
+    s0 = row_sum(s0); s1 = row_sum(s1); s2 = row_sum(s2); sd = row_sum(sd);
+    if (flags & F_WHITE_BKGD) sw = row_sum(sw);
+    if (active && l16 == 0) {
+        if (flags & F_WHITE_BKGD) {   // rendering.py:139-141
+            const float bg = 1.f - sw;
+            s0 += bg; s1 += bg; s2 += bg;
+        }
+        rgb[3 * ray + 0] = s0;
+        rgb[3 * ray + 1] = s1;
+        rgb[3 * ray + 2] = s2;
+        dist[ray] = sd;
+    }
+}
+
+template <int J>
+__global__ __launch_bounds__(256) void k_composite16_bwd(const float* __restrict__ raw4, const float* __restrict__ zv,
+                                                         int R, int S, int flags, const float* __restrict__ g_rgb,
+                                                         const float* __restrict__ g_dist,
+                                                         float* __restrict__ graw4, int n_pad) {
+    const int gtid = blockIdx.x * blockDim.x + threadIdx.x;
+    for (size_t s = (size_t)R * S + gtid; s < (size_t)n_pad; s += (size_t)gridDim.x * blockDim.x)
+        *reinterpret_cast<float4*>(graw4 + 4 * s) = make_float4(0.f, 0.f, 0.f, 0.f);
+    __shared__ float4 lraw[256 * (J + 1)];
+    const int ray = gtid >> 4;
+    const bool active = ray < R;
+    const int l16 = threadIdx.x & 15;
+    const int lgS = (S & (S - 1)) == 0 ? __builtin_ctz(S) : -1;
+    stage_raw<J>(raw4, lraw, blockIdx.x * 16, R, S, lgS);
+    __syncthreads();
+    Ray16<J> rs;
+    load_ray16<J>(lraw, zv, ray, active, S, flags, rs);
+    __syncthreads();   // lraw is reused for the gradient rows below
+    const float gc0 = active ? g_rgb[3 * ray] : 0.f, gc1 = active ? g_rgb[3 * ray + 1] : 0.f;
+    const float gc2 = active ? g_rgb[3 * ray + 2] : 0.f, gd = active ? g_dist[ray] : 0.f;
+    const float gbg = (flags & F_WHITE_BKGD) ? -(gc0 + gc1 + gc2) : 0.f;
+    float gw[J], lsum = 0.f;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        gw[j] = rs.valid[j] ? (gc0 * rs.c[j][0] + gc1 * rs.c[j][1] + gc2 * rs.c[j][2] + gd * rs.z[j] + gbg) : 0.f;
+        lsum += gw[j] * rs.w[j];
+    }
+    // suffix sums S_i = sum_{k>i} g_w_k w_k: lanes after this one, then this lane's samples
+    float suffix = dpp_f<0x101>(0.f, row_suffix_add(lsum));
+    const float z_next = dpp_f<0x101>(0.f, rs.z[0]);
+#pragma unroll
+    for (int j = J - 1; j >= 0; --j) {
+        if (!rs.valid[j]) continue;
+        const int i = l16 * J + j;
+        const size_t s = (size_t)ray * S + i;
+        const float ga = rs.T[j] * gw[j] - suffix * f_rcp(rs.f[j]);   // d alpha_i
+        suffix += gw[j] * rs.w[j];
+        const float sig = rs.sig[j];
+        const float dact = (flags & F_RELU) ? (sig > 0.f ? 1.f : 0.f) : f_softplus_grad(rs.raw[j]);
+        float graw;
+        if (flags & F_DIST_ALPHA) {
+            if (i == S - 1) {
+                graw = 0.f;
+            } else {
+                const float delta = ((j + 1 < J) ? rs.z[j + 1 < J ? j + 1 : 0] : z_next) - rs.z[j];
+                graw = ga * __expf(-1.0f * sig * delta) * delta * dact;
+            }
+        } else {
+            graw = ga * __expf(-1.0f * sig) * dact;
+        }
+        const float gcw = rs.w[j];
+        float4 o;
+        o.x = graw;
+        o.y = gcw * gc0 * (1.f - rs.c[j][0]) * rs.c[j][0];
+        o.z = gcw * gc1 * (1.f - rs.c[j][1]) * rs.c[j][1];
+        o.w = gcw * gc2 * (1.f - rs.c[j][2]) * rs.c[j][2];
+        (void)s;
+        lraw[((threadIdx.x >> 4) * 16 + l16) * (J + 1) + j] = o;
+    }
+    __syncthreads();
+    const int ray0 = blockIdx.x * 16, nr = min(16, R - ray0);
+    float4* dst = reinterpret_cast<float4*>(graw4) + (size_t)ray0 * S;
+    for (int c = threadIdx.x; c < nr * S; c += blockDim.x) {
+        int r, i;
+        split_rs(c, S, lgS, r, i);
+        dst[c] = lraw[stage_slot<J>(r, i)];
+    }
+}
+
+// ---------------------------------------------------------------------------
 // gradient back to the ray inputs (pose / ray learning)
 // ---------------------------------------------------------------------------
 template <int L, int LD>
@@ -644,11 +900,26 @@ extern "C" int nerf_heads_reduce(const float* part, int hidden, int n_pad, float
         else NERF_CHECK(false, "%s: n_samples=%d > 1024", __func__, (int)(S));     \
     } while (0)
 
+#define NERF_J16_DISPATCH(KERNEL, S, ...)                                          \
+    do {                                                                           \
+        const int J_ = ((S) + 15) / 16;                                            \
+        if (J_ <= 1) hipLaunchKernelGGL((KERNEL<1>), __VA_ARGS__);                 \
+        else if (J_ == 2) hipLaunchKernelGGL((KERNEL<2>), __VA_ARGS__);            \
+        else if (J_ <= 4) hipLaunchKernelGGL((KERNEL<4>), __VA_ARGS__);            \
+        else if (J_ <= 8) hipLaunchKernelGGL((KERNEL<8>), __VA_ARGS__);            \
+        else hipLaunchKernelGGL((KERNEL<16>), __VA_ARGS__);                        \
+    } while (0)
+
 extern "C" int nerf_composite_fwd(const float* raw4, const float* z, int n_rays, int n_samples, int flags,
                                   float* rgb, float* dist, float* alpha, void* stream) {
     NERF_CHECK_PTR(raw4); NERF_CHECK_PTR(z); NERF_CHECK_PTR(rgb); NERF_CHECK_PTR(dist); NERF_CHECK_PTR(alpha);
     NERF_CHECK_ALIGN16(raw4);
     NERF_CHECK(n_rays > 0 && n_samples > 0, "%s: empty input", __func__);
+    if (n_samples <= 256) {   // 16 lanes per ray
+        NERF_J16_DISPATCH(k_composite16_fwd, n_samples, dim3((n_rays + 15) / 16), dim3(256), 0, as_stream(stream), raw4,
+                          z, n_rays, n_samples, flags, rgb, dist, alpha);
+        return check_launch(__func__);
+    }
     const int blocks = (n_rays + 3) / 4;
     NERF_J_DISPATCH(k_composite_fwd, n_samples, dim3(blocks), dim3(256), 0, as_stream(stream), raw4, z,
                     n_rays, n_samples, flags, rgb, dist, alpha);
@@ -662,6 +933,11 @@ extern "C" int nerf_composite_bwd(const float* raw4, const float* z, int n_rays,
     NERF_CHECK_PTR(graw4);
     NERF_CHECK_ALIGN16(raw4); NERF_CHECK_ALIGN16(graw4);
     NERF_CHECK(n_rays > 0 && n_samples > 0 && (int64_t)n_rays * n_samples <= n_pad, "%s: bad sizes", __func__);
+    if (n_samples <= 256) {
+        NERF_J16_DISPATCH(k_composite16_bwd, n_samples, dim3((n_rays + 15) / 16), dim3(256), 0, as_stream(stream), raw4,
+                          z, n_rays, n_samples, flags, grad_rgb, grad_dist, graw4, n_pad);
+        return check_launch(__func__);
+    }
     const int blocks = (n_rays + 3) / 4;
     NERF_J_DISPATCH(k_composite_bwd, n_samples, dim3(blocks), dim3(256), 0, as_stream(stream), raw4, z,
                     n_rays, n_samples, flags, grad_rgb, grad_dist, graw4, n_pad);
