@@ -186,9 +186,10 @@ int nerf_pack_weights(const nerf_pack_desc* descs, int n, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Adam (torch.optim.Adam semantics, amsgrad False) over one flat fp32 buffer.
- * Replaces optimizer.step() (training.py:93-99).  hyper (device, 6 floats) =
- * {step, lr, beta1, beta2, eps, weight_decay}; the call increments step on the device
- * first, so a captured graph replays the correct bias corrections. */
+ * Replaces optimizer.step() (training.py:93-99).  hyper (device, 8 floats) =
+ * {step, lr, beta1, beta2, eps, weight_decay, 0, ticket}; the update uses step + 1 and
+ * the last workgroup to finish stores it back (one launch; a captured graph replays the
+ * correct bias corrections).  hyper[7] is a completion counter: zero it once. */
 int nerf_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                    int64_t n, float* hyper, void* stream);
 
@@ -197,6 +198,68 @@ int nerf_adam_step(float* param, const float* grad, float* exp_avg, float* exp_a
  * (losses.py:129-150): idx[i] = argmin_j |x[i] - y[j]| (first index on ties).
  * x: [p][3], y: [q][3] fp32, idx: int64 [p]. */
 int nerf_chamfer_nn(const float* x, int p, const float* y, int q, int64_t* idx, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Ray prologue / loss epilogue of the training step (rays.hip).
+ *
+ * nerf_sample_rays: R distinct pixel indices drawn uniformly from [0, n_pix), the set
+ *   torch.randperm(n_pix)[:R] draws (training.py:277-283), from a Philox-4x32-10 stream
+ *   keyed by `seed` (deterministic in (seed, n_pix, R)); optionally the pixel coordinates
+ *   of arange_pixels (common.py:13-40; pixels [R][2], needs width*height == n_pix) and the
+ *   colours img.view(3, H*W)[:, idx]^T (rgb [R][3], img = [3][H][W]).  One workgroup.
+ *   Requires R <= NERF_SAMPLE_MAX_RAYS and n_pix >= 2R.  status (optional, int) receives
+ *   the number of draw rounds used, 0 if NERF_SAMPLE_MAX_ROUNDS did not suffice. */
+#define NERF_SAMPLE_MAX_RAYS 4096
+#define NERF_SAMPLE_MAX_ROUNDS 64
+int nerf_sample_rays(int n_pix, int n_rays, uint64_t seed, int width, int height, const float* img,
+                     int64_t* idx, float* pixels, float* rgb, int* status, void* stream);
+
+/* Batched 4x4 inverse (torch.inverse / linalg.inv_ex, common.py:139-141, training.py:255-257):
+ * Gauss-Jordan with partial pivoting, a [n][4][4] -> out [n][4][4]. */
+int nerf_mat4_inv(const float* a, int n, float* out, void* stream);
+
+/* LearnPose.forward (poses.py:23-31, common.py:277-310): c2w = [Exp(r) | t; 0 0 0 1] @ init_c2w
+ * with Exp(r) = I + sin(th)/th [r]x + (1-cos th)/th^2 [r]x^2, th = |r| + 1e-15.
+ * r, t: [3]; init_c2w: [4][4] or NULL (identity). */
+int nerf_pose_c2w(const float* r, const float* t, const float* init_c2w, float* c2w, void* stream);
+
+/* Unprojection matrix M = (inv(scale) @ inv(world)) @ inv(K) (common.py:139-141, 205-208).
+ * inverses (optional, [3][4][4]) = {inv(K), inv(world), inv(scale)} for the backward. */
+int nerf_unproject_matrix(const float* K, const float* world, const float* scale, float* M,
+                          float* inverses, void* stream);
+
+/* Camera rays of Renderer.nope_nerf (rendering.py:52-80): for pixels [R][2], depth [R]
+ * (NULL = no depth prior, d_src = 1): cam [R][3] = M[:3,3]; v = M[:3,:3](x,y,1);
+ * ray_norm = |v|; ray = v/|v| (NERF_RAYS_NORMALISE) else v; d_src = |M[:3,:3](xd,yd,d)|
+ * (divided by |v| without NORMALISE); mask [R] (u8, optional) = isfinite(d_src) & d_src != 0;
+ * view [R][3] (optional) = -ray, or 1 with NERF_RAYS_VIEW_ONES (use_ray_dir False). */
+#define NERF_RAYS_NORMALISE 1
+#define NERF_RAYS_VIEW_ONES 2
+int nerf_camera_rays(const float* M, const float* pixels, const float* depth, int n_rays, int flags,
+                     float* cam, float* ray, float* view, float* ray_norm, float* d_src, uint8_t* mask,
+                     void* stream);
+/* Its backward: upstream gradients (each optional) -> gM [4][4] (row 3 zero) and
+ * g_depth [R] (optional).  One workgroup, deterministic. */
+int nerf_camera_rays_bwd(const float* M, const float* pixels, const float* depth, int n_rays, int flags,
+                         const float* g_cam, const float* g_ray, const float* g_view, const float* g_norm,
+                         const float* g_dsrc, float* gM, float* g_depth, void* stream);
+
+/* Loss.forward's render terms (losses.py:28-33, 60-66, 195-228), four device scalars:
+ * total = w_rgb l_rgb + w_depth l_depth, l_rgb = sum|e| or sum e^2 over rgb [R][3] / R,
+ * l_depth = sum over mask of |depth_pred - depth_gt| / max(count, 1), l2_mean = mean e^2;
+ * cnt receives count.
+ * depth_pred NULL = no depth term; mask NULL = all n_depth rays.  One workgroup. */
+int nerf_ray_loss(const float* rgb, const float* rgb_gt, int n_rays, const float* depth_pred,
+                  const float* depth_gt, const uint8_t* mask, int n_depth, int rgb_l1, float w_rgb,
+                  float w_depth, float* total, float* l_rgb, float* l_depth, float* l2_mean, float* cnt,
+                  void* stream);
+/* Its backward: the four upstream scalars (device, each optional) -> g_rgb [R][3],
+ * g_depth_pred [n_depth], g_depth_gt [n_depth] (each optional). */
+int nerf_ray_loss_bwd(const float* rgb, const float* rgb_gt, int n_rays, const float* depth_pred,
+                      const float* depth_gt, const uint8_t* mask, int n_depth, int rgb_l1, float w_rgb,
+                      float w_depth, const float* go_total, const float* go_rgb, const float* go_depth,
+                      const float* go_l2, const float* cnt, float* g_rgb, float* g_depth_pred,
+                      float* g_depth_gt, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Timing hooks for bench.py: when enabled, every GEMM launch is bracketed by

@@ -65,12 +65,11 @@ __global__ void k_pack(PackBatch pb) {
 //   g += wd*p; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2
 //   denom = sqrt(v)/sqrt(bc2) + eps;  p -= (lr/bc1) * m / denom
 // Hyper-parameters and the step count live in device memory (hyper = {step, lr, b1, b2,
-// eps, wd}) so a captured hipGraph replays correct bias corrections and picks up lr changes.
-__global__ void k_adam_tick(float* hyper) { hyper[0] += 1.f; }
-
+// eps, wd, -, ticket}) so a captured hipGraph replays correct bias corrections and picks up
+// lr changes.  Every workgroup uses step + 1; the last one to finish (ticket) stores it.
 __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                       float* __restrict__ v, int64_t n, const float* __restrict__ hyper) {
-    const float step = hyper[0], lr = hyper[1], b1 = hyper[2], b2 = hyper[3], eps = hyper[4], wd = hyper[5];
+                       float* __restrict__ v, int64_t n, float* __restrict__ hyper) {
+    const float step = hyper[0] + 1.f, lr = hyper[1], b1 = hyper[2], b2 = hyper[3], eps = hyper[4], wd = hyper[5];
     const float bc1 = 1.f - powf(b1, step);
     const float sbc2 = sqrtf(1.f - powf(b2, step));
     const float step_size = lr / bc1;
@@ -83,6 +82,14 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
         v[i] = vi;
         const float denom = sqrtf(vi) / sbc2 + eps;
         p[i] = p[i] + (-step_size * mi) / denom;  // addcdiv_(m, denom, value=-step_size)
+    }
+    __syncthreads();                              // this workgroup has read hyper[0]
+    if (threadIdx.x == 0) {
+        unsigned* ticket = reinterpret_cast<unsigned*>(hyper + 7);
+        if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+            hyper[0] = step;
+            *ticket = 0u;
+        }
     }
 }
 
@@ -147,9 +154,7 @@ extern "C" int nerf_adam_step(float* param, const float* grad, float* exp_avg, f
     int64_t blocks = (n + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     hipStream_t s = as_stream(stream);
-    hipLaunchKernelGGL(k_adam_tick, dim3(1), dim3(1), 0, s, hyper);
-    hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, s, param, grad, exp_avg, exp_avg_sq, n,
-                       (const float*)hyper);
+    hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, s, param, grad, exp_avg, exp_avg_sq, n, hyper);
     return check_launch(__func__);
 }
 

@@ -21,6 +21,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NERF_HIP_LIB", os.path.join(_HERE, "..", "lib", "libnerf_hip.so"))
 
 ROW_TILE = 128
+SAMPLE_MAX_RAYS = 4096      # NERF_SAMPLE_MAX_RAYS
+RAYS_NORMALISE = 1          # NERF_RAYS_NORMALISE
+RAYS_VIEW_ONES = 2          # NERF_RAYS_VIEW_ONES
 ENC_P = 64
 ENC_D = 64
 
@@ -62,6 +65,16 @@ _SIGS = {
     "nerf_gemm_get_precision": ([], _c_i),
     "nerf_gemm_debug_ablate": ([_c_i], _c_i),
     "nerf_gemm_debug_stamps": ([_c_p], _c_i),
+    "nerf_sample_rays": ([_c_i, _c_i, ctypes.c_uint64, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_mat4_inv": ([_c_p, _c_i, _c_p, _c_p], _c_i),
+    "nerf_pose_c2w": ([_c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_unproject_matrix": ([_c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_camera_rays": ([_c_p, _c_p, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_camera_rays_bwd": ([_c_p, _c_p, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_ray_loss": ([_c_p, _c_p, _c_i, _c_p, _c_p, _c_p, _c_i, _c_i, _c_f, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
+                       _c_p], _c_i),
+    "nerf_ray_loss_bwd": ([_c_p, _c_p, _c_i, _c_p, _c_p, _c_p, _c_i, _c_i, _c_f, _c_f, _c_p, _c_p, _c_p, _c_p,
+                           _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_prof_enable": ([_c_i], _c_i),
     "nerf_prof_read": ([ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_i64),
                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], _c_i),
@@ -105,7 +118,7 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
         return None
     if not t.is_cuda:
         raise RuntimeError("nerf_hip: tensor must live on the GPU (no CPU fallback)")
-    if t.dtype not in (torch.float32, torch.int64, torch.int32, torch.int16):
+    if t.dtype not in (torch.float32, torch.int64, torch.int32, torch.int16, torch.uint8, torch.bool):
         raise RuntimeError(f"nerf_hip: unsupported dtype {t.dtype}")
     return t.data_ptr()
 
@@ -211,10 +224,53 @@ def pack_weights(descs: Sequence[PackDesc]):
 
 
 def adam_step(param, grad, exp_avg, exp_avg_sq, hyper):
-    """hyper: device float32 [6] = (step, lr, beta1, beta2, eps, weight_decay); step is
-    incremented on the device before the update."""
+    """hyper: device float32 [8] = (step, lr, beta1, beta2, eps, weight_decay, -, ticket);
+    the update uses step + 1 and stores it back (ticket: zero-initialised counter)."""
+    if hyper.numel() < 8:
+        raise ValueError("adam_step: hyper needs 8 floats")
     _call("nerf_adam_step", _ptr(param), _ptr(grad), _ptr(exp_avg), _ptr(exp_avg_sq), param.numel(),
           _ptr(hyper), _stream())
+
+
+def sample_rays(n_pix, n_rays, seed, width, height, img, idx, pixels=None, rgb=None, status=None):
+    _call("nerf_sample_rays", int(n_pix), int(n_rays), int(seed) & 0xFFFFFFFFFFFFFFFF, int(width), int(height),
+          _ptr(img), _ptr(idx), _ptr(pixels), _ptr(rgb), _ptr(status), _stream())
+
+
+def mat4_inv(a, out):
+    _call("nerf_mat4_inv", _ptr(a), a.numel() // 16, _ptr(out), _stream())
+
+
+def pose_c2w(r, t, init_c2w, out):
+    _call("nerf_pose_c2w", _ptr(r), _ptr(t), _ptr(init_c2w), _ptr(out), _stream())
+
+
+def unproject_matrix(K, world, scale, M, inverses=None):
+    _call("nerf_unproject_matrix", _ptr(K), _ptr(world), _ptr(scale), _ptr(M), _ptr(inverses), _stream())
+
+
+def camera_rays(M, pixels, depth, n_rays, flags, cam, ray, view, ray_norm, d_src, mask):
+    _call("nerf_camera_rays", _ptr(M), _ptr(pixels), _ptr(depth), int(n_rays), int(flags), _ptr(cam), _ptr(ray),
+          _ptr(view), _ptr(ray_norm), _ptr(d_src), _ptr(mask), _stream())
+
+
+def camera_rays_bwd(M, pixels, depth, n_rays, flags, g_cam, g_ray, g_view, g_norm, g_dsrc, gM, g_depth):
+    _call("nerf_camera_rays_bwd", _ptr(M), _ptr(pixels), _ptr(depth), int(n_rays), int(flags), _ptr(g_cam),
+          _ptr(g_ray), _ptr(g_view), _ptr(g_norm), _ptr(g_dsrc), _ptr(gM), _ptr(g_depth), _stream())
+
+
+def ray_loss(rgb, rgb_gt, n_rays, depth_pred, depth_gt, mask, n_depth, rgb_l1, w_rgb, w_depth, out, cnt):
+    """out: four device scalars (total, l_rgb, l_depth, l2_mean)."""
+    _call("nerf_ray_loss", _ptr(rgb), _ptr(rgb_gt), int(n_rays), _ptr(depth_pred), _ptr(depth_gt), _ptr(mask),
+          int(n_depth), int(rgb_l1), float(w_rgb), float(w_depth), *[_ptr(o) for o in out], _ptr(cnt), _stream())
+
+
+def ray_loss_bwd(rgb, rgb_gt, n_rays, depth_pred, depth_gt, mask, n_depth, rgb_l1, w_rgb, w_depth, go, cnt,
+                 g_rgb, g_dp, g_dg):
+    """go: four upstream scalars (total, l_rgb, l_depth, l2_mean), each a device tensor or None."""
+    _call("nerf_ray_loss_bwd", _ptr(rgb), _ptr(rgb_gt), int(n_rays), _ptr(depth_pred), _ptr(depth_gt),
+          _ptr(mask), int(n_depth), int(rgb_l1), float(w_rgb), float(w_depth), *[_ptr(g) for g in go], _ptr(cnt),
+          _ptr(g_rgb), _ptr(g_dp), _ptr(g_dg), _stream())
 
 
 def chamfer_nn(x, y, idx):

@@ -11,6 +11,8 @@ import math
 import numpy as np
 import torch
 
+from . import rays as _rays
+
 
 def arange_pixels(resolution=(128, 128), batch_size=1, image_range=(-1.0, 1.0), device=torch.device("cpu")):
     """common.py:13-40 -> (integer (x, y) locations [B, H*W, 2], scaled locations)."""
@@ -32,14 +34,16 @@ def get_mask(t):
 
 
 def inv(m):
-    """torch.inverse without its host-side singularity check: ``torch.inverse`` reads the
-    LAPACK info back to the host (a device sync every call, 5+ per step); inv_ex runs the
-    same factorisation and leaves ``info`` on the device."""
-    return torch.linalg.inv_ex(m)[0]
+    """torch.inverse of [..., 4, 4]: the HIP batched inverse for device tensors (one launch,
+    no host-side singularity check or LAPACK info read-back), torch for host tensors."""
+    return _rays.inv(m)
 
 
 def unproject_matrix(camera_mat, world_mat, scale_mat):
-    """scale^-1 @ world^-1 @ K^-1 evaluated in the reference's association order."""
+    """scale^-1 @ world^-1 @ K^-1 evaluated in the reference's association order
+    (common.py:139-141); one camera on the device is a single HIP launch."""
+    if camera_mat.is_cuda and camera_mat.numel() == world_mat.numel() == scale_mat.numel() == 16:
+        return _rays.unproject_matrix(camera_mat, world_mat, scale_mat)
     return (inv(scale_mat) @ inv(world_mat)) @ inv(camera_mat)
 
 

@@ -300,7 +300,7 @@ class FieldRenderFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, runner: FieldRunner, pts_o, pts_d, view, noise, near, far, S, flags, *params):
-        need = torch.is_grad_enabled() and any(ctx.needs_input_grad)
+        ctx.set_materialize_grads(False)      # alpha / z (and an unused dist) get no zero fill
         rgb, dist, alpha, z, st = runner.forward(pts_o, pts_d, view, noise, near, far, S, flags, keep=True)
         ctx.runner = runner
         ctx.state = st

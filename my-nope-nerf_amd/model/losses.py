@@ -16,6 +16,7 @@ from torch.nn import functional as F
 
 from . import _hip
 from .common import inv
+from .rays import ray_loss
 
 
 class Loss_Eval(nn.Module):
@@ -176,8 +177,19 @@ class Loss(nn.Module):
         zero = torch.zeros((), device=dev)
         rgb_gt = rgb_gt.to(dev) if rgb_gt is not None else None
         w = weights
-        l_rgb = self.get_rgb_full_loss(rgb_pred, rgb_gt, rgb_loss_type) if w["rgb_weight"] != 0.0 else zero
-        l_depth = self.get_depth_loss(depth_pred, depth_gt, depth_mask) if w["depth_weight"] != 0.0 else zero
+        fused = None
+        use_depth = w["depth_weight"] != 0.0
+        if (rgb_pred is not None and rgb_pred.is_cuda and (w["rgb_weight"] != 0.0 or use_depth)
+                and (not use_depth or self.depth_loss_type == "l1")):
+            # one launch for l_rgb, l_depth, l2_mean and their weighted sum; one for the backward
+            fused = ray_loss(rgb_pred, rgb_gt, depth_pred if use_depth else None,
+                             depth_gt if use_depth else None, depth_mask if use_depth else None,
+                             rgb_loss_type == "l1", w["rgb_weight"], w["depth_weight"])
+            l_rgb = fused[1] if w["rgb_weight"] != 0.0 else zero
+            l_depth = fused[2] if use_depth else zero
+        else:
+            l_rgb = self.get_rgb_full_loss(rgb_pred, rgb_gt, rgb_loss_type) if w["rgb_weight"] != 0.0 else zero
+            l_depth = self.get_depth_loss(depth_pred, depth_gt, depth_mask) if use_depth else zero
         if w["weight_dist_2nd_loss"] != 0.0 or w["weight_dist_1st_loss"] != 0.0:
             l_d1, l_d2 = self.get_weight_dist_loss(t_list)
         else:
@@ -187,13 +199,22 @@ class Loss(nn.Module):
         l_dc = (self.get_depth_consistency_loss(d1_proj, d2, d2_proj, d1)
                 if w["depth_consistency_weight"] != 0.0 else zero)
         l_tc = self.get_t_cycle_loss(kwargs["rt_12"], kwargs["rt_12_gt"]) if w["t_cycle_weight"] != 0.0 else zero
-        if w["rgb_weight"] != 0.0 or w["depth_weight"] != 0.0:
+        if fused is not None:
+            l2_mean = fused[3]
+        elif w["rgb_weight"] != 0.0 or w["depth_weight"] != 0.0:
             l2_mean = F.mse_loss(rgb_pred, rgb_gt)
         else:
             l2_mean = zero
-        loss = (w["rgb_weight"] * l_rgb + w["depth_weight"] * l_depth + w["weight_dist_1st_loss"] * l_d1
-                + w["weight_dist_2nd_loss"] * l_d2 + w["pc_weight"] * l_pc + w["rgb_s_weight"] * l_rgbs
-                + w["depth_consistency_weight"] * l_dc + w["t_cycle_weight"] * l_tc)
+        terms = [("weight_dist_1st_loss", l_d1), ("weight_dist_2nd_loss", l_d2), ("pc_weight", l_pc),
+                 ("rgb_s_weight", l_rgbs), ("depth_consistency_weight", l_dc), ("t_cycle_weight", l_tc)]
+        if fused is not None:
+            loss = fused[0]
+        else:
+            terms = [("rgb_weight", l_rgb), ("depth_weight", l_depth)] + terms
+            loss = zero
+        for name, term in terms:        # zero-weight terms add nothing (and launch nothing)
+            if w[name] != 0.0:
+                loss = loss + w[name] * term
         # losses.py:213-214 drops into breakpoint() on NaN; that forces a host sync every
         # step and is left to the caller here.
         return {"loss": loss, "loss_rgb": l_rgb, "loss_depth": l_depth, "l2_mean": l2_mean,

@@ -37,8 +37,8 @@ class HipAdam(torch.optim.Optimizer):
         self._params = ps
         self._m = torch.zeros_like(self._flat)
         self._v = torch.zeros_like(self._flat)
-        # {step, lr, beta1, beta2, eps, weight_decay} on the device (graph-replay safe)
-        self._hyper = torch.zeros(6, device=dev, dtype=torch.float32)
+        # {step, lr, beta1, beta2, eps, weight_decay, -, ticket} on the device (graph-replay safe)
+        self._hyper = torch.zeros(8, device=dev, dtype=torch.float32)
         self._hyper_host = None
         self._sync_hyper()
 
@@ -46,7 +46,7 @@ class HipAdam(torch.optim.Optimizer):
         g = self.param_groups[0]
         h = (float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]), float(g["weight_decay"]))
         if h != self._hyper_host:      # lr schedulers edit param_groups; push the change
-            self._hyper[1:].copy_(torch.tensor(h, dtype=torch.float32), non_blocking=False)
+            self._hyper[1:6].copy_(torch.tensor(h, dtype=torch.float32), non_blocking=False)
             self._hyper_host = h
 
     def _flat_grad(self):

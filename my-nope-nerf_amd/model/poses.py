@@ -8,7 +8,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from .common import make_c2w
+from .rays import pose_c2w
 
 
 class LearnPose(nn.Module):
@@ -23,10 +23,8 @@ class LearnPose(nn.Module):
 
     def forward(self, cam_id):
         cam = int(cam_id)   # a host-side index (img.idx comes from the data dict on the CPU)
-        c2w = make_c2w(self.r[cam], self.t[cam])
-        if self.init_c2w is not None:
-            c2w = c2w @ self.init_c2w[cam]
-        return c2w
+        # one HIP launch on the device (Exp, [R|t], @ init_c2w), torch on the host
+        return pose_c2w(self.r[cam], self.t[cam], None if self.init_c2w is None else self.init_c2w[cam])
 
     def get_t(self):
         return self.t

@@ -12,6 +12,7 @@ import torch
 import torch.nn as nn
 
 from .common import get_mask, get_ndc_rays_fxfy, unproject_matrix
+from .rays import camera_rays_hip
 from .field import F_DIST_ALPHA, F_RELU, F_WHITE_BKGD, render_field, render_field_eval
 
 epsilon = 1e-6  # rendering.py:9 (applied inside the composite kernel)
@@ -81,10 +82,15 @@ class Renderer(nn.Module):
         cfg = self.cfg
         S = cfg["num_points"] - cfg.get("outside_steps", 0)
         near, far = float(self.depth_range[0]), float(self.depth_range[1])
-        cam, ray, ray_norm, d_src, mask = camera_rays(pixels, depth, camera_mat, world_mat, scale_mat,
-                                                      cfg["normalise_ray"])
+        if pixels.is_cuda:       # two launches: the unprojection matrix, then every ray
+            M = unproject_matrix(camera_mat, world_mat, scale_mat)
+            cam, ray, view, ray_norm, d_src, mask = camera_rays_hip(
+                M, pixels, depth, cfg["normalise_ray"], view_ones=not cfg["use_ray_dir"])
+        else:
+            cam, ray, ray_norm, d_src, mask = camera_rays(pixels, depth, camera_mat, world_mat, scale_mat,
+                                                          cfg["normalise_ray"])
+            view = -ray if cfg["use_ray_dir"] else torch.ones_like(ray)
         R = cam.shape[0]
-        view = -ray if cfg["use_ray_dir"] else torch.ones_like(ray)
         if cfg["sample_option"] == "ndc":        # rendering.py:169-181 (no jitter)
             fxfy = torch.cat([camera_mat[:, 0, 0], camera_mat[:, 1, 1]])
             pts_o, pts_d = get_ndc_rays_fxfy(fxfy, 1.0, cam, ray)

@@ -22,6 +22,8 @@ import torch.distributed as dist
 from torch.nn import functional as F
 
 from .common import arange_pixels, get_tensor_values, inv, project_to_cam, transform_to_world
+from .rays import can_sample_on_device
+from .rays import sample_rays as sample_rays_dev
 from .losses import Loss
 
 
@@ -133,15 +135,31 @@ class Trainer(object):
             self._pix_cache[key] = arange_pixels((h, w), 1, device=device)[1]
         return self._pix_cache[key]
 
-    def sample_rays(self, n_pix, depth_mask, need_valid):
-        """training.py:277-283: a random subset of pixels, resampled while none of them has a
-        valid depth.  The check is a device->host sync per step in the reference; here it
-        runs only when an all-invalid draw is plausible: with n_invalid of n_pix pixels
-        invalid that probability is <= (n_invalid / n_pix) ** n_points, computed on the host
-        from the data dict's CPU mask (5 % holes at 1024 rays: 1e-1332)."""
+    def sample_rays(self, n_pix, depth_mask, need_valid, img=None, hw=None):
+        """training.py:277-283 plus the colour / pixel gathers of :284-287: a random subset
+        of R pixels, resampled while none of them has a valid depth.  Returns (ray_idx,
+        pixels [B,R,2], rgb_gt [B,R,3]).
+
+        On the device one HIP launch draws the subset and gathers both (rays.sample_rays;
+        ``randperm`` sorts n_pix keys to keep R of them).  The validity check is a
+        device->host sync per step in the reference; here it runs only when an all-invalid
+        draw is plausible: with n_invalid of n_pix pixels invalid that probability is
+        <= (n_invalid / n_pix) ** R, computed on the host from the data dict's CPU mask
+        (5 % holes at 1024 rays: 1e-1332)."""
         dev = self.device
         R = self.n_training_points
-        ray_idx = torch.randperm(n_pix, device=dev)[:R]
+        h, w = hw
+        B = img.shape[0]
+        on_dev = img.is_cuda and B == 1 and can_sample_on_device(n_pix, R)
+
+        def draw():
+            if on_dev:
+                return sample_rays_dev(n_pix, R, w, h, img[0])
+            ray_idx = torch.randperm(n_pix, device=dev)[:R]
+            rgb_gt = img.view(B, 3, n_pix).permute(0, 2, 1)[:, ray_idx]
+            return ray_idx, self._pixels(h, w, dev)[:, ray_idx], rgb_gt
+
+        ray_idx, p, rgb_gt = draw()
         if need_valid and depth_mask is not None:
             if depth_mask.is_cuda:
                 risky = True
@@ -151,8 +169,8 @@ class Trainer(object):
             if risky:
                 m = depth_mask.flatten().to(dev)
                 while not m[ray_idx].any():
-                    ray_idx = torch.randperm(n_pix, device=dev)[:R]
-        return ray_idx
+                    ray_idx, p, rgb_gt = draw()
+        return ray_idx, p, rgb_gt
 
     # ------------------------------------------------------------------ loss
     def compute_loss(self, data, eval_mode=False, it=None, epoch=None, scheduling_start=None,
@@ -176,7 +194,7 @@ class Trainer(object):
         kwargs = {"weights": weights, "rgb_loss_type": rgb_loss_type}
         if self.pose_param_net is not None:
             kwargs["t_list"] = self.pose_param_net.get_t()
-        world_mat_gt = inv(pose_gt).unsqueeze(0)
+        world_mat_gt = inv(pose_gt).unsqueeze(0) if use_ref_imgs else None   # only the pair terms read it
         num_cams = self.pose_param_net.num_cams if self.pose_param_net is not None else None
         c2w = self.pose_param_net(img_idx) if self.pose_param_net is not None else pose_gt.reshape(4, 4)
         world_mat = inv(c2w).unsqueeze(0)
@@ -195,9 +213,7 @@ class Trainer(object):
         else:
             camera_mat = camera_mat_gt
 
-        ray_idx = self.sample_rays(h * w, depth_mask, data.get("img.dpt") is None)
-        rgb_gt = img.view(B, 3, h * w).permute(0, 2, 1)[:, ray_idx]
-        p = self._pixels(h, w, dev)[:, ray_idx]
+        ray_idx, p, rgb_gt = self.sample_rays(h * w, depth_mask, data.get("img.dpt") is None, img=img, hw=(h, w))
 
         rendered_rgb = rendered_depth = gt_depth = dmask = None
         if render_model:

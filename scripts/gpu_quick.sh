@@ -1,9 +1,7 @@
 set -o pipefail
-R=$GRAFT_REPO_ROOT
-cd $R
-OUT=$R/gpurun_out
-mkdir -p $OUT
-timeout -k 10 600 python -m pytest tests -q -m gpu -p no:cacheprovider > $OUT/t_all.log 2>&1
-echo "tests rc=$?"
-timeout -k 10 300 python scripts/gemm_bench.py > $OUT/gemm_bench.txt 2>&1 && echo "gemm bench ok" && \
-timeout -k 10 600 python bench.py --steps 30 --warmup 5 --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err && echo "bench ok"
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests/test_gpu_rays.py tests/test_gpu_render.py tests/test_gpu_kernels.py -q -x -p no:cacheprovider > gpurun_out/t_rays.log 2>&1; rc=$?
+tail -30 gpurun_out/t_rays.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-alt > gpurun_out/bench_rays.json 2> gpurun_out/bench_rays.err && cat gpurun_out/bench_rays.json

@@ -36,7 +36,7 @@ def test_binding_covers_the_header():
 
 
 def test_abi_version_and_error_path(lib):
-    assert lib.nerf_hip_abi_version() == 2
+    assert lib.nerf_hip_abi_version() == 3
     rc = lib.nerf_linear_fwd(None, 256, 256, None, 0, 0, None, None, 0, None, None, 256, 128, 256, 1, None, 0,
                              None)
     assert rc == -1
@@ -45,6 +45,13 @@ def test_abi_version_and_error_path(lib):
     assert rc == -1 and b"nout" in lib.nerf_hip_last_error()
     rc = lib.nerf_composite_fwd(None, None, 1, 1, 0, None, None, None, None)
     assert rc == -1
+    # ray prologue: sampler size limits, camera rays without outputs
+    rc = lib.nerf_sample_rays(100, 80, 1, 10, 10, None, 1, None, None, None, None)
+    assert rc == -1 and b"2*n_rays" in lib.nerf_hip_last_error()
+    rc = lib.nerf_sample_rays(10 ** 6, 5000, 1, 1000, 1000, None, 1, None, None, None, None)
+    assert rc == -1 and b"n_rays" in lib.nerf_hip_last_error()
+    rc = lib.nerf_camera_rays(1, 1, None, 4, 1, None, 1, None, 1, 1, None, None)
+    assert rc == -1 and b"cam" in lib.nerf_hip_last_error()
 
 
 def test_ops_refuse_cpu_tensors(lib):

@@ -346,7 +346,7 @@ def test_adam_matches_torch(dev):
     p = p0.clone().to(dev)
     m = torch.zeros_like(p)
     v = torch.zeros_like(p)
-    hyper = torch.tensor([0.0, 1e-3, 0.9, 0.999, 1e-8, 0.0], device=dev)
+    hyper = torch.tensor([0.0, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0.0, 0.0], device=dev)
     tp = torch.nn.Parameter(p0.clone())
     opt = torch.optim.Adam([tp], lr=1e-3)
     for step in range(1, 6):

@@ -128,11 +128,14 @@ def test_ray_resampling_guarantee():
     mask = torch.zeros(1, 10, 10, dtype=torch.bool)
     mask[0, 9, 9] = True                  # one valid pixel: must resample until it is drawn
     torch.manual_seed(0)
-    idx = tr.sample_rays(100, mask, True)
+    img = torch.rand(1, 3, 10, 10)
+    idx, pix, rgb = tr.sample_rays(100, mask, True, img=img, hw=(10, 10))
     assert mask.flatten()[idx].any()
+    assert torch.equal(pix, tr._pixels(10, 10, torch.device("cpu"))[:, idx])
+    assert torch.equal(rgb, img.view(1, 3, 100).permute(0, 2, 1)[:, idx])
     # a mostly valid mask skips the (sync) check: the all-invalid draw is impossible
     cfg["training"]["n_training_points"] = 64
     tr2 = mdl.Trainer(None, None, cfg["training"], device=torch.device("cpu"))
     mask2 = torch.ones(1, 100, 100, dtype=torch.bool)
     mask2[0, :5] = False
-    assert tr2.sample_rays(10000, mask2, True).shape == (64,)
+    assert tr2.sample_rays(10000, mask2, True, img=torch.rand(1, 3, 100, 100), hw=(100, 100))[0].shape == (64,)
