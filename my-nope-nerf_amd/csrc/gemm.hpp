@@ -327,6 +327,95 @@ __device__ __forceinline__ void nt_epilogue_lds(const NTArgs& p, f32x16 (&acc)[T
     }
 }
 
+// Direct NT epilogue for the operand-swapped K loop (the MFMAs compute C^T tiles, so each
+// lane holds one sample row and, per register quad 4q..4q+3, four consecutive output
+// features 8q + 4*(lane>>5) + 0..3): float4 stores straight from the accumulators, no
+// LDS round trip and no block barrier.  A wave's four quads of a 32x32 tile cover 128 B
+// of each of its 32 rows; L2 merges them into full lines.
+//   FWD: + bias, ReLU, ReLU mask word per (row, 32 features) from the nibbles of the
+//        lane pair (lane, lane ^ 32).
+//   BWD: + u[row] v[feature], masked by the input layer's ReLU bits.
+template <int TM, int TN, int EPI>
+__device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0, int wm0,
+                                                   int wn0) {
+    const int lane = lane_id();
+    const int sl = lane & 31, hf = lane >> 5;
+    if (p.ablate & 1) {
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+        p.c[(size_t)(m0 + (threadIdx.x & 127)) * p.ldc + n0 + (threadIdx.x >> 7)] = t;
+        return;
+    }
+    const int cw0 = (n0 + wn0) >> 5;
+    if (EPI == EPI_FWD) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int fb = n0 + wn0 + 32 * j + 4 * hf;
+            float4 b4[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                b4[q] = p.bias ? *reinterpret_cast<const float4*>(p.bias + fb + 8 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const size_t row = (size_t)(m0 + wm0 + 32 * i + sl);
+                uint32_t w = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    float4 x = make_float4(acc[i][j][4 * q] + b4[q].x, acc[i][j][4 * q + 1] + b4[q].y,
+                                           acc[i][j][4 * q + 2] + b4[q].z, acc[i][j][4 * q + 3] + b4[q].w);
+                    if (p.relu) x = make_float4(fmaxf(x.x, 0.f), fmaxf(x.y, 0.f), fmaxf(x.z, 0.f), fmaxf(x.w, 0.f));
+                    *reinterpret_cast<float4*>(p.c + row * p.ldc + fb + 8 * q) = x;
+                    const uint32_t nib = (x.x > 0.f ? 1u : 0u) | (x.y > 0.f ? 2u : 0u) | (x.z > 0.f ? 4u : 0u) |
+                                         (x.w > 0.f ? 8u : 0u);
+                    w |= nib << (8 * q + 4 * hf);
+                }
+                if (p.mask_out) {
+                    w |= (uint32_t)__shfl_xor((int)w, 32, 64);
+                    if (hf == 0) p.mask_out[row * p.ldmo + cw0 + j] = w;
+                }
+            }
+        }
+    } else {
+        float u[TM];
+        uint32_t mw[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const size_t row = (size_t)(m0 + wm0 + 32 * i + sl);
+            u[i] = p.u ? p.u[row * p.ldu] : 0.f;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) mw[i][j] = p.mask ? p.mask[row * p.ldmask + cw0 + j] : 0xffffffffu;
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int fb = n0 + wn0 + 32 * j + 4 * hf;
+            float4 v4[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                v4[q] = p.u ? *reinterpret_cast<const float4*>(p.v + fb + 8 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const size_t row = (size_t)(m0 + wm0 + 32 * i + sl);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t bits = mw[i][j] >> (8 * q + 4 * hf);
+                    float4 x = make_float4(acc[i][j][4 * q] + u[i] * v4[q].x, acc[i][j][4 * q + 1] + u[i] * v4[q].y,
+                                           acc[i][j][4 * q + 2] + u[i] * v4[q].z, acc[i][j][4 * q + 3] + u[i] * v4[q].w);
+                    x.x = (bits & 1u) ? x.x : 0.f;
+                    x.y = (bits & 2u) ? x.y : 0.f;
+                    x.z = (bits & 4u) ? x.z : 0.f;
+                    x.w = (bits & 8u) ? x.w : 0.f;
+                    *reinterpret_cast<float4*>(p.c + row * p.ldc + fb + 8 * q) = x;
+                }
+            }
+        }
+    }
+}
+
 // TN epilogue through the LDS writer: float4 slab stores
 template <int TM, int TN>
 __device__ __forceinline__ void tn_store_lds(const TNArgs& p, f32x16 (&acc)[TM][TN], char* smem, int split, int o0,

@@ -19,6 +19,8 @@
 //    split-K slab + bias-gradient column sums (backward-weight).
 #include "gemm.hpp"
 
+#include <cstdlib>
+
 namespace nerf {
 
 constexpr int BK = 32;
@@ -235,22 +237,26 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_tn(TNArgs p) {
     if (do_bias && tid < BM && !(p.ablate & 1)) p.bslab[(size_t)split * p.nout + o0 + tid] = bsum;
 }
 
-// sum split-K slabs into the reference-layout gradient.  A block owns 256 consecutive
-// slab columns of one output row (64 lanes x float4); its 4 waves sum interleaved
-// quarters of the splits (8 float4 loads in flight per lane), then combine through LDS
-// in wave order (deterministic).  Bias partials (bslab) ride along in the last row
-// of blocks.
-constexpr int SR_COLS = 256;
+// sum split-K slabs into the reference-layout gradient.  A block owns 64 consecutive
+// slab columns of one output row: 16 lane groups (4 per wave) of 16 lanes x float4 each
+// sum the splits of one residue class mod 16 (8 float4 loads in flight per lane, 256 B
+// contiguous per group), then the 16 partials are combined through LDS in group order
+// (deterministic).  ~4 blocks per CU at the production shapes: enough loads in flight to
+// stream the 64 MB of a 256-split slab while the GEMMs run beside it.  Bias partials
+// (bslab) ride along in the last row of blocks.
+constexpr int SR_COLS = 64;
+constexpr int SR_GROUPS = 16;
 __global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ slab, int splits, int nout,
                                                      int ldslab, int nout_ref, int kin_ref,
                                                      const float* __restrict__ bslab, float* __restrict__ gw,
                                                      float* __restrict__ gb, int accumulate) {
-    __shared__ float4 part[4][64];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    __shared__ float4 part[SR_GROUPS][16];
+    const int l16 = threadIdx.x & 15, grp = threadIdx.x >> 4;
     const int cblocks = (kin_ref + SR_COLS - 1) / SR_COLS;
-    const int o = blockIdx.x / cblocks;              // output row (o == nout_ref: the bias row)
-    const int c0 = (blockIdx.x % cblocks) * SR_COLS + 4 * lane;
-    const bool bias_row = o == nout_ref;
+    const int wblocks = nout_ref * cblocks;          // then ceil(nout_ref / SR_COLS) bias blocks
+    const bool bias_row = (int)blockIdx.x >= wblocks;
+    const int o = bias_row ? nout_ref : blockIdx.x / cblocks;
+    const int c0 = (bias_row ? blockIdx.x - wblocks : blockIdx.x % cblocks) * SR_COLS + 4 * l16;
     if (bias_row && (bslab == nullptr || gb == nullptr)) return;
     const float* src;
     size_t st;
@@ -261,35 +267,36 @@ __global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ s
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (c0 < ncol) {
         if (vec) {
-            int q = wv;
-            for (; q + 28 < splits; q += 32) {      // 8 loads in flight per lane
+            int q = grp;
+            for (; q + 7 * SR_GROUPS < splits; q += 8 * SR_GROUPS) {      // 8 loads in flight per lane
                 float4 v[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(src + (size_t)(q + 4 * u) * st + c0);
+                for (int u = 0; u < 8; ++u)
+                    v[u] = *reinterpret_cast<const float4*>(src + (size_t)(q + SR_GROUPS * u) * st + c0);
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
                 }
             }
-            for (; q < splits; q += 4) {
+            for (; q < splits; q += SR_GROUPS) {
                 const float4 v = *reinterpret_cast<const float4*>(src + (size_t)q * st + c0);
                 acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
             }
         } else {
             float a[4] = {0.f, 0.f, 0.f, 0.f};
-            for (int q = wv; q < splits; q += 4)
+            for (int q = grp; q < splits; q += SR_GROUPS)
                 for (int t = 0; t < 4; ++t)
                     if (c0 + t < ncol) a[t] += src[(size_t)q * st + c0 + t];
             acc = make_float4(a[0], a[1], a[2], a[3]);
         }
     }
-    part[wv][lane] = acc;
+    part[grp][l16] = acc;
     __syncthreads();
-    if (wv != 0 || c0 >= ncol) return;
-    float4 r = part[0][lane];
+    if (grp != 0 || c0 >= ncol) return;
+    float4 r = part[0][l16];
 #pragma unroll
-    for (int w = 1; w < 4; ++w) {
-        const float4 v = part[w][lane];
+    for (int w = 1; w < SR_GROUPS; ++w) {
+        const float4 v = part[w][l16];
         r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
     }
     float* dst = bias_row ? gb + c0 : gw + (size_t)o * kin_ref + c0;
@@ -446,11 +453,9 @@ extern "C" int nerf_slab_reduce(const float* slab, int splits, int nout, int lds
     NERF_CHECK_PTR(gw);
     NERF_CHECK(splits > 0 && nout > 0 && kin_ref > 0 && ldslab >= kin_ref && nout_ref <= nout,
                "%s: bad sizes", __func__);
-    // one block per (output row, 256 columns); one extra row of blocks for the bias
+    // one block per (output row, 64 columns), then the bias row's blocks
     const int cblocks = (kin_ref + SR_COLS - 1) / SR_COLS;
-    const int bias_blocks = (bslab && gb) ? cblocks : 0;
-    NERF_CHECK(nout_ref <= cblocks * SR_COLS || bias_blocks == 0,
-               "%s: bias row wider than the column blocks (nout_ref %d > %d)", __func__, nout_ref, cblocks * SR_COLS);
+    const int bias_blocks = (bslab && gb) ? (nout_ref + SR_COLS - 1) / SR_COLS : 0;
     const int blocks = nout_ref * cblocks + bias_blocks;
     hipLaunchKernelGGL(k_slab_reduce, dim3(blocks), dim3(256), 0, as_stream(stream), slab, splits,
                        nout, ldslab, nout_ref, kin_ref, bslab, gw, gb, accumulate);
@@ -473,6 +478,8 @@ extern "C" int nerf_linear_bwd_weight_splits(int nout, int kin, int m) {
     int tiles, target;
     if (pol == 3 && nout % 256 == 0 && kin % 256 == 0) { tiles = (nout / 256) * (kin / 256); target = 256; }
     else { tiles = ((nout + 127) / 128) * ((kin + 127) / 128); target = 512; }
+    static const int env_target = [] { const char* e = getenv("NERF_DW_BLOCKS"); return e ? atoi(e) : 0; }();
+    if (env_target > 0) target = env_target;   // experiment hook: blocks per dW launch
     int splits = 1;
     while (splits * 2 * tiles <= target && m % (splits * 2 * BK) == 0 && m / (splits * 2) >= 256) splits *= 2;
     return splits;

@@ -21,6 +21,8 @@
 //    k of one column and writes its fragment chunk with one ds_write_b128 per plane.
 #include "gemm.hpp"
 
+#include <cstdlib>
+
 namespace nerf {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -185,7 +187,7 @@ __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" :
 // the ring slot freed by iteration kt-1's split.  At the end `vmcnt(A_F4)` retires
 // every DMA but this iteration's raw A, which gets a second iteration to land.
 // ---------------------------------------------------------------------------
-template <int TM, int TN, int BM, int BN, typename Stager>
+template <int TM, int TN, int BM, int BN, bool SWAP, typename Stager>
 __device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int wn0, f32x16 (&acc)[TM][TN],
                                                Stager& st, unsigned long long* stamps = nullptr) {
     using IA = XImg<BM>;
@@ -208,16 +210,21 @@ __device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int
 #pragma unroll
         for (int j = 0; j < TN; ++j) rd(buf + boff + 32 * 16 * j, IB::PLANE, b[j]);
     };
+    // SWAP: the MFMA's A operand is the weight fragment, so acc[i][j] holds the transposed
+    // tile (lanes along samples, registers along features) for nt_epilogue_direct
+    auto mf = [&](const uint4& a, const uint4& b, const f32x16& c) {
+        return SWAP ? mfma_bf16(b, a, c) : mfma_bf16(a, b, c);
+    };
     auto mm = [&](int i, const uint4 (&a)[3], const uint4 (&b)[TN][3]) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             f32x16 c = acc[i][j];
-            c = mfma_bf16(a[1], b[j][1], c);   // mid.mid
-            c = mfma_bf16(a[0], b[j][2], c);   // hi.lo
-            c = mfma_bf16(a[2], b[j][0], c);   // lo.hi
-            c = mfma_bf16(a[0], b[j][1], c);   // hi.mid
-            c = mfma_bf16(a[1], b[j][0], c);   // mid.hi
-            c = mfma_bf16(a[0], b[j][0], c);   // hi.hi
+            c = mf(a[1], b[j][1], c);   // mid.mid
+            c = mf(a[0], b[j][2], c);   // hi.lo
+            c = mf(a[2], b[j][0], c);   // lo.hi
+            c = mf(a[0], b[j][1], c);   // hi.mid
+            c = mf(a[1], b[j][0], c);   // mid.hi
+            c = mf(a[0], b[j][0], c);   // hi.hi
             acc[i][j] = c;
         }
     };
@@ -358,7 +365,7 @@ struct NTStager {
     }
 };
 
-template <int BM, int BN, int WM, int WN, int EPI>
+template <int BM, int BN, int WM, int WN, int EPI, bool DIRECT>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt_x6(NTArgs p) {
     constexpr int NT = 64 * WM * WN;
     constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -366,7 +373,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt_x6(NTArgs p) {
     using St = NTStager<BM, BN, NT>;
     static_assert(TM >= 1 && TN >= 1, "bad tile");
     constexpr int LOOP_BYTES = 2 * (XImg<BM>::BYTES + XImg<BN>::BYTES) + St::NSLOT * St::RAW;
-    constexpr int EPI_BYTES = (NT / 64) * TileLds<TN>::BYTES + (BM * (BN / 32) + BM) * 4;
+    constexpr int EPI_BYTES = DIRECT ? 0 : (NT / 64) * TileLds<TN>::BYTES + (BM * (BN / 32) + BM) * 4;
     __shared__ __attribute__((aligned(16))) char smem[LOOP_BYTES > EPI_BYTES ? LOOP_BYTES : EPI_BYTES];
     const int wave = threadIdx.x >> 6;
     const int wm0 = (wave / WN) * WTM;
@@ -378,15 +385,22 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt_x6(NTArgs p) {
     stamp(p.stamps, 0);
     St st;
     st.init(p, m0, n0, K, smem + 2 * (XImg<BM>::BYTES + XImg<BN>::BYTES));
-    NTEpiPrefetch<BM, BN, NT, EPI> pf;
-    pf.load(p, m0, n0);
     f32x16 acc[TM][TN];
     zero_acc(acc);
-    x6_mainloop_pf<TM, TN, BM, BN>(smem, K / XK, wm0, wn0, acc, st, p.stamps);
-    dma_wait();          // the last (clamped) raw-A DMA must land before the epilogue reuses LDS
-    __syncthreads();
-    stamp(p.stamps, 2);
-    nt_epilogue_lds<BM, BN, NT, TM, TN, EPI>(p, acc, smem, m0, n0, wm0, wn0, pf);
+    if (DIRECT) {
+        x6_mainloop_pf<TM, TN, BM, BN, true>(smem, K / XK, wm0, wn0, acc, st, p.stamps);
+        stamp(p.stamps, 2);
+        nt_epilogue_direct<TM, TN, EPI>(p, acc, m0, n0, wm0, wn0);
+        dma_wait();      // the last (clamped) raw-A DMA lands before the workgroup's LDS is released
+    } else {
+        NTEpiPrefetch<BM, BN, NT, EPI> pf;
+        pf.load(p, m0, n0);
+        x6_mainloop_pf<TM, TN, BM, BN, false>(smem, K / XK, wm0, wn0, acc, st, p.stamps);
+        dma_wait();      // the last (clamped) raw-A DMA must land before the epilogue reuses LDS
+        __syncthreads();
+        stamp(p.stamps, 2);
+        nt_epilogue_lds<BM, BN, NT, TM, TN, EPI>(p, acc, smem, m0, n0, wm0, wn0, pf);
+    }
     if (p.stamps) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         stamp(p.stamps, 3);
@@ -523,9 +537,20 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_tn_x6(TNArgs p) {
     }
 }
 
+// NERF_NT_DIRECT=0 selects the LDS-transposed epilogue (A/B experiments)
+static const bool g_nt_direct = [] {
+    const char* e = getenv("NERF_NT_DIRECT");
+    return e == nullptr || atoi(e) != 0;
+}();
+
 template <int BM, int BN, int WM, int WN, int EPI>
 static void launch_nt_x6(const NTArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL((k_gemm_nt_x6<BM, BN, WM, WN, EPI>), dim3(a.m / BM, a.n / BN), dim3(64 * WM * WN), 0, s, a);
+    if (g_nt_direct)
+        hipLaunchKernelGGL((k_gemm_nt_x6<BM, BN, WM, WN, EPI, true>), dim3(a.m / BM, a.n / BN), dim3(64 * WM * WN), 0,
+                           s, a);
+    else
+        hipLaunchKernelGGL((k_gemm_nt_x6<BM, BN, WM, WN, EPI, false>), dim3(a.m / BM, a.n / BN), dim3(64 * WM * WN),
+                           0, s, a);
 }
 
 template <int EPI>

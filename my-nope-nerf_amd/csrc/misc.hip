@@ -67,22 +67,44 @@ __global__ void k_pack(PackBatch pb) {
 // Hyper-parameters and the step count live in device memory (hyper = {step, lr, b1, b2,
 // eps, wd, -, ticket}) so a captured hipGraph replays correct bias corrections and picks up
 // lr changes.  Every workgroup uses step + 1; the last one to finish (ticket) stores it.
-__global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                       float* __restrict__ v, int64_t n, float* __restrict__ hyper) {
+__device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v, float b1, float b2, float eps,
+                                          float wd, float sbc2, float step_size) {
+    if (wd != 0.f) g = g + wd * p;
+    const float mi = m + (1.f - b1) * (g - m);   // lerp_ as torch does
+    const float vi = v * b2 + (1.f - b2) * g * g;
+    m = mi;
+    v = vi;
+    const float denom = sqrtf(vi) / sbc2 + eps;
+    p = p + (-step_size * mi) / denom;           // addcdiv_(m, denom, value=-step_size)
+    return p;
+}
+
+// float4 over the flat buffer (n4 = n / 4 vectors, the n % 4 tail by thread 0 of block 0);
+// at most ADAM_BLOCKS workgroups so the completion ticket costs few atomics
+constexpr int ADAM_BLOCKS = 512;
+__global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float* __restrict__ g,
+                                              float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                              float* __restrict__ hyper) {
     const float step = hyper[0] + 1.f, lr = hyper[1], b1 = hyper[2], b2 = hyper[3], eps = hyper[4], wd = hyper[5];
     const float bc1 = 1.f - powf(b1, step);
     const float sbc2 = sqrtf(1.f - powf(b2, step));
     const float step_size = lr / bc1;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        float gi = g[i];
-        if (wd != 0.f) gi = gi + wd * p[i];
-        const float mi = m[i] + (1.f - b1) * (gi - m[i]);   // lerp_ as torch does
-        const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
-        m[i] = mi;
-        v[i] = vi;
-        const float denom = sqrtf(vi) / sbc2 + eps;
-        p[i] = p[i] + (-step_size * mi) / denom;  // addcdiv_(m, denom, value=-step_size)
+    const int64_t n4 = n >> 2;
+    float4* p4 = reinterpret_cast<float4*>(p);
+    float4* m4 = reinterpret_cast<float4*>(m);
+    float4* v4 = reinterpret_cast<float4*>(v);
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        float4 pp = p4[i], mm = m4[i], vv = v4[i];
+        const float4 gg = g4[i];
+        adam_one(pp.x, gg.x, mm.x, vv.x, b1, b2, eps, wd, sbc2, step_size);
+        adam_one(pp.y, gg.y, mm.y, vv.y, b1, b2, eps, wd, sbc2, step_size);
+        adam_one(pp.z, gg.z, mm.z, vv.z, b1, b2, eps, wd, sbc2, step_size);
+        adam_one(pp.w, gg.w, mm.w, vv.w, b1, b2, eps, wd, sbc2, step_size);
+        p4[i] = pp; m4[i] = mm; v4[i] = vv;
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (int64_t i = n4 * 4; i < n; ++i) adam_one(p[i], g[i], m[i], v[i], b1, b2, eps, wd, sbc2, step_size);
     __syncthreads();                              // this workgroup has read hyper[0]
     if (threadIdx.x == 0) {
         unsigned* ticket = reinterpret_cast<unsigned*>(hyper + 7);
@@ -151,8 +173,11 @@ extern "C" int nerf_adam_step(float* param, const float* grad, float* exp_avg, f
     NERF_CHECK_PTR(param); NERF_CHECK_PTR(grad); NERF_CHECK_PTR(exp_avg); NERF_CHECK_PTR(exp_avg_sq);
     NERF_CHECK_PTR(hyper);
     NERF_CHECK(n > 0, "%s: n=%lld", __func__, (long long)n);
-    int64_t blocks = (n + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
+    NERF_CHECK((((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) & 15) == 0,
+               "%s: buffers must be 16-byte aligned", __func__);
+    int64_t blocks = (n / 4 + 255) / 256;
+    if (blocks < 1) blocks = 1;
+    if (blocks > ADAM_BLOCKS) blocks = ADAM_BLOCKS;
     hipStream_t s = as_stream(stream);
     hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, s, param, grad, exp_avg, exp_avg_sq, n, hyper);
     return check_launch(__func__);

@@ -63,6 +63,19 @@ def compute_ssim_loss(x, y):
     return _ssim(x, y)
 
 
+_zeros = {}
+
+
+def _zero(dev):
+    """The 0-dim zero of skipped terms: one tensor per device (no fill launch per step).
+    Callers only read it; it never requires grad."""
+    key = str(dev)
+    z = _zeros.get(key)
+    if z is None:
+        z = _zeros[key] = torch.zeros((), device=dev)
+    return z
+
+
 class Loss(nn.Module):
     def __init__(self, cfg=None):
         super().__init__()
@@ -174,7 +187,7 @@ class Loss(nn.Module):
                 d1=None, weights={}, rgb_loss_type="l2", depth_mask=None, **kwargs):
         """losses.py:164-228: weighted sum + the same output dict."""
         dev = rgb_pred.device if rgb_pred is not None else (X.device if X is not None else "cpu")
-        zero = torch.zeros((), device=dev)
+        zero = _zero(dev)
         rgb_gt = rgb_gt.to(dev) if rgb_gt is not None else None
         w = weights
         fused = None
