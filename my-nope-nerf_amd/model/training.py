@@ -58,6 +58,9 @@ class Trainer(object):
             setattr(self, w, cfg[w])
         self.loss = Loss(cfg)
         self._pix_cache = {}
+        # test hook: (ray_idx, noise) replaces the next draws of compute_loss (the
+        # reference's randperm / torch.rand), so a step can be replayed on the oracle
+        self.inject = None
         self.world_size = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
     # ------------------------------------------------------------------ step
@@ -213,13 +216,22 @@ class Trainer(object):
         else:
             camera_mat = camera_mat_gt
 
-        ray_idx, p, rgb_gt = self.sample_rays(h * w, depth_mask, data.get("img.dpt") is None, img=img, hw=(h, w))
+        extra = {}
+        if self.inject is not None:
+            ray_idx, noise = self.inject
+            ray_idx = ray_idx.to(dev)
+            rgb_gt = img.view(B, 3, h * w).permute(0, 2, 1)[:, ray_idx]
+            p = self._pixels(h, w, dev)[:, ray_idx]
+            extra["noise"] = noise.to(dev)
+        else:
+            ray_idx, p, rgb_gt = self.sample_rays(h * w, depth_mask, data.get("img.dpt") is None, img=img,
+                                                  hw=(h, w))
 
         rendered_rgb = rendered_depth = gt_depth = dmask = None
         if render_model:
             out = self.model(p, ray_idx, camera_mat, world_mat, scale_mat, self.rendering_technique, it=it,
                              eval_mode=eval_mode, depth_img=depth_input, img_size=(h, w),
-                             dense_depth=not eval_mode)
+                             dense_depth=not eval_mode, **extra)
             rendered_rgb, rendered_depth, gt_depth = out["rgb"], out["depth_pred"], out["depth_gt"]
             dmask = out.get("depth_mask")
 

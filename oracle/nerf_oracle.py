@@ -426,3 +426,146 @@ def train_step_render(model: OracleNerf, optimizer, img, depth_img, camera_mat, 
     ld["loss"].backward()
     optimizer.step()
     return ld, out
+
+
+# ----------------------------------------------------------------------------
+# the full NoPe-NeRF step (config 3): pose + distortion learning, point-cloud and
+# reprojection terms of the image pair (training.py:214-416, losses.py:105-228,
+# common.py:75-109, 436-457)
+# ----------------------------------------------------------------------------
+def grid_values(tensor, p, mode="bilinear", align_corners=True):
+    """get_tensor_values, common.py:75-109, with scale=False, detach=False, detach_p=False
+    (the arguments of training.py:370, 378): grid_sample of [B,C,H,W] at p [B,N,2] -> [B,N,C]."""
+    v = F.grid_sample(tensor, p.unsqueeze(1), mode=mode, align_corners=align_corners).squeeze(2)
+    return v.permute(0, 2, 1)
+
+
+def project_to_cam(points, camera_mat):
+    """common.py:436-457: K [x, y, z, 1]^T, perspective divide, |xy| <= 1 validity."""
+    B, N, _ = points.shape
+    hom = torch.cat([points.permute(0, 2, 1), torch.ones(B, 1, N, dtype=points.dtype, device=points.device)], 1)
+    xy = (camera_mat @ hom)[:, :3].permute(0, 2, 1)
+    xy = xy[..., :2] / xy[..., 2:]
+    valid = (xy.abs().max(dim=-1)[0] <= 1).unsqueeze(-1)
+    return xy, valid
+
+
+def rgb_s_loss_ref(rgb1, rgb2, valid_points, with_ssim=False):
+    """losses.py:152-159 (+ mean_on_mask :79-87); SSIM (losses.py:232-263) when with_ssim,
+    applied to the (B,H,W,3) tensors exactly as the reference passes them."""
+    diff = (rgb1 - rgb2).abs().clamp(0, 1)
+    if with_ssim:
+        diff = 0.15 * diff + 0.85 * ssim_map(rgb1, rgb2)
+    return mean_on_mask(diff, valid_points)
+
+
+def ssim_map(x, y):
+    """losses.py:232-263: 3x3 mean-pool SSIM dissimilarity with reflection padding."""
+    pad = nn.ReflectionPad2d(1)
+    pool = nn.AvgPool2d(3, 1)
+    x, y = pad(x), pad(y)
+    mu_x, mu_y = pool(x), pool(y)
+    sx = pool(x ** 2) - mu_x ** 2
+    sy = pool(y ** 2) - mu_y ** 2
+    sxy = pool(x * y) - mu_x * mu_y
+    C1, C2 = 0.01 ** 2, 0.03 ** 2
+    n = (2 * mu_x * mu_y + C1) * (2 * sxy + C2)
+    d = (mu_x ** 2 + mu_y ** 2 + C1) * (sx + sy + C2)
+    return torch.clamp((1 - n / d) / 2, 0, 1)
+
+
+def compute_loss_full(model, pose, distortion, data, tcfg, rcfg, epoch, scheduling_start, ray_idx, noise):
+    """Trainer.compute_loss (training.py:214-416) with the reference image (the pair
+    terms of :305-405) on the CPU.  ``pose`` = {"r", "t", "init_c2w"} (LearnPose
+    parameters, poses.py:6-33), ``distortion`` = {"scales", "shifts", "fix_scaleN"}
+    (Learn_Distortion, distortions.py:4-27); ``ray_idx`` and ``noise`` are injected
+    (training.py:277, rendering.py:189)."""
+    names = ["rgb_weight", "depth_weight", "pc_weight", "rgb_s_weight", "depth_consistency_weight",
+             "weight_dist_2nd_loss", "weight_dist_1st_loss", "t_cycle_weight"]
+    w = {n: anneal(tcfg[n][0], tcfg[n][1], scheduling_start, tcfg["annealing_epochs"], epoch) for n in names}
+    rgb_loss_type = "l1" if epoch < tcfg["annealing_epochs"] + scheduling_start else "l2"     # :228
+    render_model = w["rgb_weight"] != 0.0 or w["depth_weight"] != 0.0
+    use_ref = w["pc_weight"] != 0.0 or w["rgb_s_weight"] != 0.0 or w["t_cycle_weight"] != 0.0
+    nl = tcfg["nearest_limit"]
+    img = data["img"]
+    depth_input = data["img.depth"].unsqueeze(1)
+    camera_mat = data["img.camera_mat"]
+    scale_mat = data["img.scale_mat"]
+    img_idx = int(data["img.idx"])
+    pose_gt = data["img.pose_gt"]
+    B, _, h, w_ = img.shape
+    _, _, h_depth, w_depth = depth_input.shape
+    num_cams = pose["r"].shape[0]
+    world_mat_gt = torch.inverse(pose_gt).unsqueeze(0)                        # :254
+    c2w = learn_pose_forward(pose["r"], pose["t"], pose["init_c2w"], img_idx)   # :257
+    world_mat = torch.inverse(c2w).unsqueeze(0)
+    scale_input, shift_input = learn_distortion_forward(distortion["scales"], distortion["shifts"], img_idx,
+                                                        distortion["fix_scaleN"])                 # :260-264
+    depth_input = depth_input * scale_input + shift_input                    # shift_first False
+    img_flat = img.view(B, 3, h * w_).permute(0, 2, 1)
+    rgb_gt = img_flat[:, ray_idx]                                             # :285-286
+    p = arange_pixels(h, w_, dtype=img.dtype)[1][:, ray_idx]                 # :287-288
+    out = {}
+    if render_model:                                                          # :290-303
+        depth = F.interpolate(depth_input, (h, w_), mode="area").reshape(1, -1, 1)[:, ray_idx]
+        out = render_nope_nerf(model, p, depth, camera_mat, world_mat, scale_mat, rcfg, noise)
+    terms = {}
+    if use_ref:                                                               # :305-405
+        ref_img = data["img.ref_imgs"]
+        depth_ref = data["img.ref_depths"].unsqueeze(1)
+        ref_idx = int(data["img.ref_idxs"])
+        ref_pose_gt = data["img.ref_pose_gt"]
+        ref_Rt_gt = torch.inverse(ref_pose_gt).unsqueeze(0)
+        c2w_ref = learn_pose_forward(pose["r"], pose["t"], pose["init_c2w"], ref_idx)
+        scale_ref, shift_ref = learn_distortion_forward(distortion["scales"], distortion["shifts"], ref_idx,
+                                                        distortion["fix_scaleN"])
+        depth_ref = scale_ref * depth_ref + shift_ref
+        if tcfg["detach_ref_img"]:
+            c2w_ref, scale_ref, shift_ref, depth_ref = (c2w_ref.detach(), scale_ref.detach(), shift_ref.detach(),
+                                                        depth_ref.detach())
+        ref_Rt = torch.inverse(c2w_ref).unsqueeze(0)
+        if img_idx < num_cams - 1:                                            # :329-343
+            d1, d2, img1, img2 = depth_input, depth_ref, img, ref_img
+            Rt_rel_12 = ref_Rt @ torch.inverse(world_mat)
+            Rt_rel_12_gt = ref_Rt_gt @ torch.inverse(world_mat_gt)
+            scale1 = scale_input
+        else:                                                                 # :344-358
+            d1, d2, img1, img2 = depth_ref, depth_input, ref_img, img
+            Rt_rel_12 = world_mat @ torch.inverse(ref_Rt)
+            Rt_rel_12_gt = world_mat_gt @ torch.inverse(ref_Rt_gt)
+            scale1 = scale_ref
+        R_rel_12, t_rel_12 = Rt_rel_12[:, :3, :3], Rt_rel_12[:, :3, 3]
+        res = (int(h_depth / tcfg["pc_ratio"]), int(w_depth / tcfg["pc_ratio"]))   # :360-361
+        p_pc = arange_pixels(res[0], res[1], dtype=img.dtype)[1]
+        d1 = F.interpolate(d1, res, mode="nearest")
+        d2 = F.interpolate(d2, res, mode="nearest")
+        d1 = torch.where(d1 < nl, torch.full_like(d1, nl), d1)              # d1[d1 < nl] = nl
+        d2 = torch.where(d2 < nl, torch.full_like(d2, nl), d2)
+        pc1 = transform_to_world(p_pc, d1.view(1, -1, 1), camera_mat)
+        pc2 = transform_to_world(p_pc, d2.view(1, -1, 1), camera_mat)
+        if w["rgb_s_weight"] != 0.0:                                         # :367-390
+            i1 = F.interpolate(img1, res, mode="bilinear")
+            i2 = F.interpolate(img2, res, mode="bilinear")
+            rgb_pc1 = grid_values(i1, p_pc)
+            src = pc1.detach().clone() if tcfg["detach_rgbs_scale"] else pc1
+            pc1_rot = src @ R_rel_12.transpose(1, 2) + t_rel_12
+            bad = (-pc1_rot[:, :, 2:] < nl).expand_as(pc1_rot)
+            pc1_rot = torch.where(bad, torch.full_like(pc1_rot, nl), pc1_rot)  # pc1_rotated[mask] = nl
+            p_re, valid = project_to_cam(pc1_rot, camera_mat)
+            rgb_proj = grid_values(i2, p_re)
+            terms["rgb_s"] = rgb_s_loss_ref(rgb_pc1.view(B, res[0], res[1], 3), rgb_proj.view(B, res[0], res[1], 3),
+                                            valid.view(B, res[0], res[1], 1), tcfg.get("with_ssim", False))
+        if tcfg["scale_pcs"]:                                                 # :391-393
+            pc1 = pc1 / scale1
+            pc2 = pc2 / scale1
+        X = pc1 @ R_rel_12.transpose(1, 2) + t_rel_12
+        if w["pc_weight"] != 0.0:
+            terms["pc"] = pc_loss(X, pc2)
+    rgb_pred = out.get("rgb")
+    dgt = out.get("depth_gt")
+    if render_model and tcfg["detach_gt_depth"]:
+        dgt = dgt.detach()
+    ld = total_loss(rgb_pred, rgb_gt, out.get("depth_pred"), dgt, w, rgb_loss_type, pc=terms.get("pc"),
+                    rgb_s=terms.get("rgb_s"))
+    ld["scale"], ld["shift"] = scale_input, shift_input
+    return ld

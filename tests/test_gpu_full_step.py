@@ -1,0 +1,142 @@
+"""The full NoPe-NeRF training step (BASELINE.json config 3: joint pose + depth-distortion
+learning, rgb + depth + point-cloud chamfer + reprojection losses) on the MI355X path
+against the oracle's restatement of training.py:214-416 (GPU only).
+
+Both sides start from the same NeRF, pose and distortion parameters, see the same data
+and the same injected ray draws / stratified noise, and take three Adam steps with the
+camera alternating (so both branches of training.py:329-358 run); before each step the
+HIP side is re-synchronised to the oracle's parameters.  Checked per step:
+every loss term (1e-4 relative), the gradients of the pose and distortion parameters
+and of the NeRF weights (2e-3 relative, max-entry for pose / distortion, Frobenius for the
+NeRF tensors), and the parameters after the last step."""
+import pytest
+import torch
+
+import model as mdl
+from model.optim import HipAdam
+from oracle import nerf_oracle as orc
+from tests.helpers import camera_K, make_cfg, rigid_c2w
+
+pytestmark = pytest.mark.gpu
+
+H, W, FX = 48, 72, 60.0
+R, S, D = 256, 32, 64
+
+
+def _scene(seed):
+    g = torch.Generator().manual_seed(seed)
+    yy, xx = torch.meshgrid(torch.linspace(0, 1, H), torch.linspace(0, 1, W), indexing="ij")
+    img = torch.stack([0.5 + 0.4 * torch.sin(7 * xx + 3 * yy + seed), 0.5 + 0.4 * torch.cos(6 * yy - 2 * xx),
+                       0.3 + 0.5 * xx * yy], 0).unsqueeze(0)
+    depth = 2.0 + 3.0 * xx + 0.2 * torch.rand(H, W, generator=g)
+    depth[torch.rand(H, W, generator=g) < 0.05] = 0.0
+    return img, depth.unsqueeze(0)
+
+
+def _data(cam, imgs, depths, c2w_gt, K):
+    ref = 1 - cam
+    return {"img": imgs[cam], "img.depth": depths[cam], "img.depth_mask": depths[cam] > 0,
+            "img.camera_mat": K, "img.scale_mat": torch.eye(4).unsqueeze(0), "img.pose_gt": c2w_gt[cam].unsqueeze(0),
+            "img.idx": torch.tensor([cam]), "img.ref_imgs": imgs[ref], "img.ref_depths": depths[ref],
+            "img.ref_idxs": torch.tensor([ref]), "img.ref_pose_gt": c2w_gt[ref].unsqueeze(0)}
+
+
+def _rel(a, b):
+    if a is None or b is None:      # no gradient reached the parameter (e.g. the fixed last scale)
+        z = lambda t: t is None or not bool(t.detach().abs().max() > 0)
+        return 0.0 if (z(a) and z(b)) else float("inf")
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+def _nrel(a, b):
+    """|a - b| / |b| in the Frobenius norm: the NeRF weight gradients are f32 sums over
+    R*S samples with heavy cancellation, so single entries carry ~1e-3 relative
+    summation-order noise even between two exact-f32 GEMMs."""
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def test_full_nope_nerf_step_matches_oracle(dev, gemm_precision):
+    cfg = make_cfg(hidden=D, S=S)
+    tcfg = dict(cfg["training"])
+    tcfg["n_training_points"] = R
+    tcfg["annealing_epochs"], tcfg["scheduling_start"] = 0, 0
+    rcfg = cfg["rendering"]
+    imgs, depths = zip(*[_scene(s) for s in (0, 1)])
+    c2w_gt = torch.stack([rigid_c2w(11, 0.2), rigid_c2w(12, 0.2)])
+    c2w_gt[1, :3, 3] = c2w_gt[0, :3, 3] + torch.tensor([0.05, 0.0, -0.1])   # overlapping views
+    K = camera_K(H, W, FX, FX)
+
+    # ---- parameters shared by both sides
+    torch.manual_seed(42)
+    net = mdl.OfficialStaticNerf(cfg)
+    ref = orc.OracleNerf(hidden_dim=D, white_background=rcfg["white_background"], dist_alpha=rcfg["dist_alpha"],
+                         occ_activation=cfg["model"]["occ_activation"])
+    ref.load_state_dict(net.state_dict())
+    g = torch.Generator().manual_seed(3)
+    r0, t0 = 0.01 * torch.randn(2, 3, generator=g), 0.02 * torch.randn(2, 3, generator=g)
+    scales0, shifts0 = torch.tensor([[1.15], [1.0]]), torch.tensor([[0.05], [-0.03]])
+
+    # ---- HIP side: the drop-in Trainer
+    renderer = mdl.Renderer(net, rcfg, device=dev)
+    nn_model = mdl.get_model(renderer, cfg, device=dev)
+    pose = mdl.LearnPose(2, True, True, cfg, init_c2w=c2w_gt.clone()).to(dev)
+    dist = mdl.Learn_Distortion(2, True, True, cfg).to(dev)
+    with torch.no_grad():
+        pose.r.copy_(r0); pose.t.copy_(t0)
+        dist.global_scales.copy_(scales0); dist.global_shifts.copy_(shifts0)
+    opt = HipAdam(nn_model.parameters(), lr=1e-3)
+    opt_pose = torch.optim.Adam(pose.parameters(), lr=5e-4)
+    opt_dist = torch.optim.Adam(dist.parameters(), lr=5e-4)
+    tr = mdl.Trainer(nn_model, opt, tcfg, device=dev, optimizer_pose=opt_pose, pose_param_net=pose,
+                     optimizer_distortion=opt_dist, distortion_net=dist)
+
+    # ---- oracle side
+    o_pose = {"r": r0.clone().requires_grad_(True), "t": t0.clone().requires_grad_(True), "init_c2w": c2w_gt.clone()}
+    o_dist = {"scales": scales0.clone().requires_grad_(True), "shifts": shifts0.clone().requires_grad_(True),
+              "fix_scaleN": True}
+    o_opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    o_opt_pose = torch.optim.Adam([o_pose["r"], o_pose["t"]], lr=5e-4)
+    o_opt_dist = torch.optim.Adam([o_dist["scales"], o_dist["shifts"]], lr=5e-4)
+
+    gdraw = torch.Generator().manual_seed(5)
+    keys = ("loss", "loss_rgb", "loss_depth", "loss_pc", "loss_rgb_s", "l2_mean")
+    for step, cam in enumerate((0, 1, 0)):
+        data = _data(cam, imgs, depths, c2w_gt, K)
+        ray_idx = torch.randperm(H * W, generator=gdraw)[:R]
+        noise = torch.rand(1, R, S, generator=gdraw)
+        # oracle
+        for o in (o_opt, o_opt_pose, o_opt_dist):
+            o.zero_grad()
+        lo = orc.compute_loss_full(ref, o_pose, o_dist, data, tcfg, rcfg, epoch=0, scheduling_start=0,
+                                   ray_idx=ray_idx, noise=noise)
+        lo["loss"].backward()
+        # HIP, from the oracle's current parameters: Adam's first updates are lr * sign(g),
+        # so entries with near-zero gradients would otherwise drift apart by ~lr per step
+        with torch.no_grad():
+            net.load_state_dict(ref.state_dict())          # in place: HipAdam's flat views survive
+            pose.r.copy_(o_pose["r"]); pose.t.copy_(o_pose["t"])
+            dist.global_scales.copy_(o_dist["scales"]); dist.global_shifts.copy_(o_dist["shifts"])
+        for m, o in tr._modules_and_optims():
+            o.zero_grad()
+        tr.inject = (ray_idx, noise)
+        lh = tr.compute_loss(data, it=step, epoch=0, scheduling_start=0)
+        lh["loss"].backward()
+        for k in keys:
+            a, b = float(lh[k].detach()), float(lo[k].detach())
+            assert abs(a - b) <= 1e-4 * abs(b) + 1e-6, f"step {step} {k}: HIP {a} oracle {b}"
+        assert _rel(pose.r.grad, o_pose["r"].grad) < 2e-3, ("r", pose.r.grad, o_pose["r"].grad)
+        assert _rel(pose.t.grad, o_pose["t"].grad) < 2e-3, ("t", pose.t.grad, o_pose["t"].grad)
+        assert _rel(dist.global_scales.grad, o_dist["scales"].grad) < 2e-3
+        assert _rel(dist.global_shifts.grad, o_dist["shifts"].grad) < 2e-3
+        for (n1, p1), (n2, p2) in zip(net.named_parameters(), ref.named_parameters()):
+            assert n1 == n2
+            assert _nrel(p1.grad, p2.grad) < 2e-3, (step, n1, _nrel(p1.grad, p2.grad))
+        for o in (opt, opt_pose, opt_dist, o_opt, o_opt_pose, o_opt_dist):
+            o.step()
+    # both optimisers saw the same gradients: the updated parameters agree to ~lr
+    assert _rel(pose.r, o_pose["r"]) < 1e-2 and _rel(pose.t, o_pose["t"]) < 1e-2
+    assert _rel(dist.global_scales, o_dist["scales"]) < 1e-5
+    for (n1, p1), (_, p2) in zip(net.named_parameters(), ref.named_parameters()):
+        assert (p1.detach().cpu() - p2.detach()).abs().max().item() < 2.5e-3, n1

@@ -160,3 +160,32 @@ def test_anneal_schedule():
     assert orc.anneal(0.04, 0.0, 0, 0, 0) == 0.04
     assert orc.anneal(0.04, 0.0, 0, 0, 1) == 0.0
     assert orc.anneal(1.0, 0.0, 10, 10, 15) == pytest.approx(0.5)
+
+
+def test_pair_terms_vanish_for_identical_views():
+    """training.py:305-405: two cameras with the same pose, image and depth reproject every
+    point onto itself, so the chamfer (pc) and reprojection (rgb_s) terms are 0 while the
+    render terms are not; the loss dict carries the distortion scale / shift."""
+    from tests.helpers import camera_K, make_cfg, rigid_c2w
+    H, W = 24, 32
+    cfg = make_cfg(hidden=16, S=8)
+    tcfg = dict(cfg["training"])
+    yy, xx = torch.meshgrid(torch.linspace(0, 1, H), torch.linspace(0, 1, W), indexing="ij")
+    img = torch.stack([xx, yy, xx * yy], 0).unsqueeze(0)
+    depth = (2.0 + xx).unsqueeze(0)
+    c2w = rigid_c2w(1)
+    data = {"img": img, "img.depth": depth, "img.camera_mat": camera_K(H, W, 30.0, 30.0),
+            "img.scale_mat": torch.eye(4).unsqueeze(0), "img.pose_gt": c2w.unsqueeze(0), "img.idx": torch.tensor([0]),
+            "img.ref_imgs": img.clone(), "img.ref_depths": depth.clone(), "img.ref_idxs": torch.tensor([1]),
+            "img.ref_pose_gt": c2w.unsqueeze(0)}
+    torch.manual_seed(0)
+    model = orc.OracleNerf(hidden_dim=16)
+    pose = {"r": torch.zeros(2, 3), "t": torch.zeros(2, 3), "init_c2w": torch.stack([c2w, c2w])}
+    dist = {"scales": torch.ones(2, 1), "shifts": torch.zeros(2, 1), "fix_scaleN": True}
+    g = torch.Generator().manual_seed(1)
+    ld = orc.compute_loss_full(model, pose, dist, data, tcfg, cfg["rendering"], 0, 0,
+                               torch.randperm(H * W, generator=g)[:64], torch.rand(1, 64, 8, generator=g))
+    assert ld["loss_pc"].item() < 1e-5
+    assert ld["loss_rgb_s"].item() < 1e-6
+    assert ld["loss_rgb"].item() > 0 and ld["loss_depth"].item() > 0
+    assert ld["scale"].item() == 1.0 and ld["shift"].item() == 0.0
