@@ -159,10 +159,11 @@ int nerf_composite_bwd(const float* raw4, const float* z, int n_rays, int n_samp
                        void* stream);
 
 /* Gradient w.r.t. the ray inputs of nerf_encode_samples (pose learning):
- * genc_p[s][64], genc_d[s][64] -> per ray g_pts_o[R][3] = sum_s dL/dpts,
+ * genc_p[s][64] (+ genc_p2[s][64] when not NULL: the skip layer's gradient of the same
+ * encoding), genc_d[s][64] -> per ray g_pts_o[R][3] = sum_s dL/dpts,
  * g_pts_d[R][3] = sum_s z dL/dpts, g_view[R][3] = sum_s dL/dview. */
 int nerf_encode_bwd(const float* pts_o, const float* pts_d, const float* view, const float* z,
-                    const float* genc_p, const float* genc_d, int n_rays, int n_samples,
+                    const float* genc_p, const float* genc_p2, const float* genc_d, int n_rays, int n_samples,
                     float* g_pts_o, float* g_pts_d, float* g_view, void* stream);
 
 /* ---------------------------------------------------------------------------
@@ -260,6 +261,30 @@ int nerf_ray_loss_bwd(const float* rgb, const float* rgb_gt, int n_rays, const f
                       float w_depth, const float* go_total, const float* go_rgb, const float* go_depth,
                       const float* go_l2, const float* cnt, float* g_rgb, float* g_depth_pred,
                       float* g_depth_gt, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Image-pair terms of the full step (pair.hip; training.py:359-405, losses.py:116-159):
+ * at the point-cloud resolution h x w (P = h w points, pixel grid of arange_pixels),
+ *   pc1 = (inv(K) [x d1, y d1, d1, 1])[:3], pc2 likewise (transform_to_world),
+ *   X = R (pc1 / s1) + t, Y = pc2 / s1 (s1 = NULL: 1; Rt = Rt_rel_12 [4][4]),
+ *   loss_pc = mean |X - Y[nn(X)]| + mean |Y - X[nn(Y)]| (dense chamfer, first index on ties),
+ *   loss_rgb_s = mean over valid elements of clamp(|img1(p) - img2(proj(R pc1 + t))|, 0, 1)
+ *   (bilinear, align_corners, zero padding; the rotated point is replaced by (nl, nl, nl)
+ *   when -z < nl; valid = |proj| <= 1), only when img1/img2 ([3][h][w]) are given.
+ * All operands are device pointers (K, Rt, s1 included).  work: nerf_pair_workspace floats;
+ * nn: int [2][P]; out3 = {loss_pc, loss_rgb_s, valid element count}. */
+int nerf_pair_workspace(int n_points, int* n_chunks, int64_t* floats);
+int nerf_pair_forward(const float* d1, const float* d2, int h, int w, const float* K, const float* Rt,
+                      const float* s1, float nl, const float* img1, const float* img2, float* work, int* nn,
+                      float* out3, void* stream);
+/* Backward: upstream scalars go_pc / go_rgbs (device, optional) -> g_d1, g_d2 [P] (optional),
+ * g13 = {dR (9, row-major), dt (3), ds1}; gXY: scratch [6P] floats; part13: scratch
+ * [13 * ceil(P / 256)] floats.  rgbs_detach_scale: detach_rgbs_scale (training.py:372-375). */
+int nerf_pair_backward(const float* d1, const float* d2, int h, int w, const float* K, const float* Rt,
+                       const float* s1, float nl, const float* img1, const float* img2, int rgbs_detach_scale,
+                       const float* work, const int* nn, const float* out3, const float* go_pc,
+                       const float* go_rgbs, float* gXY, float* g_d1, float* g_d2, float* g13, float* part13,
+                       void* stream);
 
 /* ---------------------------------------------------------------------------
  * Timing hooks for bench.py: when enabled, every GEMM launch is bracketed by

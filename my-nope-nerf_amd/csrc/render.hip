@@ -744,10 +744,14 @@ __global__ __launch_bounds__(256) void k_composite16_bwd(const float* __restrict
 // ---------------------------------------------------------------------------
 // gradient back to the ray inputs (pose / ray learning)
 // ---------------------------------------------------------------------------
+// g2 (optional): a second gradient of the same encoding (the skip layer's copy of enc_p),
+// summed on the fly instead of by a separate add over [N][64]
 template <int L, int LD>
-__device__ __forceinline__ void encode3_bwd(const float x[3], const float* __restrict__ g, float out[3]) {
+__device__ __forceinline__ void encode3_bwd(const float x[3], const float* __restrict__ g,
+                                            const float* __restrict__ g2, float out[3]) {
+    auto G = [&](int k) { return g2 ? g[k] + g2[k] : g[k]; };
 #pragma unroll
-    for (int c = 0; c < 3; ++c) out[c] = g[c];
+    for (int c = 0; c < 3; ++c) out[c] = G(c);
 #pragma unroll
     for (int i = 0; i < L; ++i) {
         const float f = (float)(1 << i);
@@ -755,14 +759,15 @@ __device__ __forceinline__ void encode3_bwd(const float x[3], const float* __res
         for (int c = 0; c < 3; ++c) {
             float s, co;
             sincosf(f * x[c], &s, &co);
-            out[c] += f * (co * g[3 + 6 * i + c] - s * g[6 + 6 * i + c]);
+            out[c] += f * (co * G(3 + 6 * i + c) - s * G(6 + 6 * i + c));
         }
     }
 }
 
 __global__ __launch_bounds__(256) void k_encode_bwd(const float* __restrict__ po, const float* __restrict__ pd,
                                                     const float* __restrict__ view, const float* __restrict__ zv,
-                                                    const float* __restrict__ gp, const float* __restrict__ gd,
+                                                    const float* __restrict__ gp, const float* __restrict__ gp2,
+                                                    const float* __restrict__ gd,
                                                     int R, int S, float* __restrict__ g_po,
                                                     float* __restrict__ g_pd, float* __restrict__ g_view) {
     const int ray = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -778,8 +783,8 @@ __global__ __launch_bounds__(256) void k_encode_bwd(const float* __restrict__ po
         float x[3], gx[3], gv[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) x[c] = ray_point(o[c], d[c], z);
-        encode3_bwd<10, ENC_P>(x, gp + s * ENC_P, gx);
-        encode3_bwd<4, ENC_D>(v, gd + s * ENC_D, gv);
+        encode3_bwd<10, ENC_P>(x, gp + s * ENC_P, gp2 ? gp2 + s * ENC_P : nullptr, gx);
+        encode3_bwd<4, ENC_D>(v, gd + s * ENC_D, nullptr, gv);
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             ao[c] += gx[c];
@@ -945,7 +950,7 @@ extern "C" int nerf_composite_bwd(const float* raw4, const float* z, int n_rays,
 }
 
 extern "C" int nerf_encode_bwd(const float* pts_o, const float* pts_d, const float* view, const float* z,
-                               const float* genc_p, const float* genc_d, int n_rays, int n_samples,
+                               const float* genc_p, const float* genc_p2, const float* genc_d, int n_rays, int n_samples,
                                float* g_pts_o, float* g_pts_d, float* g_view, void* stream) {
     NERF_CHECK_PTR(pts_o); NERF_CHECK_PTR(pts_d); NERF_CHECK_PTR(view); NERF_CHECK_PTR(z);
     NERF_CHECK_PTR(genc_p); NERF_CHECK_PTR(genc_d);
@@ -953,6 +958,6 @@ extern "C" int nerf_encode_bwd(const float* pts_o, const float* pts_d, const flo
     NERF_CHECK(n_rays > 0 && n_samples > 0, "%s: empty input", __func__);
     const int blocks = (n_rays + 3) / 4;
     hipLaunchKernelGGL(k_encode_bwd, dim3(blocks), dim3(256), 0, as_stream(stream), pts_o, pts_d, view, z,
-                       genc_p, genc_d, n_rays, n_samples, g_pts_o, g_pts_d, g_view);
+                       genc_p, genc_p2, genc_d, n_rays, n_samples, g_pts_o, g_pts_d, g_view);
     return check_launch(__func__);
 }

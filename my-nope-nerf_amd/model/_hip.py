@@ -56,7 +56,7 @@ _SIGS = {
     "nerf_heads_reduce": ([_c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_composite_fwd": ([_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_composite_bwd": ([_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
-    "nerf_encode_bwd": ([_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_encode_bwd": ([_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_pack_weights": ([ctypes.POINTER(PackDesc), _c_i, _c_p], _c_i),
     "nerf_adam_step": ([_c_p, _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p], _c_i),
     "nerf_chamfer_nn": ([_c_p, _c_i, _c_p, _c_i, _c_p, _c_p], _c_i),
@@ -75,6 +75,10 @@ _SIGS = {
                        _c_p], _c_i),
     "nerf_ray_loss_bwd": ([_c_p, _c_p, _c_i, _c_p, _c_p, _c_p, _c_i, _c_i, _c_f, _c_f, _c_p, _c_p, _c_p, _c_p,
                            _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_pair_workspace": ([_c_i, ctypes.POINTER(_c_i), ctypes.POINTER(_c_i64)], _c_i),
+    "nerf_pair_forward": ([_c_p, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_pair_backward": ([_c_p, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_i, _c_p, _c_p, _c_p,
+                            _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_prof_enable": ([_c_i], _c_i),
     "nerf_prof_read": ([ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_i64),
                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], _c_i),
@@ -213,9 +217,9 @@ def composite_bwd(raw4, z, n_rays, n_samples, flags, g_rgb, g_dist, graw4, n_pad
           _ptr(graw4), n_pad, _stream())
 
 
-def encode_bwd(pts_o, pts_d, view, z, genc_p, genc_d, n_rays, n_samples, g_po, g_pd, g_view):
-    _call("nerf_encode_bwd", _ptr(pts_o), _ptr(pts_d), _ptr(view), _ptr(z), _ptr(genc_p), _ptr(genc_d),
-          n_rays, n_samples, _ptr(g_po), _ptr(g_pd), _ptr(g_view), _stream())
+def encode_bwd(pts_o, pts_d, view, z, genc_p, genc_d, n_rays, n_samples, g_po, g_pd, g_view, genc_p2=None):
+    _call("nerf_encode_bwd", _ptr(pts_o), _ptr(pts_d), _ptr(view), _ptr(z), _ptr(genc_p), _ptr(genc_p2),
+          _ptr(genc_d), n_rays, n_samples, _ptr(g_po), _ptr(g_pd), _ptr(g_view), _stream())
 
 
 def pack_weights(descs: Sequence[PackDesc]):
@@ -271,6 +275,26 @@ def ray_loss_bwd(rgb, rgb_gt, n_rays, depth_pred, depth_gt, mask, n_depth, rgb_l
     _call("nerf_ray_loss_bwd", _ptr(rgb), _ptr(rgb_gt), int(n_rays), _ptr(depth_pred), _ptr(depth_gt),
           _ptr(mask), int(n_depth), int(rgb_l1), float(w_rgb), float(w_depth), *[_ptr(g) for g in go], _ptr(cnt),
           _ptr(g_rgb), _ptr(g_dp), _ptr(g_dg), _stream())
+
+
+def pair_workspace(n_points):
+    """-> (chamfer chunks, workspace floats) of nerf_pair_forward at n_points."""
+    nc = _c_i()
+    fl = _c_i64()
+    _call("nerf_pair_workspace", int(n_points), ctypes.byref(nc), ctypes.byref(fl))
+    return nc.value, fl.value
+
+
+def pair_forward(d1, d2, h, w, K, Rt, s1, nl, img1, img2, work, nn, out3):
+    _call("nerf_pair_forward", _ptr(d1), _ptr(d2), int(h), int(w), _ptr(K), _ptr(Rt), _ptr(s1), float(nl),
+          _ptr(img1), _ptr(img2), _ptr(work), _ptr(nn), _ptr(out3), _stream())
+
+
+def pair_backward(d1, d2, h, w, K, Rt, s1, nl, img1, img2, rgbs_detach_scale, work, nn, out3, go_pc, go_rgbs,
+                  gxy, g_d1, g_d2, g13, part13):
+    _call("nerf_pair_backward", _ptr(d1), _ptr(d2), int(h), int(w), _ptr(K), _ptr(Rt), _ptr(s1), float(nl),
+          _ptr(img1), _ptr(img2), int(rgbs_detach_scale), _ptr(work), _ptr(nn), _ptr(out3), _ptr(go_pc),
+          _ptr(go_rgbs), _ptr(gxy), _ptr(g_d1), _ptr(g_d2), _ptr(g13), _ptr(part13), _stream())
 
 
 def chamfer_nn(x, y, idx):

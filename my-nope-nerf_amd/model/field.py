@@ -211,10 +211,9 @@ class FieldRunner:
         if HR != D // 2:
             G(m.fc_rgb.weight).copy_(gwc[:, :D // 2])
 
-        genc_p = genc_d = None
-        if want_ray_grad:
-            genc_p = torch.zeros(Np, _hip.ENC_P, device=dev)
-            genc_d = torch.zeros(Np, _hip.ENC_D, device=dev)
+        # encoding gradients (pose learning): enc_p reaches layers l0 and l4 (skip), enc_d the
+        # colour layer; each GEMM writes its own buffer and encode_bwd sums the two enc_p ones
+        genc = {}
 
         # walk the layers backwards; dy = gradient w.r.t. the layer's pre-activation output.
         # The weight gradients (split-K GEMM + slab reduce) of layer l depend only on dy_l and
@@ -261,15 +260,13 @@ class FieldRunner:
             rows = (lambda a, b: wts[:, :, a:b]) if self.split else (lambda a, b: None)
             if name == "l0":
                 if want_ray_grad:
-                    tmp = e(Np, _hip.ENC_P)
-                    _hip.linear_bwd_data(dy, l.out_p, wt, tmp, Np, _hip.ENC_P, wt_split=wts)
-                    genc_p.add_(tmp)
+                    genc["p0"] = e(Np, _hip.ENC_P)
+                    _hip.linear_bwd_data(dy, l.out_p, wt, genc["p0"], Np, _hip.ENC_P, wt_split=wts)
                 break
             if l.seg2 and want_ray_grad:
-                tgt = genc_p if l.seg2 == "enc_p" else genc_d
-                tmp = e(Np, 64)
-                _hip.linear_bwd_data(dy, l.out_p, wt[k1:k1 + 64], tmp, Np, 64, wt_split=rows(k1, k1 + 64))
-                tgt.add_(tmp)
+                key = "p4" if l.seg2 == "enc_p" else "d"
+                genc[key] = e(Np, 64)
+                _hip.linear_bwd_data(dy, l.out_p, wt[k1:k1 + 64], genc[key], Np, 64, wt_split=rows(k1, k1 + 64))
             dx = e(Np, k1)
             # ReLU bits of this layer's input (f, the input of lr, has no activation)
             mask = None if name == "lr" else st["masks"][prev_name[name]]
@@ -286,8 +283,8 @@ class FieldRunner:
         ray = None
         if want_ray_grad:
             g_po, g_pd, g_view = e(R, 3), e(R, 3), e(R, 3)
-            _hip.encode_bwd(st["pts_o"], st["pts_d"], st["view"], st["z"], genc_p, genc_d, R, S,
-                            g_po, g_pd, g_view)
+            _hip.encode_bwd(st["pts_o"], st["pts_d"], st["view"], st["z"], genc["p0"], genc["d"], R, S,
+                            g_po, g_pd, g_view, genc_p2=genc["p4"])
             ray = (g_po, g_pd, g_view)
         return [G(p) for p in params], ray
 

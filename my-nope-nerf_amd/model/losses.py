@@ -207,8 +207,15 @@ class Loss(nn.Module):
             l_d1, l_d2 = self.get_weight_dist_loss(t_list)
         else:
             l_d1, l_d2 = zero, zero
-        l_pc = self.get_pc_loss(X, Y) if w["pc_weight"] != 0.0 else zero
-        l_rgbs = self.get_rgb_s_loss(rgb_pc1, rgb_pc1_proj, valid_points) if w["rgb_s_weight"] != 0.0 else zero
+        pair = kwargs.get("pair_losses")   # (loss_pc, loss_rgb_s) from the fused pair kernels
+        if w["pc_weight"] != 0.0:
+            l_pc = pair[0] if pair is not None else self.get_pc_loss(X, Y)
+        else:
+            l_pc = zero
+        if w["rgb_s_weight"] != 0.0:
+            l_rgbs = pair[1] if pair is not None else self.get_rgb_s_loss(rgb_pc1, rgb_pc1_proj, valid_points)
+        else:
+            l_rgbs = zero
         l_dc = (self.get_depth_consistency_loss(d1_proj, d2, d2_proj, d1)
                 if w["depth_consistency_weight"] != 0.0 else zero)
         l_tc = self.get_t_cycle_loss(kwargs["rt_12"], kwargs["rt_12_gt"]) if w["t_cycle_weight"] != 0.0 else zero

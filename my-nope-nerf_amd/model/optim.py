@@ -52,7 +52,10 @@ class HipAdam(torch.optim.Optimizer):
     def _flat_grad(self):
         gs = [p.grad for p in self._params]
         if any(g is None for g in gs):
-            gs = [torch.zeros_like(p) if p.grad is None else p.grad for p in self._params]
+            # torch.optim.Adam skips such a parameter (no moment decay, no step count); one
+            # fused update over the flat buffer cannot, so refuse instead of diverging silently
+            raise RuntimeError("HipAdam: a parameter has no gradient this step; torch.optim.Adam would skip it. "
+                               "Use HipAdam for modules whose parameters all receive gradients (the NeRF field).")
         g0 = gs[0]
         base = g0.untyped_storage().data_ptr() if g0.is_contiguous() else None
         if base is not None:

@@ -25,6 +25,7 @@ from .common import arange_pixels, get_tensor_values, inv, project_to_cam, trans
 from .rays import can_sample_on_device
 from .rays import sample_rays as sample_rays_dev
 from .losses import Loss
+from .pair import pair_losses
 
 
 class Trainer(object):
@@ -62,6 +63,7 @@ class Trainer(object):
         # reference's randperm / torch.rand), so a step can be replayed on the oracle
         self.inject = None
         self.world_size = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        self.rank = dist.get_rank() if self.world_size > 1 else 0
 
     # ------------------------------------------------------------------ step
     def _modules_and_optims(self):
@@ -157,7 +159,10 @@ class Trainer(object):
 
         def draw():
             if on_dev:
-                return sample_rays_dev(n_pix, R, w, h, img[0])
+                # host-generator seed (reproducible under torch.manual_seed), decorrelated per
+                # rank so data-parallel ranks render different rays
+                seed = int(torch.randint(0, 2 ** 62, (1,)).item()) + self.rank * 0x632BE59BD9B4E019
+                return sample_rays_dev(n_pix, R, w, h, img[0], seed=seed & 0xFFFFFFFFFFFFFFFF)
             ray_idx = torch.randperm(n_pix, device=dev)[:R]
             rgb_gt = img.view(B, 3, n_pix).permute(0, 2, 1)[:, ray_idx]
             return ray_idx, self._pixels(h, w, dev)[:, ray_idx], rgb_gt
@@ -197,7 +202,8 @@ class Trainer(object):
         kwargs = {"weights": weights, "rgb_loss_type": rgb_loss_type}
         if self.pose_param_net is not None:
             kwargs["t_list"] = self.pose_param_net.get_t()
-        world_mat_gt = inv(pose_gt).unsqueeze(0) if use_ref_imgs else None   # only the pair terms read it
+        # the ground-truth relative pose only feeds the t-cycle term (losses.py:161-162)
+        world_mat_gt = inv(pose_gt).unsqueeze(0) if (use_ref_imgs and weights["t_cycle_weight"] != 0.0) else None
         num_cams = self.pose_param_net.num_cams if self.pose_param_net is not None else None
         c2w = self.pose_param_net(img_idx) if self.pose_param_net is not None else pose_gt.reshape(4, 4)
         world_mat = inv(c2w).unsqueeze(0)
@@ -254,7 +260,8 @@ class Trainer(object):
                          out_render_path):
         """training.py:305-405: point clouds of the image pair, relative pose, reprojection."""
         B = img.shape[0]
-        ref_Rt_gt = inv(ref_pose_gt).unsqueeze(0)
+        want_gt = world_mat_gt is not None
+        ref_Rt_gt = inv(ref_pose_gt).unsqueeze(0) if want_gt else None
         c2w_ref = self.pose_param_net(ref_idx)
         scale_ref = shift_ref = None
         if self.distortion_net is not None:
@@ -271,18 +278,28 @@ class Trainer(object):
         if int(img_idx) < num_cams - 1:
             d1, d2, img1, img2 = depth_input, depth_ref, img, ref_img
             Rt_rel_12 = ref_Rt @ inv(world_mat)
-            Rt_rel_12_gt = ref_Rt_gt @ inv(world_mat_gt)
+            Rt_rel_12_gt = ref_Rt_gt @ inv(world_mat_gt) if want_gt else None
             scale1 = scale_input
         else:
             d1, d2, img1, img2 = depth_ref, depth_input, ref_img, img
             Rt_rel_12 = world_mat @ inv(ref_Rt)
-            Rt_rel_12_gt = world_mat_gt @ inv(ref_Rt_gt)
+            Rt_rel_12_gt = world_mat_gt @ inv(ref_Rt_gt) if want_gt else None
             scale1 = scale_ref
-        R_rel_12, t_rel_12 = Rt_rel_12[:, :3, :3], Rt_rel_12[:, :3, 3]
         res = (int(h_depth / self.pc_ratio), int(w_depth / self.pc_ratio))
-        pixel_locations, p_pc = arange_pixels(resolution=res, device=img.device)
         d1 = F.interpolate(d1, res, mode="nearest").clamp_min(nl)       # d[d < nl] = nl
         d2 = F.interpolate(d2, res, mode="nearest").clamp_min(nl)
+        if (img.is_cuda and not camera_mat.requires_grad and not self.loss.cfg.get("with_ssim", False)
+                and self.match_method == "dense"):
+            # pair.hip: point clouds, chamfer and reprojection terms in 4 + 4 launches
+            want_rgbs = weights["rgb_s_weight"] != 0.0
+            i1 = F.interpolate(img1, res, mode="bilinear") if want_rgbs else None
+            i2 = F.interpolate(img2, res, mode="bilinear") if want_rgbs else None
+            s = scale1 if (self.scale_pcs and scale1 is not None) else None
+            l_pc, l_rgbs = pair_losses(d1, d2, camera_mat, Rt_rel_12, s, i1, i2, res, nl, self.detach_rgbs_scale)
+            return {"pair_losses": (l_pc, l_rgbs), "sample_resolution": res, "rt_12": Rt_rel_12,
+                    "rt_12_gt": Rt_rel_12_gt}
+        R_rel_12, t_rel_12 = Rt_rel_12[:, :3, :3], Rt_rel_12[:, :3, 3]
+        pixel_locations, p_pc = arange_pixels(resolution=res, device=img.device)
         pc1 = transform_to_world(p_pc, d1.view(1, -1, 1), camera_mat)
         pc2 = transform_to_world(p_pc, d2.view(1, -1, 1), camera_mat)
         out = {}

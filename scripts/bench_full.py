@@ -1,0 +1,110 @@
+"""Benchmark of the full NoPe-NeRF training step (BASELINE.json configs[2], config 3 of
+SURVEY.md section 8(d)): joint pose + depth-distortion learning with the rgb, depth,
+point-cloud (chamfer) and reprojection (rgb_s) losses on a V_KITTI-shaped two-view scene
+(188x621, 1024 rays x 128 samples, D = 256, point clouds at 47x155 = 7285 points).
+Steps alternate the two cameras (both branches of training.py:329-358).  Inputs resident
+in HBM; synthetic data (no dataset offline).  Prints one JSON line.
+
+    python scripts/bench_full.py [--steps K --warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "my-nope-nerf_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+H, W, FOCAL = 188, 621, 362.5
+RAYS, SAMPLES, HIDDEN = 1024, 128, 256
+
+
+def scene(dev):
+    from tests.helpers import camera_K, rigid_c2w
+    g = torch.Generator().manual_seed(0)
+    yy, xx = torch.meshgrid(torch.linspace(0, 1, H), torch.linspace(0, 1, W), indexing="ij")
+    imgs, depths = [], []
+    for s in (0, 1):
+        img = torch.stack([0.5 + 0.4 * torch.sin(6 * xx + 2 * yy + 0.3 * s), 0.5 + 0.4 * torch.cos(5 * yy),
+                           0.3 + 0.3 * xx * yy], 0).unsqueeze(0)
+        imgs.append((img + 0.02 * torch.rand(img.shape, generator=g)).clamp(0, 1).to(dev))
+        d = 1.0 + 7.0 * torch.rand(1, H, W, generator=g)
+        d[torch.rand(1, H, W, generator=g) < 0.05] = 0.0
+        depths.append(d.to(dev))
+    c2w = torch.stack([rigid_c2w(0), rigid_c2w(0)])
+    c2w[1, :3, 3] += torch.tensor([0.1, 0.0, -0.2])
+    K = camera_K(H, W, FOCAL, FOCAL).to(dev)
+    datas = []
+    for cam in (0, 1):
+        ref = 1 - cam
+        datas.append({"img": imgs[cam], "img.depth": depths[cam], "img.depth_mask": (depths[cam] > 0).cpu(),
+                      "img.camera_mat": K, "img.scale_mat": torch.eye(4, device=dev).unsqueeze(0),
+                      "img.pose_gt": c2w[cam].unsqueeze(0).to(dev), "img.idx": torch.tensor([cam]),
+                      "img.ref_imgs": imgs[ref], "img.ref_depths": depths[ref], "img.ref_idxs": torch.tensor([ref]),
+                      "img.ref_pose_gt": c2w[ref].unsqueeze(0).to(dev)})
+    return datas, c2w
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    args = ap.parse_args()
+    import model as mdl
+    from model import _hip
+    from model.optim import HipAdam
+    from tests.helpers import make_cfg
+    dev = torch.device("cuda", 0)
+    _hip.load_library()
+    _hip.gemm_set_precision(1)
+    cfg = make_cfg(hidden=HIDDEN, S=SAMPLES)
+    t = cfg["training"]
+    t["n_training_points"] = RAYS
+    t["annealing_epochs"], t["scheduling_start"] = 2000, 0      # default.yaml:139: rgb l1 in the early epochs
+    datas, c2w = scene(dev)
+    torch.manual_seed(42)
+    net = mdl.OfficialStaticNerf(cfg)
+    renderer = mdl.Renderer(net, cfg["rendering"], device=dev)
+    nn_model = mdl.get_model(renderer, cfg, device=dev)
+    opt = HipAdam(nn_model.parameters(), lr=1e-3)
+    pose = mdl.LearnPose(2, True, True, cfg, init_c2w=c2w.clone()).to(dev)
+    distn = mdl.Learn_Distortion(2, True, True, cfg).to(dev)
+    opt_pose = torch.optim.Adam(pose.parameters(), lr=5e-4)          # train.py:100, :118
+    opt_dist = torch.optim.Adam(distn.parameters(), lr=5e-4)
+    tr = mdl.Trainer(nn_model, opt, t, device=dev, optimizer_pose=opt_pose, pose_param_net=pose,
+                     optimizer_distortion=opt_dist, distortion_net=distn)
+
+    def one(i):
+        return tr.train_step(datas[i % 2], it=i + 1, epoch=0, scheduling_start=0)
+
+    for i in range(args.warmup):
+        one(i)
+    torch.cuda.synchronize()
+    host = []
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        th = time.perf_counter()
+        ld = one(args.warmup + i)
+        host.append(time.perf_counter() - th)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out = {"metric": "full NoPe-NeRF training rays/sec (config 3: pose + distortion + pc + rgb_s losses)",
+           "value": RAYS * args.steps / el, "unit": "rays/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": 1e3 * el / args.steps, "dtype": "f32",
+           "gemm_arithmetic": "bf16x6", "data": "synthetic two-view V_KITTI-shaped scene",
+           "config": {"workload": "config 3: 188x621, 1024 rays x 128 samples, D=256, pose+distortion learned, "
+                                  "pc chamfer 7285 points, rgb_s reprojection"},
+           "losses": {k: float(ld[k].detach()) for k in ("loss", "loss_rgb", "loss_depth", "loss_pc", "loss_rgb_s")},
+           # host time to enqueue one step (median): close to ms_per_step = launch-bound host
+           "host_ms_per_step_median": 1e3 * sorted(host)[len(host) // 2]}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
