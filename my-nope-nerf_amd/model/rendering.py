@@ -44,6 +44,19 @@ def camera_rays(pixels, depth, camera_mat, world_mat, scale_mat, normalise_ray=T
     return cam.reshape(-1, 3), ray.reshape(-1, 3), ray_norm[0], d_src[0], mask
 
 
+def get_sphere_intersection(cam_loc, ray_directions, r=1.0):
+    """rendering.py:447-468: (near, far) distances along the rays to the sphere |x| = r,
+    0 without an intersection, clamped at 0; and the intersection mask."""
+    n_imgs, n_pix, _ = ray_directions.shape
+    cam = cam_loc.unsqueeze(-1)
+    ray_cam_dot = torch.bmm(ray_directions, cam).squeeze(-1).reshape(-1)
+    under_sqrt = ray_cam_dot ** 2 - (cam.norm(2, 1) ** 2 - r ** 2).reshape(-1).repeat_interleave(n_pix)
+    mask = under_sqrt > 0
+    root = torch.sqrt(under_sqrt.clamp_min(0)).unsqueeze(-1) * torch.tensor([-1.0, 1.0], device=cam_loc.device)
+    inter = torch.where(mask.unsqueeze(-1), root - ray_cam_dot.unsqueeze(-1), torch.zeros_like(root))
+    return inter.reshape(n_imgs, n_pix, 2).clamp_min(0.0), mask.reshape(n_imgs, n_pix)
+
+
 class Renderer(nn.Module):
     def __init__(self, model, cfg, device=None, **kwargs):
         super().__init__()
@@ -59,9 +72,102 @@ class Renderer(nn.Module):
         if rendering_technique == "nope_nerf":
             return self.nope_nerf(pixels, depth, camera_mat, world_mat, scale_mat, it=it,
                                   add_noise=add_noise, eval_=eval_, **kw)
-        raise NotImplementedError(
-            f"rendering_technique '{rendering_technique}' (phong / sphere tracing visualisation, "
-            "rendering.py:203-460) is outside the MI355X hot path")
+        if rendering_technique == "phong_renderer":
+            return self.phong_renderer(pixels, camera_mat, world_mat, scale_mat, it)
+        raise NotImplementedError(f"rendering_technique '{rendering_technique}'")
+
+    # ------------------------------------------------------------ geometry visualisation
+    def phong_renderer(self, pixels, camera_mat, world_mat, scale_mat, it):
+        """rendering.py:199-258: the occupancy surface found by ray marching, shaded with a
+        headlight (ambient 0.3 + diffuse 0.7 of the normal -d sigma_raw/dp), background 1;
+        'rgb_surf' is the field's colour at the surface.  The field evaluations (512 samples
+        per ray, 8 secant steps, the normals) run on the nerf_hip MLP kernels."""
+        B, n, _ = pixels.shape
+        dev = pixels.device
+        rad = self.cfg["radius"]
+        M = unproject_matrix(camera_mat, world_mat, scale_mat)
+        cam, ray, _, _, _, _ = camera_rays_hip(M, pixels, None, True, view_ones=True)
+        cam_w, ray = cam.view(1, n, 3), ray.view(1, n, 3)
+        light_src = cam_w[0, 0]
+        light = (light_src / light_src.norm(2)).unsqueeze(1)
+        diffuse_per = torch.tensor([0.7, 0.7, 0.7], device=dev)
+        ambient = torch.tensor([0.3, 0.3, 0.3], device=dev)
+        was_training = self.model.training
+        self.model.eval()
+        with torch.no_grad():
+            d_i = self.ray_marching(cam_w, ray, self.model, n_secant_steps=8, n_steps=[512, 513], rad=rad)
+            zero_occ = d_i == 0
+            mask_pred = get_mask(d_i)
+            dists = torch.where(mask_pred, d_i, torch.ones_like(d_i))
+            dists = torch.where(zero_occ, torch.zeros_like(dists), dists)
+            obj = (mask_pred & ~zero_occ)[0]
+            dists = dists[0]
+            cam_f, ray_f = cam_w.reshape(-1, 3), ray.reshape(-1, 3)
+            points = cam_f + ray_f * dists.unsqueeze(-1)
+            view = -ray_f
+            rgb = torch.ones_like(points)
+            surf, surf_view = points[obj], view[obj]
+            rgb_surf = torch.zeros(B * n, 3, device=dev)
+            if surf.shape[0] > 0:
+                grad = self.model.gradient(surf, it)[:, 0, :].detach()
+                normals = grad / grad.norm(2, 1, keepdim=True)
+                diffuse = torch.mm(normals, light).clamp_min(0).repeat(1, 3) * diffuse_per.unsqueeze(0)
+                rgb[obj] = (ambient.unsqueeze(0) + diffuse).clamp_max(1.0)
+                rgb_surf[obj] = self.model(surf, surf_view)
+        self.model.train(was_training)
+        return {"rgb": rgb.reshape(B, -1, 3), "normal": None, "rgb_surf": rgb_surf.reshape(B, -1, 3)}
+
+    def ray_marching(self, ray0, ray_direction, model, c=None, tau=0.5, n_steps=[128, 129], n_secant_steps=8,
+                     depth_range=[0.0, 2.4], max_points=3500000, rad=1.0):
+        """rendering.py:262-403: evaluate n_steps samples between depth_range[0] and the far
+        intersection with the sphere of radius ``rad``, take the first outside->inside sign
+        change of occupancy - tau and refine it with the secant method; inf where there is
+        none, 0 where the first sample is already occupied.  All samples are one batched
+        field evaluation (max_points chunks)."""
+        B, n_pts, _ = ray0.shape
+        dev = ray0.device
+        n_steps = int(torch.randint(n_steps[0], n_steps[1], (1,)).item())
+        d_int, _ = get_sphere_intersection(ray0[:, 0], ray_direction, r=rad)
+        d_far = d_int[..., 1]
+        t = torch.linspace(0, 1, steps=n_steps, device=dev).view(1, 1, n_steps, 1)
+        d_prop = depth_range[0] * (1.0 - t) + d_far.view(1, -1, 1, 1) * t
+        p_prop = (ray0.unsqueeze(2) + ray_direction.unsqueeze(2) * d_prop).reshape(-1, 3)
+        val = torch.cat([model(ps, only_occupancy=True) - tau for ps in torch.split(p_prop, max_points)])
+        val = val.view(B, n_pts, n_steps)
+        mask_0_not_occ = val[:, :, 0] < 0
+        sign = torch.cat([torch.sign(val[:, :, :-1] * val[:, :, 1:]), torch.ones(B, n_pts, 1, device=dev)], -1)
+        cost = sign * torch.arange(n_steps, 0, -1, device=dev).float()
+        values, idx = torch.min(cost, -1)
+        mask_sign_change = values < 0
+        mask_neg_to_pos = torch.gather(val, 2, idx.unsqueeze(-1)).squeeze(-1) < 0
+        mask = mask_sign_change & mask_neg_to_pos & mask_0_not_occ
+        dp = d_prop.expand(B, n_pts, n_steps, 1)[..., 0]
+        take = lambda a, i: torch.gather(a, 2, i.unsqueeze(-1)).squeeze(-1)[mask]
+        idx_h = torch.clamp(idx + 1, max=n_steps - 1)
+        d_low, f_low, d_high, f_high = take(dp, idx), take(val, idx), take(dp, idx_h), take(val, idx_h)
+        d_out = torch.ones(B, n_pts, device=dev)
+        if d_low.shape[0] != 0:
+            d_out[mask] = self.secant(f_low, f_high, d_low, d_high, n_secant_steps, ray0[mask],
+                                      ray_direction[mask], tau, model=model)
+        d_out = torch.where(mask, d_out, torch.full_like(d_out, float("inf")))
+        d_out = torch.where(mask_0_not_occ, d_out, torch.zeros_like(d_out))
+        return d_out
+
+    def secant(self, f_low, f_high, d_low, d_high, n_secant_steps, ray0_masked, ray_direction_masked, tau,
+               it=0, model=None):
+        """rendering.py:405-436."""
+        model = model if model is not None else self.model
+        d_pred = -f_low * (d_high - d_low) / (f_high - f_low) + d_low
+        for _ in range(n_secant_steps):
+            p_mid = ray0_masked + d_pred.unsqueeze(-1) * ray_direction_masked
+            f_mid = model(p_mid, only_occupancy=True, it=it)[..., 0] - tau
+            low = f_mid < 0
+            d_low = torch.where(low, d_pred, d_low)
+            f_low = torch.where(low, f_mid, f_low)
+            d_high = torch.where(low, d_high, d_pred)
+            f_high = torch.where(low, f_high, f_mid)
+            d_pred = -f_low * (d_high - d_low) / (f_high - f_low) + d_low
+        return d_pred
 
     def _flags(self) -> int:
         f = 0

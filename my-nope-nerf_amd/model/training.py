@@ -331,8 +331,8 @@ class Trainer(object):
 
     # ------------------------------------------------------------------ render
     def render_visdata(self, data, resolution, it, out_render_path):
-        """training.py:103-165 (colour + depth PNGs at ``resolution``; the phong geometry
-        visualisation is outside the MI355X path)."""
+        """training.py:103-165: colour + depth PNGs at ``resolution`` and, with ``vis_geo``,
+        the Phong-shaded occupancy surface (``%04d_geo.png``, Renderer.phong_renderer)."""
         from PIL import Image
         img, depth_input, camera_mat, scale_mat, img_idx, *_ = self.process_data_dict(data)
         h, w = resolution
@@ -354,4 +354,13 @@ class Trainer(object):
             dimg = np.clip(255.0 / depth.max() * (depth - depth.min()), 0, 255).astype(np.uint8)
             Image.fromarray(dimg).save(os.path.join(out_render_path, "%04d_depth.png" % int(img_idx)))
             Image.fromarray(img_out).convert("RGB").save(os.path.join(out_render_path, "%04d_img.png" % int(img_idx)))
+        if self.vis_geo:                                       # training.py:144-163
+            with torch.no_grad():
+                geo = torch.cat([self.model(pix_i, None, camera_mat, world_mat, scale_mat, "phong_renderer",
+                                            add_noise=False, eval_mode=True, it=it, depth_img=depth_input,
+                                            img_size=(h, w))["rgb"] for pix_i in torch.split(pixels, 1024, dim=1)],
+                                dim=1)
+                img_out = (geo.view(h, w, 3).cpu().numpy() * 255).astype(np.uint8)
+            if out_render_path:
+                Image.fromarray(img_out).convert("RGB").save(os.path.join(out_render_path, "%04d_geo.png" % int(img_idx)))
         return img_out

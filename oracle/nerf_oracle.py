@@ -90,6 +90,27 @@ class OracleNerf(nn.Module):
         rgb = torch.sigmoid(self.fc_rgb(h))
         return rgb, sigma
 
+    def density_raw(self, p: torch.Tensor) -> torch.Tensor:
+        """infer_occ (official_nerf.py:60-67): fc_density of the trunk."""
+        enc_p = encode_position(p, 10)
+        x = self.layers0(enc_p)
+        x = self.layers1(torch.cat([x, enc_p], dim=-1))
+        return self.fc_density(x)
+
+    def occupancy(self, p: torch.Tensor) -> torch.Tensor:
+        """forward(p, only_occupancy=True) (official_nerf.py:76-85)."""
+        sigma = self.density_raw(p)
+        sigma = F.softplus(sigma) if self.occ_activation == "softplus" else sigma.relu()
+        return sigma if self.dist_alpha else 1 - torch.exp(-1.0 * sigma)
+
+    def gradient(self, p: torch.Tensor) -> torch.Tensor:
+        """official_nerf.py:46-58: -d(fc_density)/dp as [N, 1, 3]."""
+        with torch.enable_grad():
+            p = p.detach().requires_grad_(True)
+            y = self.density_raw(p)
+            g = torch.autograd.grad(y, p, torch.ones_like(y))[0]
+        return -g.unsqueeze(1)
+
 
 # ----------------------------------------------------------------------------
 # camera helpers  (model/common.py)
@@ -569,3 +590,108 @@ def compute_loss_full(model, pose, distortion, data, tcfg, rcfg, epoch, scheduli
                     rgb_s=terms.get("rgb_s"))
     ld["scale"], ld["shift"] = scale_input, shift_input
     return ld
+
+
+# ----------------------------------------------------------------------------
+# geometry visualisation: sphere-bounded ray marching, secant refinement and Phong
+# shading of the occupancy surface (rendering.py:199-460)
+# ----------------------------------------------------------------------------
+def get_sphere_intersection(cam_loc, ray_directions, r=1.0):
+    """rendering.py:447-468: near/far distances of the rays to the sphere |x| = r (0 without
+    an intersection), clamped at 0.  cam_loc [n_imgs, 3], ray_directions [n_imgs, n_pix, 3]."""
+    n_imgs, n_pix, _ = ray_directions.shape
+    cam = cam_loc.unsqueeze(-1)
+    ray_cam_dot = torch.bmm(ray_directions, cam).squeeze()
+    under_sqrt = (ray_cam_dot ** 2 - (cam.norm(2, 1) ** 2 - r ** 2)).reshape(-1)
+    mask = under_sqrt > 0
+    inter = torch.zeros(n_imgs * n_pix, 2, dtype=ray_directions.dtype)
+    inter[mask] = torch.sqrt(under_sqrt[mask]).unsqueeze(-1) * torch.tensor([-1.0, 1.0], dtype=inter.dtype)
+    inter[mask] -= ray_cam_dot.reshape(-1)[mask].unsqueeze(-1)
+    return inter.reshape(n_imgs, n_pix, 2).clamp_min(0.0), mask.reshape(n_imgs, n_pix)
+
+
+def secant(model, f_low, f_high, d_low, d_high, n_secant_steps, ray0, ray_dir, tau):
+    """rendering.py:405-436."""
+    d_pred = -f_low * (d_high - d_low) / (f_high - f_low) + d_low
+    for _ in range(n_secant_steps):
+        p_mid = ray0 + d_pred.unsqueeze(-1) * ray_dir
+        f_mid = model.occupancy(p_mid)[..., 0] - tau
+        low = f_mid < 0
+        d_low = torch.where(low, d_pred, d_low)
+        f_low = torch.where(low, f_mid, f_low)
+        d_high = torch.where(low, d_high, d_pred)
+        f_high = torch.where(low, f_high, f_mid)
+        d_pred = -f_low * (d_high - d_low) / (f_high - f_low) + d_low
+    return d_pred
+
+
+def ray_marching(model, ray0, ray_direction, tau=0.5, n_steps=512, n_secant_steps=8, depth_range=(0.0, 2.4),
+                 rad=1.0):
+    """rendering.py:262-403: n_steps samples from depth_range[0] to the far sphere
+    intersection, first sign change of occupancy - tau from outside to inside, secant
+    refinement; inf where none, 0 where the first sample is already occupied."""
+    B, n_pts, _ = ray0.shape
+    d_int, _ = get_sphere_intersection(ray0[:, 0], ray_direction, r=rad)
+    d_far = d_int[..., 1]
+    t = torch.linspace(0, 1, steps=n_steps, dtype=ray0.dtype).view(1, 1, n_steps, 1)
+    d_prop = depth_range[0] * (1.0 - t) + d_far.view(1, -1, 1, 1) * t
+    p_prop = ray0.unsqueeze(2) + ray_direction.unsqueeze(2) * d_prop
+    val = (model.occupancy(p_prop.reshape(-1, 3)) - tau).view(B, n_pts, n_steps)
+    mask_0_not_occ = val[:, :, 0] < 0
+    sign = torch.cat([torch.sign(val[:, :, :-1] * val[:, :, 1:]), torch.ones(B, n_pts, 1, dtype=val.dtype)], -1)
+    cost = sign * torch.arange(n_steps, 0, -1, dtype=val.dtype)
+    values, idx = torch.min(cost, -1)
+    mask_sign_change = values < 0
+    mask_neg_to_pos = torch.gather(val, 2, idx.unsqueeze(-1)).squeeze(-1) < 0
+    mask = mask_sign_change & mask_neg_to_pos & mask_0_not_occ
+    dp = d_prop.expand(B, n_pts, n_steps, 1)[..., 0]
+    d_low = torch.gather(dp, 2, idx.unsqueeze(-1)).squeeze(-1)[mask]
+    f_low = torch.gather(val, 2, idx.unsqueeze(-1)).squeeze(-1)[mask]
+    idx_h = torch.clamp(idx + 1, max=n_steps - 1)
+    d_high = torch.gather(dp, 2, idx_h.unsqueeze(-1)).squeeze(-1)[mask]
+    f_high = torch.gather(val, 2, idx_h.unsqueeze(-1)).squeeze(-1)[mask]
+    d_out = torch.ones(B, n_pts, dtype=ray0.dtype)
+    if mask.any():
+        d_out[mask] = secant(model, f_low, f_high, d_low, d_high, n_secant_steps, ray0[mask],
+                             ray_direction[mask], tau)
+    d_out[~mask] = float("inf")
+    d_out[~mask_0_not_occ] = 0.0
+    return d_out
+
+
+def phong_renderer(model, pixels, camera_mat, world_mat, scale_mat, rad=4.0, n_steps=512):
+    """rendering.py:199-258: surface by ray marching, Phong-lit normals (ambient 0.3,
+    diffuse 0.7, headlight from the camera direction), background 1; also the field's
+    colour at the surface ('rgb_surf')."""
+    B, n, _ = pixels.shape
+    pix_w = image_points_to_world(pixels, camera_mat, world_mat, scale_mat)
+    cam_w = origin_to_world(n, camera_mat, world_mat, scale_mat)
+    ray = pix_w - cam_w
+    ray = ray / ray.norm(2, 2).unsqueeze(-1)
+    light_src = cam_w[0, 0]
+    light = (light_src / light_src.norm(2)).unsqueeze(1)
+    diffuse_per = torch.tensor([0.7, 0.7, 0.7], dtype=pixels.dtype)
+    ambient = torch.tensor([0.3, 0.3, 0.3], dtype=pixels.dtype)
+    with torch.no_grad():
+        d_i = ray_marching(model, cam_w, ray, n_steps=n_steps, n_secant_steps=8, rad=rad)
+    zero_occ = d_i == 0
+    mask_pred = get_mask(d_i)
+    dists = torch.ones_like(d_i)
+    dists[mask_pred] = d_i[mask_pred]
+    dists[zero_occ] = 0.0
+    obj = (mask_pred & ~zero_occ)[0]
+    dists = dists[0]
+    cam_f, ray_f = cam_w.reshape(-1, 3), ray.reshape(-1, 3)
+    points = cam_f + ray_f * dists.unsqueeze(-1)
+    view = -ray_f
+    rgb = torch.ones_like(points)
+    surf, surf_view = points[obj], view[obj]
+    grad = model.gradient(surf)[:, 0, :]
+    normals = grad / grad.norm(2, 1, keepdim=True)
+    diffuse = torch.mm(normals, light).clamp_min(0).repeat(1, 3) * diffuse_per.unsqueeze(0)
+    rgb[obj] = (ambient.unsqueeze(0) + diffuse).clamp_max(1.0)
+    rgb_surf = torch.zeros(B * n, 3, dtype=pixels.dtype)
+    with torch.no_grad():
+        rgb_surf[obj] = model(surf, surf_view)[0]
+    return {"rgb": rgb.reshape(B, -1, 3), "normal": None, "rgb_surf": rgb_surf.reshape(B, -1, 3),
+            "d_i": d_i, "mask": obj}
