@@ -236,7 +236,7 @@ def main():
             # the committed rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE); algorithmic:
             # x 134.2 MB + y 134.2 MB + ReLU bits 4.2 MB + weight image 0.4 MB = 273 MB
             t = json.load(open(tpath))
-            fwd = [x for x in t["launches"] if "k_gemm_nt_x6<256, 256, 2, 2, 0>" in x["kernel"]]
+            fwd = [x for x in t["launches"] if "k_gemm_nt_x6<256, 256, 2, 2, 0" in x["kernel"]]
             if fwd:
                 traffic = fwd[0]["bytes"]
                 traffic_note = ("k_gemm_nt_x6<256,256> forward, one launch, bytes from profiles/r01/gemm_traffic.json "

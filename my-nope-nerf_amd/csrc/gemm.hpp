@@ -337,7 +337,7 @@ __device__ __forceinline__ void nt_epilogue_lds(const NTArgs& p, f32x16 (&acc)[T
 //   BWD: + u[row] v[feature], masked by the input layer's ReLU bits.
 template <int TM, int TN, int EPI>
 __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0, int wm0,
-                                                   int wn0) {
+                                                   int wn0, uint32_t* lmask = nullptr, int mw = 0) {
     const int lane = lane_id();
     const int sl = lane & 31, hf = lane >> 5;
     if (p.ablate & 1) {
@@ -376,7 +376,12 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
                 }
                 if (p.mask_out) {
                     w |= (uint32_t)__shfl_xor((int)w, 32, 64);
-                    if (hf == 0) p.mask_out[row * p.ldmo + cw0 + j] = w;
+                    // gathered in LDS and stored as the block's contiguous mask rows by the
+                    // caller (4-byte stores at a 32-byte row stride are partial-line writes)
+                    if (hf == 0) {
+                        if (lmask) lmask[(wm0 + 32 * i + sl) * mw + (wn0 >> 5) + j] = w;
+                        else p.mask_out[row * p.ldmo + cw0 + j] = w;
+                    }
                 }
             }
         }

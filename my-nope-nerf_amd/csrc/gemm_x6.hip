@@ -373,7 +373,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt_x6(NTArgs p) {
     using St = NTStager<BM, BN, NT>;
     static_assert(TM >= 1 && TN >= 1, "bad tile");
     constexpr int LOOP_BYTES = 2 * (XImg<BM>::BYTES + XImg<BN>::BYTES) + St::NSLOT * St::RAW;
-    constexpr int EPI_BYTES = DIRECT ? 0 : (NT / 64) * TileLds<TN>::BYTES + (BM * (BN / 32) + BM) * 4;
+    constexpr int EPI_BYTES = DIRECT ? BM * (BN / 32) * 4 : (NT / 64) * TileLds<TN>::BYTES + (BM * (BN / 32) + BM) * 4;
     __shared__ __attribute__((aligned(16))) char smem[LOOP_BYTES > EPI_BYTES ? LOOP_BYTES : EPI_BYTES];
     const int wave = threadIdx.x >> 6;
     const int wm0 = (wave / WN) * WTM;
@@ -390,7 +390,20 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt_x6(NTArgs p) {
     if (DIRECT) {
         x6_mainloop_pf<TM, TN, BM, BN, true>(smem, K / XK, wm0, wn0, acc, st, p.stamps);
         stamp(p.stamps, 2);
-        nt_epilogue_direct<TM, TN, EPI>(p, acc, m0, n0, wm0, wn0);
+        constexpr int MW = BN / 32;
+        const bool gather = EPI == EPI_FWD && p.mask_out != nullptr && !(p.ablate & 1);
+        uint32_t* lmask = nullptr;
+        if (gather) {    // the mask rows reuse the staging LDS once the last (clamped) DMA landed
+            dma_wait();
+            __syncthreads();
+            lmask = reinterpret_cast<uint32_t*>(smem);
+        }
+        nt_epilogue_direct<TM, TN, EPI>(p, acc, m0, n0, wm0, wn0, lmask, MW);
+        if (gather) {
+            __syncthreads();
+            for (int e = threadIdx.x; e < BM * MW; e += NT)
+                p.mask_out[(size_t)(m0 + e / MW) * p.ldmo + (n0 >> 5) + e % MW] = lmask[e];
+        }
         dma_wait();      // the last (clamped) raw-A DMA lands before the workgroup's LDS is released
     } else {
         NTEpiPrefetch<BM, BN, NT, EPI> pf;
