@@ -33,9 +33,16 @@ def _rel(a, b):
     (64, 64, 256, {}),                                      # config 1 shape
     (256, 128, 200, {"white_background": True}),
     (128, 96, 300, {"dist_alpha": True}),
+    (128, 64, 256, {"sample_option": "ndc", "dist_alpha": True}),   # LLFF (configs/LLFF/fern.yaml:6-8)
+    (64, 32, 128, {"use_ray_dir": False, "normalise_ray": False}),
+    (64, 32, 128, {"occ_activation": "relu"}),
 ])
 def test_render_forward_matches_oracle(dev, gemm_precision, hidden, S, R, opts):
+    opts = dict(opts)
+    occ = opts.pop("occ_activation", None)
     cfg = make_cfg(hidden=hidden, S=S, **opts)
+    if occ is not None:
+        cfg["model"]["occ_activation"] = occ
     net, ref = _pair(cfg)
     b = synthetic_rays(R=R, S=S, seed=hidden + S)
     rnd = Renderer(net.to(dev), cfg["rendering"], device=dev)
