@@ -46,7 +46,10 @@ def _psnr_oracle(ref, pix, depth_flat, K, w2c, scale, img_flat, cfg):
     return orc.mse2psnr(((out["rgb"] - img_flat) ** 2).mean().item())
 
 
-@pytest.mark.parametrize("hidden,S,R,steps", [(64, 64, 256, 80)])
+@pytest.mark.parametrize("hidden,S,R,steps", [
+    (64, 64, 256, 80),          # config 1 shape
+    (256, 128, 1024, 25),       # the bench shape (config 2: D = 256, 1024 rays x 128 samples)
+])
 def test_training_psnr_parity(dev, gemm_precision, hidden, S, R, steps):
     cfg = make_cfg(hidden=hidden, S=S)
     r = cfg["rendering"]
@@ -94,7 +97,7 @@ def test_training_psnr_parity(dev, gemm_precision, hidden, S, R, steps):
     p1_o = _psnr_oracle(ref, pix, depth_flat, K, w2c, scale, img_flat, r)
 
     assert abs(p0_h - p0_o) < 1e-3, (p0_h, p0_o)                   # same initial field
-    assert p1_o > p0_o + 1.0, (p0_o, p1_o)                          # training did something
+    assert p1_o > p0_o + 0.5, (p0_o, p1_o)                          # training did something
     print(f"PSNR init {p0_h:.4f}/{p0_o:.4f} dB, after {steps} steps HIP {p1_h:.4f} dB, oracle {p1_o:.4f} dB")
     assert abs(p1_h - p1_o) < 0.1, f"PSNR after {steps} steps: HIP {p1_h:.4f} dB vs oracle {p1_o:.4f} dB"
     assert math.isclose(loss_h[0], loss_o[0], rel_tol=1e-4)
