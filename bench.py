@@ -13,9 +13,11 @@ gradient all-reduce over RCCL (N > 1), Adam.  Inputs are resident in HBM.
 Rank 0 prints ONE JSON line.  Extra objects: "roofline" (the field-MLP GEMM family,
 timed live with hipEvents around every GEMM launch of the timed steps), "cpu_baseline"
 (the oracle CPU restatement of the same step on this host's cores, bounded sample) and
-"alt_gemm" (the same workload with the other GEMM arithmetic).  The GEMMs compute f32
-products either on the exact-f32 MFMA or, by default, as a 3-word bf16 split with six
-MFMA products accumulated in f32 (f32-accurate: DESIGN.md section 4).
+"alt_gemm" (the same workload with the other GEMM arithmetics).  The GEMMs compute f32
+products on the exact-f32 MFMA (f32), as a 3-word bf16 split with six MFMA products
+accumulated in f32 (bf16x6), or -- forward and backward-data GEMMs -- as a row-scaled
+2-word fp16 split with three products (f16x3; its weight gradients as bf16x6).  All three
+are f32-accurate (DESIGN.md section 4, tests/test_gpu_kernels.py::test_split_accuracy).
 """
 from __future__ import annotations
 
@@ -88,21 +90,38 @@ def build_trainer(dev, c2w, cfg):
     return trainer, net
 
 
-def algorithmic_gemm_flops(net, n_samples):
+def algorithmic_gemm_flops(net, n_samples, split=False):
     """FP32 FLOPs of the field GEMMs one train step needs (reference shapes, no padding):
     forward and weight-gradient of every Linear, input-gradient of every Linear except
-    the first and except the encoding columns (poses fixed)."""
+    the first and except the encoding columns (poses fixed).  split: (forward + input
+    gradient, weight gradient) separately."""
     D = net.hidden_dim
     layers = [net.layers0[0], net.layers0[2], net.layers0[4], net.layers0[6], net.layers1[0], net.layers1[2],
               net.layers1[4], net.layers1[6], net.fc_feature, net.rgb_layers[0]]
-    fl = 0
+    nt = tn = 0
     for i, lin in enumerate(layers):
         out_f, in_f = lin.weight.shape
-        fl += 2 * n_samples * out_f * in_f * 2          # forward + dW
+        nt += 2 * n_samples * out_f * in_f               # forward
+        tn += 2 * n_samples * out_f * in_f               # dW
         if i > 0:
             in_x = D if lin in (net.layers1[0], net.rgb_layers[0]) else in_f
-            fl += 2 * n_samples * out_f * in_x           # dX
-    return fl
+            nt += 2 * n_samples * out_f * in_x           # dX
+    return (nt, tn) if split else nt + tn
+
+
+PRECISION = {"f32": 0, "bf16x6": 1, "f16x3": 2}
+
+
+def gemm_peak(mode, nt_flops, tn_flops):
+    """f32-equivalent MFMA peak of the GEMM family in arithmetic `mode`: the dense MFMA rate
+    divided by the products per f32 product (f32: 1 on the f32 MFMA; bf16x6: 6; f16x3: 3 for
+    forward / input gradient, 6 for the weight gradients), weighted by the FLOPs each runs."""
+    if mode == "f32":
+        return FP32_MFMA_PEAK_TFLOPS
+    if mode == "bf16x6":
+        return BF16_MFMA_PEAK_TFLOPS / 6
+    t = nt_flops / (BF16_MFMA_PEAK_TFLOPS / 3) + tn_flops / (BF16_MFMA_PEAK_TFLOPS / 6)
+    return (nt_flops + tn_flops) / t
 
 
 def cpu_baseline(budget_s=20.0):
@@ -146,11 +165,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--gemm-precision", choices=["f32", "bf16x6"], default="bf16x6",
-                    help="GEMM arithmetic: f32 emulated by a 3-word bf16 split (6 products, f32-accurate; "
-                         "default) or the exact-f32 MFMA")
+    ap.add_argument("--gemm-precision", choices=list(PRECISION), default="bf16x6",
+                    help="GEMM arithmetic: f32 emulated by a 3-word bf16 split (bf16x6, default), by a row-scaled "
+                         "2-word fp16 split (f16x3), or the exact-f32 MFMA (f32); all f32-accurate")
     ap.add_argument("--no-alt", dest="alt", action="store_false",
-                    help="skip timing the other GEMM arithmetic (reported as alt_gemm)")
+                    help="skip timing the other GEMM arithmetics (reported as alt_gemm)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -169,7 +188,7 @@ def main():
 
     def measure(precision):
         """W warm-up + K timed train steps with the GEMMs in `precision` (0 exact-f32 MFMA,
-        1 split-bf16); returns (max-over-ranks seconds, last loss dict, GEMM hook stats)."""
+        1 split-bf16, 2 fp16 pair); returns (max-over-ranks seconds, last loss dict, GEMM hook stats)."""
         _hip.gemm_set_precision(precision)
         trainer, net = build_trainer(dev, c2w, cfg)
         torch.cuda.manual_seed(1000 + rank)                 # each rank samples its own rays
@@ -199,15 +218,18 @@ def main():
             el = t.item()
         return el, ld, stats, net
 
-    main_prec = 1 if args.gemm_precision == "bf16x6" else 0
+    main_prec = PRECISION[args.gemm_precision]
     elapsed, ld, (gemm_ms, gemm_launches, _, gemm_union_ms), net = measure(main_prec)
     alt = None
     if args.alt:
-        # the other GEMM arithmetic on the same workload, reported beside the headline
-        el2, ld2, _, _ = measure(1 - main_prec)
-        alt = {"gemm_arithmetic": "f32" if main_prec == 1 else "bf16x6",
-               "value": world * RAYS / (el2 / args.steps), "ms_per_step": 1e3 * el2 / args.steps,
-               "final_loss": ld2["loss"].detach().item()}
+        # the other GEMM arithmetics on the same workload, reported beside the headline
+        alt = []
+        for name, prec in PRECISION.items():
+            if prec == main_prec:
+                continue
+            el2, ld2, _, _ = measure(prec)
+            alt.append({"gemm_arithmetic": name, "value": world * RAYS / (el2 / args.steps),
+                        "ms_per_step": 1e3 * el2 / args.steps, "final_loss": ld2["loss"].detach().item()})
         _hip.gemm_set_precision(main_prec)
     loss = ld["loss"].detach().item()
     psnr = -10.0 * math.log10(max(ld["l2_mean"].detach().item(), 1e-10))
@@ -216,27 +238,30 @@ def main():
 
     if rank == 0:
         ms = 1e3 * elapsed / args.steps
-        alg = algorithmic_gemm_flops(net, RAYS * SAMPLES) * args.steps
+        nt_fl, tn_fl = algorithmic_gemm_flops(net, RAYS * SAMPLES, split=True)
+        alg = (nt_fl + tn_fl) * args.steps
         achieved = alg / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else None
         # achieved: algorithmic FLOPs / summed per-launch durations (the contract's per-launch
         # average).  The dW GEMMs run on a side stream concurrently with the dX chain, which
         # stretches each launch; achieved_union divides by the union of the launch intervals.
         achieved_union = alg / (gemm_union_ms * 1e-3) / 1e12 if gemm_union_ms > 0 else None
-        if args.gemm_precision == "bf16x6":
-            # 6 bf16 MFMA products per f32 product: the f32-equivalent peak is bf16 dense / 6
-            peak = BF16_MFMA_PEAK_TFLOPS / 6
-            kname = "k_gemm_nt_x6/k_gemm_tn_x6 (f32 as 3xbf16, 6 products on MFMA 32x32x16 bf16, field MLP)"
-        else:
-            peak = FP32_MFMA_PEAK_TFLOPS
-            kname = "k_gemm_nt/k_gemm_tn (FP32 MFMA 32x32x2, field MLP)"
+        peak = gemm_peak(args.gemm_precision, nt_fl, tn_fl)
+        kname = {"bf16x6": "k_gemm_nt_x6/k_gemm_tn_x6 (f32 as 3xbf16, 6 products on MFMA 32x32x16 bf16, field MLP)",
+                 "f16x3": "k_gemm_nt_x6<H> (f32 as row-scaled 2xfp16, 3 products on MFMA 32x32x16 f16; fwd + dX) / "
+                          "k_gemm_tn_x6 (bf16x6; dW), field MLP",
+                 "f32": "k_gemm_nt/k_gemm_tn (FP32 MFMA 32x32x2, field MLP)"}[args.gemm_precision]
         traffic, traffic_note = None, None
         tpath = os.path.join(ROOT, "profiles", "r01", "gemm_traffic.json")
-        if args.gemm_precision == "bf16x6" and os.path.exists(tpath):
+        # template arguments of the 256x256-tile forward launch per arithmetic (older summaries
+        # predate the trailing fp16-pair flag)
+        fwd_tags = {"bf16x6": ("<256, 256, 2, 2, 0, true>", "<256, 256, 2, 2, 0, true, false>"),
+                    "f16x3": ("<256, 256, 2, 2, 0, true, true>",)}.get(args.gemm_precision, ())
+        if fwd_tags and os.path.exists(tpath):
             # HBM bytes of one 256x256-tile forward launch (131072 x 256 x 256, mask out) from
             # the committed rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE); algorithmic:
             # x 134.2 MB + y 134.2 MB + ReLU bits 4.2 MB + weight image 0.4 MB = 273 MB
             t = json.load(open(tpath))
-            fwd = [x for x in t["launches"] if "k_gemm_nt_x6<256, 256, 2, 2, 0" in x["kernel"]]
+            fwd = [x for x in t["launches"] if any(tag in x["kernel"] for tag in fwd_tags)]
             if fwd:
                 traffic = fwd[0]["bytes"]
                 traffic_note = ("k_gemm_nt_x6<256,256> forward, one launch, bytes from profiles/r01/gemm_traffic.json "

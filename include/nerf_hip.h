@@ -47,11 +47,13 @@ const char* nerf_hip_last_error(void);
  * enc_p : [n_pad][64]  = [x(3), sin(2^i x)(3), cos(2^i x)(3) ... i<10, 0]   (63 + 1 pad)
  * enc_d : [n_pad][64]  = same with L=4 on view (27 + 37 pad)
  * z     : [n_pad]; rows >= R*S of all outputs are written as 0.
+ * enc_p_rmax, enc_d_rmax (optional, [n_pad]): max |.| of each encoding row (the row scales
+ * of GEMM precision mode 2).
  */
 int nerf_encode_samples(const float* pts_o, const float* pts_d, const float* view,
                         const float* noise, int n_rays, int n_samples, int n_pad,
                         float near_z, float far_z, float* z, float* enc_p, float* enc_d,
-                        void* stream);
+                        float* enc_p_rmax, float* enc_d_rmax, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Linear layer forward on FP32 MFMA (v_mfma_f32_32x32x2_f32).
@@ -66,11 +68,17 @@ int nerf_encode_samples(const float* pts_o, const float* pts_d, const float* vie
  * image (nerf_pack_weights dst_s): element (plane p, row r, col c) at
  * w_split[((p*(K/8) + c/8)*w_split_rows + r)*8 + c%8], K = k1+k2; w_split may point at
  * a row offset inside a larger image whose row count is w_split_rows.  NULL: this call
- * runs on the exact-f32 kernel even in mode 1.
+ * runs on the exact-f32 kernel even in modes 1 and 2.  In mode 2 the image is the fp16
+ * pair form written by nerf_pack_weights in that mode.
+ * x1_rmax / x2_rmax ([m], precision mode 2, required there): max |x| over each row of the
+ * segment (as written by the producer of x: nerf_encode_samples, this function, ...).
+ * y_rmax (optional, mode 2 only): receives max |y| per row; with n > 256 (several column
+ * blocks) it is max-accumulated and must be zeroed by the caller.
  */
 int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2, int k2,
                     const float* w, const uint16_t* w_split, int w_split_rows, const float* bias, float* y,
-                    int ldy, int m, int n, int relu, uint32_t* mask_out, int ldmo, void* stream);
+                    int ldy, int m, int n, int relu, uint32_t* mask_out, int ldmo,
+                    const float* x1_rmax, const float* x2_rmax, float* y_rmax, void* stream);
 
 /* Backward w.r.t. the layer input (autograd of official_nerf.py:62-91).
  *   dx[m, j] = ( sum_o dy[m,o] wt[j,o]  + (u ? u[m*ldu] * v[j] : 0) ) * (mask ? bit(m,j) : 1)
@@ -78,10 +86,12 @@ int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2
  * (n = number of input columns produced, k = layer outputs), mask: ReLU mask bits of
  * the previous layer's output as written by nerf_linear_fwd (ldmask words per row) or
  * NULL.  m%128==0, n%64==0, k%32==0.  wt_split / wt_split_rows: optional bf16x3 image of
- * wt as for nerf_linear_fwd (K = k). */
+ * wt as for nerf_linear_fwd (K = k).  dy_rmax / dx_rmax: row maxima as x1_rmax / y_rmax of
+ * nerf_linear_fwd (mode 2). */
 int nerf_linear_bwd_data(const float* dy, int lddy, int k, const float* wt, const uint16_t* wt_split,
                          int wt_split_rows, const float* u, int ldu, const float* v, const uint32_t* mask,
-                         int ldmask, float* dx, int lddx, int m, int n, void* stream);
+                         int ldmask, float* dx, int lddx, int m, int n, const float* dy_rmax, float* dx_rmax,
+                         void* stream);
 
 /* Backward w.r.t. weight and bias, split over sample rows:
  *   slab[split][o][col0 + j] = sum_{rows of split} dy[row, o] * x[row, j]   (j < kin)
@@ -114,6 +124,12 @@ int nerf_gemm_set_policy(int nt_policy, int tn_policy);
  *      words (exact), the six cross products >= 2^-16 |a||b| accumulated in f32.
  *      nerf_linear_fwd / nerf_linear_bwd_data use it when given the weight's split
  *      image (w_split / wt_split), nerf_linear_bwd_weight always.
+ *   2  as 1 for nerf_linear_bwd_weight; nerf_linear_fwd / nerf_linear_bwd_data emulate
+ *      f32 on v_mfma_f32_32x32x16_f16: every operand row is scaled by a power of two
+ *      (row max -> [2^14, 2^15)) and split into two fp16 words (exact to 2^-22), the
+ *      three products hi.lo + lo.hi + hi.hi accumulated in f32, the scales undone in the
+ *      epilogue.  Needs the row maxima of the A operand (x1_rmax, ...) and the fp16 pair
+ *      weight image (nerf_pack_weights in mode 2).
  * Returns NERF_EINVAL for other modes. */
 int nerf_gemm_set_precision(int mode);
 int nerf_gemm_get_precision(void);
@@ -138,7 +154,7 @@ int nerf_heads_fwd(const float* h8, int ld8, const float* hr, int ldr, int hidde
 int nerf_heads_part_size(int hidden, int n_pad);
 int nerf_heads_bwd(const float* graw4, const float* h8, int ld8, const float* hr, int ldr,
                    int hidden, const float* wc, float* dyr, int lddyr, float* part, int n_pad,
-                   void* stream);
+                   float* dyr_rmax, void* stream);   /* dyr_rmax optional: max |dyr| per row */
 /* Reduce the heads partials into gwd[hidden], gbd[1], gwc[3][hidden/2], gbc[3]. */
 int nerf_heads_reduce(const float* part, int hidden, int n_pad, float* gwd, float* gbd,
                       float* gwc, float* gbc, int accumulate, void* stream);
@@ -172,7 +188,11 @@ int nerf_encode_bwd(const float* pts_o, const float* pts_d, const float* view, c
  * rows c >= cols zero).  Padding rows/cols outside the written ranges keep their
  * previous contents (callers zero the buffers once).  Up to NERF_MAX_PACK descriptors.
  * dst_s / dst_ts (optional): the whole padded dst / dst_t as bf16x3 split images, the B
- * operand format of GEMM precision mode 1 (hi, mid, lo planes; ld_dst, ld_t % 8 == 0). */
+ * operand format of GEMM precision mode 1 (hi, mid, lo planes; ld_dst, ld_t % 8 == 0).
+ * In GEMM precision mode 2 the same buffers receive the fp16 pair form instead: each image
+ * row r scaled by 2^e_r (row max -> [2^14, 2^15)), planes 0 / 1 = fp16 hi / lo, and e_r as
+ * an int32 in the first word of plane 2's chunk 0 of that row (u16 index
+ * ((2*K/8)*rows + r)*8). */
 #define NERF_MAX_PACK 16
 typedef struct {
     const float* src;

@@ -51,7 +51,7 @@ void prof_end(hipStream_t s, double flops) {
 
 extern "C" {
 
-int nerf_hip_abi_version(void) { return 3; }
+int nerf_hip_abi_version(void) { return 4; }
 
 const char* nerf_hip_last_error(void) { return nerf::g_err; }
 

@@ -43,6 +43,16 @@ constexpr int kWave = 64;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// row max -> the power-of-two exponent e with max 2^e in [2^14, 2^15) (0 for a zero row):
+// the row scale of GEMM precision mode 2 (fp16 pair operands)
+__device__ __forceinline__ int row_exp(float rmax) {
+    const int ex = (int)((__float_as_uint(rmax) >> 23) & 0xff);
+    return rmax == 0.f ? 0 : (ex ? 141 - ex : 140);
+}
+
+// GEMM arithmetic mode (nerf_gemm_set_precision), host side
+int gemm_precision();
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);

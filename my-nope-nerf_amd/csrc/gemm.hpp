@@ -42,7 +42,17 @@ struct NTArgs {
     unsigned long long* stamps;   // diagnostics (nerf_gemm_debug_stamps): per-block phase clocks or NULL
     int ablate;   // diagnostics only (nerf_gemm_debug_ablate): 1 = no epilogue stores, 2 = no K-loop loads
                   // (f32 kernels; the split-bf16 kernels honour 1 only)
+    // precision mode 2 (fp16 pair): max |a| per row of each A segment (ar2 may be NULL),
+    // and (optional) the row max of the output written by the epilogue
+    const float* ar1; const float* ar2;
+    float* c_rmax;
 };
+
+// max |a| over row m of the (one or two segment) A operand
+__device__ __forceinline__ float a_rowmax(const NTArgs& p, int m) {
+    const float r1 = p.ar1[m];
+    return p.ar2 ? fmaxf(r1, p.ar2[m]) : r1;
+}
 
 enum { EPI_FWD = 0, EPI_BWD = 1 };
 
@@ -335,11 +345,37 @@ __device__ __forceinline__ void nt_epilogue_lds(const NTArgs& p, f32x16 (&acc)[T
 //   FWD: + bias, ReLU, ReLU mask word per (row, 32 features) from the nibbles of the
 //        lane pair (lane, lane ^ 32).
 //   BWD: + u[row] v[feature], masked by the input layer's ReLU bits.
-template <int TM, int TN, int EPI>
+//   H (precision mode 2): the accumulators carry the row scales 2^(ea[row] + eb[feature])
+//        (LDS arrays lea / leb, block-local indices), undone first; the row max of the
+//        stored values is max-accumulated into lrm (LDS, float bits) for NTArgs::c_rmax.
+template <int TM, int TN, int EPI, bool H = false>
 __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0, int wm0,
-                                                   int wn0, uint32_t* lmask = nullptr, int mw = 0) {
+                                                   int wn0, uint32_t* lmask = nullptr, int mw = 0,
+                                                   const int* leb = nullptr, const int* lea = nullptr,
+                                                   uint32_t* lrm = nullptr) {
     const int lane = lane_id();
     const int sl = lane & 31, hf = lane >> 5;
+    int er[TM];
+    float rmx[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        er[i] = H ? lea[wm0 + 32 * i + sl] : 0;
+        rmx[i] = 0.f;
+    }
+    // undo the operand scales of register quad q (features fl .. fl+3, block-local)
+    auto unscale = [&](int i, int j, int q) {
+        if constexpr (H) {
+            const int4 eb = *reinterpret_cast<const int4*>(leb + wn0 + 32 * j + 4 * hf + 8 * q);
+            acc[i][j][4 * q + 0] = __builtin_amdgcn_ldexpf(acc[i][j][4 * q + 0], -(er[i] + eb.x));
+            acc[i][j][4 * q + 1] = __builtin_amdgcn_ldexpf(acc[i][j][4 * q + 1], -(er[i] + eb.y));
+            acc[i][j][4 * q + 2] = __builtin_amdgcn_ldexpf(acc[i][j][4 * q + 2], -(er[i] + eb.z));
+            acc[i][j][4 * q + 3] = __builtin_amdgcn_ldexpf(acc[i][j][4 * q + 3], -(er[i] + eb.w));
+        }
+    };
+    auto track = [&](int i, const float4& x) {
+        if constexpr (H)
+            rmx[i] = fmaxf(rmx[i], fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+    };
     if (p.ablate & 1) {
         float t = 0.f;
 #pragma unroll
@@ -366,9 +402,11 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
                 uint32_t w = 0;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
+                    unscale(i, j, q);
                     float4 x = make_float4(acc[i][j][4 * q] + b4[q].x, acc[i][j][4 * q + 1] + b4[q].y,
                                            acc[i][j][4 * q + 2] + b4[q].z, acc[i][j][4 * q + 3] + b4[q].w);
                     if (p.relu) x = make_float4(fmaxf(x.x, 0.f), fmaxf(x.y, 0.f), fmaxf(x.z, 0.f), fmaxf(x.w, 0.f));
+                    track(i, x);
                     *reinterpret_cast<float4*>(p.c + row * p.ldc + fb + 8 * q) = x;
                     const uint32_t nib = (x.x > 0.f ? 1u : 0u) | (x.y > 0.f ? 2u : 0u) | (x.z > 0.f ? 4u : 0u) |
                                          (x.w > 0.f ? 8u : 0u);
@@ -407,6 +445,7 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
                 const size_t row = (size_t)(m0 + wm0 + 32 * i + sl);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
+                    unscale(i, j, q);
                     const uint32_t bits = mw[i][j] >> (8 * q + 4 * hf);
                     float4 x = make_float4(acc[i][j][4 * q] + u[i] * v4[q].x, acc[i][j][4 * q + 1] + u[i] * v4[q].y,
                                            acc[i][j][4 * q + 2] + u[i] * v4[q].z, acc[i][j][4 * q + 3] + u[i] * v4[q].w);
@@ -414,9 +453,19 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
                     x.y = (bits & 2u) ? x.y : 0.f;
                     x.z = (bits & 4u) ? x.z : 0.f;
                     x.w = (bits & 8u) ? x.w : 0.f;
+                    track(i, x);
                     *reinterpret_cast<float4*>(p.c + row * p.ldc + fb + 8 * q) = x;
                 }
             }
+        }
+    }
+    if constexpr (H) {
+        // the lane pair (lane, lane ^ 32) holds one row's features of this wave; the other
+        // waves along N meet in LDS (non-negative floats order like their bits)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const float m = fmaxf(rmx[i], __shfl_xor(rmx[i], 32, 64));
+            if (hf == 0) atomicMax(lrm + wm0 + 32 * i + sl, __float_as_uint(m));
         }
     }
 }
@@ -438,7 +487,7 @@ __device__ __forceinline__ void tn_store_lds(const TNArgs& p, f32x16 (&acc)[TM][
 }
 
 // split-bf16 launchers (gemm_x6.hip); policy as nerf_gemm_set_policy
-int dispatch_nt_x6(const NTArgs& a, int epi, int policy, hipStream_t s, double flops);
+int dispatch_nt_x6(const NTArgs& a, int epi, int policy, hipStream_t s, double flops, bool h16 = false);
 int dispatch_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, hipStream_t s, double flops);
 
 }  // namespace nerf

@@ -335,10 +335,15 @@ static int g_precision = 0;
 template <int EPI>
 static int dispatch_nt(const NTArgs& a, hipStream_t s, double flops) {
     const int pol = g_nt_policy ? g_nt_policy : 3;
-    if (g_precision == 1 && a.bs != nullptr) {   // the split path needs the weight image
+    if (g_precision >= 1 && a.bs != nullptr) {   // the split paths need the weight image
         NTArgs b = a;
         b.ablate = g_ablate;
         b.stamps = g_stamps;
+        if (g_precision == 2) {
+            NERF_CHECK(a.ar1 != nullptr && (a.a2 == nullptr || a.ar2 != nullptr),
+                       "GEMM precision mode 2 needs the row max of every A segment (x_rmax / dy_rmax)");
+            return dispatch_nt_x6(b, EPI, pol, s, flops, true);
+        }
         return dispatch_nt_x6(b, EPI, pol, s, flops);
     }
     if (pol == 3 && a.m % 256 == 0 && a.n % 256 == 0) return launch_nt<256, 256, 2, 4, EPI>(a, s, flops);
@@ -368,7 +373,7 @@ static int check_nt(const NTArgs& a, const char* fn) {
 extern "C" int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2, int k2,
                                const float* w, const uint16_t* w_split, int w_split_rows, const float* bias,
                                float* y, int ldy, int m, int n, int relu, uint32_t* mask_out, int ldmo,
-                               void* stream) {
+                               const float* x1_rmax, const float* x2_rmax, float* y_rmax, void* stream) {
     NTArgs a{};
     a.a1 = x1; a.lda1 = ldx1; a.k1 = k1;
     a.a2 = x2; a.lda2 = x2 ? ldx2 : 0; a.k2 = x2 ? k2 : 0;
@@ -376,6 +381,7 @@ extern "C" int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x
     a.bs = w_split; a.bs_rows = w_split_rows;
     a.bias = bias; a.c = y; a.ldc = ldy; a.m = m; a.n = n; a.relu = relu;
     a.mask_out = mask_out; a.ldmo = ldmo;
+    a.ar1 = x1_rmax; a.ar2 = x2 ? x2_rmax : nullptr; a.c_rmax = y_rmax;
     int rc = check_nt(a, __func__);
     if (rc) return rc;
     NERF_CHECK(mask_out == nullptr || ldmo >= n / 32, "%s: ldmo=%d < n/32", __func__, ldmo);
@@ -386,13 +392,14 @@ extern "C" int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x
 extern "C" int nerf_linear_bwd_data(const float* dy, int lddy, int k, const float* wt,
                                     const uint16_t* wt_split, int wt_split_rows, const float* u, int ldu,
                                     const float* v, const uint32_t* mask, int ldmask, float* dx, int lddx,
-                                    int m, int n, void* stream) {
+                                    int m, int n, const float* dy_rmax, float* dx_rmax, void* stream) {
     NTArgs a{};
     a.a1 = dy; a.lda1 = lddy; a.k1 = k;
     a.a2 = nullptr; a.lda2 = 0; a.k2 = 0;
     a.b = wt; a.ldb = k;
     a.bs = wt_split; a.bs_rows = wt_split_rows;
     a.u = u; a.ldu = ldu; a.v = v; a.mask = mask; a.ldmask = ldmask;
+    a.ar1 = dy_rmax; a.c_rmax = dx_rmax;
     a.c = dx; a.ldc = lddx; a.m = m; a.n = n;
     int rc = check_nt(a, __func__);
     if (rc) return rc;
@@ -424,7 +431,7 @@ extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const
     hipStream_t s = as_stream(stream);
     const double fl = 2.0 * m * nout * (double)kin;
     const int pol = g_tn_policy ? g_tn_policy : 3;
-    if (g_precision == 1) return dispatch_tn_x6(a, nout, kin, splits, pol, s, fl);
+    if (g_precision >= 1) return dispatch_tn_x6(a, nout, kin, splits, pol, s, fl);   // mode 2: bf16x6 dW
     prof_begin(s);
     if (pol == 3 && nout % 256 == 0 && kin % 256 == 0) {
         dim3 grid(nout / 256, kin / 256, splits);
@@ -486,9 +493,13 @@ extern "C" int nerf_linear_bwd_weight_splits(int nout, int kin, int m) {
 }
 
 extern "C" int nerf_gemm_set_precision(int mode) {
-    NERF_CHECK(mode == 0 || mode == 1, "%s: mode must be 0 (f32 MFMA) or 1 (split-bf16)", __func__);
+    NERF_CHECK(mode >= 0 && mode <= 2, "%s: mode must be 0 (f32 MFMA), 1 (split-bf16) or 2 (fp16 pair)", __func__);
     g_precision = mode;
     return NERF_OK;
+}
+
+namespace nerf {
+int gemm_precision() { return g_precision; }
 }
 
 extern "C" int nerf_gemm_get_precision(void) { return g_precision; }

@@ -19,6 +19,16 @@
 //  * K-contiguous operands ([m][k], [n][k]) load as float4 along k; sample-major ones
 //    (dy[s][o], x[s][j]) load as 8-row column strips so each thread owns 8 consecutive
 //    k of one column and writes its fragment chunk with one ds_write_b128 per plane.
+//
+// Precision mode 2 (H = true, the NT kernels only) replaces the bf16 triple by an fp16
+// pair: every operand row is scaled by a power of two 2^e (row max -> [2^14, 2^15),
+// exact), split into x 2^e = hi + lo (RNE fp16 each: 11 + 11 significand bits, the
+// remainder <= 2^-22 |x|), and a.b = hi.lo + lo.hi + hi.hi on v_mfma_f32_32x32x16_f16
+// (the dropped lo.lo <= 2^-22 |a||b|) -- three products instead of six, two LDS planes
+// instead of three.  The epilogue undoes the scales (2^-(e_row + e_feature), exact).
+// Row scales come from the producers: every kernel that writes an A operand also writes
+// its row max (max |x| over the row), read here as NTArgs::ar1 / ar2; the weight image's
+// per-row exponents sit in plane 2 of the image (nerf_pack_weights).
 #include "gemm.hpp"
 
 #include <cstdlib>
@@ -27,6 +37,8 @@ namespace nerf {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int XK = 16;   // K per LDS tile
@@ -45,17 +57,36 @@ __device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& 
     l = pk_bf16(ra - __uint_as_float(m << 16), rb - __uint_as_float(m & 0xffff0000u));
 }
 
-// bytes of one k-half image of ROWS rows (+128 B bank offset between the halves)
-template <int ROWS>
+__device__ __forceinline__ uint32_t pk_f16(float a, float b) {
+    f32x2 v = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2v));   // RNE
+}
+
+// (a, b) scaled by 2^e -> packed fp16 pairs hi, lo with a 2^e = hi.x + lo.x (+ <= 2^-22 |a| 2^e)
+__device__ __forceinline__ void split2h(float a, float b, int e, uint32_t& h, uint32_t& l) {
+    a = __builtin_amdgcn_ldexpf(a, e);
+    b = __builtin_amdgcn_ldexpf(b, e);
+    h = pk_f16(a, b);
+    const f16x2v hv = __builtin_bit_cast(f16x2v, h);
+    l = pk_f16(a - (float)hv[0], b - (float)hv[1]);
+}
+
+// bytes of one k-half image of ROWS rows (+128 B bank offset between the halves);
+// NP planes (3: bf16 hi/mid/lo, 2: fp16 hi/lo)
+template <int ROWS, int NP = 3>
 struct XImg {
     static constexpr int HALF = ROWS * 16 + 128;
     static constexpr int PLANE = 2 * HALF;
-    static constexpr int BYTES = 3 * PLANE;
+    static constexpr int BYTES = NP * PLANE;
 };
 
 __device__ __forceinline__ f32x16 mfma_bf16(const uint4& a, const uint4& b, const f32x16& c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
                                                    0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mfma_f16(const uint4& a, const uint4& b, const f32x16& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                  0, 0, 0);
 }
 
 // float4 along k at (row, k = 4q) -> the three planes' 8-byte pieces of that row's chunk
@@ -69,6 +100,18 @@ __device__ __forceinline__ void put_row4(char* img, int row, int q, float4 v) {
     *reinterpret_cast<uint2*>(d) = make_uint2(h0, h1);
     *reinterpret_cast<uint2*>(d + I::PLANE) = make_uint2(m0, m1);
     *reinterpret_cast<uint2*>(d + 2 * I::PLANE) = make_uint2(l0, l1);
+}
+
+// fp16 pair form of put_row4 (row scale 2^e)
+template <int ROWS>
+__device__ __forceinline__ void put_row4h(char* img, int row, int q, float4 v, int e) {
+    using I = XImg<ROWS, 2>;
+    uint32_t h0, l0, h1, l1;
+    split2h(v.x, v.y, e, h0, l0);
+    split2h(v.z, v.w, e, h1, l1);
+    char* d = img + (q >> 1) * I::HALF + row * 16 + (q & 1) * 8;
+    *reinterpret_cast<uint2*>(d) = make_uint2(h0, h1);
+    *reinterpret_cast<uint2*>(d + I::PLANE) = make_uint2(l0, l1);
 }
 
 // 8 consecutive k of column c (k-half g) -> one 16-byte chunk per plane
@@ -190,45 +233,54 @@ __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" :
 template <int TM, int TN, int BM, int BN, bool SWAP, typename Stager>
 __device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int wn0, f32x16 (&acc)[TM][TN],
                                                Stager& st, unsigned long long* stamps = nullptr) {
-    using IA = XImg<BM>;
-    using IB = XImg<BN>;
+    constexpr bool H = Stager::H;          // fp16 pair (3 products) instead of bf16 triple (6)
+    constexpr int NP = H ? 2 : 3;
+    constexpr int NPROD = H ? 3 : 6;
+    using IA = XImg<BM, NP>;
+    using IB = XImg<BN, NP>;
     constexpr int BUF = IA::BYTES + IB::BYTES;
     const int lane = lane_id();
     const int l32 = lane & 31, hi = lane >> 5;
     const int aoff = hi * IA::HALF + (wm0 + l32) * 16;
     const int boff = IA::BYTES + hi * IB::HALF + (wn0 + l32) * 16;
-    auto rd = [&](const char* q, int plane, uint4 (&f)[3]) {
-        f[0] = *reinterpret_cast<const uint4*>(q);
-        f[1] = *reinterpret_cast<const uint4*>(q + plane);
-        f[2] = *reinterpret_cast<const uint4*>(q + 2 * plane);
+    auto rd = [&](const char* q, int plane, uint4 (&f)[NP]) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) f[p] = *reinterpret_cast<const uint4*>(q + p * plane);
     };
-    auto rdA = [&](const char* buf, uint4 (&a)[TM][3], int i0, int i1) {
+    auto rdA = [&](const char* buf, uint4 (&a)[TM][NP], int i0, int i1) {
 #pragma unroll
         for (int i = i0; i < i1; ++i) rd(buf + aoff + 32 * 16 * i, IA::PLANE, a[i]);
     };
-    auto rdB = [&](const char* buf, uint4 (&b)[TN][3]) {
+    auto rdB = [&](const char* buf, uint4 (&b)[TN][NP]) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) rd(buf + boff + 32 * 16 * j, IB::PLANE, b[j]);
     };
     // SWAP: the MFMA's A operand is the weight fragment, so acc[i][j] holds the transposed
     // tile (lanes along samples, registers along features) for nt_epilogue_direct
     auto mf = [&](const uint4& a, const uint4& b, const f32x16& c) {
-        return SWAP ? mfma_bf16(b, a, c) : mfma_bf16(a, b, c);
+        if constexpr (H) return SWAP ? mfma_f16(b, a, c) : mfma_f16(a, b, c);
+        else return SWAP ? mfma_bf16(b, a, c) : mfma_bf16(a, b, c);
     };
-    auto mm = [&](int i, const uint4 (&a)[3], const uint4 (&b)[TN][3]) {
+    auto mm = [&](int i, const uint4 (&a)[NP], const uint4 (&b)[TN][NP]) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             f32x16 c = acc[i][j];
-            c = mf(a[1], b[j][1], c);   // mid.mid
-            c = mf(a[0], b[j][2], c);   // hi.lo
-            c = mf(a[2], b[j][0], c);   // lo.hi
-            c = mf(a[0], b[j][1], c);   // hi.mid
-            c = mf(a[1], b[j][0], c);   // mid.hi
-            c = mf(a[0], b[j][0], c);   // hi.hi
+            if constexpr (H) {
+                c = mf(a[0], b[j][1], c);            // hi.lo
+                c = mf(a[1], b[j][0], c);            // lo.hi
+                c = mf(a[0], b[j][0], c);            // hi.hi
+            } else {
+                c = mf(a[1], b[j][1], c);            // mid.mid
+                c = mf(a[0], b[j][2], c);            // hi.lo
+                c = mf(a[2], b[j][0], c);            // lo.hi
+                c = mf(a[0], b[j][1], c);            // hi.mid
+                c = mf(a[1], b[j][0], c);            // mid.hi
+                c = mf(a[0], b[j][0], c);            // hi.hi
+            }
             acc[i][j] = c;
         }
     };
-    uint4 aX[TM][3], bX[TN][3], aY[TM][3], bY[TN][3];
+    uint4 aX[TM][NP], bX[TN][NP], aY[TM][NP], bY[TN][NP];
 
     st.prologue3(smem, nkt);        // tiles 0, 1 in image buffers 0, 1; raw tiles 2, 3 in the ring
     rdA(smem, aX, 0, TM);
@@ -236,29 +288,33 @@ __device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int
     __syncthreads();                // buffer 0 is restaged in iteration 0
     stamp(stamps, 1);
 
-    auto iter = [&](int kt, uint4 (&ac)[TM][3], uint4 (&bc)[TN][3], uint4 (&an)[TM][3], uint4 (&bn)[TN][3]) {
+    auto iter = [&](int kt, uint4 (&ac)[TM][NP], uint4 (&bc)[TN][NP], uint4 (&an)[TM][NP], uint4 (&bn)[TN][NP]) {
         char* wimg = smem + (kt & 1) * BUF;
         const char* nbuf = smem + ((kt + 1) & 1) * BUF;
-        constexpr int H = (TM + 1) / 2;
+        constexpr int HT = (TM + 1) / 2;
+        // row tiles whose MFMAs carry the split VALU: 6 products per tile leave room for it
+        // in row tile 0's gaps, 3 products need two row tiles
+        constexpr int R0 = (H && TM >= 2) ? 2 : 1;
         st.dma3(kt, nkt, wimg + IA::BYTES);   // B image of tile kt+2, then raw A of tile kt+4
         float4 raw[Stager::A_F4];
         st.read_raw3(kt, raw);                 // raw A of tile kt+2
         rdB(nbuf, bn);
-        rdA(nbuf, an, 0, H);
+        rdA(nbuf, an, 0, HT);
         st.split_raw(raw, wimg);
-        mm(0, ac[0], bc);
 #pragma unroll
-        for (int q = 0; q < 6 * TN; ++q) {
+        for (int i = 0; i < R0; ++i) mm(i, ac[i], bc);
+#pragma unroll
+        for (int q = 0; q < NPROD * TN * R0; ++q) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int i = 1; i < H; ++i) mm(i, ac[i], bc);
+        for (int i = R0; i < HT; ++i) mm(i, ac[i], bc);
         __builtin_amdgcn_sched_barrier(0);
-        rdA(nbuf, an, H, TM);
+        rdA(nbuf, an, HT, TM);
 #pragma unroll
-        for (int i = H; i < TM; ++i) mm(i, ac[i], bc);
+        for (int i = (HT > R0 ? HT : R0); i < TM; ++i) mm(i, ac[i], bc);
         if (kt == 5) stamp(stamps, 6);
         st.wait3();
         if (kt == 5) stamp(stamps, 7);
@@ -277,18 +333,21 @@ __device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int
 // moves 16 rows x 64 B), split from there into the A image.  B: fragments loaded
 // straight from the pre-split weight image (p.bs, L2-resident).  No staging registers.
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int NT>
+template <int BM, int BN, int NT, bool HH = false>
 struct NTStager {
+    static constexpr bool H = HH;                   // fp16 pair images (precision mode 2)
+    static constexpr int NP = H ? 2 : 3;
     static constexpr int A_F4 = BM * XK / 4 / NT;   // raw A float4 (= DMA instructions) per thread and tile
     static constexpr int RSTEP = NT / 4;            // rows per pass of the block
     static constexpr int RAW = BM * XK * 4;         // bytes of one raw A slot
     static constexpr int NSLOT = 3;
-    static constexpr int B_CH = 6 * BN;             // 16-B chunks of a tile's B image
+    static constexpr int B_CH = 2 * NP * BN;        // 16-B chunks of a tile's B image
     static constexpr int B_C = (B_CH + NT - 1) / NT;
     static_assert(A_F4 >= 1 && BN % 64 == 0, "bad tile");
     const float* a1b; const float* a2b; const uint16_t* bsb;
     int lda1, lda2, k1, bs_rows, Kc;
     int r0, q0;
+    int ea[A_F4];                                   // H: row scale exponents of this thread's rows
     char* raw;
 
     __device__ __forceinline__ void init(const NTArgs& p, int m0, int n0, int K, char* raw_ring) {
@@ -298,6 +357,10 @@ struct NTStager {
         bsb = p.bs + (size_t)n0 * 8;
         r0 = threadIdx.x >> 2; q0 = threadIdx.x & 3;
         raw = raw_ring;
+        if (H) {
+#pragma unroll
+            for (int i = 0; i < A_F4; ++i) ea[i] = row_exp(a_rowmax(p, m0 + r0 + i * RSTEP));
+        }
     }
     __device__ __forceinline__ void dma_a(int kt, int slot) {
         const int kk = kt * XK;
@@ -318,7 +381,7 @@ struct NTStager {
             const int idx = threadIdx.x + NT * i;
             const int n = idx % BN, pk = idx / BN;
             dma16(bt + (((size_t)(pk >> 1) * Kc + (pk & 1)) * bs_rows + n) * 8,
-                  Bimg + (pk >> 1) * XImg<BN>::PLANE + (pk & 1) * XImg<BN>::HALF + (n - lane) * 16);
+                  Bimg + (pk >> 1) * XImg<BN, NP>::PLANE + (pk & 1) * XImg<BN, NP>::HALF + (n - lane) * 16);
         }
     }
     __device__ __forceinline__ void read_slot(int slot, float4 (&v)[A_F4]) {
@@ -328,18 +391,21 @@ struct NTStager {
     }
     __device__ __forceinline__ void put(const float4 (&v)[A_F4], char* Aimg) {
 #pragma unroll
-        for (int i = 0; i < A_F4; ++i) put_row4<BM>(Aimg, r0 + i * RSTEP, q0, v[i]);
+        for (int i = 0; i < A_F4; ++i) {
+            if constexpr (H) put_row4h<BM>(Aimg, r0 + i * RSTEP, q0, v[i], ea[i]);
+            else put_row4<BM>(Aimg, r0 + i * RSTEP, q0, v[i]);
+        }
     }
     __device__ __forceinline__ int clamp(int t, int nkt) const { return t < nkt ? t : nkt - 1; }
     // tiles 0, 1 in image buffers 0, 1 (raw tile t lives in slot t % 3); raw tiles 2 (landed)
     // and 3 (in flight) in the ring
     __device__ __forceinline__ void prologue3(char* smem, int nkt) {
-        constexpr int BUF = XImg<BM>::BYTES + XImg<BN>::BYTES;
+        constexpr int BUF = XImg<BM, NP>::BYTES + XImg<BN, NP>::BYTES;
         dma_a(0, 0);
         dma_a(clamp(1, nkt), 1);
         dma_a(clamp(2, nkt), 2);
-        dma_b(0, smem + XImg<BM>::BYTES);
-        dma_b(clamp(1, nkt), smem + BUF + XImg<BM>::BYTES);
+        dma_b(0, smem + XImg<BM, NP>::BYTES);
+        dma_b(clamp(1, nkt), smem + BUF + XImg<BM, NP>::BYTES);
         dma_wait();
         __syncthreads();
         float4 v[A_F4];
@@ -365,26 +431,45 @@ struct NTStager {
     }
 };
 
-template <int BM, int BN, int WM, int WN, int EPI, bool DIRECT>
+template <int BM, int BN, int WM, int WN, int EPI, bool DIRECT, bool H = false>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt_x6(NTArgs p) {
     constexpr int NT = 64 * WM * WN;
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
-    using St = NTStager<BM, BN, NT>;
+    constexpr int NP = H ? 2 : 3;
+    using St = NTStager<BM, BN, NT, H>;
     static_assert(TM >= 1 && TN >= 1, "bad tile");
-    constexpr int LOOP_BYTES = 2 * (XImg<BM>::BYTES + XImg<BN>::BYTES) + St::NSLOT * St::RAW;
+    static_assert(!H || DIRECT, "the fp16 pair kernels use the direct epilogue");
+    constexpr int IMG_BYTES = 2 * (XImg<BM, NP>::BYTES + XImg<BN, NP>::BYTES);
+    constexpr int LOOP_BYTES = IMG_BYTES + St::NSLOT * St::RAW;
     constexpr int EPI_BYTES = DIRECT ? BM * (BN / 32) * 4 : (NT / 64) * TileLds<TN>::BYTES + (BM * (BN / 32) + BM) * 4;
-    __shared__ __attribute__((aligned(16))) char smem[LOOP_BYTES > EPI_BYTES ? LOOP_BYTES : EPI_BYTES];
+    constexpr int MAIN_BYTES = LOOP_BYTES > EPI_BYTES ? LOOP_BYTES : EPI_BYTES;
+    constexpr int SCALE_BYTES = H ? (BN + 2 * BM) * 4 : 0;   // leb[BN], lea[BM], lrm[BM]
+    __shared__ __attribute__((aligned(16))) char smem[MAIN_BYTES + SCALE_BYTES];
     const int wave = threadIdx.x >> 6;
     const int wm0 = (wave / WN) * WTM;
     const int wn0 = (wave % WN) * WTN;
     const int m0 = blockIdx.x * BM;
     const int n0 = blockIdx.y * BN;
     const int K = p.k1 + p.k2;
+    int* leb = reinterpret_cast<int*>(smem + MAIN_BYTES);
+    int* lea = leb + BN;
+    uint32_t* lrm = reinterpret_cast<uint32_t*>(lea + BM);
 
     stamp(p.stamps, 0);
+    if (H) {
+        // weight row exponents (plane 2 of the image, one int per 16-byte row chunk), row
+        // exponents of A and the output row-max accumulators; published by the prologue's
+        // first barrier
+        const int* eimg = reinterpret_cast<const int*>(p.bs + (size_t)2 * (K / 8) * p.bs_rows * 8);
+        for (int e = threadIdx.x; e < BN; e += NT) leb[e] = eimg[(size_t)(n0 + e) * 4];
+        for (int e = threadIdx.x; e < BM; e += NT) {
+            lea[e] = row_exp(a_rowmax(p, m0 + e));
+            lrm[e] = 0u;
+        }
+    }
     St st;
-    st.init(p, m0, n0, K, smem + 2 * (XImg<BM>::BYTES + XImg<BN>::BYTES));
+    st.init(p, m0, n0, K, smem + IMG_BYTES);
     f32x16 acc[TM][TN];
     zero_acc(acc);
     if (DIRECT) {
@@ -398,11 +483,19 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt_x6(NTArgs p) {
             __syncthreads();
             lmask = reinterpret_cast<uint32_t*>(smem);
         }
-        nt_epilogue_direct<TM, TN, EPI>(p, acc, m0, n0, wm0, wn0, lmask, MW);
-        if (gather) {
+        nt_epilogue_direct<TM, TN, EPI, H>(p, acc, m0, n0, wm0, wn0, lmask, MW, leb, lea, lrm);
+        if (gather || (H && p.c_rmax)) {
             __syncthreads();
-            for (int e = threadIdx.x; e < BM * MW; e += NT)
-                p.mask_out[(size_t)(m0 + e / MW) * p.ldmo + (n0 >> 5) + e % MW] = lmask[e];
+            if (gather)
+                for (int e = threadIdx.x; e < BM * MW; e += NT)
+                    p.mask_out[(size_t)(m0 + e / MW) * p.ldmo + (n0 >> 5) + e % MW] = lmask[e];
+            if (H && p.c_rmax) {
+                // one column block: plain stores; several: max-accumulate (caller zeroes c_rmax)
+                for (int e = threadIdx.x; e < BM; e += NT) {
+                    if (gridDim.y == 1) p.c_rmax[m0 + e] = __uint_as_float(lrm[e]);
+                    else atomicMax(reinterpret_cast<uint32_t*>(p.c_rmax) + m0 + e, lrm[e]);
+                }
+            }
         }
         dma_wait();      // the last (clamped) raw-A DMA lands before the workgroup's LDS is released
     } else {
@@ -557,8 +650,11 @@ static const bool g_nt_direct = [] {
 }();
 
 template <int BM, int BN, int WM, int WN, int EPI>
-static void launch_nt_x6(const NTArgs& a, hipStream_t s) {
-    if (g_nt_direct)
+static void launch_nt_x6(const NTArgs& a, hipStream_t s, bool h16) {
+    if (h16)
+        hipLaunchKernelGGL((k_gemm_nt_x6<BM, BN, WM, WN, EPI, true, true>), dim3(a.m / BM, a.n / BN),
+                           dim3(64 * WM * WN), 0, s, a);
+    else if (g_nt_direct)
         hipLaunchKernelGGL((k_gemm_nt_x6<BM, BN, WM, WN, EPI, true>), dim3(a.m / BM, a.n / BN), dim3(64 * WM * WN), 0,
                            s, a);
     else
@@ -567,19 +663,19 @@ static void launch_nt_x6(const NTArgs& a, hipStream_t s) {
 }
 
 template <int EPI>
-static void pick_nt_x6(const NTArgs& a, int pol, hipStream_t s) {
-    if (pol == 3 && a.m % 256 == 0 && a.n % 256 == 0) launch_nt_x6<256, 256, 2, 2, EPI>(a, s);
-    else if (pol >= 2 && a.n % 256 == 0) launch_nt_x6<128, 256, 2, 2, EPI>(a, s);
-    else if (a.n % 128 == 0) launch_nt_x6<128, 128, 2, 2, EPI>(a, s);
-    else launch_nt_x6<128, 64, 2, 2, EPI>(a, s);
+static void pick_nt_x6(const NTArgs& a, int pol, hipStream_t s, bool h16) {
+    if (pol == 3 && a.m % 256 == 0 && a.n % 256 == 0) launch_nt_x6<256, 256, 2, 2, EPI>(a, s, h16);
+    else if (pol >= 2 && a.n % 256 == 0) launch_nt_x6<128, 256, 2, 2, EPI>(a, s, h16);
+    else if (a.n % 128 == 0) launch_nt_x6<128, 128, 2, 2, EPI>(a, s, h16);
+    else launch_nt_x6<128, 64, 2, 2, EPI>(a, s, h16);
 }
 
-int dispatch_nt_x6(const NTArgs& a, int epi, int policy, hipStream_t s, double flops) {
+int dispatch_nt_x6(const NTArgs& a, int epi, int policy, hipStream_t s, double flops, bool h16) {
     prof_begin(s);
-    if (epi == EPI_FWD) pick_nt_x6<EPI_FWD>(a, policy, s);
-    else pick_nt_x6<EPI_BWD>(a, policy, s);
+    if (epi == EPI_FWD) pick_nt_x6<EPI_FWD>(a, policy, s, h16);
+    else pick_nt_x6<EPI_BWD>(a, policy, s, h16);
     prof_end(s, flops);
-    return check_launch("k_gemm_nt_x6");
+    return check_launch(h16 ? "k_gemm_nt_x6 (fp16 pair)" : "k_gemm_nt_x6");
 }
 
 int dispatch_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, hipStream_t s, double flops) {

@@ -8,6 +8,7 @@ namespace nerf {
 struct PackBatch {
     nerf_pack_desc d[NERF_MAX_PACK];
     int n;
+    int f16;   // GEMM precision mode 2: images in the fp16 pair form (k_pack_h), not bf16x3
 };
 
 // x -> three bf16 words (RNE each) with x = hi + mid + lo (same split as gemm_x6.hip)
@@ -42,7 +43,7 @@ __global__ void k_pack(PackBatch pb) {
         const int r = e / d.ld_dst, c = e % d.ld_dst;
         const float x = (c < d.cols && r < d.rows) ? d.src[(size_t)r * d.cols + c] : 0.f;
         if (r < d.rows) d.dst[e] = x;
-        if (d.dst_s != nullptr) put_split(d.dst_s, rows_s, d.ld_dst, r, c, x);
+        if (d.dst_s != nullptr && !pb.f16) put_split(d.dst_s, rows_s, d.ld_dst, r, c, x);
     }
     if (d.dst_t != nullptr) {
         const int tt = d.rows_t * d.rows;  // dst_t[c][r], c < rows_t, r < rows
@@ -51,12 +52,58 @@ __global__ void k_pack(PackBatch pb) {
             d.dst_t[(size_t)c * d.ld_t + r] = c < d.cols ? d.src[(size_t)r * d.cols + c] : 0.f;
         }
     }
-    if (d.dst_ts != nullptr) {
+    if (d.dst_ts != nullptr && !pb.f16) {
         const int tt = d.rows_t * d.ld_t;  // whole image of dst_t, zero past the source
         for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < tt; e += gridDim.x * blockDim.x) {
             const int c = e / d.ld_t, r = e % d.ld_t;   // dst_t row c, column r
             const float x = (c < d.cols && r < d.rows) ? d.src[(size_t)r * d.cols + c] : 0.f;
             put_split(d.dst_ts, d.rows_t, d.ld_t, c, r, x);
+        }
+    }
+}
+
+// Row r of the fp16 pair image of a [N][K] operand (x(c) = element (r, c)): one wave per
+// row; the row max sets the scale 2^e, planes 0 / 1 get hi / lo of x 2^e (RNE fp16 each),
+// e goes into the first word of the row's plane-2 chunk 0 (gemm_x6.hip, mode 2).
+template <typename F>
+__device__ __forceinline__ void put_row_h(uint16_t* img, int N, int K, int r, F&& x) {
+    const int lane = lane_id();
+    float m = 0.f;
+    for (int c = lane; c < K; c += kWave) m = fmaxf(m, fabsf(x(c)));
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    const int e = row_exp(m);
+    const size_t plane = (size_t)K * N;
+    for (int c = lane; c < K; c += kWave) {
+        const float v = __builtin_amdgcn_ldexpf(x(c), e);
+        const _Float16 h = (_Float16)v;
+        const _Float16 l = (_Float16)(v - (float)h);
+        const size_t o = ((size_t)(c >> 3) * N + r) * 8 + (c & 7);
+        img[o] = __builtin_bit_cast(uint16_t, h);
+        img[o + plane] = __builtin_bit_cast(uint16_t, l);
+    }
+    if (lane == 0) *reinterpret_cast<int*>(img + 2 * plane + (size_t)r * 8) = e;
+}
+
+// fp16 pair images of the packed weights (GEMM precision mode 2); blockIdx.y = descriptor,
+// one wave per image row, rows of dst_s then of dst_ts
+__global__ __launch_bounds__(256) void k_pack_h(PackBatch pb) {
+    const nerf_pack_desc& d = pb.d[blockIdx.y];
+    const int rows_s = d.rows_s > d.rows ? d.rows_s : d.rows;
+    const int ns = d.dst_s ? rows_s : 0, nt = d.dst_ts ? d.rows_t : 0;
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (int w = wave; w < ns + nt; w += nwaves) {
+        if (w < ns) {
+            const int r = w;
+            put_row_h(d.dst_s, rows_s, d.ld_dst, r, [&](int c) {
+                return (c < d.cols && r < d.rows) ? d.src[(size_t)r * d.cols + c] : 0.f;
+            });
+        } else {
+            const int c = w - ns;   // dst_t row = source column c, its columns = source rows
+            put_row_h(d.dst_ts, d.rows_t, d.ld_t, c, [&](int r) {
+                return (c < d.cols && r < d.rows) ? d.src[(size_t)r * d.cols + c] : 0.f;
+            });
         }
     }
 }
@@ -164,7 +211,11 @@ extern "C" int nerf_pack_weights(const nerf_pack_desc* descs, int n, void* strea
                    __func__, i);
         pb.d[i] = d;
     }
+    pb.f16 = gemm_precision() == 2;
+    bool images = false;
+    for (int i = 0; i < n; ++i) images = images || descs[i].dst_s != nullptr || descs[i].dst_ts != nullptr;
     hipLaunchKernelGGL(k_pack, dim3(64, n), dim3(256), 0, as_stream(stream), pb);
+    if (pb.f16 && images) hipLaunchKernelGGL(k_pack_h, dim3(32, n), dim3(256), 0, as_stream(stream), pb);
     return check_launch(__func__);
 }
 

@@ -45,7 +45,9 @@ struct RowWriter {
     float4* dst;
     float buf[4];
     int n;
+    float amax;   // max |v| of the row (row scale of GEMM precision mode 2)
     __device__ __forceinline__ void put(float v) {
+        amax = fmaxf(amax, fabsf(v));
         buf[n & 3] = v;
         ++n;
         if ((n & 3) == 0) dst[(n >> 2) - 1] = make_float4(buf[0], buf[1], buf[2], buf[3]);
@@ -57,8 +59,8 @@ struct RowWriter {
 
 // encode_position (official_nerf.py:99-119): [x, sin(2^0 x), cos(2^0 x), ...], zero padded to W
 template <int L, int W>
-__device__ __forceinline__ void encode3(const float x[3], float* row) {
-    RowWriter<W> w{reinterpret_cast<float4*>(row), {0.f, 0.f, 0.f, 0.f}, 0};
+__device__ __forceinline__ float encode3(const float x[3], float* row) {
+    RowWriter<W> w{reinterpret_cast<float4*>(row), {0.f, 0.f, 0.f, 0.f}, 0, 0.f};
 #pragma unroll
     for (int c = 0; c < 3; ++c) w.put(x[c]);
 #pragma unroll
@@ -73,13 +75,15 @@ __device__ __forceinline__ void encode3(const float x[3], float* row) {
         for (int c = 0; c < 3; ++c) w.put(co[c]);
     }
     w.finish();
+    return w.amax;
 }
 
 __global__ __launch_bounds__(256) void k_encode_samples(const float* __restrict__ po, const float* __restrict__ pd,
                                  const float* __restrict__ view, const float* __restrict__ noise,
                                  int R, int S, int n_pad, float nz, float fz,
                                  float* __restrict__ z_out, float* __restrict__ enc_p,
-                                 float* __restrict__ enc_d) {
+                                 float* __restrict__ enc_d, float* __restrict__ rmax_p,
+                                 float* __restrict__ rmax_d) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_pad) return;
     const int total = R * S;
@@ -99,9 +103,11 @@ __global__ __launch_bounds__(256) void k_encode_samples(const float* __restrict_
             x[c] = ray_point(po[3 * r + c], pd[3 * r + c], z);  // rendering.py:193-194
             v[c] = view[3 * r + c];
         }
-        encode3<10, ENC_P>(x, rp);
-        encode3<4, ENC_D>(v, rd);
+        const float mp = encode3<10, ENC_P>(x, rp);
+        const float md = encode3<4, ENC_D>(v, rd);
         z_out[s] = z;
+        if (rmax_p) rmax_p[s] = mp;
+        if (rmax_d) rmax_d[s] = md;
     } else {
         const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -109,6 +115,8 @@ __global__ __launch_bounds__(256) void k_encode_samples(const float* __restrict_
 #pragma unroll
         for (int q = 0; q < ENC_D / 4; ++q) reinterpret_cast<float4*>(rd)[q] = zero;
         z_out[s] = 0.f;
+        if (rmax_p) rmax_p[s] = 0.f;
+        if (rmax_d) rmax_d[s] = 0.f;
     }
 }
 
@@ -212,7 +220,8 @@ __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ gra
                                                    const float* __restrict__ hr, int ldr,
                                                    const float* __restrict__ wc,
                                                    float* __restrict__ dyr, int lddyr,
-                                                   float* __restrict__ part, int n_pad) {
+                                                   float* __restrict__ part, int n_pad,
+                                                   float* __restrict__ dyr_rmax) {
     constexpr int H = 64 * NH, HR = 64 * NR, PART = H + 3 * HR + 4;
     __shared__ float red[4][PART];
     const int lane = lane_id();
@@ -240,14 +249,22 @@ __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ gra
             const float4 gr = *reinterpret_cast<const float4*>(graw4 + 4 * s);
 #pragma unroll
             for (int q = 0; q < NH; ++q) awd[q] += gr.x * h8[s * ld8 + lane + 64 * q];
+            float dmax = 0.f;
 #pragma unroll
             for (int q = 0; q < NR; ++q) {
                 const float x = hr[s * ldr + lane + 64 * q];
                 float d = gr.y * wcr[0][q] + gr.z * wcr[1][q] + gr.w * wcr[2][q];
-                dyr[s * lddyr + lane + 64 * q] = x > 0.f ? d : 0.f;
+                d = x > 0.f ? d : 0.f;
+                dyr[s * lddyr + lane + 64 * q] = d;
+                dmax = fmaxf(dmax, fabsf(d));
                 awc[0][q] += gr.y * x;
                 awc[1][q] += gr.z * x;
                 awc[2][q] += gr.w * x;
+            }
+            if (dyr_rmax) {   // row max of dyr (row scale of GEMM precision mode 2)
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, off, 64));
+                if (lane == 0) dyr_rmax[s] = dmax;
             }
             abd += gr.x;
             abc[0] += gr.y; abc[1] += gr.z; abc[2] += gr.w;
@@ -561,6 +578,19 @@ __device__ __forceinline__ void stage_raw(const float* __restrict__ raw4, float4
     const int nr = min(16, R - ray0);
     if (nr <= 0) return;
     const float4* src = reinterpret_cast<const float4*>(raw4) + (size_t)ray0 * S;
+    if (nr == 16 && S == 16 * J) {
+        // whole block, S = 16 J: each thread's J loads are issued back to back (J 16-byte
+        // loads in flight per lane instead of one)
+        float4 v[J];
+#pragma unroll
+        for (int q = 0; q < J; ++q) v[q] = src[threadIdx.x + q * 256];
+#pragma unroll
+        for (int q = 0; q < J; ++q) {
+            const int c = threadIdx.x + q * 256;
+            lds[stage_slot<J>(c / S, c % S)] = v[q];
+        }
+        return;
+    }
     for (int c = threadIdx.x; c < nr * S; c += blockDim.x) {
         int r, i;
         split_rs(c, S, lgS, r, i);
@@ -734,6 +764,14 @@ __global__ __launch_bounds__(256) void k_composite16_bwd(const float* __restrict
     __syncthreads();
     const int ray0 = blockIdx.x * 16, nr = min(16, R - ray0);
     float4* dst = reinterpret_cast<float4*>(graw4) + (size_t)ray0 * S;
+    if (nr == 16 && S == 16 * J) {
+#pragma unroll
+        for (int q = 0; q < J; ++q) {
+            const int c = threadIdx.x + q * 256;
+            dst[c] = lraw[stage_slot<J>(c / S, c % S)];
+        }
+        return;
+    }
     for (int c = threadIdx.x; c < nr * S; c += blockDim.x) {
         int r, i;
         split_rs(c, S, lgS, r, i);
@@ -815,7 +853,7 @@ using namespace nerf;
 extern "C" int nerf_encode_samples(const float* pts_o, const float* pts_d, const float* view,
                                    const float* noise, int n_rays, int n_samples, int n_pad,
                                    float near_z, float far_z, float* z, float* enc_p, float* enc_d,
-                                   void* stream) {
+                                   float* enc_p_rmax, float* enc_d_rmax, void* stream) {
     NERF_CHECK_PTR(pts_o); NERF_CHECK_PTR(pts_d); NERF_CHECK_PTR(view);
     NERF_CHECK_PTR(z); NERF_CHECK_PTR(enc_p); NERF_CHECK_PTR(enc_d);
     NERF_CHECK_ALIGN16(enc_p); NERF_CHECK_ALIGN16(enc_d);
@@ -823,7 +861,8 @@ extern "C" int nerf_encode_samples(const float* pts_o, const float* pts_d, const
                "%s: n_pad=%d < R*S=%lld", __func__, n_pad, (long long)n_rays * n_samples);
     const int blocks = (n_pad + 255) / 256;
     hipLaunchKernelGGL(k_encode_samples, dim3(blocks), dim3(256), 0, as_stream(stream), pts_o, pts_d,
-                       view, noise, n_rays, n_samples, n_pad, near_z, far_z, z, enc_p, enc_d);
+                       view, noise, n_rays, n_samples, n_pad, near_z, far_z, z, enc_p, enc_d, enc_p_rmax,
+                       enc_d_rmax);
     return check_launch(__func__);
 }
 
@@ -863,7 +902,7 @@ extern "C" int nerf_heads_part_size(int hidden, int n_pad) {
 
 extern "C" int nerf_heads_bwd(const float* graw4, const float* h8, int ld8, const float* hr, int ldr,
                               int hidden, const float* wc, float* dyr, int lddyr, float* part,
-                              int n_pad, void* stream) {
+                              int n_pad, float* dyr_rmax, void* stream) {
     NERF_CHECK_PTR(graw4); NERF_CHECK_PTR(h8); NERF_CHECK_PTR(hr); NERF_CHECK_PTR(wc);
     NERF_CHECK_PTR(dyr); NERF_CHECK_PTR(part);
     NERF_CHECK_ALIGN16(graw4);
@@ -872,13 +911,13 @@ extern "C" int nerf_heads_bwd(const float* graw4, const float* h8, int ld8, cons
     hipStream_t s = as_stream(stream);
     dim3 g(heads_blocks(n_pad)), b(256);
     if (hidden == 256 && hrw == 128)
-        hipLaunchKernelGGL((k_heads_bwd<4, 2>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad);
+        hipLaunchKernelGGL((k_heads_bwd<4, 2>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax);
     else if (hidden == 128 && hrw == 64)
-        hipLaunchKernelGGL((k_heads_bwd<2, 1>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad);
+        hipLaunchKernelGGL((k_heads_bwd<2, 1>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax);
     else if (hidden == 64 && hrw == 64)
-        hipLaunchKernelGGL((k_heads_bwd<1, 1>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad);
+        hipLaunchKernelGGL((k_heads_bwd<1, 1>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax);
     else if (hidden == 512 && hrw == 256)
-        hipLaunchKernelGGL((k_heads_bwd<8, 4>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad);
+        hipLaunchKernelGGL((k_heads_bwd<8, 4>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax);
     else
         NERF_CHECK(false, "%s: unsupported hidden width %d (64/128/256/512)", __func__, hidden);
     return check_launch(__func__);

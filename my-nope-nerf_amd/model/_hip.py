@@ -42,17 +42,18 @@ class PackDesc(ctypes.Structure):
 _SIGS = {
     "nerf_hip_abi_version": ([], _c_i),
     "nerf_hip_last_error": ([], ctypes.c_char_p),
-    "nerf_encode_samples": ([_c_p, _c_p, _c_p, _c_p, _c_i, _c_i, _c_i, _c_f, _c_f, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_encode_samples": ([_c_p, _c_p, _c_p, _c_p, _c_i, _c_i, _c_i, _c_f, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
+                             _c_p], _c_i),
     "nerf_linear_fwd": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_p, _c_i, _c_i, _c_i, _c_i,
-                         _c_p, _c_i, _c_p], _c_i),
+                         _c_p, _c_i, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_linear_bwd_data": ([_c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_i,
-                              _c_i, _c_p], _c_i),
+                              _c_i, _c_p, _c_p, _c_p], _c_i),
     "nerf_linear_bwd_weight": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p], _c_i),
     "nerf_linear_bwd_weight_splits": ([_c_i, _c_i, _c_i], _c_i),
     "nerf_slab_reduce": ([_c_p, _c_i, _c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_heads_fwd": ([_c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_heads_part_size": ([_c_i, _c_i], _c_i),
-    "nerf_heads_bwd": ([_c_p, _c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_p], _c_i),
+    "nerf_heads_bwd": ([_c_p, _c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_p, _c_p], _c_i),
     "nerf_heads_reduce": ([_c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_composite_fwd": ([_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_composite_bwd": ([_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
@@ -139,9 +140,13 @@ def _ld(t: torch.Tensor) -> int:
 
 
 # --------------------------------------------------------------------------------------
-def encode_samples(pts_o, pts_d, view, noise, n_rays, n_samples, n_pad, near, far, z, enc_p, enc_d):
+def encode_samples(pts_o, pts_d, view, noise, n_rays, n_samples, n_pad, near, far, z, enc_p, enc_d,
+                   enc_p_rmax=None, enc_d_rmax=None):
+    """enc_p_rmax / enc_d_rmax: optional [n_pad] outputs, max |.| per encoding row (the row
+    scales GEMM precision mode 2 needs)."""
     _call("nerf_encode_samples", _ptr(pts_o), _ptr(pts_d), _ptr(view), _ptr(noise), n_rays, n_samples,
-          n_pad, float(near), float(far), _ptr(z), _ptr(enc_p), _ptr(enc_d), _stream())
+          n_pad, float(near), float(far), _ptr(z), _ptr(enc_p), _ptr(enc_d), _ptr(enc_p_rmax), _ptr(enc_d_rmax),
+          _stream())
 
 
 def _split_args(ws):
@@ -154,24 +159,29 @@ def _split_args(ws):
 
 
 def split_image(rows: int, k: int, device) -> "torch.Tensor":
-    """Zeroed bf16x3 image buffer for a [rows][k] operand (nerf_pack_desc.dst_s layout)."""
+    """Zeroed bf16x3 image buffer for a [rows][k] operand (nerf_pack_desc.dst_s layout); in
+    GEMM precision mode 2 the pack writes the fp16 pair form into the same buffer."""
     return torch.zeros(3, k // 8, rows, 8, dtype=torch.int16, device=device)
 
 
-def linear_fwd(x1, k1, x2, k2, w, bias, y, m, n, relu, mask_out=None, w_split=None):
-    """mask_out: int32 [m][n/32] ReLU mask bits of y (optional).  w_split: optional bf16x3
-    image of w (used by GEMM precision mode 1)."""
+def linear_fwd(x1, k1, x2, k2, w, bias, y, m, n, relu, mask_out=None, w_split=None, x1_rmax=None, x2_rmax=None,
+               y_rmax=None):
+    """mask_out: int32 [m][n/32] ReLU mask bits of y (optional).  w_split: optional split
+    image of w (used by GEMM precision modes 1 and 2).  x1_rmax / x2_rmax: max |x| per row of
+    each input segment (required in mode 2); y_rmax: optional [m] output, max |y| per row."""
     wsp, wsr = _split_args(w_split)
     _call("nerf_linear_fwd", _ptr(x1), _ld(x1), k1, _ptr(x2), _ld(x2) if x2 is not None else 0, k2,
           _ptr(w), wsp, wsr, _ptr(bias), _ptr(y), _ld(y), m, n, int(relu), _ptr(mask_out),
-          _ld(mask_out) if mask_out is not None else 0, _stream())
+          _ld(mask_out) if mask_out is not None else 0, _ptr(x1_rmax), _ptr(x2_rmax), _ptr(y_rmax), _stream())
 
 
-def linear_bwd_data(dy, k, wt, dx, m, n, mask=None, u=None, ldu=1, v=None, wt_split=None):
-    """mask: int32 ReLU mask bits [m][words] from linear_fwd(mask_out=...)."""
+def linear_bwd_data(dy, k, wt, dx, m, n, mask=None, u=None, ldu=1, v=None, wt_split=None, dy_rmax=None,
+                    dx_rmax=None):
+    """mask: int32 ReLU mask bits [m][words] from linear_fwd(mask_out=...).  dy_rmax / dx_rmax:
+    row maxima as x1_rmax / y_rmax of linear_fwd."""
     wsp, wsr = _split_args(wt_split)
     _call("nerf_linear_bwd_data", _ptr(dy), _ld(dy), k, _ptr(wt), wsp, wsr, _ptr(u), int(ldu), _ptr(v), _ptr(mask),
-          _ld(mask) if mask is not None else 0, _ptr(dx), _ld(dx), m, n, _stream())
+          _ld(mask) if mask is not None else 0, _ptr(dx), _ld(dx), m, n, _ptr(dy_rmax), _ptr(dx_rmax), _stream())
 
 
 def linear_bwd_weight(dy, nout, x, kin, m, splits, slab, ldslab, col0, bslab):
@@ -197,9 +207,9 @@ def heads_part_size(hidden, n_pad) -> int:
     return int(lib().nerf_heads_part_size(hidden, n_pad))
 
 
-def heads_bwd(graw4, h8, hr, hidden, wc, dyr, part, n_pad):
+def heads_bwd(graw4, h8, hr, hidden, wc, dyr, part, n_pad, dyr_rmax=None):
     _call("nerf_heads_bwd", _ptr(graw4), _ptr(h8), _ld(h8), _ptr(hr), _ld(hr), hidden, _ptr(wc), _ptr(dyr),
-          _ld(dyr), _ptr(part), n_pad, _stream())
+          _ld(dyr), _ptr(part), n_pad, _ptr(dyr_rmax), _stream())
 
 
 def heads_reduce(part, hidden, n_pad, gwd, gbd, gwc, gbc, accumulate=False):
@@ -306,7 +316,9 @@ def gemm_set_policy(nt: int = 0, tn: int = 0):
 
 
 def gemm_set_precision(mode):
-    """0 = exact-f32 MFMA, 1 = f32 emulated on bf16 MFMA (3-word split, 6 products)."""
+    """0 = exact-f32 MFMA, 1 = f32 emulated on bf16 MFMA (3-word split, 6 products),
+    2 = f32 emulated on fp16 MFMA for the forward / backward-data GEMMs (row-scaled 2-word
+    split, 3 products; weight gradients as mode 1)."""
     _call("nerf_gemm_set_precision", int(mode))
 
 

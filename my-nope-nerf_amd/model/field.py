@@ -100,8 +100,11 @@ class FieldRunner:
             raise RuntimeError("nerf_hip: the field must live on the GPU (no CPU fallback)")
         if self.device != dev:
             self._alloc(dev)
-        # split images only when the GEMMs run in the split-bf16 mode
-        self.split = _hip.gemm_get_precision() == 1
+        # split images only when the GEMMs run in a split mode (1: bf16x3, 2: fp16 pair;
+        # the pack kernel writes the form of the current mode)
+        prec = _hip.gemm_get_precision()
+        self.split = prec >= 1
+        self.h16 = prec == 2
         descs = []
         for l in self.layers:
             W = l.linear.weight
@@ -135,7 +138,11 @@ class FieldRunner:
         z = e(Np)
         enc_p = e(Np, _hip.ENC_P)
         enc_d = e(Np, _hip.ENC_D)
-        _hip.encode_samples(pts_o, pts_d, view, noise, R, S, Np, near, far, z, enc_p, enc_d)
+        # precision mode 2: every GEMM A operand travels with its row max (written by its producer)
+        rm = self._rmax_alloc(Np, dev)
+        enc_p_rm, enc_d_rm = rm(64), rm(64)
+        _hip.encode_samples(pts_o, pts_d, view, noise, R, S, Np, near, far, z, enc_p, enc_d,
+                            enc_p_rmax=enc_p_rm, enc_d_rmax=enc_d_rm)
         acts = []
         if keep:
             outs = [e(Np, D) for _ in range(9)] + [e(Np, HR)]
@@ -143,7 +150,9 @@ class FieldRunner:
             ping = [e(Np, D), e(Np, D)]
             outs = [ping[i % 2] for i in range(9)] + [e(Np, HR)]
         x = enc_p
+        x_rm = enc_p_rm
         segs = {"enc_p": enc_p, "enc_d": enc_d}
+        seg_rm = {"enc_p": enc_p_rm, "enc_d": enc_d_rm}
         masks = {}
         for i, l in enumerate(self.layers):
             y = outs[i]
@@ -153,10 +162,13 @@ class FieldRunner:
             if keep and l.relu and l.name != "lr":   # ReLU bits for the backward's input masks
                 mo = torch.empty(Np, l.out_p // 32, device=dev, dtype=torch.int32)
                 masks[l.name] = mo
+            y_rm = rm(l.out_p)
             _hip.linear_fwd(x, k1, x2, _hip.ENC_P if x2 is not None else 0, self.w[l.name], self.bias(l), y,
-                            Np, l.out_p, l.relu, mask_out=mo, w_split=self.ws[l.name] if self.split else None)
+                            Np, l.out_p, l.relu, mask_out=mo, w_split=self.ws[l.name] if self.split else None,
+                            x1_rmax=x_rm, x2_rmax=seg_rm[l.seg2] if l.seg2 else None, y_rmax=y_rm)
             acts.append(y)
             x = y
+            x_rm = y_rm
             if l.name == "l7":
                 h8 = y
         hr = acts[9]
@@ -175,6 +187,14 @@ class FieldRunner:
             state = dict(R=R, S=S, Np=Np, flags=flags, z=z, enc_p=enc_p, enc_d=enc_d, acts=acts, raw4=raw4,
                          masks=masks, pts_o=pts_o, pts_d=pts_d, view=view)
         return rgb, dist, alpha, z[:N].view(R, S), state
+
+    def _rmax_alloc(self, Np: int, dev):
+        """Row-max buffer factory for precision mode 2 (None otherwise): a buffer for an
+        operand of `width` columns; wider than one 256-column GEMM block it is max-accumulated
+        by the kernel and starts at zero."""
+        if not self.h16:
+            return lambda width: None
+        return lambda width: (torch.zeros if width > 256 else torch.empty)(Np, device=dev, dtype=torch.float32)
 
     # ------------------------------------------------------------------ backward
     def param_list(self) -> List[torch.nn.Parameter]:
@@ -205,7 +225,9 @@ class FieldRunner:
         # heads: d(fc_density), d(fc_rgb), dY of the colour layer
         dyr = e(Np, HR)
         part = e(_hip.heads_part_size(D, Np))
-        _hip.heads_bwd(graw4, h["l7"], h["lr"], D, self.wc, dyr, part, Np)
+        rm = self._rmax_alloc(Np, dev)
+        dy_rm = rm(HR)
+        _hip.heads_bwd(graw4, h["l7"], h["lr"], D, self.wc, dyr, part, Np, dyr_rmax=dy_rm)
         gwc = G(m.fc_rgb.weight) if HR == D // 2 else e(3, HR)
         _hip.heads_reduce(part, D, Np, G(m.fc_density.weight), G(m.fc_density.bias), gwc, G(m.fc_rgb.bias))
         if HR != D // 2:
@@ -261,21 +283,25 @@ class FieldRunner:
             if name == "l0":
                 if want_ray_grad:
                     genc["p0"] = e(Np, _hip.ENC_P)
-                    _hip.linear_bwd_data(dy, l.out_p, wt, genc["p0"], Np, _hip.ENC_P, wt_split=wts)
+                    _hip.linear_bwd_data(dy, l.out_p, wt, genc["p0"], Np, _hip.ENC_P, wt_split=wts, dy_rmax=dy_rm)
                 break
             if l.seg2 and want_ray_grad:
                 key = "p4" if l.seg2 == "enc_p" else "d"
                 genc[key] = e(Np, 64)
-                _hip.linear_bwd_data(dy, l.out_p, wt[k1:k1 + 64], genc[key], Np, 64, wt_split=rows(k1, k1 + 64))
+                _hip.linear_bwd_data(dy, l.out_p, wt[k1:k1 + 64], genc[key], Np, 64, wt_split=rows(k1, k1 + 64),
+                                     dy_rmax=dy_rm)
             dx = e(Np, k1)
+            dx_rm = rm(k1)
             # ReLU bits of this layer's input (f, the input of lr, has no activation)
             mask = None if name == "lr" else st["masks"][prev_name[name]]
             if name == "lf":   # + density path: d sigma_raw (graw4[:,0]) x w_density
                 _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask, u=graw4, ldu=4,
-                                     v=m.fc_density.weight, wt_split=rows(0, k1))
+                                     v=m.fc_density.weight, wt_split=rows(0, k1), dy_rmax=dy_rm, dx_rmax=dx_rm)
             else:
-                _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask, wt_split=rows(0, k1))
+                _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask, wt_split=rows(0, k1),
+                                     dy_rmax=dy_rm, dx_rmax=dx_rm)
             dy = dx
+            dy_rm = dx_rm
 
         done = torch.cuda.Event()
         done.record(side)

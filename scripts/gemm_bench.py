@@ -39,23 +39,34 @@ def main():
     mask = torch.empty(M, D // 32, device=dev, dtype=torch.int32)
     dy = torch.rand(M, D, device=dev, generator=g) - 0.5
     u = torch.rand(M, 4, device=dev, generator=g)
-    # bf16x3 images of W (forward B operand) and of W as the transposed backward operand
-    ws, wts = _hip.split_image(D, D, dev), _hip.split_image(D, D, dev)
-    Wp, Wt = torch.zeros(D, D, device=dev), torch.zeros(D, D, device=dev)
-    _hip.pack_weights([_hip.PackDesc(W.data_ptr(), Wp.data_ptr(), Wt.data_ptr(), D, D, D, D, D, ws.data_ptr(),
-                                     wts.data_ptr())])
+    # split images of W (forward B operand) and of W as the transposed backward operand, in
+    # both split forms (mode 1 bf16x3, mode 2 fp16 pair: the pack writes the current mode's)
+    imgs = {}
+    for mode in (1, 2):
+        _hip.gemm_set_precision(mode)
+        ws, wts = _hip.split_image(D, D, dev), _hip.split_image(D, D, dev)
+        Wp, Wt = torch.zeros(D, D, device=dev), torch.zeros(D, D, device=dev)
+        _hip.pack_weights([_hip.PackDesc(W.data_ptr(), Wp.data_ptr(), Wt.data_ptr(), D, D, D, D, D, ws.data_ptr(),
+                                         wts.data_ptr())])
+        ws4 = _hip.split_image(D, D + 64, dev)
+        W4p, W4t = torch.zeros(D, D + 64, device=dev), torch.zeros(D + 64, D, device=dev)
+        _hip.pack_weights([_hip.PackDesc(W4.data_ptr(), W4p.data_ptr(), W4t.data_ptr(), D, D + 64, D + 64, D + 64, D,
+                                         ws4.data_ptr(), None)])
+        imgs[mode] = (ws, wts, ws4)
+    _hip.gemm_set_precision(0)
+    im = lambda i: imgs[max(1, _hip.gemm_get_precision())][i]
+    # row maxima of the A operands (mode 2 only; the other modes ignore them)
+    x_rm, enc_rm, dy_rm = x.abs().amax(1), enc.abs().amax(1), dy.abs().amax(1)
+    y_rm = torch.empty(M, device=dev)
     cases = {}
-    ws4 = _hip.split_image(D, D + 64, dev)
-    W4p, W4t = torch.zeros(D, D + 64, device=dev), torch.zeros(D + 64, D, device=dev)
-    _hip.pack_weights([_hip.PackDesc(W4.data_ptr(), W4p.data_ptr(), W4t.data_ptr(), D, D + 64, D + 64, D + 64, D,
-                                     ws4.data_ptr(), None)])
     # split images are passed everywhere; the exact-f32 mode ignores them
-    cases["fwd 256x256"] = (lambda: _hip.linear_fwd(x, D, None, 0, W, b, y, M, D, 1, mask_out=mask, w_split=ws),
-                            2 * M * D * D)
-    cases["fwd skip 320"] = (lambda: _hip.linear_fwd(x, D, enc, 64, W4, b, y, M, D, 1, w_split=ws4),
-                             2 * M * D * (D + 64))
+    cases["fwd 256x256"] = (lambda: _hip.linear_fwd(x, D, None, 0, W, b, y, M, D, 1, mask_out=mask, w_split=im(0),
+                                                    x1_rmax=x_rm, y_rmax=y_rm), 2 * M * D * D)
+    cases["fwd skip 320"] = (lambda: _hip.linear_fwd(x, D, enc, 64, W4, b, y, M, D, 1, w_split=im(2), x1_rmax=x_rm,
+                                                     x2_rmax=enc_rm, y_rmax=y_rm), 2 * M * D * (D + 64))
     cases["bwd-data mask+u"] = (lambda: _hip.linear_bwd_data(dy, D, W, y, M, D, mask=mask, u=u, ldu=4, v=b,
-                                                             wt_split=wts), 2 * M * D * D)
+                                                             wt_split=im(1), dy_rmax=dy_rm, dx_rmax=y_rm),
+                                2 * M * D * D)
     for sp in (64, 128, 256):
         slab = torch.empty(sp * D * D, device=dev)
         bslab = torch.empty(sp * D, device=dev)
@@ -63,6 +74,8 @@ def main():
                                      _hip.linear_bwd_weight(dy, D, x, D, M, sp, slab, D, 0, bslab)), 2 * M * D * D)
     if "--x6" in sys.argv:
         _hip.gemm_set_precision(1)
+    if "--h16" in sys.argv:
+        _hip.gemm_set_precision(2)
     if "--stamps" in sys.argv:   # per-block phase clocks of the split-bf16 NT kernel
         import numpy as np
         for name in ("fwd 256x256", "bwd-data mask+u"):
@@ -112,10 +125,10 @@ def main():
             print(f"ablate={ab} dW splits=256: {us:8.1f} us {fl / us / 1e6:6.1f} TF/s")
         _hip.lib().nerf_gemm_debug_ablate(0)
         return
-    if "--prec" in sys.argv:   # exact-f32 MFMA vs split-bf16, default tile policy
+    if "--prec" in sys.argv:   # exact-f32 MFMA vs split-bf16 vs fp16 pair, default tile policy
         res = {}
         for rnd in range(3):
-            for prec in (0, 1):
+            for prec in (0, 1, 2):
                 _hip.gemm_set_precision(prec)
                 for name, (fn, fl) in cases.items():
                     res.setdefault((name, prec), []).append(timeit(fn))

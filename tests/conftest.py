@@ -21,9 +21,9 @@ def dev():
     return torch.device("cuda:0")
 
 
-@pytest.fixture(params=[0, 1], ids=["f32mfma", "bf16x6"])
+@pytest.fixture(params=[0, 1, 2], ids=["f32mfma", "bf16x6", "f16x3"])
 def gemm_precision(request, dev):
-    """Run a GPU test under both GEMM arithmetic modes (nerf_gemm_set_precision)."""
+    """Run a GPU test under every GEMM arithmetic mode (nerf_gemm_set_precision)."""
     from model import _hip
     old = _hip.gemm_get_precision()
     _hip.gemm_set_precision(request.param)

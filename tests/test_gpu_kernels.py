@@ -2,8 +2,9 @@
 
 Tolerances: FP32 MFMA GEMMs are exact-f32 fma chains, so against an fp64 reference the
 error is ~1e-7 * sqrt(K) * |a||b|; we require max |err| <= 2e-5 * scale (rel 2e-5).  The
-GEMM tests run under both arithmetic modes (conftest.gemm_precision); the split-bf16
-emulation must also be no less accurate than the exact-f32 MFMA (test_split_bf16_accuracy)."""
+GEMM tests run under every arithmetic mode (conftest.gemm_precision); the split-bf16 and
+fp16-pair emulations must also be about as accurate as the exact-f32 MFMA
+(test_split_accuracy)."""
 import pytest
 import torch
 
@@ -17,8 +18,16 @@ def _rand(*s, g=None):
     return torch.rand(*s, generator=g) * 2 - 1
 
 
+def _rm(x):
+    """Row max |x| (the A-operand row scales of precision mode 2), None in other modes."""
+    if _hip.gemm_get_precision() != 2 or x is None:
+        return None
+    return x.abs().amax(1).contiguous()
+
+
 def _images(W, dev):
-    """W [n][k] (device) -> (bf16x3 image of W, image of W^T) via nerf_pack_weights."""
+    """W [n][k] (device) -> (split image of W, image of W^T) via nerf_pack_weights, in the
+    form of the current precision mode (bf16x3, or the fp16 pair in mode 2)."""
     n, k = W.shape
     Wp, Wt = torch.zeros(n, k, device=dev), torch.zeros(k, n, device=dev)
     ws, wts = _hip.split_image(n, k, dev), _hip.split_image(k, n, dev)
@@ -38,15 +47,19 @@ def test_linear_fwd(dev, gemm_precision, m, n, k1, k2, relu):
     y = torch.empty(m, n, device=dev)
     mo = torch.empty(m, n // 32, device=dev, dtype=torch.int32)
     Wd = W.to(dev)
-    ws = _images(Wd, dev)[0] if gemm_precision == 1 else None
-    _hip.linear_fwd(x1.to(dev), k1, x2.to(dev) if x2 is not None else None, k2, Wd, b.to(dev), y, m, n, relu,
-                    mask_out=mo, w_split=ws)
+    ws = _images(Wd, dev)[0] if gemm_precision >= 1 else None
+    x1d, x2d = x1.to(dev), (x2.to(dev) if x2 is not None else None)
+    y_rm = torch.full((m,), -1.0, device=dev) if gemm_precision == 2 else None
+    _hip.linear_fwd(x1d, k1, x2d, k2, Wd, b.to(dev), y, m, n, relu, mask_out=mo, w_split=ws, x1_rmax=_rm(x1d),
+                    x2_rmax=_rm(x2d), y_rmax=y_rm)
     xc = torch.cat([x1, x2], 1) if x2 is not None else x1
     ref = xc.double() @ W.double().t() + b.double()
     if relu:
         ref = ref.clamp_min(0)
     torch.cuda.synchronize()
     assert (y.cpu().double() - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
+    if y_rm is not None:                                              # exact row maxima of y
+        assert torch.equal(y_rm, y.abs().amax(1))
     bits = ((mo.cpu().long() & 0xffffffff).unsqueeze(-1) >> torch.arange(32)) & 1
     assert torch.equal(bits.view(m, n).bool(), y.cpu() > 0)          # ReLU bits agree with y
 
@@ -58,8 +71,9 @@ def test_linear_fwd_asymmetric_identity(dev, gemm_precision):
     W = torch.arange(n * k, dtype=torch.float32).view(n, k) / (n * k)
     y = torch.empty(m, n, device=dev)
     Wd = W.to(dev)
-    ws = _images(Wd, dev)[0] if gemm_precision == 1 else None
-    _hip.linear_fwd(x.to(dev), k, None, 0, Wd, None, y, m, n, 0, w_split=ws)
+    ws = _images(Wd, dev)[0] if gemm_precision >= 1 else None
+    xd = x.to(dev)
+    _hip.linear_fwd(xd, k, None, 0, Wd, None, y, m, n, 0, w_split=ws, x1_rmax=_rm(xd))
     assert torch.equal(y.cpu(), W.t().contiguous())
 
 
@@ -76,13 +90,17 @@ def test_linear_bwd_data(dev, gemm_precision):
     words = bits.sum(-1)
     words = torch.where(words >= 2 ** 31, words - 2 ** 32, words).to(torch.int32)
     Wtd = Wt.to(dev)
-    ws = _images(Wtd, dev)[0] if gemm_precision == 1 else None     # image of wt itself ([n][k])
-    _hip.linear_bwd_data(dy.to(dev), k, Wtd, dx, m, n, mask=words.to(dev), u=u.to(dev), ldu=4, v=v.to(dev),
-                         wt_split=ws)
+    ws = _images(Wtd, dev)[0] if gemm_precision >= 1 else None     # image of wt itself ([n][k])
+    dyd = dy.to(dev)
+    dx_rm = torch.full((m,), -1.0, device=dev) if gemm_precision == 2 else None
+    _hip.linear_bwd_data(dyd, k, Wtd, dx, m, n, mask=words.to(dev), u=u.to(dev), ldu=4, v=v.to(dev),
+                         wt_split=ws, dy_rmax=_rm(dyd), dx_rmax=dx_rm)
     ref = dy.double() @ Wt.double().t() + u[:, 0:1].double() * v.double()
     ref = torch.where(mask > 0, ref, torch.zeros_like(ref))
     torch.cuda.synchronize()
     assert (dx.cpu().double() - ref).abs().max().item() < 2e-5 * ref.abs().max().item()
+    if dx_rm is not None:
+        assert torch.equal(dx_rm, dx.abs().amax(1))
 
 
 @pytest.mark.parametrize("nout,kin,m,splits", [(256, 256, 4096, 8), (128, 320, 2048, 4), (256, 64, 1024, 1),
@@ -132,30 +150,38 @@ def test_slab_reduce_accumulate(dev):
     assert torch.allclose(gw2, 2 * (gw - gw0), atol=1e-4)
 
 
-@pytest.mark.parametrize("scale_a,scale_b", [(1.0, 0.1), (1e-3, 1e3), (1e-20, 1.0)])
-def test_split_bf16_accuracy(dev, scale_a, scale_b):
-    """The split-bf16 GEMM (mode 1) against fp64: its error must stay within 1.5x (+ a
-    few ulps) of the exact-f32 MFMA's on the same operands, over K = 320 (two segments),
-    including operands far from 1 (the three bf16 words share f32's exponent range)."""
+@pytest.mark.parametrize("scale_a,scale_b,spread", [(1.0, 0.1, 0), (1e-3, 1e3, 0), (1e-20, 1.0, 0), (1.0, 0.1, 8),
+                                                    (1e-7, 1.0, 12), (1e4, 1e-6, 0)])
+def test_split_accuracy(dev, scale_a, scale_b, spread):
+    """The split-bf16 GEMM (mode 1) and the fp16-pair GEMM (mode 2) against fp64: their
+    errors must stay within 1.5x (+ a few ulps) of the exact-f32 MFMA's on the same operands,
+    over K = 320 (two segments), including operands far from 1 (bf16 words share f32's
+    exponent range; the fp16 pair carries per-row power-of-two scales) and rows whose
+    magnitudes differ by up to 2^spread (row-scale independence)."""
     g = torch.Generator().manual_seed(11)
     m, n, k1, k2 = 512, 256, 256, 64
-    x1, x2 = _rand(m, k1, g=g) * scale_a, _rand(m, k2, g=g) * scale_a
+    rs = 2.0 ** (torch.randint(-spread, spread + 1, (m, 1), generator=g).float()) if spread else 1.0
+    x1, x2 = _rand(m, k1, g=g) * scale_a * rs, _rand(m, k2, g=g) * scale_a * rs
     W = _rand(n, k1 + k2, g=g) * scale_b
     ref = torch.cat([x1, x2], 1).double() @ W.double().t()
     errs = []
     Wd = W.to(dev)
-    ws = _images(Wd, dev)[0]
-    for mode in (0, 1):
+    x1d, x2d = x1.to(dev), x2.to(dev)
+    for mode in (0, 1, 2):
         _hip.gemm_set_precision(mode)
         try:
+            ws = _images(Wd, dev)[0]
             y = torch.empty(m, n, device=dev)
-            _hip.linear_fwd(x1.to(dev), k1, x2.to(dev), k2, Wd, None, y, m, n, 0, w_split=ws)
+            _hip.linear_fwd(x1d, k1, x2d, k2, Wd, None, y, m, n, 0, w_split=ws, x1_rmax=_rm(x1d), x2_rmax=_rm(x2d))
             torch.cuda.synchronize()
         finally:
             _hip.gemm_set_precision(0)
-        errs.append((y.cpu().double() - ref).abs().max().item())
-    tiny = 4 * 2.0 ** -24 * ref.abs().max().item()
+        # per-row error relative to the row's scale (rows differ by 2^spread)
+        rowscale = ref.abs().amax(1, keepdim=True).clamp_min(1e-300)
+        errs.append(((y.cpu().double() - ref).abs() / rowscale).max().item())
+    tiny = 4 * 2.0 ** -24
     assert errs[1] <= 1.5 * errs[0] + tiny, errs
+    assert errs[2] <= 1.5 * errs[0] + tiny, errs
 
 
 def _split3_ref(x):
@@ -193,25 +219,60 @@ def test_pack_split_images(dev):
     assert torch.equal((h + m + lo).float(), dst.cpu())
 
 
+def test_pack_f16_pair_images(dev):
+    """Mode 2 images: per row r an exponent e_r with max|row| 2^e_r in [2^14, 2^15), fp16
+    hi / lo planes with hi = fp16(x 2^e_r) and lo = fp16(x 2^e_r - hi) (RNE), so that
+    (hi + lo) 2^-e_r is x to 2^-22 of the row max; zero rows get e = 0."""
+    g = torch.Generator().manual_seed(6)
+    rows, cols, ld, rows_t, ld_t, rows_s = 200, 300, 320, 320, 256, 256
+    W = (_rand(rows, cols, g=g) * torch.logspace(-6, 2, rows).unsqueeze(1)).to(dev)
+    dst = torch.zeros(rows, ld, device=dev)
+    dst_t = torch.zeros(rows_t, ld_t, device=dev)
+    ws = _hip.split_image(rows_s, ld, dev) - 1
+    wts = _hip.split_image(rows_t, ld_t, dev) - 1
+    _hip.gemm_set_precision(2)
+    try:
+        _hip.pack_weights([_hip.PackDesc(W.data_ptr(), dst.data_ptr(), dst_t.data_ptr(), rows, cols, ld, rows_t,
+                                         ld_t, ws.data_ptr(), wts.data_ptr(), rows_s)])
+        torch.cuda.synchronize()
+    finally:
+        _hip.gemm_set_precision(0)
+    for img, mat in ((ws.cpu(), torch.cat([dst.cpu(), torch.zeros(rows_s - rows, ld)])), (wts.cpu(), dst_t.cpu())):
+        N, K = mat.shape
+        e = img[2, 0, :, 0:2].contiguous().view(torch.int32).view(N).long()
+        rmax = mat.abs().amax(1)
+        e_ref = torch.where(rmax > 0, 14 - torch.floor(torch.log2(rmax.double().clamp_min(1e-300))).long(),
+                            torch.zeros_like(e))
+        assert torch.equal(e, e_ref)
+        xs = mat.double() * torch.pow(2.0, e.double()).unsqueeze(1)
+        h = img[0].permute(1, 0, 2).reshape(N, K).view(torch.float16)
+        lo = img[1].permute(1, 0, 2).reshape(N, K).view(torch.float16)
+        assert torch.equal(h, xs.float().half())
+        assert torch.equal(lo, (xs.float() - h.float()).half())
+        rec = (h.double() + lo.double()) * torch.pow(2.0, -e.double()).unsqueeze(1)
+        assert ((rec - mat.double()).abs() <= 2.0 ** -22 * rmax.double().unsqueeze(1) + 1e-45).all()
+
+
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("m,n,k1,k2", [(256, 256, 256, 64), (128, 64, 64, 0), (384, 128, 256, 0), (512, 256, 64, 64)])
-def test_split_weight_operand(dev, m, n, k1, k2):
-    """Mode 1 with the pre-split weight images: forward (two K segments) and
+def test_split_weight_operand(dev, mode, m, n, k1, k2):
+    """Modes 1 / 2 with the pre-split weight images: forward (two K segments) and
     backward-data through a row slice of the transposed image, against fp64."""
     g = torch.Generator().manual_seed(m + k2)
     x1 = _rand(m, k1, g=g).to(dev)
     x2 = _rand(m, k2, g=g).to(dev) if k2 else None
     W = (_rand(n, k1 + k2, g=g) * 0.1).to(dev)
     b = _rand(n, g=g).to(dev)
-    ws, wts = _images(W, dev)
     Wt = W.t().contiguous()
     dy = torch.rand(m, n, device=dev) - 0.5
     lo, hi = (k1, k1 + k2) if k2 else (0, k1)
-    _hip.gemm_set_precision(1)
+    _hip.gemm_set_precision(mode)
     try:
+        ws, wts = _images(W, dev)
         y = torch.empty(m, n, device=dev)
-        _hip.linear_fwd(x1, k1, x2, k2, W, b, y, m, n, 1, w_split=ws)
+        _hip.linear_fwd(x1, k1, x2, k2, W, b, y, m, n, 1, w_split=ws, x1_rmax=_rm(x1), x2_rmax=_rm(x2))
         d = torch.empty(m, hi - lo, device=dev)
-        _hip.linear_bwd_data(dy, n, Wt[lo:hi], d, m, hi - lo, wt_split=wts[:, :, lo:hi])
+        _hip.linear_bwd_data(dy, n, Wt[lo:hi], d, m, hi - lo, wt_split=wts[:, :, lo:hi], dy_rmax=_rm(dy))
         torch.cuda.synchronize()
     finally:
         _hip.gemm_set_precision(0)
@@ -282,7 +343,8 @@ def test_heads_fwd_bwd(dev, hidden):
     graw = torch.randn(Np, 4, generator=g)
     dyr = torch.empty(Np, HR, device=dev)
     part = torch.empty(_hip.heads_part_size(hidden, Np), device=dev)
-    _hip.heads_bwd(graw.to(dev), h8.to(dev), hr.to(dev), hidden, wc.to(dev), dyr, part, Np)
+    dyr_rm = torch.full((Np,), -1.0, device=dev)
+    _hip.heads_bwd(graw.to(dev), h8.to(dev), hr.to(dev), hidden, wc.to(dev), dyr, part, Np, dyr_rmax=dyr_rm)
     gwd, gbd = torch.empty(hidden, device=dev), torch.empty(1, device=dev)
     gwc, gbc = torch.empty(3, HR, device=dev), torch.empty(3, device=dev)
     _hip.heads_reduce(part, hidden, Np, gwd, gbd, gwc, gbc)
@@ -290,6 +352,7 @@ def test_heads_fwd_bwd(dev, hidden):
     r_dyr = torch.where(hr > 0, G[:, 1:] @ wc.double(), torch.zeros(Np, HR, dtype=torch.float64))
     torch.cuda.synchronize()
     assert (dyr.cpu().double() - r_dyr).abs().max().item() < 1e-5 * max(1, r_dyr.abs().max().item())
+    assert torch.equal(dyr_rm, dyr.abs().amax(1))                    # row scales of precision mode 2
     assert (gwd.cpu().double() - G[:, 0] @ h8.double()).abs().max().item() < 1e-4 * Np
     assert (gwc.cpu().double() - G[:, 1:].t() @ hr.double()).abs().max().item() < 1e-4 * Np
     assert (gbd.cpu().double() - G[:, 0].sum()).abs().item() < 1e-3
@@ -307,7 +370,9 @@ def test_encode_samples(dev):
     z = torch.empty(Np, device=dev)
     ep = torch.empty(Np, 64, device=dev)
     ed = torch.empty(Np, 64, device=dev)
-    _hip.encode_samples(o.to(dev), d.to(dev), view.to(dev), noise.to(dev), R, S, Np, 0.01, 10.0, z, ep, ed)
+    rp, rd = torch.full((Np,), -1.0, device=dev), torch.full((Np,), -1.0, device=dev)
+    _hip.encode_samples(o.to(dev), d.to(dev), view.to(dev), noise.to(dev), R, S, Np, 0.01, 10.0, z, ep, ed,
+                        enc_p_rmax=rp, enc_d_rmax=rd)
     oz = orc.stratified_z(R, S, 0.01, 10.0, noise.view(1, R, S))[0]
     pts = (o.unsqueeze(1) + d.unsqueeze(1) * oz.unsqueeze(-1)).reshape(-1, 3)
     ref_p = orc.encode_position(pts, 10)
@@ -321,6 +386,7 @@ def test_encode_samples(dev):
     assert (ed.cpu()[:R * S, :27] - ref_d).abs().max().item() < 2e-6
     assert ep.cpu()[:, 63].abs().max().item() == 0 and ed.cpu()[:, 27:].abs().max().item() == 0
     assert ep.cpu()[R * S:].abs().max().item() == 0
+    assert torch.equal(rp, ep.abs().amax(1)) and torch.equal(rd, ed.abs().amax(1))
 
 
 def test_chamfer_nn(dev):
