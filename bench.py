@@ -165,9 +165,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--gemm-precision", choices=list(PRECISION), default="bf16x6",
-                    help="GEMM arithmetic: f32 emulated by a 3-word bf16 split (bf16x6, default), by a row-scaled "
-                         "2-word fp16 split (f16x3), or the exact-f32 MFMA (f32); all f32-accurate")
+    ap.add_argument("--gemm-precision", choices=list(PRECISION), default="f16x3",
+                    help="GEMM arithmetic: f32 emulated by a row-scaled 2-word fp16 split (f16x3, default), by a "
+                         "3-word bf16 split (bf16x6), or the exact-f32 MFMA (f32); all f32-accurate")
     ap.add_argument("--no-alt", dest="alt", action="store_false",
                     help="skip timing the other GEMM arithmetics (reported as alt_gemm)")
     args = ap.parse_args()
@@ -186,7 +186,7 @@ def main():
     cfg = make_cfg()
     data, c2w = synthetic_scene(dev)
 
-    def measure(precision):
+    def measure(precision, with_hooks=True):
         """W warm-up + K timed train steps with the GEMMs in `precision` (0 exact-f32 MFMA,
         1 split-bf16, 2 fp16 pair); returns (max-over-ranks seconds, last loss dict, GEMM hook stats)."""
         _hip.gemm_set_precision(precision)
@@ -196,30 +196,38 @@ def main():
         def one(it):
             return trainer.train_step(data, it=it, epoch=0, scheduling_start=0)
 
+        def timed(it0, hooks):
+            """K steps between barrier + synchronize; hooks: hipEvent pairs around every GEMM
+            launch (they serialise neighbouring launches a little, so `value` is timed without
+            them and the roofline in a second, instrumented pass of the same K steps)."""
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            _hip.prof_enable(hooks)
+            t0 = time.perf_counter()
+            for i in range(args.steps):
+                ld = one(it0 + i)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t1 = time.perf_counter()
+            stats = _hip.prof_read() if hooks else None
+            _hip.prof_enable(False)
+            el = t1 - t0
+            if world > 1:
+                t = torch.tensor([el], device=dev, dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                el = t.item()
+            return el, ld, stats
+
         for i in range(args.warmup):
             one(i)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        _hip.prof_enable(True)
-        t0 = time.perf_counter()
-        for i in range(args.steps):
-            ld = one(args.warmup + i)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t1 = time.perf_counter()
-        stats = _hip.prof_read()
-        _hip.prof_enable(False)
-        el = t1 - t0
-        if world > 1:
-            t = torch.tensor([el], device=dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = t.item()
-        return el, ld, stats, net
+        el, ld, _ = timed(args.warmup, False)
+        el_h, _, stats = timed(args.warmup + args.steps, True) if with_hooks else (None, None, None)
+        return el, ld, stats, net, el_h
 
     main_prec = PRECISION[args.gemm_precision]
-    elapsed, ld, (gemm_ms, gemm_launches, _, gemm_union_ms), net = measure(main_prec)
+    elapsed, ld, (gemm_ms, gemm_launches, _, gemm_union_ms), net, elapsed_hooks = measure(main_prec)
     alt = None
     if args.alt:
         # the other GEMM arithmetics on the same workload, reported beside the headline
@@ -227,7 +235,7 @@ def main():
         for name, prec in PRECISION.items():
             if prec == main_prec:
                 continue
-            el2, ld2, _, _ = measure(prec)
+            el2, ld2, _, _, _ = measure(prec, with_hooks=False)
             alt.append({"gemm_arithmetic": name, "value": world * RAYS / (el2 / args.steps),
                         "ms_per_step": 1e3 * el2 / args.steps, "final_loss": ld2["loss"].detach().item()})
         _hip.gemm_set_precision(main_prec)
@@ -275,6 +283,8 @@ def main():
                 "launches_per_step": gemm_launches / args.steps,
                 "avg_launch_us": 1e3 * gemm_ms / max(1, gemm_launches),
                 "gemm_ms_per_step": gemm_ms / args.steps,
+                "timing": "second timed pass of the same K steps with hipEvent pairs around every GEMM launch "
+                          "(ms_per_step of that pass: %.3f)" % (1e3 * elapsed_hooks / args.steps),
                 "gemm_union_ms_per_step": gemm_union_ms / args.steps}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:

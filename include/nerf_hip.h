@@ -48,12 +48,15 @@ const char* nerf_hip_last_error(void);
  * enc_d : [n_pad][64]  = same with L=4 on view (27 + 37 pad)
  * z     : [n_pad]; rows >= R*S of all outputs are written as 0.
  * enc_p_rmax, enc_d_rmax (optional, [n_pad]): max |.| of each encoding row (the row scales
- * of GEMM precision mode 2).
+ * of GEMM precision mode 2).  enc_p_cmax, enc_d_cmax (optional, [n_pad/128][64], n_pad %
+ * 128 == 0): per 128-row group an upper bound of max |.| per column -- exact for the three
+ * coordinate columns, 1 for the sin / cos columns, 0 for the pad (column scales of mode 2).
  */
 int nerf_encode_samples(const float* pts_o, const float* pts_d, const float* view,
                         const float* noise, int n_rays, int n_samples, int n_pad,
                         float near_z, float far_z, float* z, float* enc_p, float* enc_d,
-                        float* enc_p_rmax, float* enc_d_rmax, void* stream);
+                        float* enc_p_rmax, float* enc_d_rmax, float* enc_p_cmax, float* enc_d_cmax,
+                        void* stream);
 
 /* ---------------------------------------------------------------------------
  * Linear layer forward on FP32 MFMA (v_mfma_f32_32x32x2_f32).
@@ -74,11 +77,13 @@ int nerf_encode_samples(const float* pts_o, const float* pts_d, const float* vie
  * segment (as written by the producer of x: nerf_encode_samples, this function, ...).
  * y_rmax (optional, mode 2 only): receives max |y| per row; with n > 256 (several column
  * blocks) it is max-accumulated and must be zeroed by the caller.
+ * y_cmax (optional, mode 2 only): receives max |y| per column and 128-row group,
+ * [m/128][n] (the column scales of nerf_linear_bwd_weight in mode 2).
  */
 int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2, int k2,
                     const float* w, const uint16_t* w_split, int w_split_rows, const float* bias, float* y,
                     int ldy, int m, int n, int relu, uint32_t* mask_out, int ldmo,
-                    const float* x1_rmax, const float* x2_rmax, float* y_rmax, void* stream);
+                    const float* x1_rmax, const float* x2_rmax, float* y_rmax, float* y_cmax, void* stream);
 
 /* Backward w.r.t. the layer input (autograd of official_nerf.py:62-91).
  *   dx[m, j] = ( sum_o dy[m,o] wt[j,o]  + (u ? u[m*ldu] * v[j] : 0) ) * (mask ? bit(m,j) : 1)
@@ -86,22 +91,25 @@ int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2
  * (n = number of input columns produced, k = layer outputs), mask: ReLU mask bits of
  * the previous layer's output as written by nerf_linear_fwd (ldmask words per row) or
  * NULL.  m%128==0, n%64==0, k%32==0.  wt_split / wt_split_rows: optional bf16x3 image of
- * wt as for nerf_linear_fwd (K = k).  dy_rmax / dx_rmax: row maxima as x1_rmax / y_rmax of
- * nerf_linear_fwd (mode 2). */
+ * wt as for nerf_linear_fwd (K = k).  dy_rmax / dx_rmax / dx_cmax: row and column maxima as
+ * x1_rmax / y_rmax / y_cmax of nerf_linear_fwd (mode 2). */
 int nerf_linear_bwd_data(const float* dy, int lddy, int k, const float* wt, const uint16_t* wt_split,
                          int wt_split_rows, const float* u, int ldu, const float* v, const uint32_t* mask,
                          int ldmask, float* dx, int lddx, int m, int n, const float* dy_rmax, float* dx_rmax,
-                         void* stream);
+                         float* dx_cmax, void* stream);
 
 /* Backward w.r.t. weight and bias, split over sample rows:
  *   slab[split][o][col0 + j] = sum_{rows of split} dy[row, o] * x[row, j]   (j < kin)
  *   bslab[split][o]          = sum_{rows of split} dy[row, o]   (if bslab != NULL)
  * dy: [m][lddy] (nout columns), x: [m][ldx] (kin columns), slab row stride ldslab.
  * Rows are split into `splits` equal chunks; nout % 64 == 0, kin % 64 == 0,
- * m % (32*splits) == 0. */
+ * m % (32*splits) == 0.  dy_cmax [m/128][nout], x_cmax [m/128][kin] (optional, mode 2): upper
+ * bounds of max |.| per column and 128-row group (as y_cmax of nerf_linear_fwd); given both and
+ * splits of whole 128-row groups, mode 2 runs the fp16 pair kernel (column-scaled operands,
+ * three products), else the bf16x3 one. */
 int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const float* x, int ldx,
                            int kin, int m, int splits, float* slab, int ldslab, int col0,
-                           float* bslab, void* stream);
+                           float* bslab, const float* dy_cmax, const float* x_cmax, void* stream);
 
 /* Recommended `splits` for nerf_linear_bwd_weight at this shape and tile policy. */
 int nerf_linear_bwd_weight_splits(int nout, int kin, int m);
@@ -154,7 +162,9 @@ int nerf_heads_fwd(const float* h8, int ld8, const float* hr, int ldr, int hidde
 int nerf_heads_part_size(int hidden, int n_pad);
 int nerf_heads_bwd(const float* graw4, const float* h8, int ld8, const float* hr, int ldr,
                    int hidden, const float* wc, float* dyr, int lddyr, float* part, int n_pad,
-                   float* dyr_rmax, void* stream);   /* dyr_rmax optional: max |dyr| per row */
+                   float* dyr_rmax, float* dyr_cmax, void* stream);
+/* dyr_rmax (optional): max |dyr| per row; dyr_cmax (optional, [n_pad/128][hidden/2 padded to
+ * 64], n_pad % 128 == 0): max |dyr| per column and 128-row group (mode 2 scales). */
 /* Reduce the heads partials into gwd[hidden], gbd[1], gwc[3][hidden/2], gbc[3]. */
 int nerf_heads_reduce(const float* part, int hidden, int n_pad, float* gwd, float* gbd,
                       float* gwc, float* gbc, int accumulate, void* stream);

@@ -43,9 +43,11 @@ struct NTArgs {
     int ablate;   // diagnostics only (nerf_gemm_debug_ablate): 1 = no epilogue stores, 2 = no K-loop loads
                   // (f32 kernels; the split-bf16 kernels honour 1 only)
     // precision mode 2 (fp16 pair): max |a| per row of each A segment (ar2 may be NULL),
-    // and (optional) the row max of the output written by the epilogue
+    // and (optional) the row max of the output written by the epilogue; c_cmax (optional):
+    // column maxima of the output per 128-row group, [m/128][ldcm]
     const float* ar1; const float* ar2;
     float* c_rmax;
+    float* c_cmax; int ldcm;
 };
 
 // max |a| over row m of the (one or two segment) A operand
@@ -64,6 +66,10 @@ struct TNArgs {
     float* slab; int ldslab; int col0; size_t slab_stride;
     float* bslab; int nout;
     int ablate;   // diagnostics: 1 = no slab stores, 2 = no K-loop loads, 4 = no bias column sums
+    // precision mode 2: column maxima of dy and x per 128-row group ([m/128][ld]); the
+    // fp16 pair kernel scales each split's columns by them
+    const float* cm_dy; int ldcm_dy;
+    const float* cm_x; int ldcm_x;
 };
 
 // Backward-data epilogue operands (ReLU bits, rank-1 column), prefetched into registers
@@ -337,6 +343,25 @@ __device__ __forceinline__ void nt_epilogue_lds(const NTArgs& p, f32x16 (&acc)[T
     }
 }
 
+// One halving step of a max-butterfly over the lanes of a half-wave: lanes whose STEP bit is
+// set keep the upper HALF values, the rest the lower, each merged with its partner's copy;
+// base tracks the first feature index kept.  HALF = 0: no halving, plain exchange.
+template <int HALF, int STEP, int NV>
+__device__ __forceinline__ void bfly_max(float (&v)[NV], int sl, int& base) {
+    const bool bit = (sl & STEP) != 0;
+    if constexpr (HALF >= 1) {
+#pragma unroll
+        for (int t = 0; t < HALF; ++t) {
+            const float keep = bit ? v[t + HALF] : v[t];
+            const float send = bit ? v[t] : v[t + HALF];
+            v[t] = fmaxf(keep, __shfl_xor(send, STEP, 64));
+        }
+        base += bit ? HALF : 0;
+    } else {
+        v[0] = fmaxf(v[0], __shfl_xor(v[0], STEP, 64));
+    }
+}
+
 // Direct NT epilogue for the operand-swapped K loop (the MFMAs compute C^T tiles, so each
 // lane holds one sample row and, per register quad 4q..4q+3, four consecutive output
 // features 8q + 4*(lane>>5) + 0..3): float4 stores straight from the accumulators, no
@@ -352,11 +377,15 @@ template <int TM, int TN, int EPI, bool H = false>
 __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0, int wm0,
                                                    int wn0, uint32_t* lmask = nullptr, int mw = 0,
                                                    const int* leb = nullptr, const int* lea = nullptr,
-                                                   uint32_t* lrm = nullptr) {
+                                                   uint32_t* lrm = nullptr, uint32_t* lcm = nullptr, int lcm_ld = 0) {
     const int lane = lane_id();
     const int sl = lane & 31, hf = lane >> 5;
     int er[TM];
     float rmx[TM];
+    constexpr int NV = 16 * TN;       // this lane's features (j, q, c) -> index 16 j + 4 q + c
+    float cmx[NV];
+#pragma unroll
+    for (int f = 0; f < NV; ++f) cmx[f] = 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
         er[i] = H ? lea[wm0 + 32 * i + sl] : 0;
@@ -372,9 +401,22 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
             acc[i][j][4 * q + 3] = __builtin_amdgcn_ldexpf(acc[i][j][4 * q + 3], -(er[i] + eb.w));
         }
     };
-    auto track = [&](int i, const float4& x) {
-        if constexpr (H)
+    auto track = [&](int i, int j, int q, const float4& x) {
+        if constexpr (H) {
             rmx[i] = fmaxf(rmx[i], fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+            if (lcm) {
+#pragma unroll
+                for (int jj = 0; jj < TN; ++jj)
+#pragma unroll
+                    for (int qq = 0; qq < 4; ++qq)
+                        if (jj == j && qq == q) {
+                            cmx[16 * jj + 4 * qq + 0] = fmaxf(cmx[16 * jj + 4 * qq + 0], fabsf(x.x));
+                            cmx[16 * jj + 4 * qq + 1] = fmaxf(cmx[16 * jj + 4 * qq + 1], fabsf(x.y));
+                            cmx[16 * jj + 4 * qq + 2] = fmaxf(cmx[16 * jj + 4 * qq + 2], fabsf(x.z));
+                            cmx[16 * jj + 4 * qq + 3] = fmaxf(cmx[16 * jj + 4 * qq + 3], fabsf(x.w));
+                        }
+            }
+        }
     };
     if (p.ablate & 1) {
         float t = 0.f;
@@ -406,7 +448,7 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
                     float4 x = make_float4(acc[i][j][4 * q] + b4[q].x, acc[i][j][4 * q + 1] + b4[q].y,
                                            acc[i][j][4 * q + 2] + b4[q].z, acc[i][j][4 * q + 3] + b4[q].w);
                     if (p.relu) x = make_float4(fmaxf(x.x, 0.f), fmaxf(x.y, 0.f), fmaxf(x.z, 0.f), fmaxf(x.w, 0.f));
-                    track(i, x);
+                    track(i, j, q, x);
                     *reinterpret_cast<float4*>(p.c + row * p.ldc + fb + 8 * q) = x;
                     const uint32_t nib = (x.x > 0.f ? 1u : 0u) | (x.y > 0.f ? 2u : 0u) | (x.z > 0.f ? 4u : 0u) |
                                          (x.w > 0.f ? 8u : 0u);
@@ -453,7 +495,7 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
                     x.y = (bits & 2u) ? x.y : 0.f;
                     x.z = (bits & 4u) ? x.z : 0.f;
                     x.w = (bits & 8u) ? x.w : 0.f;
-                    track(i, x);
+                    track(i, j, q, x);
                     *reinterpret_cast<float4*>(p.c + row * p.ldc + fb + 8 * q) = x;
                 }
             }
@@ -467,13 +509,33 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
             const float m = fmaxf(rmx[i], __shfl_xor(rmx[i], 32, 64));
             if (hf == 0) atomicMax(lrm + wm0 + 32 * i + sl, __float_as_uint(m));
         }
+        if (lcm) {
+            // column maxima over this wave's rows: a halving butterfly over the 32 lanes of each
+            // half-wave (xor 16 .. 1) leaves lane sl with features base + t; the waves along M
+            // of one 128-row group meet in LDS
+            int base = 0;
+            bfly_max<NV / 2, 16>(cmx, sl, base);
+            bfly_max<NV / 4, 8>(cmx, sl, base);
+            bfly_max<NV / 8, 4>(cmx, sl, base);
+            bfly_max<NV / 16, 2>(cmx, sl, base);
+            bfly_max<NV / 32, 1>(cmx, sl, base);
+            constexpr int n = NV / 32 > 1 ? NV / 32 : 1;   // features left per lane
+            uint32_t* g = lcm + (wm0 / 128) * lcm_ld;
+#pragma unroll
+            for (int t = 0; t < n; ++t) {
+                const int f = base + t;
+                atomicMax(g + wn0 + 32 * (f >> 4) + 4 * hf + 8 * ((f >> 2) & 3) + (f & 3), __float_as_uint(cmx[t]));
+            }
+        }
     }
 }
 
-// TN epilogue through the LDS writer: float4 slab stores
-template <int TM, int TN>
+// TN epilogue through the LDS writer: float4 slab stores.  H: undo the scales 2^(ea[row] +
+// eb[col]) of the fp16 pair kernel (block-local exponent arrays in LDS).
+template <int TM, int TN, bool H = false>
 __device__ __forceinline__ void tn_store_lds(const TNArgs& p, f32x16 (&acc)[TM][TN], char* smem, int split, int o0,
-                                             int j0, int wm0, int wn0) {
+                                             int j0, int wm0, int wn0, const int* lea = nullptr,
+                                             const int* leb = nullptr) {
     using T = TileLds<TN>;
     if (p.ablate & 1) {
         tn_store(p, acc, split, o0, j0, wm0, wn0);
@@ -482,12 +544,21 @@ __device__ __forceinline__ void tn_store_lds(const TNArgs& p, f32x16 (&acc)[TM][
     float* slab = p.slab + (size_t)split * p.slab_stride;
     float* wlds = reinterpret_cast<float*>(smem + (threadIdx.x >> 6) * T::BYTES);
     write_tile_lds<TM, TN>(acc, wlds, [&](int rl, int c4, float4 v) {
+        if constexpr (H) {
+            const int ea = lea[wm0 + rl];
+            const int4 eb = *reinterpret_cast<const int4*>(leb + wn0 + c4);
+            v.x = __builtin_amdgcn_ldexpf(v.x, -(ea + eb.x));
+            v.y = __builtin_amdgcn_ldexpf(v.y, -(ea + eb.y));
+            v.z = __builtin_amdgcn_ldexpf(v.z, -(ea + eb.z));
+            v.w = __builtin_amdgcn_ldexpf(v.w, -(ea + eb.w));
+        }
         *reinterpret_cast<float4*>(slab + (size_t)(o0 + wm0 + rl) * p.ldslab + p.col0 + j0 + wn0 + c4) = v;
     });
 }
 
 // split-bf16 launchers (gemm_x6.hip); policy as nerf_gemm_set_policy
 int dispatch_nt_x6(const NTArgs& a, int epi, int policy, hipStream_t s, double flops, bool h16 = false);
-int dispatch_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, hipStream_t s, double flops);
+int dispatch_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, hipStream_t s, double flops,
+                   bool h16 = false);
 
 }  // namespace nerf

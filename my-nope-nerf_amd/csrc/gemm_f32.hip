@@ -373,7 +373,8 @@ static int check_nt(const NTArgs& a, const char* fn) {
 extern "C" int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2, int k2,
                                const float* w, const uint16_t* w_split, int w_split_rows, const float* bias,
                                float* y, int ldy, int m, int n, int relu, uint32_t* mask_out, int ldmo,
-                               const float* x1_rmax, const float* x2_rmax, float* y_rmax, void* stream) {
+                               const float* x1_rmax, const float* x2_rmax, float* y_rmax, float* y_cmax,
+                               void* stream) {
     NTArgs a{};
     a.a1 = x1; a.lda1 = ldx1; a.k1 = k1;
     a.a2 = x2; a.lda2 = x2 ? ldx2 : 0; a.k2 = x2 ? k2 : 0;
@@ -382,6 +383,7 @@ extern "C" int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x
     a.bias = bias; a.c = y; a.ldc = ldy; a.m = m; a.n = n; a.relu = relu;
     a.mask_out = mask_out; a.ldmo = ldmo;
     a.ar1 = x1_rmax; a.ar2 = x2 ? x2_rmax : nullptr; a.c_rmax = y_rmax;
+    a.c_cmax = y_cmax; a.ldcm = n;
     int rc = check_nt(a, __func__);
     if (rc) return rc;
     NERF_CHECK(mask_out == nullptr || ldmo >= n / 32, "%s: ldmo=%d < n/32", __func__, ldmo);
@@ -392,7 +394,8 @@ extern "C" int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x
 extern "C" int nerf_linear_bwd_data(const float* dy, int lddy, int k, const float* wt,
                                     const uint16_t* wt_split, int wt_split_rows, const float* u, int ldu,
                                     const float* v, const uint32_t* mask, int ldmask, float* dx, int lddx,
-                                    int m, int n, const float* dy_rmax, float* dx_rmax, void* stream) {
+                                    int m, int n, const float* dy_rmax, float* dx_rmax, float* dx_cmax,
+                                    void* stream) {
     NTArgs a{};
     a.a1 = dy; a.lda1 = lddy; a.k1 = k;
     a.a2 = nullptr; a.lda2 = 0; a.k2 = 0;
@@ -400,6 +403,7 @@ extern "C" int nerf_linear_bwd_data(const float* dy, int lddy, int k, const floa
     a.bs = wt_split; a.bs_rows = wt_split_rows;
     a.u = u; a.ldu = ldu; a.v = v; a.mask = mask; a.ldmask = ldmask;
     a.ar1 = dy_rmax; a.c_rmax = dx_rmax;
+    a.c_cmax = dx_cmax; a.ldcm = n;
     a.c = dx; a.ldc = lddx; a.m = m; a.n = n;
     int rc = check_nt(a, __func__);
     if (rc) return rc;
@@ -411,7 +415,7 @@ extern "C" int nerf_linear_bwd_data(const float* dy, int lddy, int k, const floa
 
 extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const float* x, int ldx,
                                       int kin, int m, int splits, float* slab, int ldslab, int col0,
-                                      float* bslab, void* stream) {
+                                      float* bslab, const float* dy_cmax, const float* x_cmax, void* stream) {
     NERF_CHECK_PTR(dy);
     NERF_CHECK_PTR(x);
     NERF_CHECK_PTR(slab);
@@ -428,10 +432,14 @@ extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const
     a.slab = slab; a.ldslab = ldslab; a.col0 = col0; a.slab_stride = (size_t)nout * ldslab;
     a.bslab = bslab; a.nout = nout;
     a.ablate = g_ablate >> 4;
+    a.cm_dy = dy_cmax; a.ldcm_dy = nout; a.cm_x = x_cmax; a.ldcm_x = kin;
+    // mode 2 runs the fp16 pair kernel when the column maxima are there and every split is
+    // whole 128-row groups; otherwise the bf16x3 kernel (it needs no scales)
+    const bool h16 = g_precision == 2 && dy_cmax && x_cmax && (m / splits) % 128 == 0;
     hipStream_t s = as_stream(stream);
     const double fl = 2.0 * m * nout * (double)kin;
     const int pol = g_tn_policy ? g_tn_policy : 3;
-    if (g_precision >= 1) return dispatch_tn_x6(a, nout, kin, splits, pol, s, fl);   // mode 2: bf16x6 dW
+    if (g_precision >= 1) return dispatch_tn_x6(a, nout, kin, splits, pol, s, fl, h16);
     prof_begin(s);
     if (pol == 3 && nout % 256 == 0 && kin % 256 == 0) {
         dim3 grid(nout / 256, kin / 256, splits);

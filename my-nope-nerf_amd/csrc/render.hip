@@ -83,13 +83,15 @@ __global__ __launch_bounds__(256) void k_encode_samples(const float* __restrict_
                                  int R, int S, int n_pad, float nz, float fz,
                                  float* __restrict__ z_out, float* __restrict__ enc_p,
                                  float* __restrict__ enc_d, float* __restrict__ rmax_p,
-                                 float* __restrict__ rmax_d) {
+                                 float* __restrict__ rmax_d, float* __restrict__ cmax_p,
+                                 float* __restrict__ cmax_d) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n_pad) return;
     const int total = R * S;
     float* rp = enc_p + (size_t)s * ENC_P;
     float* rd = enc_d + (size_t)s * ENC_D;
-    if (s < total) {
+    float ax[3] = {0.f, 0.f, 0.f}, av[3] = {0.f, 0.f, 0.f};   // |coordinates| (column bounds)
+    if (s >= n_pad) {
+    } else if (s < total) {
         const int r = s / S, i = s - r * S;
         float z = lerp_z(linspace01(i, S), nz, fz);
         if (noise != nullptr) {  // rendering.py:187-191
@@ -105,6 +107,8 @@ __global__ __launch_bounds__(256) void k_encode_samples(const float* __restrict_
         }
         const float mp = encode3<10, ENC_P>(x, rp);
         const float md = encode3<4, ENC_D>(v, rd);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { ax[c] = fabsf(x[c]); av[c] = fabsf(v[c]); }
         z_out[s] = z;
         if (rmax_p) rmax_p[s] = mp;
         if (rmax_d) rmax_d[s] = md;
@@ -118,6 +122,38 @@ __global__ __launch_bounds__(256) void k_encode_samples(const float* __restrict_
         if (rmax_p) rmax_p[s] = 0.f;
         if (rmax_d) rmax_d[s] = 0.f;
     }
+    if (cmax_p != nullptr) {
+        // per 128-row group: exact max of the coordinate columns (wave max, then the group's
+        // two waves in LDS), 1 for the sin / cos columns (|sin|, |cos| <= 1), 0 for the pad
+        __shared__ float wm[4][6];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                ax[c] = fmaxf(ax[c], __shfl_xor(ax[c], off, 64));
+                av[c] = fmaxf(av[c], __shfl_xor(av[c], off, 64));
+            }
+        }
+        const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+        if (l == 0)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { wm[w][c] = ax[c]; wm[w][3 + c] = av[c]; }
+        __syncthreads();
+        const size_t grp = (size_t)blockIdx.x * 2 + (w >> 1);
+        if ((w & 1) == 0 && grp * 128 < (size_t)n_pad) {
+            const int w0 = w & ~1;
+            float vp, vd;
+            if (l < 3) {
+                vp = fmaxf(wm[w0][l], wm[w0 + 1][l]);
+                vd = fmaxf(wm[w0][3 + l], wm[w0 + 1][3 + l]);
+            } else {
+                vp = l < 63 ? 1.f : 0.f;
+                vd = l < 27 ? 1.f : 0.f;
+            }
+            cmax_p[grp * ENC_P + l] = vp;
+            cmax_d[grp * ENC_D + l] = vd;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -126,7 +162,9 @@ __global__ __launch_bounds__(256) void k_encode_samples(const float* __restrict_
 // halving butterfly (17 shuffles for 16 samples) that leaves the total of sample
 // (lane >> 2) in every lane.
 // ---------------------------------------------------------------------------
+template <bool MAX = false>
 __device__ __forceinline__ float reduce16(float (&v)[16]) {
+    auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : a + b; };
     const int lane = lane_id();
     float w8[8], w4[4], w2[2];
     {
@@ -135,7 +173,7 @@ __device__ __forceinline__ float reduce16(float (&v)[16]) {
         for (int j = 0; j < 8; ++j) {
             const float keep = h ? v[j + 8] : v[j];
             const float send = h ? v[j] : v[j + 8];
-            w8[j] = keep + __shfl_xor(send, 32, 64);
+            w8[j] = op(keep, __shfl_xor(send, 32, 64));
         }
     }
     {
@@ -144,7 +182,7 @@ __device__ __forceinline__ float reduce16(float (&v)[16]) {
         for (int j = 0; j < 4; ++j) {
             const float keep = h ? w8[j + 4] : w8[j];
             const float send = h ? w8[j] : w8[j + 4];
-            w4[j] = keep + __shfl_xor(send, 16, 64);
+            w4[j] = op(keep, __shfl_xor(send, 16, 64));
         }
     }
     {
@@ -153,13 +191,13 @@ __device__ __forceinline__ float reduce16(float (&v)[16]) {
         for (int j = 0; j < 2; ++j) {
             const float keep = h ? w4[j + 2] : w4[j];
             const float send = h ? w4[j] : w4[j + 2];
-            w2[j] = keep + __shfl_xor(send, 8, 64);
+            w2[j] = op(keep, __shfl_xor(send, 8, 64));
         }
     }
     const bool h = (lane >> 2) & 1;
-    float w = (h ? w2[1] : w2[0]) + __shfl_xor(h ? w2[0] : w2[1], 4, 64);
-    w += __shfl_xor(w, 2, 64);
-    w += __shfl_xor(w, 1, 64);
+    float w = op(h ? w2[1] : w2[0], __shfl_xor(h ? w2[0] : w2[1], 4, 64));
+    w = op(w, __shfl_xor(w, 2, 64));
+    w = op(w, __shfl_xor(w, 1, 64));
     return w;
 }
 
@@ -221,7 +259,7 @@ __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ gra
                                                    const float* __restrict__ wc,
                                                    float* __restrict__ dyr, int lddyr,
                                                    float* __restrict__ part, int n_pad,
-                                                   float* __restrict__ dyr_rmax) {
+                                                   float* __restrict__ dyr_rmax, float* __restrict__ dyr_cmax) {
     constexpr int H = 64 * NH, HR = 64 * NR, PART = H + 3 * HR + 4;
     __shared__ float red[4][PART];
     const int lane = lane_id();
@@ -241,9 +279,16 @@ __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ gra
 #pragma unroll
         for (int q = 0; q < NR; ++q) awc[c][q] = 0.f;
 
-    for (int g = gwave; g * 16 < n_pad; g += nwaves) {
+    // each wave walks whole 128-row chunks (8 groups of 16 samples) so that the column
+    // maxima of dyr (mode 2 scales) come out per chunk without atomics
+    for (int ch = gwave; ch * 128 < n_pad; ch += nwaves) {
+      float cm[NR];
+#pragma unroll
+      for (int q = 0; q < NR; ++q) cm[q] = 0.f;
+      for (int g = ch * 8; g < ch * 8 + 8 && g * 16 < n_pad; ++g) {
         const size_t s0 = (size_t)g * 16;
-#pragma unroll 4
+        float dm[16];   // this lane's max |dyr| per sample of the group
+#pragma unroll
         for (int t = 0; t < 16; ++t) {
             const size_t s = s0 + t;
             const float4 gr = *reinterpret_cast<const float4*>(graw4 + 4 * s);
@@ -257,18 +302,23 @@ __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ gra
                 d = x > 0.f ? d : 0.f;
                 dyr[s * lddyr + lane + 64 * q] = d;
                 dmax = fmaxf(dmax, fabsf(d));
+                cm[q] = fmaxf(cm[q], fabsf(d));
                 awc[0][q] += gr.y * x;
                 awc[1][q] += gr.z * x;
                 awc[2][q] += gr.w * x;
             }
-            if (dyr_rmax) {   // row max of dyr (row scale of GEMM precision mode 2)
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, off, 64));
-                if (lane == 0) dyr_rmax[s] = dmax;
-            }
+            dm[t] = dmax;
             abd += gr.x;
             abc[0] += gr.y; abc[1] += gr.z; abc[2] += gr.w;
         }
+        if (dyr_rmax) {   // row maxima of dyr (row scales of GEMM precision mode 2): one butterfly per group
+            const float m = reduce16<true>(dm);
+            if ((lane & 3) == 0) dyr_rmax[s0 + (lane >> 2)] = m;
+        }
+      }
+      if (dyr_cmax)
+#pragma unroll
+        for (int q = 0; q < NR; ++q) dyr_cmax[(size_t)ch * HR + lane + 64 * q] = cm[q];
     }
     float* rw = red[wave];
 #pragma unroll
@@ -853,16 +903,19 @@ using namespace nerf;
 extern "C" int nerf_encode_samples(const float* pts_o, const float* pts_d, const float* view,
                                    const float* noise, int n_rays, int n_samples, int n_pad,
                                    float near_z, float far_z, float* z, float* enc_p, float* enc_d,
-                                   float* enc_p_rmax, float* enc_d_rmax, void* stream) {
+                                   float* enc_p_rmax, float* enc_d_rmax, float* enc_p_cmax, float* enc_d_cmax,
+                                   void* stream) {
     NERF_CHECK_PTR(pts_o); NERF_CHECK_PTR(pts_d); NERF_CHECK_PTR(view);
     NERF_CHECK_PTR(z); NERF_CHECK_PTR(enc_p); NERF_CHECK_PTR(enc_d);
+    NERF_CHECK((enc_p_cmax == nullptr) == (enc_d_cmax == nullptr) && (enc_p_cmax == nullptr || n_pad % 128 == 0),
+               "%s: enc_p_cmax / enc_d_cmax go together and need n_pad %% 128 == 0", __func__);
     NERF_CHECK_ALIGN16(enc_p); NERF_CHECK_ALIGN16(enc_d);
     NERF_CHECK(n_rays > 0 && n_samples > 0 && (int64_t)n_rays * n_samples <= n_pad,
                "%s: n_pad=%d < R*S=%lld", __func__, n_pad, (long long)n_rays * n_samples);
     const int blocks = (n_pad + 255) / 256;
     hipLaunchKernelGGL(k_encode_samples, dim3(blocks), dim3(256), 0, as_stream(stream), pts_o, pts_d,
                        view, noise, n_rays, n_samples, n_pad, near_z, far_z, z, enc_p, enc_d, enc_p_rmax,
-                       enc_d_rmax);
+                       enc_d_rmax, enc_p_cmax, enc_d_cmax);
     return check_launch(__func__);
 }
 
@@ -902,22 +955,23 @@ extern "C" int nerf_heads_part_size(int hidden, int n_pad) {
 
 extern "C" int nerf_heads_bwd(const float* graw4, const float* h8, int ld8, const float* hr, int ldr,
                               int hidden, const float* wc, float* dyr, int lddyr, float* part,
-                              int n_pad, float* dyr_rmax, void* stream) {
+                              int n_pad, float* dyr_rmax, float* dyr_cmax, void* stream) {
     NERF_CHECK_PTR(graw4); NERF_CHECK_PTR(h8); NERF_CHECK_PTR(hr); NERF_CHECK_PTR(wc);
     NERF_CHECK_PTR(dyr); NERF_CHECK_PTR(part);
     NERF_CHECK_ALIGN16(graw4);
     NERF_CHECK(n_pad % 16 == 0, "%s: n_pad %% 16 != 0", __func__);
+    NERF_CHECK(dyr_cmax == nullptr || n_pad % 128 == 0, "%s: dyr_cmax needs n_pad %% 128 == 0", __func__);
     const int hrw = hidden / 2 < 64 ? 64 : hidden / 2;
     hipStream_t s = as_stream(stream);
     dim3 g(heads_blocks(n_pad)), b(256);
     if (hidden == 256 && hrw == 128)
-        hipLaunchKernelGGL((k_heads_bwd<4, 2>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax);
+        hipLaunchKernelGGL((k_heads_bwd<4, 2>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax);
     else if (hidden == 128 && hrw == 64)
-        hipLaunchKernelGGL((k_heads_bwd<2, 1>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax);
+        hipLaunchKernelGGL((k_heads_bwd<2, 1>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax);
     else if (hidden == 64 && hrw == 64)
-        hipLaunchKernelGGL((k_heads_bwd<1, 1>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax);
+        hipLaunchKernelGGL((k_heads_bwd<1, 1>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax);
     else if (hidden == 512 && hrw == 256)
-        hipLaunchKernelGGL((k_heads_bwd<8, 4>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax);
+        hipLaunchKernelGGL((k_heads_bwd<8, 4>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax);
     else
         NERF_CHECK(false, "%s: unsupported hidden width %d (64/128/256/512)", __func__, hidden);
     return check_launch(__func__);

@@ -43,17 +43,18 @@ _SIGS = {
     "nerf_hip_abi_version": ([], _c_i),
     "nerf_hip_last_error": ([], ctypes.c_char_p),
     "nerf_encode_samples": ([_c_p, _c_p, _c_p, _c_p, _c_i, _c_i, _c_i, _c_f, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
-                             _c_p], _c_i),
+                             _c_p, _c_p, _c_p], _c_i),
     "nerf_linear_fwd": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_p, _c_i, _c_i, _c_i, _c_i,
-                         _c_p, _c_i, _c_p, _c_p, _c_p, _c_p], _c_i),
+                         _c_p, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_linear_bwd_data": ([_c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_i,
-                              _c_i, _c_p, _c_p, _c_p], _c_i),
-    "nerf_linear_bwd_weight": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p], _c_i),
+                              _c_i, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_linear_bwd_weight": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p,
+                                _c_p], _c_i),
     "nerf_linear_bwd_weight_splits": ([_c_i, _c_i, _c_i], _c_i),
     "nerf_slab_reduce": ([_c_p, _c_i, _c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_heads_fwd": ([_c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_heads_part_size": ([_c_i, _c_i], _c_i),
-    "nerf_heads_bwd": ([_c_p, _c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_p, _c_p], _c_i),
+    "nerf_heads_bwd": ([_c_p, _c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_p, _c_p, _c_p], _c_i),
     "nerf_heads_reduce": ([_c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_composite_fwd": ([_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_composite_bwd": ([_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
@@ -141,12 +142,13 @@ def _ld(t: torch.Tensor) -> int:
 
 # --------------------------------------------------------------------------------------
 def encode_samples(pts_o, pts_d, view, noise, n_rays, n_samples, n_pad, near, far, z, enc_p, enc_d,
-                   enc_p_rmax=None, enc_d_rmax=None):
+                   enc_p_rmax=None, enc_d_rmax=None, enc_p_cmax=None, enc_d_cmax=None):
     """enc_p_rmax / enc_d_rmax: optional [n_pad] outputs, max |.| per encoding row (the row
-    scales GEMM precision mode 2 needs)."""
+    scales GEMM precision mode 2 needs); enc_p_cmax / enc_d_cmax: optional [n_pad/128][64]
+    column bounds per 128-row group (its column scales)."""
     _call("nerf_encode_samples", _ptr(pts_o), _ptr(pts_d), _ptr(view), _ptr(noise), n_rays, n_samples,
           n_pad, float(near), float(far), _ptr(z), _ptr(enc_p), _ptr(enc_d), _ptr(enc_p_rmax), _ptr(enc_d_rmax),
-          _stream())
+          _ptr(enc_p_cmax), _ptr(enc_d_cmax), _stream())
 
 
 def _split_args(ws):
@@ -165,28 +167,33 @@ def split_image(rows: int, k: int, device) -> "torch.Tensor":
 
 
 def linear_fwd(x1, k1, x2, k2, w, bias, y, m, n, relu, mask_out=None, w_split=None, x1_rmax=None, x2_rmax=None,
-               y_rmax=None):
+               y_rmax=None, y_cmax=None):
     """mask_out: int32 [m][n/32] ReLU mask bits of y (optional).  w_split: optional split
     image of w (used by GEMM precision modes 1 and 2).  x1_rmax / x2_rmax: max |x| per row of
-    each input segment (required in mode 2); y_rmax: optional [m] output, max |y| per row."""
+    each input segment (required in mode 2); y_rmax: optional [m] output, max |y| per row;
+    y_cmax: optional [m/128][n] output, max |y| per column and 128-row group (mode 2)."""
     wsp, wsr = _split_args(w_split)
     _call("nerf_linear_fwd", _ptr(x1), _ld(x1), k1, _ptr(x2), _ld(x2) if x2 is not None else 0, k2,
           _ptr(w), wsp, wsr, _ptr(bias), _ptr(y), _ld(y), m, n, int(relu), _ptr(mask_out),
-          _ld(mask_out) if mask_out is not None else 0, _ptr(x1_rmax), _ptr(x2_rmax), _ptr(y_rmax), _stream())
+          _ld(mask_out) if mask_out is not None else 0, _ptr(x1_rmax), _ptr(x2_rmax), _ptr(y_rmax), _ptr(y_cmax),
+          _stream())
 
 
 def linear_bwd_data(dy, k, wt, dx, m, n, mask=None, u=None, ldu=1, v=None, wt_split=None, dy_rmax=None,
-                    dx_rmax=None):
-    """mask: int32 ReLU mask bits [m][words] from linear_fwd(mask_out=...).  dy_rmax / dx_rmax:
-    row maxima as x1_rmax / y_rmax of linear_fwd."""
+                    dx_rmax=None, dx_cmax=None):
+    """mask: int32 ReLU mask bits [m][words] from linear_fwd(mask_out=...).  dy_rmax / dx_rmax /
+    dx_cmax: row and column maxima as x1_rmax / y_rmax / y_cmax of linear_fwd."""
     wsp, wsr = _split_args(wt_split)
     _call("nerf_linear_bwd_data", _ptr(dy), _ld(dy), k, _ptr(wt), wsp, wsr, _ptr(u), int(ldu), _ptr(v), _ptr(mask),
-          _ld(mask) if mask is not None else 0, _ptr(dx), _ld(dx), m, n, _ptr(dy_rmax), _ptr(dx_rmax), _stream())
+          _ld(mask) if mask is not None else 0, _ptr(dx), _ld(dx), m, n, _ptr(dy_rmax), _ptr(dx_rmax), _ptr(dx_cmax),
+          _stream())
 
 
-def linear_bwd_weight(dy, nout, x, kin, m, splits, slab, ldslab, col0, bslab):
+def linear_bwd_weight(dy, nout, x, kin, m, splits, slab, ldslab, col0, bslab, dy_cmax=None, x_cmax=None):
+    """dy_cmax [m/128][nout] / x_cmax [m/128][kin]: column bounds per 128-row group; with both,
+    precision mode 2 runs the fp16 pair kernel."""
     _call("nerf_linear_bwd_weight", _ptr(dy), _ld(dy), nout, _ptr(x), _ld(x), kin, m, splits,
-          _ptr(slab), ldslab, col0, _ptr(bslab), _stream())
+          _ptr(slab), ldslab, col0, _ptr(bslab), _ptr(dy_cmax), _ptr(x_cmax), _stream())
 
 
 def bwd_weight_splits(nout, kin, m) -> int:
@@ -207,9 +214,9 @@ def heads_part_size(hidden, n_pad) -> int:
     return int(lib().nerf_heads_part_size(hidden, n_pad))
 
 
-def heads_bwd(graw4, h8, hr, hidden, wc, dyr, part, n_pad, dyr_rmax=None):
+def heads_bwd(graw4, h8, hr, hidden, wc, dyr, part, n_pad, dyr_rmax=None, dyr_cmax=None):
     _call("nerf_heads_bwd", _ptr(graw4), _ptr(h8), _ld(h8), _ptr(hr), _ld(hr), hidden, _ptr(wc), _ptr(dyr),
-          _ld(dyr), _ptr(part), n_pad, _ptr(dyr_rmax), _stream())
+          _ld(dyr), _ptr(part), n_pad, _ptr(dyr_rmax), _ptr(dyr_cmax), _stream())
 
 
 def heads_reduce(part, hidden, n_pad, gwd, gbd, gwc, gbc, accumulate=False):

@@ -139,10 +139,11 @@ class FieldRunner:
         enc_p = e(Np, _hip.ENC_P)
         enc_d = e(Np, _hip.ENC_D)
         # precision mode 2: every GEMM A operand travels with its row max (written by its producer)
-        rm = self._rmax_alloc(Np, dev)
+        rm, cm = self._rmax_alloc(Np, dev), self._cmax_alloc(Np, dev, keep)
         enc_p_rm, enc_d_rm = rm(64), rm(64)
+        enc_p_cm, enc_d_cm = cm(64), cm(64)
         _hip.encode_samples(pts_o, pts_d, view, noise, R, S, Np, near, far, z, enc_p, enc_d,
-                            enc_p_rmax=enc_p_rm, enc_d_rmax=enc_d_rm)
+                            enc_p_rmax=enc_p_rm, enc_d_rmax=enc_d_rm, enc_p_cmax=enc_p_cm, enc_d_cmax=enc_d_cm)
         acts = []
         if keep:
             outs = [e(Np, D) for _ in range(9)] + [e(Np, HR)]
@@ -154,6 +155,7 @@ class FieldRunner:
         segs = {"enc_p": enc_p, "enc_d": enc_d}
         seg_rm = {"enc_p": enc_p_rm, "enc_d": enc_d_rm}
         masks = {}
+        cmaxes = {"enc_p": enc_p_cm, "enc_d": enc_d_cm}
         for i, l in enumerate(self.layers):
             y = outs[i]
             x2 = segs[l.seg2] if l.seg2 else None
@@ -163,9 +165,11 @@ class FieldRunner:
                 mo = torch.empty(Np, l.out_p // 32, device=dev, dtype=torch.int32)
                 masks[l.name] = mo
             y_rm = rm(l.out_p)
+            y_cm = cm(l.out_p) if l.name != "lr" else None     # hr feeds no weight gradient GEMM
+            cmaxes[l.name] = y_cm
             _hip.linear_fwd(x, k1, x2, _hip.ENC_P if x2 is not None else 0, self.w[l.name], self.bias(l), y,
                             Np, l.out_p, l.relu, mask_out=mo, w_split=self.ws[l.name] if self.split else None,
-                            x1_rmax=x_rm, x2_rmax=seg_rm[l.seg2] if l.seg2 else None, y_rmax=y_rm)
+                            x1_rmax=x_rm, x2_rmax=seg_rm[l.seg2] if l.seg2 else None, y_rmax=y_rm, y_cmax=y_cm)
             acts.append(y)
             x = y
             x_rm = y_rm
@@ -185,7 +189,7 @@ class FieldRunner:
         state = None
         if keep:
             state = dict(R=R, S=S, Np=Np, flags=flags, z=z, enc_p=enc_p, enc_d=enc_d, acts=acts, raw4=raw4,
-                         masks=masks, pts_o=pts_o, pts_d=pts_d, view=view)
+                         masks=masks, pts_o=pts_o, pts_d=pts_d, view=view, cmaxes=cmaxes)
         return rgb, dist, alpha, z[:N].view(R, S), state
 
     def _rmax_alloc(self, Np: int, dev):
@@ -195,6 +199,13 @@ class FieldRunner:
         if not self.h16:
             return lambda width: None
         return lambda width: (torch.zeros if width > 256 else torch.empty)(Np, device=dev, dtype=torch.float32)
+
+    def _cmax_alloc(self, Np: int, dev, keep: bool = True):
+        """Column-max buffer factory (mode 2, training only): [Np/128][width] per 128-row
+        group, the column scales of the weight-gradient GEMMs."""
+        if not (self.h16 and keep):
+            return lambda width: None
+        return lambda width: torch.empty(Np // 128, width, device=dev, dtype=torch.float32)
 
     # ------------------------------------------------------------------ backward
     def param_list(self) -> List[torch.nn.Parameter]:
@@ -225,9 +236,12 @@ class FieldRunner:
         # heads: d(fc_density), d(fc_rgb), dY of the colour layer
         dyr = e(Np, HR)
         part = e(_hip.heads_part_size(D, Np))
-        rm = self._rmax_alloc(Np, dev)
-        dy_rm = rm(HR)
-        _hip.heads_bwd(graw4, h["l7"], h["lr"], D, self.wc, dyr, part, Np, dyr_rmax=dy_rm)
+        rm, cm = self._rmax_alloc(Np, dev), self._cmax_alloc(Np, dev)
+        dy_rm, dy_cm = rm(HR), cm(HR)
+        _hip.heads_bwd(graw4, h["l7"], h["lr"], D, self.wc, dyr, part, Np, dyr_rmax=dy_rm, dyr_cmax=dy_cm)
+        fcm = st.get("cmaxes", {})
+        prev_cm = {"l0": "enc_p", "l1": "l0", "l2": "l1", "l3": "l2", "l4": "l3", "l5": "l4", "l6": "l5",
+                   "l7": "l6", "lf": "l7", "lr": "lf"}
         gwc = G(m.fc_rgb.weight) if HR == D // 2 else e(3, HR)
         _hip.heads_reduce(part, D, Np, G(m.fc_density.weight), G(m.fc_density.bias), gwc, G(m.fc_rgb.bias))
         if HR != D // 2:
@@ -264,13 +278,17 @@ class FieldRunner:
             ev.record(main)
             side.wait_event(ev)
             dy.record_stream(side)          # dy_l is freed by the main loop while side reads it
+            if dy_cm is not None:
+                dy_cm.record_stream(side)
             with torch.cuda.stream(side):
                 splits = _hip.bwd_weight_splits(l.out_p, k1, Np)
                 slab = e(splits * l.out_p * l.kp)
                 bslab = e(splits * l.out_p)
-                _hip.linear_bwd_weight(dy, l.out_p, x_in, k1, Np, splits, slab, l.kp, 0, bslab)
+                _hip.linear_bwd_weight(dy, l.out_p, x_in, k1, Np, splits, slab, l.kp, 0, bslab, dy_cmax=dy_cm,
+                                       x_cmax=fcm.get(prev_cm[name]))
                 if l.seg2:
-                    _hip.linear_bwd_weight(dy, l.out_p, seg_buf[l.seg2], 64, Np, splits, slab, l.kp, k1, None)
+                    _hip.linear_bwd_weight(dy, l.out_p, seg_buf[l.seg2], 64, Np, splits, slab, l.kp, k1, None,
+                                           dy_cmax=dy_cm, x_cmax=fcm.get(l.seg2))
                 gb = G(l.linear.bias) if l.out_p == nout_ref else e(l.out_p)
                 gw = G(W)
                 _hip.slab_reduce(slab, splits, l.out_p, l.kp, nout_ref, kin_ref, bslab, gw, gb)
@@ -291,17 +309,18 @@ class FieldRunner:
                 _hip.linear_bwd_data(dy, l.out_p, wt[k1:k1 + 64], genc[key], Np, 64, wt_split=rows(k1, k1 + 64),
                                      dy_rmax=dy_rm)
             dx = e(Np, k1)
-            dx_rm = rm(k1)
+            dx_rm, dx_cm = rm(k1), cm(k1)
             # ReLU bits of this layer's input (f, the input of lr, has no activation)
             mask = None if name == "lr" else st["masks"][prev_name[name]]
             if name == "lf":   # + density path: d sigma_raw (graw4[:,0]) x w_density
                 _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask, u=graw4, ldu=4,
-                                     v=m.fc_density.weight, wt_split=rows(0, k1), dy_rmax=dy_rm, dx_rmax=dx_rm)
+                                     v=m.fc_density.weight, wt_split=rows(0, k1), dy_rmax=dy_rm, dx_rmax=dx_rm,
+                                     dx_cmax=dx_cm)
             else:
                 _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask, wt_split=rows(0, k1),
-                                     dy_rmax=dy_rm, dx_rmax=dx_rm)
+                                     dy_rmax=dy_rm, dx_rmax=dx_rm, dx_cmax=dx_cm)
             dy = dx
-            dy_rm = dx_rm
+            dy_rm, dy_cm = dx_rm, dx_cm
 
         done = torch.cuda.Event()
         done.record(side)

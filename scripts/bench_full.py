@@ -55,6 +55,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--gemm-precision", choices=["f32", "bf16x6", "f16x3"], default="f16x3")
     args = ap.parse_args()
     import model as mdl
     from model import _hip
@@ -62,7 +63,7 @@ def main():
     from tests.helpers import make_cfg
     dev = torch.device("cuda", 0)
     _hip.load_library()
-    _hip.gemm_set_precision(1)
+    _hip.gemm_set_precision({"f32": 0, "bf16x6": 1, "f16x3": 2}[args.gemm_precision])
     cfg = make_cfg(hidden=HIDDEN, S=SAMPLES)
     t = cfg["training"]
     t["n_training_points"] = RAYS
@@ -97,7 +98,7 @@ def main():
     out = {"metric": "full NoPe-NeRF training rays/sec (config 3: pose + distortion + pc + rgb_s losses)",
            "value": RAYS * args.steps / el, "unit": "rays/s", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": 1e3 * el / args.steps, "dtype": "f32",
-           "gemm_arithmetic": "bf16x6", "data": "synthetic two-view V_KITTI-shaped scene",
+           "gemm_arithmetic": args.gemm_precision, "data": "synthetic two-view V_KITTI-shaped scene",
            "config": {"workload": "config 3: 188x621, 1024 rays x 128 samples, D=256, pose+distortion learned, "
                                   "pc chamfer 7285 points, rgb_s reprojection"},
            "losses": {k: float(ld[k].detach()) for k in ("loss", "loss_rgb", "loss_depth", "loss_pc", "loss_rgb_s")},

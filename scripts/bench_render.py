@@ -28,7 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--gemm-precision", choices=["f32", "bf16x6"], default="bf16x6")
+    ap.add_argument("--gemm-precision", choices=["f32", "bf16x6", "f16x3"], default="f16x3")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -45,7 +45,7 @@ def main():
     from oracle.nerf_oracle import arange_pixels   # pixel grid formula only (common.py:13-40)
     from tests.helpers import camera_K, make_cfg, rigid_c2w
     _hip.load_library()
-    _hip.gemm_set_precision(1 if args.gemm_precision == "bf16x6" else 0)
+    _hip.gemm_set_precision({"f32": 0, "bf16x6": 1, "f16x3": 2}[args.gemm_precision])
     cfg = make_cfg(hidden=HIDDEN, S=S)
     torch.manual_seed(42)
     net = OfficialStaticNerf(cfg).to(dev)

@@ -57,6 +57,7 @@ def main():
     im = lambda i: imgs[max(1, _hip.gemm_get_precision())][i]
     # row maxima of the A operands (mode 2 only; the other modes ignore them)
     x_rm, enc_rm, dy_rm = x.abs().amax(1), enc.abs().amax(1), dy.abs().amax(1)
+    x_cm, dy_cm = x.abs().view(M // 128, 128, D).amax(1), dy.abs().view(M // 128, 128, D).amax(1)
     y_rm = torch.empty(M, device=dev)
     cases = {}
     # split images are passed everywhere; the exact-f32 mode ignores them
@@ -71,7 +72,12 @@ def main():
         slab = torch.empty(sp * D * D, device=dev)
         bslab = torch.empty(sp * D, device=dev)
         cases[f"dW splits={sp}"] = ((lambda sp=sp, slab=slab, bslab=bslab:
-                                     _hip.linear_bwd_weight(dy, D, x, D, M, sp, slab, D, 0, bslab)), 2 * M * D * D)
+                                     _hip.linear_bwd_weight(dy, D, x, D, M, sp, slab, D, 0, bslab, dy_cmax=dy_cm,
+                                                            x_cmax=x_cm)), 2 * M * D * D)
+    slab = torch.rand(256 * D * D, device=dev, generator=g)
+    bslab = torch.rand(256 * D, device=dev, generator=g)
+    gw, gb = torch.empty(D, D, device=dev), torch.empty(D, device=dev)
+    cases["slab_reduce 256"] = (lambda: _hip.slab_reduce(slab, 256, D, D, D, D, bslab, gw, gb), 0)
     if "--x6" in sys.argv:
         _hip.gemm_set_precision(1)
     if "--h16" in sys.argv:
@@ -136,7 +142,8 @@ def main():
         for (name, prec), v in sorted(res.items()):
             fl = cases[name][1]
             best = min(v)
-            print(f"{name:22s} precision {prec}: {best:8.1f} us  {fl / best / 1e6:6.1f} TF/s (f32-equivalent)")
+            print(f"{name:22s} precision {prec}: {best:8.1f} us  {fl / best / 1e6:6.1f} TF/s (f32-equivalent)"
+                  + (f"  {4 * 257 * D * D / best / 1e3:6.0f} GB/s" if fl == 0 else ""))
         return
     res = {}
     for rnd in range(3):

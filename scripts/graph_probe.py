@@ -17,7 +17,7 @@ def main():
     dev = torch.device("cuda")
     from model import _hip
     _hip.load_library()
-    _hip.gemm_set_precision(1 if "--x6" in sys.argv else 0)
+    _hip.gemm_set_precision(2 if "--h16" in sys.argv else 1 if "--x6" in sys.argv else 0)
     cfg = bench.make_cfg()
     data, c2w = bench.synthetic_scene(dev)
     trainer, net = bench.build_trainer(dev, c2w, cfg)
@@ -38,7 +38,15 @@ def main():
         step()
     torch.cuda.synchronize()
     eager = (time.perf_counter() - t0) / 20
-    print(f"eager: {eager * 1e3:.3f} ms/step", flush=True)
+    host = []
+    for _ in range(20):                     # host enqueue time of one step (GPU drained first)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        step()
+        host.append(time.perf_counter() - t1)
+    torch.cuda.synchronize()
+    host.sort()
+    print(f"eager: {eager * 1e3:.3f} ms/step  host enqueue median {host[10] * 1e3:.3f} ms/step", flush=True)
     g = torch.cuda.CUDAGraph()
     try:
         with torch.cuda.graph(g):

@@ -38,10 +38,10 @@ def test_binding_covers_the_header():
 def test_abi_version_and_error_path(lib):
     assert lib.nerf_hip_abi_version() == 4
     rc = lib.nerf_linear_fwd(None, 256, 256, None, 0, 0, None, None, 0, None, None, 256, 128, 256, 1, None, 0,
-                             None, None, None, None)
+                             None, None, None, None, None)
     assert rc == -1
     assert b"null" in lib.nerf_hip_last_error()
-    rc = lib.nerf_linear_bwd_weight(1, 256, 100, 1, 256, 256, 1024, 4, 1, 256, 0, None, None)
+    rc = lib.nerf_linear_bwd_weight(1, 256, 100, 1, 256, 256, 1024, 4, 1, 256, 0, None, None, None, None)
     assert rc == -1 and b"nout" in lib.nerf_hip_last_error()
     rc = lib.nerf_composite_fwd(None, None, 1, 1, 0, None, None, None, None)
     assert rc == -1

@@ -25,6 +25,13 @@ def _rm(x):
     return x.abs().amax(1).contiguous()
 
 
+def _cm(x):
+    """Column max |x| per 128-row group ([m/128][cols], the dW column scales of mode 2)."""
+    if _hip.gemm_get_precision() != 2 or x is None or x.shape[0] % 128:
+        return None
+    return x.abs().view(x.shape[0] // 128, 128, x.shape[1]).amax(1).contiguous()
+
+
 def _images(W, dev):
     """W [n][k] (device) -> (split image of W, image of W^T) via nerf_pack_weights, in the
     form of the current precision mode (bf16x3, or the fp16 pair in mode 2)."""
@@ -50,16 +57,18 @@ def test_linear_fwd(dev, gemm_precision, m, n, k1, k2, relu):
     ws = _images(Wd, dev)[0] if gemm_precision >= 1 else None
     x1d, x2d = x1.to(dev), (x2.to(dev) if x2 is not None else None)
     y_rm = torch.full((m,), -1.0, device=dev) if gemm_precision == 2 else None
+    y_cm = torch.full((m // 128, n), -1.0, device=dev) if gemm_precision == 2 else None
     _hip.linear_fwd(x1d, k1, x2d, k2, Wd, b.to(dev), y, m, n, relu, mask_out=mo, w_split=ws, x1_rmax=_rm(x1d),
-                    x2_rmax=_rm(x2d), y_rmax=y_rm)
+                    x2_rmax=_rm(x2d), y_rmax=y_rm, y_cmax=y_cm)
     xc = torch.cat([x1, x2], 1) if x2 is not None else x1
     ref = xc.double() @ W.double().t() + b.double()
     if relu:
         ref = ref.clamp_min(0)
     torch.cuda.synchronize()
     assert (y.cpu().double() - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
-    if y_rm is not None:                                              # exact row maxima of y
+    if y_rm is not None:                                              # exact row / column maxima of y
         assert torch.equal(y_rm, y.abs().amax(1))
+        assert torch.equal(y_cm, y.abs().view(m // 128, 128, n).amax(1))
     bits = ((mo.cpu().long() & 0xffffffff).unsqueeze(-1) >> torch.arange(32)) & 1
     assert torch.equal(bits.view(m, n).bool(), y.cpu() > 0)          # ReLU bits agree with y
 
@@ -93,14 +102,16 @@ def test_linear_bwd_data(dev, gemm_precision):
     ws = _images(Wtd, dev)[0] if gemm_precision >= 1 else None     # image of wt itself ([n][k])
     dyd = dy.to(dev)
     dx_rm = torch.full((m,), -1.0, device=dev) if gemm_precision == 2 else None
+    dx_cm = torch.full((m // 128, n), -1.0, device=dev) if gemm_precision == 2 else None
     _hip.linear_bwd_data(dyd, k, Wtd, dx, m, n, mask=words.to(dev), u=u.to(dev), ldu=4, v=v.to(dev),
-                         wt_split=ws, dy_rmax=_rm(dyd), dx_rmax=dx_rm)
+                         wt_split=ws, dy_rmax=_rm(dyd), dx_rmax=dx_rm, dx_cmax=dx_cm)
     ref = dy.double() @ Wt.double().t() + u[:, 0:1].double() * v.double()
     ref = torch.where(mask > 0, ref, torch.zeros_like(ref))
     torch.cuda.synchronize()
     assert (dx.cpu().double() - ref).abs().max().item() < 2e-5 * ref.abs().max().item()
     if dx_rm is not None:
         assert torch.equal(dx_rm, dx.abs().amax(1))
+        assert torch.equal(dx_cm, dx.abs().view(m // 128, 128, n).amax(1))
 
 
 @pytest.mark.parametrize("nout,kin,m,splits", [(256, 256, 4096, 8), (128, 320, 2048, 4), (256, 64, 1024, 1),
@@ -114,9 +125,12 @@ def test_linear_bwd_weight_and_reduce(dev, gemm_precision, nout, kin, m, splits)
     slab = torch.empty(splits * nout * kin, device=dev)
     bslab = torch.empty(splits * nout, device=dev)
     dyd, xd = dy.to(dev), x.to(dev)
-    _hip.linear_bwd_weight(dyd, nout, xd[:, :k_main], k_main, m, splits, slab, kin, 0, bslab)
+    x1, x2 = xd[:, :k_main].contiguous(), xd[:, k_main:].contiguous()
+    _hip.linear_bwd_weight(dyd, nout, x1, k_main, m, splits, slab, kin, 0, bslab, dy_cmax=_cm(dyd),
+                           x_cmax=_cm(x1))
     if k_main < kin:
-        _hip.linear_bwd_weight(dyd, nout, xd[:, k_main:], kin - k_main, m, splits, slab, kin, k_main, None)
+        _hip.linear_bwd_weight(dyd, nout, x2, kin - k_main, m, splits, slab, kin, k_main, None,
+                               dy_cmax=_cm(dyd), x_cmax=_cm(x2))
     kin_ref = kin - 1
     gw = torch.empty(nout, kin_ref, device=dev)
     gb = torch.empty(nout, device=dev)
@@ -179,6 +193,37 @@ def test_split_accuracy(dev, scale_a, scale_b, spread):
         # per-row error relative to the row's scale (rows differ by 2^spread)
         rowscale = ref.abs().amax(1, keepdim=True).clamp_min(1e-300)
         errs.append(((y.cpu().double() - ref).abs() / rowscale).max().item())
+    tiny = 4 * 2.0 ** -24
+    assert errs[1] <= 1.5 * errs[0] + tiny, errs
+    assert errs[2] <= 1.5 * errs[0] + tiny, errs
+
+
+@pytest.mark.parametrize("spread", [0, 10])
+def test_split_accuracy_weight_gradient(dev, spread):
+    """Weight-gradient GEMM (sum over 32768 samples in 64 splits) in every mode against fp64:
+    the fp16 pair kernel (column scales per split) within 1.5x (+ulps) of the exact-f32 MFMA,
+    also with columns whose magnitudes differ by up to 2^spread."""
+    g = torch.Generator().manual_seed(21)
+    m, nout, kin, splits = 32768, 256, 256, 64
+    cs = 2.0 ** torch.randint(-spread, spread + 1, (1, nout), generator=g).float() if spread else 1.0
+    dy = _rand(m, nout, g=g) * cs
+    x = _rand(m, kin, g=g)
+    ref = dy.double().t() @ x.double()
+    rowscale = (dy.double().abs().t() @ x.double().abs()).amax(1, keepdim=True)
+    dyd, xd = dy.to(dev), x.to(dev)
+    errs = []
+    for mode in (0, 1, 2):
+        _hip.gemm_set_precision(mode)
+        try:
+            slab = torch.empty(splits * nout * kin, device=dev)
+            gw = torch.empty(nout, kin, device=dev)
+            _hip.linear_bwd_weight(dyd, nout, xd, kin, m, splits, slab, kin, 0, None, dy_cmax=_cm(dyd),
+                                   x_cmax=_cm(xd))
+            _hip.slab_reduce(slab, splits, nout, kin, nout, kin, None, gw, None)
+            torch.cuda.synchronize()
+        finally:
+            _hip.gemm_set_precision(0)
+        errs.append(((gw.cpu().double() - ref).abs() / rowscale).max().item())
     tiny = 4 * 2.0 ** -24
     assert errs[1] <= 1.5 * errs[0] + tiny, errs
     assert errs[2] <= 1.5 * errs[0] + tiny, errs
@@ -344,7 +389,9 @@ def test_heads_fwd_bwd(dev, hidden):
     dyr = torch.empty(Np, HR, device=dev)
     part = torch.empty(_hip.heads_part_size(hidden, Np), device=dev)
     dyr_rm = torch.full((Np,), -1.0, device=dev)
-    _hip.heads_bwd(graw.to(dev), h8.to(dev), hr.to(dev), hidden, wc.to(dev), dyr, part, Np, dyr_rmax=dyr_rm)
+    dyr_cm = torch.full((Np // 128, HR), -1.0, device=dev)
+    _hip.heads_bwd(graw.to(dev), h8.to(dev), hr.to(dev), hidden, wc.to(dev), dyr, part, Np, dyr_rmax=dyr_rm,
+                   dyr_cmax=dyr_cm)
     gwd, gbd = torch.empty(hidden, device=dev), torch.empty(1, device=dev)
     gwc, gbc = torch.empty(3, HR, device=dev), torch.empty(3, device=dev)
     _hip.heads_reduce(part, hidden, Np, gwd, gbd, gwc, gbc)
@@ -353,6 +400,7 @@ def test_heads_fwd_bwd(dev, hidden):
     torch.cuda.synchronize()
     assert (dyr.cpu().double() - r_dyr).abs().max().item() < 1e-5 * max(1, r_dyr.abs().max().item())
     assert torch.equal(dyr_rm, dyr.abs().amax(1))                    # row scales of precision mode 2
+    assert torch.equal(dyr_cm, dyr.abs().view(Np // 128, 128, HR).amax(1))   # its column scales
     assert (gwd.cpu().double() - G[:, 0] @ h8.double()).abs().max().item() < 1e-4 * Np
     assert (gwc.cpu().double() - G[:, 1:].t() @ hr.double()).abs().max().item() < 1e-4 * Np
     assert (gbd.cpu().double() - G[:, 0].sum()).abs().item() < 1e-3
@@ -371,8 +419,9 @@ def test_encode_samples(dev):
     ep = torch.empty(Np, 64, device=dev)
     ed = torch.empty(Np, 64, device=dev)
     rp, rd = torch.full((Np,), -1.0, device=dev), torch.full((Np,), -1.0, device=dev)
+    cp, cd = torch.full((Np // 128, 64), -1.0, device=dev), torch.full((Np // 128, 64), -1.0, device=dev)
     _hip.encode_samples(o.to(dev), d.to(dev), view.to(dev), noise.to(dev), R, S, Np, 0.01, 10.0, z, ep, ed,
-                        enc_p_rmax=rp, enc_d_rmax=rd)
+                        enc_p_rmax=rp, enc_d_rmax=rd, enc_p_cmax=cp, enc_d_cmax=cd)
     oz = orc.stratified_z(R, S, 0.01, 10.0, noise.view(1, R, S))[0]
     pts = (o.unsqueeze(1) + d.unsqueeze(1) * oz.unsqueeze(-1)).reshape(-1, 3)
     ref_p = orc.encode_position(pts, 10)
@@ -387,6 +436,12 @@ def test_encode_samples(dev):
     assert ep.cpu()[:, 63].abs().max().item() == 0 and ed.cpu()[:, 27:].abs().max().item() == 0
     assert ep.cpu()[R * S:].abs().max().item() == 0
     assert torch.equal(rp, ep.abs().amax(1)) and torch.equal(rd, ed.abs().amax(1))
+    # column bounds per 128-row group: exact on the coordinates, >= the sin / cos maxima, 0 on the pad
+    for c, e in ((cp, ep), (cd, ed)):
+        ex = e.abs().view(Np // 128, 128, 64).amax(1)
+        assert torch.equal(c[:, :3], ex[:, :3]) and (c >= ex).all()
+    assert (cp[:, 3:63] == 1).all() and (cp[:, 63] == 0).all()
+    assert (cd[:, 3:27] == 1).all() and (cd[:, 27:] == 0).all()
 
 
 def test_chamfer_nn(dev):
