@@ -148,6 +148,33 @@ int nerf_gemm_debug_stamps(void* buf);
 int nerf_gemm_debug_ablate(int mask);
 
 /* ---------------------------------------------------------------------------
+ * Fused forward chain of the whole field MLP (GEMM precision mode 2, hidden width 256,
+ * colour width 128).  Replaces OfficialStaticNerf.infer_occ / forward's ten linears with
+ * their ReLUs, the skip concat and the colour concat (official_nerf.py:60-91) -- the ten
+ * nerf_linear_fwd calls -- by ONE launch that keeps each 128-row tile's activations in
+ * registers from layer to layer (row-scaled fp16 pairs, three MFMA products, as mode 2).
+ * layers[10] = l0..l7, fc_feature, rgb_layers[0]; per layer the fp16 pair weight image
+ * written by nerf_pack_weights in mode 2 ([out_p][K]: K = 64, 256, 256, 256, 320, 256,
+ * 256, 256, 256, 320; out_p = 256 except 128 for the colour layer) and the bias; optional
+ * outputs: the f32 activation (the backward's saved tensor; NULL in eval renders), the ReLU
+ * bits and the column maxima per 128-row group (mode 2's weight-gradient scales; not for
+ * the colour layer).  enc_p / enc_d and their row maxima as written by nerf_encode_samples.
+ * n_pad % 128 == 0. */
+typedef struct {
+    const uint16_t* img;   /* fp16 pair image of the packed weight */
+    int img_rows;          /* its rows (>= the layer's outputs) */
+    const float* bias;     /* [outputs] (the colour layer: padded to 128) */
+    float* out; int ldo;   /* f32 output [n_pad][ldo] or NULL */
+    uint32_t* mask; int ldmask;   /* ReLU bits [n_pad][ldmask words] or NULL */
+    float* cmax;           /* [n_pad/128][outputs] or NULL */
+} nerf_chain_layer;
+int nerf_mlp_chain_fwd(const float* enc_p, const float* enc_d, const float* enc_p_rmax,
+                       const float* enc_d_rmax, int n_pad, const nerf_chain_layer* layers, void* stream);
+/* Diagnostics only: per-block phase cycles of nerf_mlp_chain_fwd into buf[(n_pad/128)*6]
+ * uint64 (DMA wait, barrier, MFMA section, epilogue, total, end time); NULL switches off. */
+int nerf_chain_debug_stamps(void* buf);
+
+/* ---------------------------------------------------------------------------
  * Output heads (density + colour logits), forward and backward.
  * Replaces fc_density and fc_rgb (official_nerf.py:66, 91).
  *   raw4[s] = ( h8[s].wd + bd,  hr[s].Wc[c] + bc[c] for c<3 )

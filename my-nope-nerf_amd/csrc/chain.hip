@@ -1,0 +1,427 @@
+// Fused forward chain of the field MLP (GEMM precision mode 2, hidden width 256).
+//
+// OfficialStaticNerf's ten linears (official_nerf.py:20-37, 60-91) run in ONE launch: a
+// block owns 128 sample rows (4 waves x 32 rows) and walks them through
+//   l0 [enc_p] -> l1 -> l2 -> l3 -> l4 [h3, enc_p] -> l5 -> l6 -> l7 -> lf -> lr [f, enc_d]
+// with the activation tile resident in registers between layers.  Per layer a wave holds
+//   * its A operand: 32 rows x K as row-scaled fp16 pairs (x 2^e = hi + lo, the split of
+//     gemm_x6.hip precision mode 2), 4 VGPRs per plane and 16-deep k-step;
+//   * the accumulators: 32 rows x 256 outputs in AGPRs (operand-swapped MFMAs, so a lane
+//     owns one sample row and 16 features per 32x32 tile, gemm.hpp nt_epilogue_direct).
+// The weights stream through a 5-slot LDS ring by LDS-DMA (pre-split fp16 pair images of
+// nerf_pack_weights, 16 KB per k-step); their schedule does not depend on the activations,
+// so the ring runs ahead across layer boundaries and the next layer's first k-steps land
+// during the epilogue.  The epilogue undoes the scales, adds the bias, applies the ReLU,
+// stores the f32 activation (the backward's saved tensor; skipped when `out` is NULL, as in
+// eval renders), the ReLU bits and the per-feature column maxima of the 128-row group (the
+// weight-gradient GEMM's scales), then re-splits the tile as the next layer's A operand:
+// the row max over both half-wave lanes sets the new exponent and one v_permlane32_swap per
+// VGPR pair turns the accumulator layout (lane halves hold alternating feature quads) into
+// the fragment layout (lane halves hold 8 consecutive features).
+//
+// Against one launch per layer (gemm_x6.hip) this removes the read of every layer input
+// (134 MB per 256-wide layer at 1024 x 128 samples), every per-layer prologue, launch gap
+// and tail, and keeps the weight stream off the critical path.
+#include "gemm.hpp"
+
+namespace nerf {
+namespace {
+
+typedef _Float16 ch16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 ch16x2 __attribute__((ext_vector_type(2)));
+typedef float cf32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int CNL = 10;                     // layers
+constexpr int CROWS = 128;                  // rows per block (4 waves x 32)
+constexpr int NSLOT = 5;                    // weight ring slots
+constexpr int SHALF = 256 * 16 + 128;       // one k-half of a 256-row slot (+ bank offset)
+constexpr int SPLANE = 2 * SHALF;
+constexpr int SBYTES = 2 * SPLANE;          // two planes (fp16 hi / lo)
+constexpr int DMA_PER_STEP = 4;             // LDS-DMA instructions per wave and k-step
+
+// topology (hidden width 256, colour width 128): k-steps of each layer's weight image,
+// k-steps taken from the register tile, from an encoding, output width
+constexpr int L_KS[CNL] = {4, 16, 16, 16, 20, 16, 16, 16, 16, 20};
+constexpr int L_OUT[CNL] = {256, 256, 256, 256, 256, 256, 256, 256, 256, 128};
+
+__device__ __forceinline__ f32x16 cmfma(const uint4& w, const uint4& a, const f32x16& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(ch16x8, w), __builtin_bit_cast(ch16x8, a), c,
+                                                  0, 0, 0);
+}
+__device__ __forceinline__ uint32_t cpk(float a, float b) {
+    cf32x2 v = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, ch16x2));   // RNE
+}
+// already scaled (a, b) -> fp16 pair words (hi, lo)
+__device__ __forceinline__ void csplit(float a, float b, uint32_t& h, uint32_t& l) {
+    h = cpk(a, b);
+    const ch16x2 hv = __builtin_bit_cast(ch16x2, h);
+    l = cpk(a - (float)hv[0], b - (float)hv[1]);
+}
+
+typedef __attribute__((address_space(3))) void clds_t;
+// 16 bytes per lane from sbase + voff (wave-uniform base in SGPRs, 32-bit lane offset: no
+// 64-bit per-lane addresses to keep live) into LDS at lds_wave_base + 16 lane
+__device__ __forceinline__ void cdma16(const void* sbase, uint32_t voff, char* lds_wave_base) {
+    const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(clds_t*)lds_wave_base);
+    asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(l) : "memory", "m0");
+}
+
+// 8 consecutive f32 (k = 8 hf .. 8 hf + 7 of one k-step) scaled by 2^e -> fragment planes
+__device__ __forceinline__ void frag_from8(const float4& u, const float4& v, int e, uint4& hi, uint4& lo) {
+    const float s0 = __builtin_amdgcn_ldexpf(u.x, e), s1 = __builtin_amdgcn_ldexpf(u.y, e);
+    const float s2 = __builtin_amdgcn_ldexpf(u.z, e), s3 = __builtin_amdgcn_ldexpf(u.w, e);
+    const float s4 = __builtin_amdgcn_ldexpf(v.x, e), s5 = __builtin_amdgcn_ldexpf(v.y, e);
+    const float s6 = __builtin_amdgcn_ldexpf(v.z, e), s7 = __builtin_amdgcn_ldexpf(v.w, e);
+    csplit(s0, s1, hi.x, lo.x);
+    csplit(s2, s3, hi.y, lo.y);
+    csplit(s4, s5, hi.z, lo.z);
+    csplit(s6, s7, hi.w, lo.w);
+}
+
+}  // namespace
+
+struct ChainFwdArgs {
+    const float* enc_p; const float* enc_d;   // [n_pad][64]
+    const float* rp; const float* rd;         // row maxima of enc_p / enc_d
+    int n_pad;
+    nerf_chain_layer L[CNL];
+    unsigned long long* stamps;   // diagnostics (nerf_chain_debug_stamps): per-block phase cycles or NULL
+};
+
+constexpr int kbase(int l) { return l == 0 ? 0 : kbase(l - 1) + L_KS[l - 1]; }
+constexpr int CT = kbase(CNL);   // k-steps of the whole chain
+
+// per-block state of the chain (all register arrays statically indexed after inlining)
+struct ChainState {
+    char* ring; char* leb16; float* lbias; uint32_t* lcm;   // leb16: [2][256 rows][16 B], exponent in word 0
+    char* lenc; float* lrp; float* lrd;                      // encoding tile [128][64], row maxima [128] x 2
+    int tid, lane, sl, hf;
+    size_t m0, row;
+    int er;                          // row exponent of the current A operand
+    uint4 act_hi[16], act_lo[16];    // register tile: 16 k-steps of the 256 activations
+    uint4 enc_hi[4], enc_lo[4];      // encoding segment of the current layer
+    f32x16 acc[8];
+    unsigned long long t_wait, t_bar, t_mma, t_epi, t_last;   // diagnostics (stamps)
+};
+
+__device__ __forceinline__ void chain_tick(const ChainFwdArgs& p, ChainState& st, unsigned long long& bucket) {
+    if (p.stamps == nullptr) return;
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    bucket += t - st.t_last;
+    st.t_last = t;
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+constexpr bool first_step(int tt) {
+    for (int l = 0; l < CNL; ++l)
+        if (kbase(l) == tt) return true;
+    return false;
+}
+constexpr int ENC_D_STEP = 4 + 16 * 3 + 20;   // kbase(5): the enc_d tile replaces enc_p once l4 is done
+// LDS-DMA instructions every wave issues with global k-step tt (uniform across waves):
+// 4 for the weight ring, +2 at a layer's first step (weight-row exponents, biases), +10 at
+// step 0 (enc_p tile 8, enc_p / enc_d row maxima 1 + 1), +8 at ENC_D_STEP (enc_d tile)
+constexpr int dma_count(int tt) {
+    return tt >= CT ? 0 : DMA_PER_STEP + (first_step(tt) ? 2 : 0) + (tt == 0 ? 10 : 0) + (tt == ENC_D_STEP ? 8 : 0);
+}
+// DMAs issued after those of step tt by the time step tt is consumed (steps tt+1 .. tt+NSLOT-2)
+constexpr int dma_after(int tt) {
+    int n = 0;
+    for (int u = tt + 1; u <= tt + NSLOT - 2; ++u) n += dma_count(u);
+    return n;
+}
+
+// the 128-row x 64 encoding tile of the block into LDS: wave w moves rows 32 w .. 32 w + 31,
+// four 256-byte rows per instruction
+__device__ __forceinline__ void chain_dma_enc(const float* enc, ChainState& st) {
+    const int w = st.tid >> 6;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int r = 32 * w + 4 * i + (st.lane >> 4);
+        cdma16(enc + st.m0 * 64, (uint32_t)(r * 256 + (st.lane & 15) * 16), st.lenc + (32 * w + 4 * i) * 256);
+    }
+}
+
+// global k-step TT -> ring slot TT % NSLOT, plus the extras of dma_count(TT)
+template <int TT>
+__device__ __forceinline__ void chain_dma(const ChainFwdArgs& p, ChainState& st) {
+    if constexpr (TT < CT) {
+        constexpr int l = [] { int i = 0; while (kbase(i + 1) <= TT) ++i; return i; }();
+        constexpr int s = TT - kbase(l);
+        constexpr int ks = L_KS[l];
+        const nerf_chain_layer& L = p.L[l];
+        const int w = st.tid >> 6;
+        char* slot = st.ring + (TT % NSLOT) * SBYTES;
+#pragma unroll
+        for (int i = 0; i < DMA_PER_STEP; ++i) {
+            int n, ph;   // image row, plane * 2 + k-half
+            if (L_OUT[l] == 256) { n = st.tid; ph = i; }
+            else { n = st.tid & 127; ph = ((st.tid >> 7) + 2 * i) & 3; }   // 128 rows: i = 2, 3 repeat i = 0, 1
+            const uint32_t off = (uint32_t)(((ph >> 1) * (2 * ks) + 2 * s + (ph & 1)) * L.img_rows + n) * 16;
+            cdma16(L.img, off, slot + (ph >> 1) * SPLANE + (ph & 1) * SHALF + (n - st.lane) * 16);
+        }
+        if constexpr (s == 0) {
+            // this layer's weight-row exponents (the 16-byte plane-2 chunk 0 of each image row,
+            // exponent in its first word) and biases, into the layer's LDS parity buffers
+            const int wr = L_OUT[l] == 256 ? w : (w & 1);
+            const int n = 64 * wr + st.lane;
+            cdma16(L.img, (uint32_t)((2 * (2 * ks) * L.img_rows + n) * 16), st.leb16 + (l & 1) * 4096 + 64 * wr * 16);
+            // one instruction with lanes 0-15 active (lane l lands at base + 16 l): 64 biases
+            if (st.lane < 16)
+                cdma16(L.bias, (uint32_t)((64 * wr + 4 * st.lane) * 4), reinterpret_cast<char*>(st.lbias + (l & 1) * 256 + 64 * wr));
+        }
+        if constexpr (TT == 0) {
+            chain_dma_enc(p.enc_p, st);
+            if (st.lane < 8) {   // 32 row maxima per wave
+                cdma16(p.rp + st.m0, (uint32_t)((32 * w + 4 * st.lane) * 4), reinterpret_cast<char*>(st.lrp + 32 * w));
+                cdma16(p.rd + st.m0, (uint32_t)((32 * w + 4 * st.lane) * 4), reinterpret_cast<char*>(st.lrd + 32 * w));
+            }
+        }
+        if constexpr (TT == ENC_D_STEP) chain_dma_enc(p.enc_d, st);
+    }
+}
+
+// one k-step of layer l: wait for its slot, publish, refill the ring, MFMAs
+template <int l, int s>
+__device__ __forceinline__ void chain_kstep(const ChainFwdArgs& p, ChainState& st) {
+    constexpr int TT = kbase(l) + s;
+    constexpr int nreg = l == 0 ? 0 : 16;
+    constexpr int ntj = L_OUT[l] / 32;
+    chain_tick(p, st, st.t_mma);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(dma_after(TT)) : "memory");   // this step's DMAs landed
+    chain_tick(p, st, st.t_wait);
+    __syncthreads();
+    chain_tick(p, st, st.t_bar);
+    chain_dma<TT + NSLOT - 1>(p, st);
+    if constexpr (s == 0) {
+        // layer prologue (behind a barrier): the previous layer's column maxima out, this
+        // layer's column-max accumulators zeroed (its exponents and biases arrived by DMA)
+        if constexpr (l > 0) {
+            if (p.L[l - 1].cmax)
+                p.L[l - 1].cmax[(st.m0 / 128) * L_OUT[l - 1] + st.tid] =
+                    __uint_as_float(st.lcm[((l - 1) & 1) * 256 + st.tid]);
+        }
+        st.lcm[(l & 1) * 256 + st.tid] = 0u;
+    }
+    const char* slot = st.ring + (TT % NSLOT) * SBYTES;
+    const uint4& ah = s < nreg ? st.act_hi[s < nreg ? s : 0] : st.enc_hi[s < nreg ? 0 : s - nreg];
+    const uint4& al = s < nreg ? st.act_lo[s < nreg ? s : 0] : st.enc_lo[s < nreg ? 0 : s - nreg];
+#pragma unroll
+    for (int j = 0; j < ntj; ++j) {
+        const char* b = slot + st.hf * SHALF + (32 * j + st.sl) * 16;
+        const uint4 bh = *reinterpret_cast<const uint4*>(b);
+        const uint4 bl = *reinterpret_cast<const uint4*>(b + SPLANE);
+        st.acc[j] = cmfma(bh, al, st.acc[j]);   // hi . lo
+        st.acc[j] = cmfma(bl, ah, st.acc[j]);   // lo . hi
+        st.acc[j] = cmfma(bh, ah, st.acc[j]);   // hi . hi
+    }
+    // weight fragments one tile ahead of their MFMAs (keeps few fragments live)
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+    for (int j = 1; j < ntj; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+}
+
+template <int l, int s>
+__device__ __forceinline__ void chain_ksteps(const ChainFwdArgs& p, ChainState& st) {
+    if constexpr (s < L_KS[l]) {
+        chain_kstep<l, s>(p, st);
+        chain_ksteps<l, s + 1>(p, st);
+    }
+}
+
+// this lane's 8-feature chunks of the encoding row (LDS tile) -> the 4 encoding k-steps of
+// the current A operand at exponent st.er
+__device__ __forceinline__ void enc_frags(ChainState& st, int rl) {
+    const float4* src = reinterpret_cast<const float4*>(st.lenc + rl * 256);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+        frag_from8(src[4 * s + 2 * st.hf], src[4 * s + 2 * st.hf + 1], st.er, st.enc_hi[s], st.enc_lo[s]);
+}
+
+// layer l: k-loop, epilogue (features f = 32 j + 8 q + 4 hf + c of row st.row), next A
+template <int l>
+__device__ __forceinline__ void chain_layer(const ChainFwdArgs& p, ChainState& st) {
+    constexpr int ntj = L_OUT[l] / 32;
+    constexpr bool relu = l != 8;
+    const nerf_chain_layer& L = p.L[l];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st.acc[j][r] = 0.f;
+    chain_ksteps<l, 0>(p, st);
+    chain_tick(p, st, st.t_mma);
+
+    const char* eb = st.leb16 + (l & 1) * 4096;
+    const float* bb = st.lbias + (l & 1) * 256;
+    float rmx = 0.f;
+#pragma unroll
+    for (int j = 0; j < ntj; ++j) {
+        float cm[16];
+        uint32_t w = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int f0 = 32 * j + 8 * q + 4 * st.hf;
+            const int4 e4 = make_int4(*reinterpret_cast<const int*>(eb + 16 * f0), *reinterpret_cast<const int*>(eb + 16 * (f0 + 1)),
+                                      *reinterpret_cast<const int*>(eb + 16 * (f0 + 2)), *reinterpret_cast<const int*>(eb + 16 * (f0 + 3)));
+            const float4 b4 = *reinterpret_cast<const float4*>(bb + f0);
+            float4 x;
+            x.x = __builtin_amdgcn_ldexpf(st.acc[j][4 * q + 0], -(st.er + e4.x)) + b4.x;
+            x.y = __builtin_amdgcn_ldexpf(st.acc[j][4 * q + 1], -(st.er + e4.y)) + b4.y;
+            x.z = __builtin_amdgcn_ldexpf(st.acc[j][4 * q + 2], -(st.er + e4.z)) + b4.z;
+            x.w = __builtin_amdgcn_ldexpf(st.acc[j][4 * q + 3], -(st.er + e4.w)) + b4.w;
+            if (relu) x = make_float4(fmaxf(x.x, 0.f), fmaxf(x.y, 0.f), fmaxf(x.z, 0.f), fmaxf(x.w, 0.f));
+            st.acc[j][4 * q + 0] = x.x; st.acc[j][4 * q + 1] = x.y;
+            st.acc[j][4 * q + 2] = x.z; st.acc[j][4 * q + 3] = x.w;
+            if (L.out) *reinterpret_cast<float4*>(L.out + st.row * L.ldo + f0) = x;
+            w |= ((x.x > 0.f ? 1u : 0u) | (x.y > 0.f ? 2u : 0u) | (x.z > 0.f ? 4u : 0u) | (x.w > 0.f ? 8u : 0u))
+                 << (8 * q + 4 * st.hf);
+            cm[4 * q + 0] = fabsf(x.x); cm[4 * q + 1] = fabsf(x.y);
+            cm[4 * q + 2] = fabsf(x.z); cm[4 * q + 3] = fabsf(x.w);
+            rmx = fmaxf(rmx, fmaxf(fmaxf(cm[4 * q], cm[4 * q + 1]), fmaxf(cm[4 * q + 2], cm[4 * q + 3])));
+        }
+        if (L.mask) {
+            w |= (uint32_t)__shfl_xor((int)w, 32, 64);
+            if (st.hf == 0) L.mask[st.row * L.ldmask + j] = w;
+        }
+        if (L.cmax) {
+            // column maxima of this tile over the wave's 32 rows (halving butterfly: lane sl
+            // keeps feature `base` of the 16 its half-wave holds), then over the waves in LDS
+            int base = 0;
+            bfly_max<8, 16>(cm, st.sl, base);
+            bfly_max<4, 8>(cm, st.sl, base);
+            bfly_max<2, 4>(cm, st.sl, base);
+            bfly_max<1, 2>(cm, st.sl, base);
+            bfly_max<0, 1>(cm, st.sl, base);
+            atomicMax(st.lcm + (l & 1) * 256 + 32 * j + 8 * (base >> 2) + 4 * st.hf + (base & 3),
+                      __float_as_uint(cm[0]));
+        }
+    }
+    chain_tick(p, st, st.t_epi);
+    if constexpr (l < CNL - 1) {
+        // next layer's A operand: row exponent over the row's 256 features (and the encoding
+        // joined in the next layer), fp16 pairs, quad exchange between the lane halves
+        float m = fmaxf(rmx, __shfl_xor(rmx, 32, 64));
+        const int rl = (st.tid >> 6) * 32 + st.sl;   // row inside the block
+        if constexpr (l == 3) m = fmaxf(m, st.lrp[rl]);
+        if constexpr (l == 8) m = fmaxf(m, st.lrd[rl]);
+        st.er = row_exp(m);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const int j = s >> 1, qa = 2 * (s & 1), qb = qa + 1;
+            const int e = st.er;
+            uint32_t ha0, la0, ha1, la1, hb0, lb0, hb1, lb1;
+            csplit(__builtin_amdgcn_ldexpf(st.acc[j][4 * qa + 0], e), __builtin_amdgcn_ldexpf(st.acc[j][4 * qa + 1], e),
+                   ha0, la0);
+            csplit(__builtin_amdgcn_ldexpf(st.acc[j][4 * qa + 2], e), __builtin_amdgcn_ldexpf(st.acc[j][4 * qa + 3], e),
+                   ha1, la1);
+            csplit(__builtin_amdgcn_ldexpf(st.acc[j][4 * qb + 0], e), __builtin_amdgcn_ldexpf(st.acc[j][4 * qb + 1], e),
+                   hb0, lb0);
+            csplit(__builtin_amdgcn_ldexpf(st.acc[j][4 * qb + 2], e), __builtin_amdgcn_ldexpf(st.acc[j][4 * qb + 3], e),
+                   hb1, lb1);
+            // low lanes keep quad a and take the high lanes' quad a; high lanes take the low
+            // lanes' quad b and keep quad b: v_permlane32_swap(vdst = a, vsrc = b) gives both
+            const auto h0 = __builtin_amdgcn_permlane32_swap(ha0, hb0, false, false);
+            const auto h1 = __builtin_amdgcn_permlane32_swap(ha1, hb1, false, false);
+            const auto l0 = __builtin_amdgcn_permlane32_swap(la0, lb0, false, false);
+            const auto l1 = __builtin_amdgcn_permlane32_swap(la1, lb1, false, false);
+            st.act_hi[s] = make_uint4(h0[0], h1[0], h0[1], h1[1]);
+            st.act_lo[s] = make_uint4(l0[0], l1[0], l0[1], l1[1]);
+        }
+        if constexpr (l == 3 || l == 8) enc_frags(st, rl);   // the enc_p / enc_d tile in LDS
+        chain_tick(p, st, st.t_epi);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mlp_chain_fwd(ChainFwdArgs p) {
+    constexpr int RING = NSLOT * SBYTES, LEB = 2 * 4096, LBIAS = 2 * 256 * 4, LCM = 2 * 256 * 4, LENC = 128 * 256;
+    __shared__ __attribute__((aligned(16))) char smem[RING + LEB + LBIAS + LCM + LENC + 2 * 512];
+    ChainState st;
+    st.ring = smem;
+    st.leb16 = smem + RING;
+    st.lbias = reinterpret_cast<float*>(smem + RING + LEB);
+    st.lcm = reinterpret_cast<uint32_t*>(smem + RING + LEB + LBIAS);
+    st.lenc = smem + RING + LEB + LBIAS + LCM;
+    st.lrp = reinterpret_cast<float*>(st.lenc + LENC);
+    st.lrd = st.lrp + 128;
+    st.tid = threadIdx.x;
+    st.lane = st.tid & 63; st.sl = st.lane & 31; st.hf = st.lane >> 5;
+    st.m0 = (size_t)blockIdx.x * CROWS;
+    st.row = st.m0 + 32 * (st.tid >> 6) + st.sl;
+    st.t_wait = st.t_bar = st.t_mma = st.t_epi = 0;
+    st.t_last = __builtin_amdgcn_s_memtime();
+    const unsigned long long t_start = st.t_last;
+
+    chain_dma<0>(p, st);
+    chain_dma<1>(p, st);
+    chain_dma<2>(p, st);
+    chain_dma<3>(p, st);
+    static_assert(NSLOT == 5, "prologue issues NSLOT - 1 k-steps");
+    // step 0's group (with the enc_p tile and the row maxima) landed, published to the block
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(dma_count(1) + dma_count(2) + dma_count(3)) : "memory");
+    __syncthreads();
+    const int rl = (st.tid >> 6) * 32 + st.sl;
+    st.er = row_exp(st.lrp[rl]);
+    enc_frags(st, rl);
+
+    chain_layer<0>(p, st);
+    chain_layer<1>(p, st);
+    chain_layer<2>(p, st);
+    chain_layer<3>(p, st);
+    chain_layer<4>(p, st);
+    chain_layer<5>(p, st);
+    chain_layer<6>(p, st);
+    chain_layer<7>(p, st);
+    chain_layer<8>(p, st);
+    chain_layer<9>(p, st);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every DMA landed before the LDS is released
+    if (p.stamps && st.tid == 0) {
+        unsigned long long* o = p.stamps + (size_t)blockIdx.x * 6;
+        o[0] = st.t_wait; o[1] = st.t_bar; o[2] = st.t_mma; o[3] = st.t_epi;
+        o[4] = __builtin_amdgcn_s_memtime() - t_start; o[5] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+}  // namespace nerf
+
+using namespace nerf;
+
+static unsigned long long* g_chain_stamps = nullptr;
+
+extern "C" int nerf_mlp_chain_fwd(const float* enc_p, const float* enc_d, const float* enc_p_rmax,
+                                  const float* enc_d_rmax, int n_pad, const nerf_chain_layer* layers, void* stream) {
+    NERF_CHECK_PTR(enc_p); NERF_CHECK_PTR(enc_d); NERF_CHECK_PTR(enc_p_rmax); NERF_CHECK_PTR(enc_d_rmax);
+    NERF_CHECK_PTR(layers);
+    NERF_CHECK(n_pad > 0 && n_pad % CROWS == 0, "%s: n_pad=%d must be a positive multiple of %d", __func__, n_pad,
+               CROWS);
+    NERF_CHECK(gemm_precision() == 2, "%s: the fused chain runs in GEMM precision mode 2 (fp16 pair images)", __func__);
+    NERF_CHECK_ALIGN16(enc_p); NERF_CHECK_ALIGN16(enc_d);
+    ChainFwdArgs a{};
+    a.enc_p = enc_p; a.enc_d = enc_d; a.rp = enc_p_rmax; a.rd = enc_d_rmax; a.n_pad = n_pad;
+    for (int l = 0; l < CNL; ++l) {
+        const nerf_chain_layer& L = layers[l];
+        NERF_CHECK(L.img && L.bias, "%s: layer %d needs its weight image and bias", __func__, l);
+        NERF_CHECK(L.img_rows >= L_OUT[l] && (((uintptr_t)L.img) & 15u) == 0,
+                   "%s: layer %d: image rows %d < %d or image not 16-byte aligned", __func__, l, L.img_rows, L_OUT[l]);
+        NERF_CHECK(L.out == nullptr || (L.ldo >= L_OUT[l] && L.ldo % 4 == 0 && (((uintptr_t)L.out) & 15u) == 0),
+                   "%s: layer %d: bad output (ldo %d)", __func__, l, L.ldo);
+        NERF_CHECK(L.mask == nullptr || L.ldmask >= L_OUT[l] / 32, "%s: layer %d: ldmask %d", __func__, l, L.ldmask);
+        NERF_CHECK(l != CNL - 1 || L.cmax == nullptr, "%s: the colour layer has no column maxima", __func__);
+        a.L[l] = L;
+    }
+    a.stamps = g_chain_stamps;
+    hipLaunchKernelGGL(k_mlp_chain_fwd, dim3(n_pad / CROWS), dim3(256), 0, as_stream(stream), a);
+    return check_launch(__func__);
+}
+
+// diagnostics: per-block phase cycles of the chain kernel (wait, barrier, MFMA section,
+// epilogue, total, end realtime) into a device buffer of (n_pad / 128) * 6 uint64; NULL off
+extern "C" int nerf_chain_debug_stamps(void* buf) {
+    g_chain_stamps = reinterpret_cast<unsigned long long*>(buf);
+    return NERF_OK;
+}

@@ -39,6 +39,12 @@ class PackDesc(ctypes.Structure):
                 ("rows_s", _c_i)]
 
 
+class ChainLayer(ctypes.Structure):
+    """nerf_chain_layer (include/nerf_hip.h)."""
+    _fields_ = [("img", _c_p), ("img_rows", _c_i), ("bias", _c_p), ("out", _c_p), ("ldo", _c_i), ("mask", _c_p),
+                ("ldmask", _c_i), ("cmax", _c_p)]
+
+
 _SIGS = {
     "nerf_hip_abi_version": ([], _c_i),
     "nerf_hip_last_error": ([], ctypes.c_char_p),
@@ -60,6 +66,8 @@ _SIGS = {
     "nerf_composite_bwd": ([_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_encode_bwd": ([_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_pack_weights": ([ctypes.POINTER(PackDesc), _c_i, _c_p], _c_i),
+    "nerf_mlp_chain_fwd": ([_c_p, _c_p, _c_p, _c_p, _c_i, ctypes.POINTER(ChainLayer), _c_p], _c_i),
+    "nerf_chain_debug_stamps": ([_c_p], _c_i),
     "nerf_adam_step": ([_c_p, _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p], _c_i),
     "nerf_chamfer_nn": ([_c_p, _c_i, _c_p, _c_i, _c_p, _c_p], _c_i),
     "nerf_gemm_set_policy": ([_c_i, _c_i], _c_i),
@@ -242,6 +250,15 @@ def encode_bwd(pts_o, pts_d, view, z, genc_p, genc_d, n_rays, n_samples, g_po, g
 def pack_weights(descs: Sequence[PackDesc]):
     arr = (PackDesc * len(descs))(*descs)
     _call("nerf_pack_weights", arr, len(descs), _stream())
+
+
+def mlp_chain_fwd(enc_p, enc_d, enc_p_rmax, enc_d_rmax, n_pad, layers: Sequence[ChainLayer]):
+    """All ten field linears in one launch (GEMM precision mode 2, hidden 256 / colour 128)."""
+    if len(layers) != 10:
+        raise ValueError("mlp_chain_fwd: needs the 10 layer descriptors")
+    arr = (ChainLayer * 10)(*layers)
+    _call("nerf_mlp_chain_fwd", _ptr(enc_p), _ptr(enc_d), _ptr(enc_p_rmax), _ptr(enc_d_rmax), int(n_pad), arr,
+          _stream())
 
 
 def adam_step(param, grad, exp_avg, exp_avg_sq, hyper):

@@ -16,6 +16,7 @@ Data layout in HBM (N_pad = R*S rounded up to 128 rows, samples ray-major):
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
 
@@ -156,7 +157,26 @@ class FieldRunner:
         seg_rm = {"enc_p": enc_p_rm, "enc_d": enc_d_rm}
         masks = {}
         cmaxes = {"enc_p": enc_p_cm, "enc_d": enc_d_cm}
-        for i, l in enumerate(self.layers):
+        if self.use_chain(keep):
+            # all ten linears in one launch, activations resident in registers (chain.hip)
+            descs = []
+            for i, l in enumerate(self.layers):
+                y = outs[i] if (keep or l.name in ("l7", "lr")) else None
+                mo = None
+                if keep and l.relu and l.name != "lr":
+                    mo = torch.empty(Np, l.out_p // 32, device=dev, dtype=torch.int32)
+                    masks[l.name] = mo
+                y_cm = cm(l.out_p) if l.name != "lr" else None
+                cmaxes[l.name] = y_cm
+                ws = self.ws[l.name]
+                descs.append(_hip.ChainLayer(ws.data_ptr(), ws.shape[2], self.bias(l).data_ptr(),
+                                             y.data_ptr() if y is not None else None, l.out_p,
+                                             mo.data_ptr() if mo is not None else None, l.out_p // 32,
+                                             y_cm.data_ptr() if y_cm is not None else None))
+                acts.append(y if y is not None else outs[i])
+            _hip.mlp_chain_fwd(enc_p, enc_d, enc_p_rm, enc_d_rm, Np, descs)
+            h8 = acts[7]
+        for i, l in enumerate(self.layers if not self.use_chain(keep) else []):
             y = outs[i]
             x2 = segs[l.seg2] if l.seg2 else None
             k1 = l.k1
@@ -191,6 +211,18 @@ class FieldRunner:
             state = dict(R=R, S=S, Np=Np, flags=flags, z=z, enc_p=enc_p, enc_d=enc_d, acts=acts, raw4=raw4,
                          masks=masks, pts_o=pts_o, pts_d=pts_d, view=view, cmaxes=cmaxes)
         return rgb, dist, alpha, z[:N].view(R, S), state
+
+    def use_chain(self, keep: bool = False) -> bool:
+        """The fused layer chain (chain.hip) covers precision mode 2 at hidden 256 / colour
+        128.  It is the default where no activation is saved (eval renders: 775 vs 877 us per
+        131072 samples); saving all nine activations for the backward its row-per-lane stores
+        cost more than the per-layer kernels' direct epilogues (1160 vs 923 us,
+        profiles/r01/chain_bench.txt), so training keeps one launch per layer unless
+        NERF_CHAIN=1; NERF_CHAIN=0 disables it everywhere."""
+        if not (_hip.gemm_get_precision() == 2 and self.D == 256 and self.HR == 128):
+            return False
+        env = os.environ.get("NERF_CHAIN")
+        return env == "1" if env is not None else not keep
 
     def _rmax_alloc(self, Np: int, dev):
         """Row-max buffer factory for precision mode 2 (None otherwise): a buffer for an

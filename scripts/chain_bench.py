@@ -1,0 +1,63 @@
+"""Fused layer chain (nerf_mlp_chain_fwd) vs one launch per layer at the cfg2 shape
+(1024 rays x 128 samples, hidden 256), GEMM precision mode 2, plus the chain's per-block
+phase cycles (nerf_chain_debug_stamps).
+
+    python scripts/chain_bench.py
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "my-nope-nerf_amd"))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from model import _hip  # noqa: E402
+from model.official_nerf import OfficialStaticNerf  # noqa: E402
+from tests.helpers import make_cfg  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda")
+    _hip.gemm_set_precision(2)
+    torch.manual_seed(0)
+    net = OfficialStaticNerf(make_cfg(hidden=256, S=128)).to(dev)
+    R, S = 1024, 128
+    o = (torch.rand(R, 3, device=dev) - 0.5) * 4
+    d = torch.nn.functional.normalize(torch.rand(R, 3, device=dev) - 0.5, dim=-1)
+    noise = torch.rand(R, S, device=dev)
+    runner = net.hip_runner()
+
+    def fwd(keep=True):
+        return runner.forward(o, d, -d, noise, 0.01, 10.0, S, 0, keep=keep)
+
+    for chain in ("1", "0", "1"):
+        os.environ["NERF_CHAIN"] = chain
+        for keep in (True, False):
+            for _ in range(3):
+                fwd(keep)
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(10):
+                fwd(keep)
+            e.record()
+            torch.cuda.synchronize()
+            print(f"chain={chain} keep={keep}: forward {s.elapsed_time(e) / 10 * 1e3:8.1f} us", flush=True)
+    os.environ["NERF_CHAIN"] = "1"
+    Np = R * S
+    buf = torch.zeros((Np // 128) * 6, dtype=torch.int64, device=dev)
+    _hip.lib().nerf_chain_debug_stamps(ctypes.c_void_p(buf.data_ptr()))
+    fwd(True)
+    torch.cuda.synchronize()
+    _hip.lib().nerf_chain_debug_stamps(None)
+    st = buf.cpu().numpy().reshape(-1, 6).astype(np.float64)
+    med = np.median(st[:, :5], axis=0)
+    print(f"chain phase cycles per block (median over {len(st)} blocks, wave 0): dma wait {med[0]:.0f}  "
+          f"barrier {med[1]:.0f}  mfma section {med[2]:.0f}  epilogue {med[3]:.0f}  total {med[4]:.0f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

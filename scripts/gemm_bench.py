@@ -88,7 +88,7 @@ def main():
             fn, fl = cases[name]
             for _ in range(20):
                 fn()
-            buf = torch.zeros((M // 256) * 10 * 2, dtype=torch.int64, device=dev)
+            buf = torch.zeros((M // 128) * 10 * 2, dtype=torch.int64, device=dev)   # 128-row tiles: M/128 blocks
             _hip.lib().nerf_gemm_debug_stamps(ctypes.c_void_p(buf.data_ptr()))
             fn()
             torch.cuda.synchronize()

@@ -1,0 +1,115 @@
+"""The fused layer chain (chain.hip, GEMM precision mode 2) against one launch per layer
+(gemm_x6.hip, same mode): every saved activation, ReLU bit, column maximum, the rendered
+outputs and the parameter gradients (GPU only)."""
+import os
+
+import pytest
+import torch
+
+from model import _hip
+from model.field import render_field, render_field_eval
+from model.official_nerf import OfficialStaticNerf
+from tests.helpers import make_cfg, synthetic_rays
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(net, b, dev, chain: bool, keep=True):
+    os.environ["NERF_CHAIN"] = "1" if chain else "0"
+    try:
+        runner = net.hip_runner()
+        assert runner.use_chain(keep) == chain
+        R, S = b["R"], b["S"]
+        o, d = b["o"].to(dev), b["d"].to(dev)
+        rgb, dist, alpha, z, st = runner.forward(o, d, -d, b["noise"].to(dev), 0.01, 10.0, S, 0, keep=keep)
+        torch.cuda.synchronize()
+        return rgb, dist, st
+    finally:
+        os.environ.pop("NERF_CHAIN", None)
+
+
+@pytest.fixture
+def h16(dev):
+    old = _hip.gemm_get_precision()
+    _hip.gemm_set_precision(2)
+    yield
+    _hip.gemm_set_precision(old)
+
+
+def _net(dev, seed=0):
+    torch.manual_seed(seed)
+    net = OfficialStaticNerf(make_cfg(hidden=256, S=64)).to(dev)
+    with torch.no_grad():   # spread the weights' scales over layers and rows
+        for i, p in enumerate(net.parameters()):
+            if p.dim() == 2:
+                p.mul_(torch.logspace(-1, 1, p.shape[0], device=dev).unsqueeze(1) * (0.5 + 0.1 * i))
+    return net
+
+
+def _rays(R, S, seed):
+    g = torch.Generator().manual_seed(seed)
+    o = (torch.rand(R, 3, generator=g) - 0.5) * 4
+    d = torch.nn.functional.normalize(torch.rand(R, 3, generator=g) - 0.5, dim=-1)
+    return {"R": R, "S": S, "o": o, "d": d, "noise": torch.rand(R, S, generator=g)}
+
+
+@pytest.mark.parametrize("R,S", [(64, 64), (300, 32), (1024, 128)])
+def test_chain_matches_per_layer(dev, h16, R, S):
+    net = _net(dev)
+    b = _rays(R, S, seed=R + S)
+    rgb1, dist1, st1 = _run(net, b, dev, chain=True)
+    rgb0, dist0, st0 = _run(net, b, dev, chain=False)
+    rel = lambda a, r: ((a - r).abs().max() / r.abs().max().clamp_min(1e-30)).item()
+    for i, (a1, a0) in enumerate(zip(st1["acts"], st0["acts"])):
+        assert rel(a1, a0) < 2e-6, f"activation {i}: {rel(a1, a0)}"
+    for k, m0 in st0["masks"].items():
+        m1 = st1["masks"][k]
+        act = st0["acts"][[l.name for l in net.hip_runner().layers].index(k)]
+        # ReLU bits agree wherever the activation is not within rounding of zero
+        bits = lambda m: ((m.long() & 0xffffffff).unsqueeze(-1) >> torch.arange(32, device=dev)) & 1
+        differ = (bits(m1) != bits(m0)).view(act.shape)
+        assert (act[differ].abs() < 1e-5).all(), k
+    for k, c0 in st0["cmaxes"].items():
+        if c0 is None or k.startswith("enc"):
+            continue
+        assert rel(st1["cmaxes"][k], c0) < 2e-6, k
+    assert rel(rgb1, rgb0) < 1e-5 and rel(dist1, dist0) < 1e-5
+
+
+def test_chain_eval_skips_intermediate_stores(dev, h16):
+    """keep=False (eval renders): only the trunk output and the colour hidden are stored."""
+    net = _net(dev, seed=1)
+    b = _rays(512, 64, seed=3)
+    o, d = b["o"].to(dev), b["d"].to(dev)
+    os.environ["NERF_CHAIN"] = "1"
+    try:
+        rgb1, dist1, _, _ = render_field_eval(net, o, d, -d, 0.01, 10.0, 64, 0, ray_chunk=200)
+    finally:
+        os.environ.pop("NERF_CHAIN", None)
+    os.environ["NERF_CHAIN"] = "0"
+    try:
+        rgb0, dist0, _, _ = render_field_eval(net, o, d, -d, 0.01, 10.0, 64, 0, ray_chunk=200)
+    finally:
+        os.environ.pop("NERF_CHAIN", None)
+    torch.cuda.synchronize()
+    assert ((rgb1 - rgb0).abs().max() / rgb0.abs().max()).item() < 1e-5
+    assert ((dist1 - dist0).abs().max() / dist0.abs().max()).item() < 1e-5
+
+
+def test_chain_gradients_match_per_layer(dev, h16):
+    net = _net(dev, seed=2)
+    b = _rays(256, 64, seed=5)
+    grads = []
+    for chain in (True, False):
+        os.environ["NERF_CHAIN"] = "1" if chain else "0"
+        try:
+            net.zero_grad()
+            o, d = b["o"].to(dev).requires_grad_(), b["d"].to(dev)
+            rgb, dist, _, _ = render_field(net, o, d, -d, b["noise"].to(dev), 0.01, 10.0, 64, 0)
+            (rgb.square().sum() + 0.1 * dist.sum()).backward()
+            torch.cuda.synchronize()
+            grads.append([p.grad.clone() for p in net.parameters()] + [o.grad.clone()])
+        finally:
+            os.environ.pop("NERF_CHAIN", None)
+    for g1, g0 in zip(*grads):
+        assert ((g1 - g0).norm() / g0.norm().clamp_min(1e-30)).item() < 1e-5
