@@ -38,6 +38,7 @@ constexpr int SHALF = 256 * 16 + 128;       // one k-half of a 256-row slot (+ b
 constexpr int SPLANE = 2 * SHALF;
 constexpr int SBYTES = 2 * SPLANE;          // two planes (fp16 hi / lo)
 constexpr int DMA_PER_STEP = 4;             // LDS-DMA instructions per wave and k-step
+constexpr int STG_LD = 36;                  // floats per row of a wave's epilogue staging tile (32 + pad)
 
 // topology (hidden width 256, colour width 128): k-steps of each layer's weight image,
 // k-steps taken from the register tile, from an encoding, output width
@@ -96,6 +97,7 @@ constexpr int CT = kbase(CNL);   // k-steps of the whole chain
 struct ChainState {
     char* ring; char* leb16; float* lbias; uint32_t* lcm;   // leb16: [2][256 rows][16 B], exponent in word 0
     char* lenc; float* lrp; float* lrd;                      // encoding tile [128][64], row maxima [128] x 2
+    float* stage;                                            // this wave's [32][STG_LD] epilogue tile
     int tid, lane, sl, hf;
     size_t m0, row;
     int er;                          // row exponent of the current A operand
@@ -208,23 +210,46 @@ __device__ __forceinline__ void chain_kstep(const ChainFwdArgs& p, ChainState& s
     const char* slot = st.ring + (TT % NSLOT) * SBYTES;
     const uint4& ah = s < nreg ? st.act_hi[s < nreg ? s : 0] : st.enc_hi[s < nreg ? 0 : s - nreg];
     const uint4& al = s < nreg ? st.act_lo[s < nreg ? s : 0] : st.enc_lo[s < nreg ? 0 : s - nreg];
+    // weight fragments two tiles ahead of their MFMAs (3 rotating pairs); the scheduling
+    // barriers pin the order so every LDS read has two MFMA groups (~190 cycles) to land
+    const char* bbase = slot + st.hf * SHALF + st.sl * 16;
+    uint4 bh[3], bl[3];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        bh[j] = *reinterpret_cast<const uint4*>(bbase + 32 * 16 * j);
+        bl[j] = *reinterpret_cast<const uint4*>(bbase + 32 * 16 * j + SPLANE);
+    }
 #pragma unroll
     for (int j = 0; j < ntj; ++j) {
-        const char* b = slot + st.hf * SHALF + (32 * j + st.sl) * 16;
-        const uint4 bh = *reinterpret_cast<const uint4*>(b);
-        const uint4 bl = *reinterpret_cast<const uint4*>(b + SPLANE);
-        st.acc[j] = cmfma(bh, al, st.acc[j]);   // hi . lo
-        st.acc[j] = cmfma(bl, ah, st.acc[j]);   // lo . hi
-        st.acc[j] = cmfma(bh, ah, st.acc[j]);   // hi . hi
-    }
-    // weight fragments one tile ahead of their MFMAs (keeps few fragments live)
-    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        if (j + 2 < ntj) {
+            bh[(j + 2) % 3] = *reinterpret_cast<const uint4*>(bbase + 32 * 16 * (j + 2));
+            bl[(j + 2) % 3] = *reinterpret_cast<const uint4*>(bbase + 32 * 16 * (j + 2) + SPLANE);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        st.acc[j] = cmfma(bh[j % 3], al, st.acc[j]);   // hi . lo
+        st.acc[j] = cmfma(bl[j % 3], ah, st.acc[j]);   // lo . hi
+        st.acc[j] = cmfma(bh[j % 3], ah, st.acc[j]);   // hi . hi
+        if constexpr (l > 0 && s < nreg) {
+            if (j == 1 && p.L[l - 1].out) {
+                // the previous layer's output, stored beside this layer's MFMAs instead of in a
+                // burst at its epilogue: this k-step's 8 features of the row, rebuilt from the
+                // fp16 pair (hi + lo) 2^-e -- the value the next layer consumed, within 2^-22
+                // relative of the f32 epilogue result
+                const ch16x2* h = reinterpret_cast<const ch16x2*>(&ah);
+                const ch16x2* o = reinterpret_cast<const ch16x2*>(&al);
+                float v[8];
 #pragma unroll
-    for (int j = 1; j < ntj; ++j) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+                for (int t = 0; t < 4; ++t) {
+                    v[2 * t] = __builtin_amdgcn_ldexpf((float)h[t][0] + (float)o[t][0], -st.er);
+                    v[2 * t + 1] = __builtin_amdgcn_ldexpf((float)h[t][1] + (float)o[t][1], -st.er);
+                }
+                float* dst = p.L[l - 1].out + st.row * p.L[l - 1].ldo + 16 * s + 8 * st.hf;
+                *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+                *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
 }
 
 template <int l, int s>
@@ -257,12 +282,14 @@ __device__ __forceinline__ void chain_layer(const ChainFwdArgs& p, ChainState& s
     chain_ksteps<l, 0>(p, st);
     chain_tick(p, st, st.t_mma);
 
+    // the colour layer stores its output here; every other layer's output is stored by the
+    // next layer's k-steps (chain_kstep)
+    const bool store_here = l == CNL - 1 && L.out != nullptr;
     const char* eb = st.leb16 + (l & 1) * 4096;
     const float* bb = st.lbias + (l & 1) * 256;
     float rmx = 0.f;
 #pragma unroll
     for (int j = 0; j < ntj; ++j) {
-        float cm[16];
         uint32_t w = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -278,28 +305,47 @@ __device__ __forceinline__ void chain_layer(const ChainFwdArgs& p, ChainState& s
             if (relu) x = make_float4(fmaxf(x.x, 0.f), fmaxf(x.y, 0.f), fmaxf(x.z, 0.f), fmaxf(x.w, 0.f));
             st.acc[j][4 * q + 0] = x.x; st.acc[j][4 * q + 1] = x.y;
             st.acc[j][4 * q + 2] = x.z; st.acc[j][4 * q + 3] = x.w;
-            if (L.out) *reinterpret_cast<float4*>(L.out + st.row * L.ldo + f0) = x;
             w |= ((x.x > 0.f ? 1u : 0u) | (x.y > 0.f ? 2u : 0u) | (x.z > 0.f ? 4u : 0u) | (x.w > 0.f ? 8u : 0u))
                  << (8 * q + 4 * st.hf);
-            cm[4 * q + 0] = fabsf(x.x); cm[4 * q + 1] = fabsf(x.y);
-            cm[4 * q + 2] = fabsf(x.z); cm[4 * q + 3] = fabsf(x.w);
-            rmx = fmaxf(rmx, fmaxf(fmaxf(cm[4 * q], cm[4 * q + 1]), fmaxf(cm[4 * q + 2], cm[4 * q + 3])));
+            rmx = fmaxf(rmx, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+            if (store_here || L.cmax)   // this lane's quad into the wave's staging tile (row sl, 32 features)
+                *reinterpret_cast<float4*>(st.stage + st.sl * STG_LD + 8 * q + 4 * st.hf) = x;
         }
         if (L.mask) {
             w |= (uint32_t)__shfl_xor((int)w, 32, 64);
             if (st.hf == 0) L.mask[st.row * L.ldmask + j] = w;
         }
-        if (L.cmax) {
-            // column maxima of this tile over the wave's 32 rows (halving butterfly: lane sl
-            // keeps feature `base` of the 16 its half-wave holds), then over the waves in LDS
-            int base = 0;
-            bfly_max<8, 16>(cm, st.sl, base);
-            bfly_max<4, 8>(cm, st.sl, base);
-            bfly_max<2, 4>(cm, st.sl, base);
-            bfly_max<1, 2>(cm, st.sl, base);
-            bfly_max<0, 1>(cm, st.sl, base);
-            atomicMax(st.lcm + (l & 1) * 256 + 32 * j + 8 * (base >> 2) + 4 * st.hf + (base & 3),
-                      __float_as_uint(cm[0]));
+        if (store_here || L.cmax) {
+            // read the tile back row-contiguous: lane l holds rows 8 r + (l >> 3) and features
+            // 4 (l & 7) .. + 3, so each store covers 8 whole 128-byte row pieces (the
+            // accumulator layout would scatter 64 16-byte pieces over 32 rows); the column
+            // maxima reduce over 4 rows in-lane and over the 8 lanes of equal (l & 7)
+            const int rr = st.lane >> 3, cq = st.lane & 7;
+            float4 cmx = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float4 v = *reinterpret_cast<const float4*>(st.stage + (8 * r + rr) * STG_LD + 4 * cq);
+                if (store_here)
+                    *reinterpret_cast<float4*>(L.out + (st.m0 + 32 * (st.tid >> 6) + 8 * r + rr) * L.ldo + 32 * j + 4 * cq) = v;
+                cmx = make_float4(fmaxf(cmx.x, fabsf(v.x)), fmaxf(cmx.y, fabsf(v.y)), fmaxf(cmx.z, fabsf(v.z)),
+                                  fmaxf(cmx.w, fabsf(v.w)));
+            }
+            if (L.cmax) {
+#pragma unroll
+                for (int off = 8; off <= 32; off <<= 1) {
+                    cmx.x = fmaxf(cmx.x, __shfl_xor(cmx.x, off, 64));
+                    cmx.y = fmaxf(cmx.y, __shfl_xor(cmx.y, off, 64));
+                    cmx.z = fmaxf(cmx.z, __shfl_xor(cmx.z, off, 64));
+                    cmx.w = fmaxf(cmx.w, __shfl_xor(cmx.w, off, 64));
+                }
+                if (st.lane < 8) {
+                    uint32_t* g = st.lcm + (l & 1) * 256 + 32 * j + 4 * cq;
+                    atomicMax(g + 0, __float_as_uint(cmx.x));
+                    atomicMax(g + 1, __float_as_uint(cmx.y));
+                    atomicMax(g + 2, __float_as_uint(cmx.z));
+                    atomicMax(g + 3, __float_as_uint(cmx.w));
+                }
+            }
         }
     }
     chain_tick(p, st, st.t_epi);
@@ -340,7 +386,8 @@ __device__ __forceinline__ void chain_layer(const ChainFwdArgs& p, ChainState& s
 
 __global__ __launch_bounds__(256) void k_mlp_chain_fwd(ChainFwdArgs p) {
     constexpr int RING = NSLOT * SBYTES, LEB = 2 * 4096, LBIAS = 2 * 256 * 4, LCM = 2 * 256 * 4, LENC = 128 * 256;
-    __shared__ __attribute__((aligned(16))) char smem[RING + LEB + LBIAS + LCM + LENC + 2 * 512];
+    constexpr int LSTG = 4 * 32 * STG_LD * 4;
+    __shared__ __attribute__((aligned(16))) char smem[RING + LEB + LBIAS + LCM + LENC + 2 * 512 + LSTG];
     ChainState st;
     st.ring = smem;
     st.leb16 = smem + RING;
@@ -349,6 +396,7 @@ __global__ __launch_bounds__(256) void k_mlp_chain_fwd(ChainFwdArgs p) {
     st.lenc = smem + RING + LEB + LBIAS + LCM;
     st.lrp = reinterpret_cast<float*>(st.lenc + LENC);
     st.lrd = st.lrp + 128;
+    st.stage = reinterpret_cast<float*>(st.lenc + LENC + 2 * 512) + (threadIdx.x >> 6) * 32 * STG_LD;
     st.tid = threadIdx.x;
     st.lane = st.tid & 63; st.sl = st.lane & 31; st.hf = st.lane >> 5;
     st.m0 = (size_t)blockIdx.x * CROWS;

@@ -48,15 +48,16 @@ def main():
             print(f"chain={chain} keep={keep}: forward {s.elapsed_time(e) / 10 * 1e3:8.1f} us", flush=True)
     os.environ["NERF_CHAIN"] = "1"
     Np = R * S
-    buf = torch.zeros((Np // 128) * 6, dtype=torch.int64, device=dev)
-    _hip.lib().nerf_chain_debug_stamps(ctypes.c_void_p(buf.data_ptr()))
-    fwd(True)
-    torch.cuda.synchronize()
-    _hip.lib().nerf_chain_debug_stamps(None)
-    st = buf.cpu().numpy().reshape(-1, 6).astype(np.float64)
-    med = np.median(st[:, :5], axis=0)
-    print(f"chain phase cycles per block (median over {len(st)} blocks, wave 0): dma wait {med[0]:.0f}  "
-          f"barrier {med[1]:.0f}  mfma section {med[2]:.0f}  epilogue {med[3]:.0f}  total {med[4]:.0f}", flush=True)
+    for keep in (True, False):
+        buf = torch.zeros((Np // 128) * 6, dtype=torch.int64, device=dev)
+        _hip.lib().nerf_chain_debug_stamps(ctypes.c_void_p(buf.data_ptr()))
+        fwd(keep)
+        torch.cuda.synchronize()
+        _hip.lib().nerf_chain_debug_stamps(None)
+        st = buf.cpu().numpy().reshape(-1, 6).astype(np.float64)
+        med = np.median(st[:, :5], axis=0)
+        print(f"keep={keep}: chain phase cycles per block (median over {len(st)} blocks, wave 0): dma wait {med[0]:.0f}  "
+              f"barrier {med[1]:.0f}  mfma section {med[2]:.0f}  epilogue {med[3]:.0f}  total {med[4]:.0f}", flush=True)
 
 
 if __name__ == "__main__":
