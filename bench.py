@@ -262,8 +262,8 @@ def main():
         tpath = os.path.join(ROOT, "profiles", "r01", "gemm_traffic.json")
         # template arguments of the 256x256-tile forward launch per arithmetic (older summaries
         # predate the trailing fp16-pair flag)
-        fwd_tags = {"bf16x6": ("<256, 256, 2, 2, 0, true>", "<256, 256, 2, 2, 0, true, false>"),
-                    "f16x3": ("<256, 256, 2, 2, 0, true, true>",)}.get(args.gemm_precision, ())
+        fwd_tags = {"bf16x6": ("<256, 256, 2, 2, 0, true>", "<256, 256, 2, 2, 0, true, false"),
+                    "f16x3": ("<128, 256, 2, 2, 0, true, true, 2>",)}.get(args.gemm_precision, ())
         if fwd_tags and os.path.exists(tpath):
             # HBM bytes of one 256x256-tile forward launch (131072 x 256 x 256, mask out) from
             # the committed rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE); algorithmic:
@@ -272,8 +272,8 @@ def main():
             fwd = [x for x in t["launches"] if any(tag in x["kernel"] for tag in fwd_tags)]
             if fwd:
                 traffic = fwd[0]["bytes"]
-                traffic_note = ("k_gemm_nt_x6<256,256> forward, one launch, bytes from profiles/r01/gemm_traffic.json "
-                                "(algorithmic 2.73e8)")
+                traffic_note = (f"{fwd[0]['kernel'].split('(')[0]} forward 131072x256x256, one launch, bytes from "
+                                "profiles/r01/gemm_traffic.json (algorithmic 2.73e8)")
         roof = {"bound": "mfma", "kernel": kname,
                 "achieved": achieved, "peak": peak, "unit": "TFLOP/s (f32-equivalent)",
                 "frac": (achieved / peak) if achieved else None, "traffic": traffic, "traffic_note": traffic_note,

@@ -270,7 +270,10 @@ int nerf_chamfer_nn(const float* x, int p, const float* y, int q, int64_t* idx, 
 #define NERF_SAMPLE_MAX_RAYS 4096
 #define NERF_SAMPLE_MAX_ROUNDS 64
 int nerf_sample_rays(int n_pix, int n_rays, uint64_t seed, int width, int height, const float* img,
-                     int64_t* idx, float* pixels, float* rgb, int* status, void* stream);
+                     int64_t* idx, float* pixels, float* rgb, int* status, uint64_t* seed_counter,
+                     void* stream);
+/* seed_counter (optional, device uint64): mixed into the Philox key and advanced by one per
+ * launch on the device -- successive replays of a captured hipGraph draw new rays. */
 
 /* Batched 4x4 inverse (torch.inverse / linalg.inv_ex, common.py:139-141, training.py:255-257):
  * Gauss-Jordan with partial pivoting, a [n][4][4] -> out [n][4][4]. */

@@ -56,10 +56,19 @@ constexpr int SR_MAX_ROUNDS = NERF_SAMPLE_MAX_ROUNDS;
 __global__ __launch_bounds__(SR_THREADS) void k_sample_rays(int n_pix, int R, uint2 key, int width, int height,
                                                             const float* __restrict__ img,
                                                             int64_t* __restrict__ idx, float* __restrict__ pix,
-                                                            float* __restrict__ rgb, int* __restrict__ status) {
+                                                            float* __restrict__ rgb, int* __restrict__ status,
+                                                            unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t table[SR_TABLE];
     __shared__ uint32_t owner[SR_TABLE];
     const int tid = threadIdx.x;
+    // device step counter (graph replays): the key mixes in the counter, thread 0 advances it
+    // once every thread has read it (the kernel is a single workgroup)
+    const unsigned long long c = ctr ? *ctr : 0ull;
+    if (ctr) {
+        const unsigned long long m = (c + 1) * 0x9E3779B97F4A7C15ull;
+        key.x ^= (uint32_t)m;
+        key.y ^= (uint32_t)(m >> 32);
+    }
     for (int i = tid; i < SR_TABLE; i += SR_THREADS) {
         table[i] = SR_EMPTY;
         owner[i] = 0xFFFFFFFFu;
@@ -117,6 +126,10 @@ __global__ __launch_bounds__(SR_THREADS) void k_sample_rays(int n_pix, int R, ui
             rgb[3 * j + 1] = img[hw + v];
             rgb[3 * j + 2] = img[2 * hw + v];
         }
+    }
+    if (ctr != nullptr) {
+        __syncthreads();
+        if (tid == 0) *ctr = c + 1;
     }
 }
 
@@ -402,7 +415,8 @@ __global__ void k_ray_loss_bwd(const float* __restrict__ rgb, const float* __res
 using namespace nerf;
 
 extern "C" int nerf_sample_rays(int n_pix, int n_rays, uint64_t seed, int width, int height, const float* img,
-                                int64_t* idx, float* pixels, float* rgb, int* status, void* stream) {
+                                int64_t* idx, float* pixels, float* rgb, int* status, uint64_t* seed_counter,
+                                void* stream) {
     NERF_CHECK_PTR(idx);
     NERF_CHECK(n_rays > 0 && n_rays <= NERF_SAMPLE_MAX_RAYS, "%s: n_rays=%d outside 1..%d", __func__, n_rays,
                NERF_SAMPLE_MAX_RAYS);
@@ -414,7 +428,8 @@ extern "C" int nerf_sample_rays(int n_pix, int n_rays, uint64_t seed, int width,
                __func__);
     const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
     hipLaunchKernelGGL(k_sample_rays, dim3(1), dim3(SR_THREADS), 0, as_stream(stream), n_pix, n_rays, key,
-                       width, height, img, idx, pixels, rgb, status);
+                       width, height, img, idx, pixels, rgb, status,
+                       reinterpret_cast<unsigned long long*>(seed_counter));
     return check_launch(__func__);
 }
 

@@ -75,7 +75,7 @@ _SIGS = {
     "nerf_gemm_get_precision": ([], _c_i),
     "nerf_gemm_debug_ablate": ([_c_i], _c_i),
     "nerf_gemm_debug_stamps": ([_c_p], _c_i),
-    "nerf_sample_rays": ([_c_i, _c_i, ctypes.c_uint64, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_sample_rays": ([_c_i, _c_i, ctypes.c_uint64, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_mat4_inv": ([_c_p, _c_i, _c_p, _c_p], _c_i),
     "nerf_pose_c2w": ([_c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_unproject_matrix": ([_c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
@@ -270,9 +270,11 @@ def adam_step(param, grad, exp_avg, exp_avg_sq, hyper):
           _ptr(hyper), _stream())
 
 
-def sample_rays(n_pix, n_rays, seed, width, height, img, idx, pixels=None, rgb=None, status=None):
+def sample_rays(n_pix, n_rays, seed, width, height, img, idx, pixels=None, rgb=None, status=None, seed_counter=None):
+    """seed_counter: optional device int64 [1], mixed into the key and advanced on the device
+    (graph replays draw new rays)."""
     _call("nerf_sample_rays", int(n_pix), int(n_rays), int(seed) & 0xFFFFFFFFFFFFFFFF, int(width), int(height),
-          _ptr(img), _ptr(idx), _ptr(pixels), _ptr(rgb), _ptr(status), _stream())
+          _ptr(img), _ptr(idx), _ptr(pixels), _ptr(rgb), _ptr(status), _ptr(seed_counter), _stream())
 
 
 def mat4_inv(a, out):

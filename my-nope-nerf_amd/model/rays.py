@@ -228,10 +228,11 @@ def ray_loss(rgb, rgb_gt, depth_pred, depth_gt, depth_mask, rgb_l1: bool, w_rgb:
 
 
 # ------------------------------------------------------------------ ray sampling
-def sample_rays(n_pix, n_rays, width, height, img=None, seed=None, device=None):
+def sample_rays(n_pix, n_rays, width, height, img=None, seed=None, device=None, seed_counter=None):
     """Device replacement of ``randperm(n_pix)[:n_rays]`` + the pixel / colour gathers:
     returns (ray_idx int64 [R], pixels [1,R,2], rgb_gt [1,R,3] or None).  ``seed``
-    defaults to a draw from torch's host generator (deterministic under manual_seed)."""
+    defaults to a draw from torch's host generator (deterministic under manual_seed);
+    ``seed_counter`` (device int64 [1]) makes the draw advance on the device instead."""
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item())
     dev = device if device is not None else img.device
@@ -242,7 +243,7 @@ def sample_rays(n_pix, n_rays, width, height, img=None, seed=None, device=None):
     if img is not None:
         imc = _f32c(img)
         rgb = torch.empty(1, n_rays, 3, device=dev, dtype=torch.float32)
-    _hip.sample_rays(n_pix, n_rays, seed, width, height, imc, idx, pix, rgb)
+    _hip.sample_rays(n_pix, n_rays, seed, width, height, imc, idx, pix, rgb, seed_counter=seed_counter)
     return idx, pix, rgb
 
 

@@ -64,6 +64,14 @@ class Trainer(object):
         self.inject = None
         self.world_size = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank() if self.world_size > 1 else 0
+        # graph-capture mode (enable_graph_rng): the ray draw keys on a device step counter
+        self.seed_counter = None
+
+    def enable_graph_rng(self):
+        """Make a step replayable from a captured hipGraph with fresh randomness: the ray
+        sampler keys on a device counter it advances itself (stratified noise comes from
+        torch.rand, whose Philox offsets graph replays already advance)."""
+        self.seed_counter = torch.zeros(1, dtype=torch.int64, device=self.device)
 
     # ------------------------------------------------------------------ step
     def _modules_and_optims(self):
@@ -159,6 +167,11 @@ class Trainer(object):
 
         def draw():
             if on_dev:
+                if self.seed_counter is not None:
+                    # graph-capture mode: a fixed per-rank key and a device step counter, so a
+                    # replayed step draws new rays without a host-side seed
+                    seed = (0x2545F4914F6CDD1D + self.rank * 0x632BE59BD9B4E019) & 0xFFFFFFFFFFFFFFFF
+                    return sample_rays_dev(n_pix, R, w, h, img[0], seed=seed, seed_counter=self.seed_counter)
                 # host-generator seed (reproducible under torch.manual_seed), decorrelated per
                 # rank so data-parallel ranks render different rays
                 seed = int(torch.randint(0, 2 ** 62, (1,)).item()) + self.rank * 0x632BE59BD9B4E019

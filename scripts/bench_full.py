@@ -51,19 +51,13 @@ def scene(dev):
     return datas, c2w
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--gemm-precision", choices=["f32", "bf16x6", "f16x3"], default="f16x3")
-    args = ap.parse_args()
+def setup(dev, capturable=False):
+    """Trainer with pose + distortion learning and the image-pair terms (config 3) on the
+    two-view synthetic scene -> (trainer, [data view 0, data view 1]).  capturable: the
+    pose / distortion Adams keep their step counts on the device (hipGraph capture)."""
     import model as mdl
-    from model import _hip
     from model.optim import HipAdam
     from tests.helpers import make_cfg
-    dev = torch.device("cuda", 0)
-    _hip.load_library()
-    _hip.gemm_set_precision({"f32": 0, "bf16x6": 1, "f16x3": 2}[args.gemm_precision])
     cfg = make_cfg(hidden=HIDDEN, S=SAMPLES)
     t = cfg["training"]
     t["n_training_points"] = RAYS
@@ -76,13 +70,52 @@ def main():
     opt = HipAdam(nn_model.parameters(), lr=1e-3)
     pose = mdl.LearnPose(2, True, True, cfg, init_c2w=c2w.clone()).to(dev)
     distn = mdl.Learn_Distortion(2, True, True, cfg).to(dev)
-    opt_pose = torch.optim.Adam(pose.parameters(), lr=5e-4)          # train.py:100, :118
-    opt_dist = torch.optim.Adam(distn.parameters(), lr=5e-4)
+    opt_pose = torch.optim.Adam(pose.parameters(), lr=5e-4, capturable=capturable)   # train.py:100, :118
+    opt_dist = torch.optim.Adam(distn.parameters(), lr=5e-4, capturable=capturable)
     tr = mdl.Trainer(nn_model, opt, t, device=dev, optimizer_pose=opt_pose, pose_param_net=pose,
                      optimizer_distortion=opt_dist, distortion_net=distn)
+    return tr, datas
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--gemm-precision", choices=["f32", "bf16x6", "f16x3"], default="f16x3")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay hipGraphs of the two views' captured train_steps (the ray draw keys on a "
+                         "device counter, so every replay trains on new rays) instead of eager enqueue")
+    args = ap.parse_args()
+    from model import _hip
+    dev = torch.device("cuda", 0)
+    _hip.load_library()
+    _hip.gemm_set_precision({"f32": 0, "bf16x6": 1, "f16x3": 2}[args.gemm_precision])
+    tr, datas = setup(dev, capturable=args.graph)
 
     def one(i):
         return tr.train_step(datas[i % 2], it=i + 1, epoch=0, scheduling_start=0)
+
+    if args.graph:
+        # the host enqueue of this step (~4.4 ms: pose / distortion autograd, two torch Adams,
+        # ~150 launches) exceeds its GPU time; one graph per view replays the same launches
+        tr.enable_graph_rng()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for i in range(args.warmup):
+                one(i)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        graphs, outs = [], []
+        for v in range(2):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                outs.append(tr.train_step(datas[v], it=1, epoch=0, scheduling_start=0))
+            graphs.append(g)
+
+        def one(i):  # noqa: F811
+            graphs[i % 2].replay()
+            return outs[i % 2]
 
     for i in range(args.warmup):
         one(i)
@@ -99,6 +132,8 @@ def main():
            "value": RAYS * args.steps / el, "unit": "rays/s", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": 1e3 * el / args.steps, "dtype": "f32",
            "gemm_arithmetic": args.gemm_precision, "data": "synthetic two-view V_KITTI-shaped scene",
+           "execution": ("hipGraph replay of the captured train_step per view (device ray-draw counter: new rays "
+                         "every replay)") if args.graph else "eager enqueue",
            "config": {"workload": "config 3: 188x621, 1024 rays x 128 samples, D=256, pose+distortion learned, "
                                   "pc chamfer 7285 points, rgb_s reprojection"},
            "losses": {k: float(ld[k].detach()) for k in ("loss", "loss_rgb", "loss_depth", "loss_pc", "loss_rgb_s")},

@@ -46,9 +46,9 @@ def test_abi_version_and_error_path(lib):
     rc = lib.nerf_composite_fwd(None, None, 1, 1, 0, None, None, None, None)
     assert rc == -1
     # ray prologue: sampler size limits, camera rays without outputs
-    rc = lib.nerf_sample_rays(100, 80, 1, 10, 10, None, 1, None, None, None, None)
+    rc = lib.nerf_sample_rays(100, 80, 1, 10, 10, None, 1, None, None, None, None, None)
     assert rc == -1 and b"2*n_rays" in lib.nerf_hip_last_error()
-    rc = lib.nerf_sample_rays(10 ** 6, 5000, 1, 1000, 1000, None, 1, None, None, None, None)
+    rc = lib.nerf_sample_rays(10 ** 6, 5000, 1, 1000, 1000, None, 1, None, None, None, None, None)
     assert rc == -1 and b"n_rays" in lib.nerf_hip_last_error()
     rc = lib.nerf_camera_rays(1, 1, None, 4, 1, None, 1, None, 1, 1, None, None)
     assert rc == -1 and b"cam" in lib.nerf_hip_last_error()

@@ -202,3 +202,19 @@ def test_ray_loss_matches_torch(dev, kind, mask_kind):
     assert _rel(r_d.grad, r_c.grad) < 1e-5
     assert _rel(dp_d.grad, dp_c.grad) < 1e-5 if mask_kind != "none_valid" else dp_d.grad.abs().max() == 0
     assert _rel(dg_d.grad, dg_c.grad) < 1e-5 if mask_kind != "none_valid" else dg_d.grad.abs().max() == 0
+
+
+def test_sample_rays_device_counter(dev):
+    """seed_counter: each launch advances the device counter by one and keys the draw on
+    it, so identical launches (a replayed hipGraph) draw different, still distinct, sets."""
+    H, W, R = 40, 50, 512
+    img = torch.rand(3, H, W, device=dev)
+    ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+    draws = [rays.sample_rays(H * W, R, W, H, img, seed=99, seed_counter=ctr)[0].cpu() for _ in range(3)]
+    assert ctr.item() == 3
+    for d in draws:
+        assert d.unique().numel() == R
+    assert not torch.equal(draws[0], draws[1]) and not torch.equal(draws[1], draws[2])
+    ctr.zero_()
+    again = rays.sample_rays(H * W, R, W, H, img, seed=99, seed_counter=ctr)[0].cpu()
+    assert torch.equal(again, draws[0])                       # deterministic in (seed, counter)
