@@ -15,9 +15,17 @@ timed live with hipEvents around every GEMM launch of the timed steps), "cpu_bas
 (the oracle CPU restatement of the same step on this host's cores, bounded sample) and
 "alt_gemm" (the same workload with the other GEMM arithmetics).  The GEMMs compute f32
 products on the exact-f32 MFMA (f32), as a 3-word bf16 split with six MFMA products
-accumulated in f32 (bf16x6), or -- forward and backward-data GEMMs -- as a row-scaled
-2-word fp16 split with three products (f16x3; its weight gradients as bf16x6).  All three
-are f32-accurate (DESIGN.md section 4, tests/test_gpu_kernels.py::test_split_accuracy).
+accumulated in f32 (bf16x6), or as a row-scaled 2-word fp16 split with three products
+(f16x3, default; forward, input gradient and weight gradient).  All three are f32-accurate
+(DESIGN.md section 4, tests/test_gpu_kernels.py::test_split_accuracy); the exact-f32
+number of the same run is "value_exact_f32".
+
+"roofline" names the GEMM kind with the most time per step (per_kind lists all three)
+and prices it against BOTH ceilings: its MFMA work at the dense MFMA rate of the
+arithmetic that ran, and its algorithmic HBM bytes at 8 TB/s; "bound" is the ceiling
+with the larger ideal time.
+
+    python bench.py --gpus N     (N > 1 without WORLD_SIZE: spawns N ranks itself)
 """
 from __future__ import annotations
 
@@ -110,40 +118,77 @@ def algorithmic_gemm_flops(net, n_samples, split=False):
 
 
 PRECISION = {"f32": 0, "bf16x6": 1, "f16x3": 2}
+DTYPE = {"f32": "f32", "bf16x6": "f32 (bf16x6 emulation)", "f16x3": "f32 (f16x3 emulation)"}
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+KIND_NAMES = {
+    "fwd": "forward NT (nerf_linear_fwd)",
+    "dx": "input-gradient NT (nerf_linear_bwd_data)",
+    "dw": "weight-gradient TN (nerf_linear_bwd_weight; algorithmic bytes exclude the split-K slabs)",
+}
+KERNEL = {
+    "f16x3": {"fwd": "k_gemm_nt_x6<128,256,2,2,0,true,true,2> (fp16 pair, 3 products)",
+              "dx": "k_gemm_nt_x6<128,256,2,2,1,true,true,2> (fp16 pair, 3 products)",
+              "dw": "k_gemm_tn_x6<256,256,2,2,true> (fp16 pair, 3 products)"},
+    "bf16x6": {"fwd": "k_gemm_nt_x6<256,256,2,2,0,true> (bf16x3 split, 6 products)",
+               "dx": "k_gemm_nt_x6<256,256,2,2,1,true> (bf16x3 split, 6 products)",
+               "dw": "k_gemm_tn_x6<256,256,2,2,false> (bf16x3 split, 6 products)"},
+    "f32": {"fwd": "k_gemm_nt<256,256,2,4,0> (f32 MFMA 32x32x2)", "dx": "k_gemm_nt<256,256,2,4,1> (f32 MFMA 32x32x2)",
+            "dw": "k_gemm_tn<256,256,2,4> (f32 MFMA 32x32x2)"},
+}
 
 
-def gemm_peak(mode, nt_flops, tn_flops):
-    """f32-equivalent MFMA peak of the GEMM family in arithmetic `mode`: the dense MFMA rate
-    divided by the products per f32 product (f32: 1 on the f32 MFMA; bf16x6: 6; f16x3: 3 for
-    forward / input gradient, 6 for the weight gradients), weighted by the FLOPs each runs."""
-    if mode == "f32":
-        return FP32_MFMA_PEAK_TFLOPS
-    if mode == "bf16x6":
-        return BF16_MFMA_PEAK_TFLOPS / 6
-    t = nt_flops / (BF16_MFMA_PEAK_TFLOPS / 3) + tn_flops / (BF16_MFMA_PEAK_TFLOPS / 6)
-    return (nt_flops + tn_flops) / t
+def kind_roofline(rec):
+    """Both ceilings of one GEMM kind from its live hipEvent records (per-launch averages):
+    MFMA -- the launches' MFMA work (f32 FLOPs x products per f32 product) at the dense
+    MFMA rate of the arithmetic that ran; HBM -- their algorithmic bytes at 8 TB/s.  The
+    binding ceiling is the one with the larger ideal time."""
+    if rec["launches"] == 0 or rec["ms"] <= 0:
+        return None
+    n = rec["launches"]
+    us = 1e3 * rec["ms"] / n
+    peak_rate = FP32_MFMA_PEAK_TFLOPS if rec["exact_f32"] else BF16_MFMA_PEAK_TFLOPS
+    t_mfma_us = rec["mfma_flops"] / n / (peak_rate * 1e12) * 1e6
+    t_hbm_us = rec["bytes"] / n / (HBM_PEAK_GBS * 1e9) * 1e6
+    products = rec["mfma_flops"] / rec["flops"] if rec["flops"] else 1.0
+    return {"launches_per_step": None, "avg_launch_us": us,
+            "gflop_per_launch": rec["flops"] / n / 1e9, "mbytes_per_launch": rec["bytes"] / n / 1e6,
+            "products_per_f32_product": products,
+            "mfma": {"achieved_tflops_f32eq": rec["flops"] / n / (us * 1e-6) / 1e12,
+                     "peak_tflops_f32eq": peak_rate / products, "frac": t_mfma_us / us},
+            "hbm": {"achieved_gbs": rec["bytes"] / n / (us * 1e-6) / 1e9, "peak_gbs": HBM_PEAK_GBS,
+                    "frac": t_hbm_us / us},
+            "binding": "hbm" if t_hbm_us >= t_mfma_us else "mfma"}
+
+
+def lscpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def cpu_baseline(budget_s=20.0):
     """The oracle (CPU restatement of the reference step) on this host's cores."""
     from oracle import nerf_oracle as orc
-    from tests.helpers import synthetic_rays
     threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     if os.environ.get("OMP_NUM_THREADS", "").isdigit():      # the box's CPU share
         threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
     threads = max(1, threads)
     torch.set_num_threads(threads)
-    torch.manual_seed(42)
+    torch.manual_seed(42)                                   # the GPU run's NeRF init (build_trainer)
     net = orc.OracleNerf(hidden_dim=HIDDEN)
     opt = torch.optim.Adam(net.parameters(), lr=1e-3)
-    b = synthetic_rays(R=RAYS, S=SAMPLES, seed=3)
-    img = torch.rand(1, 3, H, W)
-    depth_img = 1.0 + 7.0 * torch.rand(1, 1, H, W)
-    ray_idx = torch.randperm(H * W)[:RAYS]
+    data, c2w = synthetic_scene(torch.device("cpu"))        # the GPU run's scene
+    g = torch.Generator().manual_seed(3)
+    ray_idx = torch.randperm(H * W, generator=g)[:RAYS]
+    noise = torch.rand(1, RAYS, SAMPLES, generator=g)
 
     def step():
-        orc.train_step_render(net, opt, img, depth_img, b["K"], b["c2w"], b["scale"], ray_idx,
-                              b["noise"], {"num_points": SAMPLES})
+        orc.train_step_render(net, opt, data["img"], data["img.depth"].unsqueeze(1), data["img.camera_mat"], c2w,
+                              data["img.scale_mat"], ray_idx, noise, {"num_points": SAMPLES})
 
     step()                                                  # warm-up
     n, t0 = 0, time.perf_counter()
@@ -153,9 +198,81 @@ def cpu_baseline(budget_s=20.0):
         el = time.perf_counter() - t0
         if el > budget_s or n >= 20:
             break
-    return {"value": RAYS * n / el, "unit": "rays/s", "cores": threads, "kind": "port",
-            "sample": f"oracle train step (torch CPU fp32), {RAYS} rays x {SAMPLES} samples, D={HIDDEN}, "
+    return {"value": RAYS * n / el, "unit": "rays/s", "cores": threads, "kind": "port", "cpu_model": lscpu_model(),
+            "sample": f"oracle train step (torch CPU fp32) on the GPU run's synthetic scene and NeRF init, "
+                      f"{RAYS} rays x {SAMPLES} samples, D={HIDDEN}, one fixed ray draw and noise (seed 3), "
                       f"{n} timed steps after 1 warm-up ({el:.1f} s)"}
+
+
+def spawn_ranks(n, argv, script=None):
+    """--gpus N > 1 without a launcher: run this script under torch.distributed.run as a
+    CHILD process (N ranks, one per GPU, rendezvous on 127.0.0.1) and return its exit
+    code.  Called before anything touches the GPU; the parent never initialises HIP."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")       # dmabuf IPC only on this driver
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__)] + list(argv)
+    log(f"bench: launching {n} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd, env=env)
+
+
+def init_ranks(args):
+    """(world, rank, local, device) from the launcher's env; refuses a --gpus that
+    disagrees with WORLD_SIZE."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU")
+    if args.plumbing:
+        if world > 1:
+            dist.init_process_group("gloo")
+        return world, rank, local, torch.device("cpu")
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local, torch.device("cuda", local)
+
+
+def plumbing(args, world, rank):
+    """CPU check of the multi-rank path (gloo): the launcher, the rank env and the
+    Trainer's fixed-layout gradient all-reduce on the real model / pose / distortion
+    parameter set, with rank 1 missing a gradient.  Prints a JSON line that says it is
+    a plumbing check, not a measurement."""
+    import model as mdl
+    cfg = make_cfg()
+    torch.manual_seed(0)
+    net = mdl.OfficialStaticNerf(cfg)
+    pose = mdl.LearnPose(2, True, True, cfg)
+    dist_net = mdl.Learn_Distortion(2, True, True, cfg)
+    tr = mdl.Trainer(net, None, cfg["training"], device=torch.device("cpu"), pose_param_net=pose,
+                     distortion_net=dist_net)
+    params = tr.bucket_params()
+    for i, p in enumerate(params):
+        p.grad = None if (rank == 1 and i == 0) else torch.full_like(p, float(rank + 1 + i))
+    t0 = time.perf_counter()
+    if world > 1:
+        tr.allreduce_grads()
+    el = time.perf_counter() - t0
+    for i, p in enumerate(params):
+        ranks_with = [r for r in range(world) if not (r == 1 and i == 0)]
+        want = sum(r + 1 + i for r in ranks_with) / world
+        if p.grad is None or not torch.allclose(p.grad, torch.full_like(p, want)):
+            raise RuntimeError(f"plumbing: parameter {i} not averaged over the ranks")
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({"plumbing": True, "n_gpus": world, "world_size": dist.get_world_size() if world > 1 else 1,
+                          "bucket_params": len(params), "bucket_elems": sum(p.numel() for p in params),
+                          "allreduce_s": el, "data": "CPU gloo plumbing check of the launcher and gradient "
+                                                    "all-reduce; not a measurement"}), flush=True)
 
 
 def main():
@@ -170,16 +287,19 @@ def main():
                          "3-word bf16 split (bf16x6), or the exact-f32 MFMA (f32); all f32-accurate")
     ap.add_argument("--no-alt", dest="alt", action="store_false",
                     help="skip timing the other GEMM arithmetics (reported as alt_gemm)")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="CPU gloo check of the rank launcher + gradient all-reduce (tests), no GPU")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world, rank, local, dev = init_ranks(args)
+    if args.plumbing:
+        plumbing(args, world, rank)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    world = dist.get_world_size() if world > 1 else 1
     from model import _hip
     _hip.load_library()
 
@@ -188,7 +308,8 @@ def main():
 
     def measure(precision, with_hooks=True):
         """W warm-up + K timed train steps with the GEMMs in `precision` (0 exact-f32 MFMA,
-        1 split-bf16, 2 fp16 pair); returns (max-over-ranks seconds, last loss dict, GEMM hook stats)."""
+        1 split-bf16, 2 fp16 pair); returns (max-over-ranks seconds, last loss dict, GEMM
+        hook stats, per-kind records, net, seconds of the instrumented pass)."""
         _hip.gemm_set_precision(precision)
         trainer, net = build_trainer(dev, c2w, cfg)
         torch.cuda.manual_seed(1000 + rank)                 # each rank samples its own rays
@@ -211,6 +332,7 @@ def main():
             if world > 1:
                 dist.barrier()
             t1 = time.perf_counter()
+            kinds = _hip.prof_read_kinds() if hooks else None
             stats = _hip.prof_read() if hooks else None
             _hip.prof_enable(False)
             el = t1 - t0
@@ -218,16 +340,19 @@ def main():
                 t = torch.tensor([el], device=dev, dtype=torch.float64)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 el = t.item()
-            return el, ld, stats
+            return el, ld, stats, kinds
 
         for i in range(args.warmup):
             one(i)
-        el, ld, _ = timed(args.warmup, False)
-        el_h, _, stats = timed(args.warmup + args.steps, True) if with_hooks else (None, None, None)
-        return el, ld, stats, net, el_h
+        el, ld, _, _ = timed(args.warmup, False)
+        if with_hooks:
+            el_h, _, stats, kinds = timed(args.warmup + args.steps, True)
+        else:
+            el_h = stats = kinds = None
+        return el, ld, stats, kinds, net, el_h
 
     main_prec = PRECISION[args.gemm_precision]
-    elapsed, ld, (gemm_ms, gemm_launches, _, gemm_union_ms), net, elapsed_hooks = measure(main_prec)
+    elapsed, ld, (gemm_ms, gemm_launches, _, gemm_union_ms), kinds, net, elapsed_hooks = measure(main_prec)
     alt = None
     if args.alt:
         # the other GEMM arithmetics on the same workload, reported beside the headline
@@ -235,8 +360,8 @@ def main():
         for name, prec in PRECISION.items():
             if prec == main_prec:
                 continue
-            el2, ld2, _, _, _ = measure(prec, with_hooks=False)
-            alt.append({"gemm_arithmetic": name, "value": world * RAYS / (el2 / args.steps),
+            el2, ld2, _, _, _, _ = measure(prec, with_hooks=False)
+            alt.append({"gemm_arithmetic": name, "dtype": DTYPE[name], "value": world * RAYS / (el2 / args.steps),
                         "ms_per_step": 1e3 * el2 / args.steps, "final_loss": ld2["loss"].detach().item()})
         _hip.gemm_set_precision(main_prec)
     loss = ld["loss"].detach().item()
@@ -246,54 +371,63 @@ def main():
 
     if rank == 0:
         ms = 1e3 * elapsed / args.steps
-        nt_fl, tn_fl = algorithmic_gemm_flops(net, RAYS * SAMPLES, split=True)
-        alg = (nt_fl + tn_fl) * args.steps
-        achieved = alg / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else None
-        # achieved: algorithmic FLOPs / summed per-launch durations (the contract's per-launch
-        # average).  The dW GEMMs run on a side stream concurrently with the dX chain, which
-        # stretches each launch; achieved_union divides by the union of the launch intervals.
-        achieved_union = alg / (gemm_union_ms * 1e-3) / 1e12 if gemm_union_ms > 0 else None
-        peak = gemm_peak(args.gemm_precision, nt_fl, tn_fl)
-        kname = {"bf16x6": "k_gemm_nt_x6/k_gemm_tn_x6 (f32 as 3xbf16, 6 products on MFMA 32x32x16 bf16, field MLP)",
-                 "f16x3": "k_gemm_nt_x6<H> (f32 as row-scaled 2xfp16, 3 products on MFMA 32x32x16 f16; fwd + dX) / "
-                          "k_gemm_tn_x6 (bf16x6; dW), field MLP",
-                 "f32": "k_gemm_nt/k_gemm_tn (FP32 MFMA 32x32x2, field MLP)"}[args.gemm_precision]
+        # per-kind rooflines (MFMA and HBM ceilings, per-launch averages of the live records)
+        per_kind = {}
+        for k, rec in kinds.items():
+            r = kind_roofline(rec)
+            if r is not None:
+                r["launches_per_step"] = rec["launches"] / args.steps
+                r["ms_per_step"] = rec["ms"] / args.steps
+                r["what"] = KIND_NAMES[k]
+                r["kernel"] = KERNEL[args.gemm_precision][k]
+                per_kind[k] = r
+        dom = max(per_kind, key=lambda k: per_kind[k]["ms_per_step"])
+        d = per_kind[dom]
+        bound = d["binding"]
+        ach, peak, unit = ((d["hbm"]["achieved_gbs"], HBM_PEAK_GBS, "GB/s") if bound == "hbm" else
+                           (d["mfma"]["achieved_tflops_f32eq"], d["mfma"]["peak_tflops_f32eq"],
+                            "TFLOP/s (f32-equivalent)"))
         traffic, traffic_note = None, None
-        tpath = os.path.join(ROOT, "profiles", "r01", "gemm_traffic.json")
-        # template arguments of the 256x256-tile forward launch per arithmetic (older summaries
-        # predate the trailing fp16-pair flag)
-        fwd_tags = {"bf16x6": ("<256, 256, 2, 2, 0, true>", "<256, 256, 2, 2, 0, true, false"),
-                    "f16x3": ("<128, 256, 2, 2, 0, true, true, 2>",)}.get(args.gemm_precision, ())
-        if fwd_tags and os.path.exists(tpath):
-            # HBM bytes of one 256x256-tile forward launch (131072 x 256 x 256, mask out) from
-            # the committed rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE); algorithmic:
-            # x 134.2 MB + y 134.2 MB + ReLU bits 4.2 MB + weight image 0.4 MB = 273 MB
+        tpath = os.path.join(ROOT, "profiles", "r02", "gemm_traffic.json")
+        if os.path.exists(tpath) and args.gemm_precision == "f16x3":
+            # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC
+            # passes (FETCH_SIZE x2 + WRITE_SIZE, the guide's gfx950 correction)
             t = json.load(open(tpath))
-            fwd = [x for x in t["launches"] if any(tag in x["kernel"] for tag in fwd_tags)]
-            if fwd:
-                traffic = fwd[0]["bytes"]
-                traffic_note = (f"{fwd[0]['kernel'].split('(')[0]} forward 131072x256x256, one launch, bytes from "
-                                "profiles/r01/gemm_traffic.json (algorithmic 2.73e8)")
-        roof = {"bound": "mfma", "kernel": kname,
-                "achieved": achieved, "peak": peak, "unit": "TFLOP/s (f32-equivalent)",
-                "frac": (achieved / peak) if achieved else None, "traffic": traffic, "traffic_note": traffic_note,
-                "achieved_union": achieved_union,
-                "frac_union": (achieved_union / peak) if achieved_union else None,
-                "algorithmic_gflop_per_step": alg / args.steps / 1e9,
-                "launches_per_step": gemm_launches / args.steps,
-                "avg_launch_us": 1e3 * gemm_ms / max(1, gemm_launches),
-                "gemm_ms_per_step": gemm_ms / args.steps,
-                "timing": "second timed pass of the same K steps with hipEvent pairs around every GEMM launch "
-                          "(ms_per_step of that pass: %.3f)" % (1e3 * elapsed_hooks / args.steps),
-                "gemm_union_ms_per_step": gemm_union_ms / args.steps}
+            hit = [x for x in t.get("launches", []) if x.get("kind") == dom]
+            if hit:
+                traffic = hit[0]["bytes"]
+                traffic_note = hit[0].get("note")
+        nt_fl, tn_fl = algorithmic_gemm_flops(net, RAYS * SAMPLES, split=True)
+        fam_ms = sum(rec["ms"] for rec in kinds.values())
+        fam_mfma = sum(rec["mfma_flops"] for rec in kinds.values())
+        roof = {"bound": bound, "kernel": d["kernel"], "what": d["what"],
+                "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak, "traffic": traffic,
+                "traffic_note": traffic_note,
+                "other_ceiling": ({"mfma_frac": d["mfma"]["frac"], "mfma_achieved_tflops_f32eq":
+                                   d["mfma"]["achieved_tflops_f32eq"], "mfma_peak_tflops_f32eq":
+                                   d["mfma"]["peak_tflops_f32eq"]} if bound == "hbm" else
+                                  {"hbm_frac": d["hbm"]["frac"], "hbm_achieved_gbs": d["hbm"]["achieved_gbs"]}),
+                "per_kind": per_kind,
+                "family": {"gemm_ms_per_step": gemm_ms / args.steps, "union_ms_per_step": gemm_union_ms / args.steps,
+                           "launches_per_step": gemm_launches / args.steps,
+                           "algorithmic_gflop_per_step": (nt_fl + tn_fl) / 1e9,
+                           "mfma_frac_per_launch": (fam_mfma / (BF16_MFMA_PEAK_TFLOPS * 1e12 if
+                                                                args.gemm_precision != "f32" else
+                                                                FP32_MFMA_PEAK_TFLOPS * 1e12)) / (fam_ms * 1e-3)},
+                "timing": "per-kind hipEvent pairs around every GEMM launch on its own stream, second timed "
+                          "pass of the same K steps (ms_per_step of that pass: %.3f)" % (1e3 * elapsed_hooks /
+                                                                                          args.steps)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             log("timing the CPU baseline (oracle) ...")
             cpu = cpu_baseline(args.cpu_budget)
+        exact = next((a for a in (alt or []) if a["gemm_arithmetic"] == "f32"), None)
         out = {"metric": METRIC, "value": world * RAYS / (elapsed / args.steps), "unit": "rays/s",
                "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
-               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-               "gemm_arithmetic": args.gemm_precision,
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": DTYPE[args.gemm_precision], "gemm_arithmetic": args.gemm_precision,
+               "value_exact_f32": exact["value"] if exact else None,
+               "ms_per_step_exact_f32": exact["ms_per_step"] if exact else None,
                "data": "synthetic (V_KITTI-shaped scene, random-init NeRF D=256; no dataset offline)",
                "config": {"workload": "config 2: V_KITTI scene-1 shape 188x621, 1024 rays x 128 samples per GPU, "
                                       "poses fixed, full train_step (render fwd+bwd, rgb-l2+depth-l1, Adam)",

@@ -34,6 +34,8 @@ extern "C" {
 /* Row tile of every per-sample GEMM: sample buffers are padded to a multiple of it. */
 #define NERF_ROW_TILE 128
 
+/* ABI version: 5 added nerf_prof_read_kinds (round 2). */
+#define NERF_HIP_ABI_VERSION 5
 int nerf_hip_abi_version(void);
 const char* nerf_hip_last_error(void);
 
@@ -354,6 +356,30 @@ int nerf_pair_backward(const float* d1, const float* d2, int h, int w, const flo
  * synchronises the events. */
 int nerf_prof_enable(int on);
 int nerf_prof_read(double* gemm_ms, int64_t* gemm_launches, double* gemm_flops, double* union_ms);
+
+/* Per-kind breakdown of the same records (call before nerf_prof_read, which resets them):
+ * kind 0 = forward NT (nerf_linear_fwd), 1 = input gradient NT (nerf_linear_bwd_data),
+ * 2 = weight gradient TN (nerf_linear_bwd_weight).  flops: algorithmic f32 FLOPs of the
+ * launches (2*m*n*k, padded shapes); bytes: their algorithmic HBM bytes (operands read
+ * once, outputs written once: A, B, C and the ReLU bit masks; for the weight gradient the
+ * dY and X panels plus ONE nout x kin gradient, not the split-K slabs); mfma_flops: flops
+ * times the MFMA products each f32 product costs in the arithmetic that ran (1 exact f32,
+ * 6 bf16x6, 3 fp16 pair) -- divided by the dense bf16/f16 MFMA rate it gives the
+ * launches' MFMA-bound time; exact_f32: 1 if any launch ran on the f32 MFMA (then
+ * mfma_flops / f32 peak). */
+#define NERF_PROF_FWD 0
+#define NERF_PROF_DX 1
+#define NERF_PROF_DW 2
+#define NERF_PROF_KINDS 3
+typedef struct nerf_prof_kind {
+    double ms;
+    int64_t launches;
+    double flops;
+    double bytes;
+    double mfma_flops;
+    int exact_f32;
+} nerf_prof_kind;
+int nerf_prof_read_kinds(nerf_prof_kind* out, int n_kinds);
 
 #ifdef __cplusplus
 }

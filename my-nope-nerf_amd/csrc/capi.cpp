@@ -19,12 +19,21 @@ void set_error(const char* fmt, ...) {
 // ---- GEMM timing: hipEvent pairs around each GEMM launch (bench.py roofline) ----
 struct ProfRec {
     hipEvent_t a, b;
-    double flops;
+    double flops, bytes;
+    int kind, products;
 };
 static std::mutex g_prof_mu;
 static bool g_prof_on = false;
 static std::vector<ProfRec> g_pool;
 static size_t g_used = 0;
+
+static thread_local int g_next_kind = 0;
+static thread_local double g_next_bytes = 0;
+
+void prof_next(int kind, double bytes) {
+    g_next_kind = kind;
+    g_next_bytes = bytes;
+}
 
 void prof_begin(hipStream_t s) {
     if (!g_prof_on) return;
@@ -33,17 +42,22 @@ void prof_begin(hipStream_t s) {
         ProfRec r;
         (void)hipEventCreate(&r.a);
         (void)hipEventCreate(&r.b);
-        r.flops = 0;
+        r.flops = r.bytes = 0;
+        r.kind = 0;
+        r.products = 1;
         g_pool.push_back(r);
     }
     (void)hipEventRecord(g_pool[g_used].a, s);
 }
 
-void prof_end(hipStream_t s, double flops) {
+void prof_end(hipStream_t s, double flops, int products) {
     if (!g_prof_on) return;
     std::lock_guard<std::mutex> lk(g_prof_mu);
     (void)hipEventRecord(g_pool[g_used].b, s);
     g_pool[g_used].flops = flops;
+    g_pool[g_used].bytes = g_next_bytes;
+    g_pool[g_used].kind = g_next_kind;
+    g_pool[g_used].products = products;
     ++g_used;
 }
 
@@ -51,7 +65,7 @@ void prof_end(hipStream_t s, double flops) {
 
 extern "C" {
 
-int nerf_hip_abi_version(void) { return 4; }
+int nerf_hip_abi_version(void) { return NERF_HIP_ABI_VERSION; }
 
 const char* nerf_hip_last_error(void) { return nerf::g_err; }
 
@@ -59,6 +73,27 @@ int nerf_prof_enable(int on) {
     std::lock_guard<std::mutex> lk(nerf::g_prof_mu);
     nerf::g_prof_on = on != 0;
     nerf::g_used = 0;
+    return NERF_OK;
+}
+
+int nerf_prof_read_kinds(nerf_prof_kind* out, int n_kinds) {
+    NERF_CHECK_PTR(out);
+    NERF_CHECK(n_kinds >= NERF_PROF_KINDS, "%s: need %d slots", __func__, NERF_PROF_KINDS);
+    std::lock_guard<std::mutex> lk(nerf::g_prof_mu);
+    for (int k = 0; k < n_kinds; ++k) out[k] = nerf_prof_kind{};
+    for (size_t i = 0; i < nerf::g_used; ++i) {
+        const auto& r = nerf::g_pool[i];
+        (void)hipEventSynchronize(r.b);
+        float t = 0;
+        (void)hipEventElapsedTime(&t, r.a, r.b);
+        nerf_prof_kind& o = out[r.kind];
+        o.ms += t;
+        o.launches += 1;
+        o.flops += r.flops;
+        o.bytes += r.bytes;
+        o.mfma_flops += r.flops * r.products;
+        o.exact_f32 |= r.products == 1;
+    }
     return NERF_OK;
 }
 

@@ -35,9 +35,13 @@ inline int check_launch(const char* fn) {
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
-// GEMM timing hooks (prof.cpp)
+// GEMM timing hooks (capi.cpp): kind = NERF_PROF_FWD / _DX / _DW; flops and bytes are the
+// launch's algorithmic f32 FLOPs and HBM bytes; products = MFMA products per f32 product
+// (1 exact f32, 6 bf16x6, 3 f16x3) -- it prices the launch against its MFMA peak
+// prof_next: set by the C-ABI entry before it dispatches (kind, algorithmic bytes)
+void prof_next(int kind, double bytes);
 void prof_begin(hipStream_t s);
-void prof_end(hipStream_t s, double flops);
+void prof_end(hipStream_t s, double flops, int products);
 
 constexpr int kWave = 64;
 

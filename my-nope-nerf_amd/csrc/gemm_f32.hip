@@ -320,7 +320,7 @@ static int launch_nt(const NTArgs& a, hipStream_t s, double flops) {
     b.ablate = g_ablate;
     prof_begin(s);
     hipLaunchKernelGGL((k_gemm_nt<BM, BN, WM, WN, EPI>), grid, dim3(64 * WM * WN), 0, s, b);
-    prof_end(s, flops);
+    prof_end(s, flops, 1);
     return check_launch("k_gemm_nt");
 }
 
@@ -388,6 +388,9 @@ extern "C" int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x
     if (rc) return rc;
     NERF_CHECK(mask_out == nullptr || ldmo >= n / 32, "%s: ldmo=%d < n/32", __func__, ldmo);
     const double fl = 2.0 * m * n * (double)(k1 + a.k2);
+    // algorithmic bytes: x1 (+ x2), W, y, ReLU bits
+    prof_next(NERF_PROF_FWD, 4.0 * m * (double)(k1 + a.k2) + 4.0 * n * (double)(k1 + a.k2) + 4.0 * m * (double)n +
+                                 (mask_out ? m * (double)n / 8 : 0.0));
     return dispatch_nt<EPI_FWD>(a, as_stream(stream), fl);
 }
 
@@ -410,6 +413,9 @@ extern "C" int nerf_linear_bwd_data(const float* dy, int lddy, int k, const floa
     NERF_CHECK(u == nullptr || v != nullptr, "%s: u without v", __func__);
     NERF_CHECK(mask == nullptr || ldmask >= n / 32, "%s: ldmask=%d < n/32 words", __func__, ldmask);
     const double fl = 2.0 * m * n * (double)k;
+    // algorithmic bytes: dy, W^T, dx, the input layer's ReLU bits, the rank-1 term's u / v
+    prof_next(NERF_PROF_DX, 4.0 * m * (double)k + 4.0 * n * (double)k + 4.0 * m * (double)n +
+                                (mask ? m * (double)n / 8 : 0.0) + (u ? 4.0 * m + 4.0 * n : 0.0));
     return dispatch_nt<EPI_BWD>(a, as_stream(stream), fl);
 }
 
@@ -438,6 +444,9 @@ extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const
     const bool h16 = g_precision == 2 && dy_cmax && x_cmax && (m / splits) % 128 == 0;
     hipStream_t s = as_stream(stream);
     const double fl = 2.0 * m * nout * (double)kin;
+    // algorithmic bytes: the dy and x panels and one nout x kin gradient (+ bias); the
+    // split-K slabs are structural traffic of this design, not algorithmic
+    prof_next(NERF_PROF_DW, 4.0 * m * (double)(nout + kin) + 4.0 * nout * (double)kin + (bslab ? 4.0 * nout : 0.0));
     const int pol = g_tn_policy ? g_tn_policy : 3;
     if (g_precision >= 1) return dispatch_tn_x6(a, nout, kin, splits, pol, s, fl, h16);
     prof_begin(s);
@@ -457,7 +466,7 @@ extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const
         dim3 grid(nout / 64, kin / 64, splits);
         hipLaunchKernelGGL((k_gemm_tn<64, 64, 2, 2>), grid, dim3(256), 0, s, a);
     }
-    prof_end(s, fl);
+    prof_end(s, fl, 1);
     return check_launch(__func__);
 }
 

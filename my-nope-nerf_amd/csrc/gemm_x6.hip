@@ -760,7 +760,7 @@ int dispatch_nt_x6(const NTArgs& a, int epi, int policy, hipStream_t s, double f
     prof_begin(s);
     if (epi == EPI_FWD) pick_nt_x6<EPI_FWD>(a, policy, s, h16);
     else pick_nt_x6<EPI_BWD>(a, policy, s, h16);
-    prof_end(s, flops);
+    prof_end(s, flops, h16 ? 3 : 6);
     return check_launch(h16 ? "k_gemm_nt_x6 (fp16 pair)" : "k_gemm_nt_x6");
 }
 
@@ -783,7 +783,7 @@ int dispatch_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, h
     prof_begin(s);
     if (h16) pick_tn_x6<true>(a, nout, kin, splits, policy, s);
     else pick_tn_x6<false>(a, nout, kin, splits, policy, s);
-    prof_end(s, flops);
+    prof_end(s, flops, h16 ? 3 : 6);
     return check_launch(h16 ? "k_gemm_tn_x6 (fp16 pair)" : "k_gemm_tn_x6");
 }
 

@@ -39,6 +39,16 @@ class PackDesc(ctypes.Structure):
                 ("rows_s", _c_i)]
 
 
+class ProfKind(ctypes.Structure):
+    """nerf_prof_kind (include/nerf_hip.h)."""
+    _fields_ = [("ms", ctypes.c_double), ("launches", _c_i64), ("flops", ctypes.c_double),
+                ("bytes", ctypes.c_double), ("mfma_flops", ctypes.c_double), ("exact_f32", _c_i)]
+
+
+PROF_KINDS = ("fwd", "dx", "dw")   # NERF_PROF_FWD / _DX / _DW
+ABI_VERSION = 5                    # NERF_HIP_ABI_VERSION
+
+
 class ChainLayer(ctypes.Structure):
     """nerf_chain_layer (include/nerf_hip.h)."""
     _fields_ = [("img", _c_p), ("img_rows", _c_i), ("bias", _c_p), ("out", _c_p), ("ldo", _c_i), ("mask", _c_p),
@@ -90,6 +100,7 @@ _SIGS = {
     "nerf_pair_backward": ([_c_p, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_f, _c_p, _c_p, _c_i, _c_p, _c_p, _c_p,
                             _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_prof_enable": ([_c_i], _c_i),
+    "nerf_prof_read_kinds": ([ctypes.POINTER(ProfKind), _c_i], _c_i),
     "nerf_prof_read": ([ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_i64),
                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], _c_i),
 }
@@ -103,6 +114,13 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
             f"nerf_hip: HIP library not found at {path}; build it with `make -C my-nope-nerf_amd` "
             "(or __graft_entry__.build()). There is no CPU fallback.")
     lib = ctypes.CDLL(path)
+    lib.nerf_hip_abi_version.restype = _c_i
+    ver = lib.nerf_hip_abi_version()
+    if ver != ABI_VERSION:
+        # signatures change between ABI versions (v4 added nerf_sample_rays' seed_counter);
+        # calling a stale library through these argtypes would pass mismatched arguments
+        raise ImportError(f"nerf_hip: {path} has ABI version {ver}, this binding needs {ABI_VERSION}; "
+                          "rebuild it with `make -C my-nope-nerf_amd`")
     for name, (args, res) in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = args
@@ -354,6 +372,14 @@ def gemm_get_precision():
 
 def prof_enable(on: bool):
     _call("nerf_prof_enable", int(on))
+
+
+def prof_read_kinds():
+    """Per-kind GEMM records since prof_enable (call before prof_read, which resets them):
+    {"fwd"|"dx"|"dw": {ms, launches, flops, bytes, mfma_flops, exact_f32}}."""
+    arr = (ProfKind * len(PROF_KINDS))()
+    _call("nerf_prof_read_kinds", arr, len(PROF_KINDS))
+    return {name: {f: getattr(arr[i], f) for f, _ in ProfKind._fields_} for i, name in enumerate(PROF_KINDS)}
 
 
 def prof_read():

@@ -66,6 +66,9 @@ class Trainer(object):
         self.rank = dist.get_rank() if self.world_size > 1 else 0
         # graph-capture mode (enable_graph_rng): the ray draw keys on a device step counter
         self.seed_counter = None
+        # fixed gradient-bucket layout for the data-parallel all-reduce (bucket_params)
+        self._bucket = None
+        self._flag_cache = {}
 
     def enable_graph_rng(self):
         """Make a step replayable from a captured hipGraph with fresh randomness: the ray
@@ -95,18 +98,53 @@ class Trainer(object):
                 o.step()
         return loss_dict
 
+    def bucket_params(self):
+        """The fixed gradient-bucket layout: every trainable parameter of the NeRF, pose,
+        focal and distortion modules, in module order.  It depends on the model alone, so
+        every rank sends the same element count whatever gradients it produced."""
+        if self._bucket is None:
+            self._bucket = [p for m, _ in self._modules_and_optims() for p in m.parameters() if p.requires_grad]
+        return self._bucket
+
     def allreduce_grads(self):
-        """Average every gradient over the ranks with one flat RCCL all-reduce."""
-        grads = []
-        for m, _ in self._modules_and_optims():
-            grads += [p.grad for p in m.parameters() if p.grad is not None]
-        if not grads:
+        """Average every gradient over the ranks with ONE flat all-reduce (RCCL on the GPU).
+
+        The bucket has a fixed layout (``bucket_params``) plus one presence flag per
+        parameter: a parameter without a gradient on this rank contributes zeros (DDP's
+        convention), so the ranks always agree on the collective's size.  After the
+        reduction every parameter some rank produced a gradient for holds the average over
+        ``world_size``; one no rank produced a gradient for stays ``None`` (torch Adam then
+        skips it on every rank alike).  Only a rank that lacked a gradient reads the flags
+        back (one host sync); the common all-present case stays sync-free."""
+        params = self.bucket_params()
+        if not params:
             return
-        flat = torch._utils._flatten_dense_tensors(grads)
+        missing = [p.grad is None for p in params]
+        dev = next((p.grad.device for p in params if p.grad is not None), params[0].device)
+        flags = self._flag_cache.get(tuple(missing))
+        if flags is None:
+            flags = torch.tensor([0.0 if m else 1.0 for m in missing], dtype=torch.float32, device=dev)
+            self._flag_cache[tuple(missing)] = flags
+        parts = [torch.zeros(p.numel(), dtype=torch.float32, device=dev) if p.grad is None
+                 else p.grad.reshape(-1) for p in params]
+        flat = torch.cat(parts + [flags])
         dist.all_reduce(flat, op=dist.ReduceOp.SUM)
-        flat.mul_(1.0 / self.world_size)
-        for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
-            g.copy_(f)
+        n = len(params)
+        grads = flat[:-n].mul_(1.0 / self.world_size)
+        present = flat[-n:].tolist() if any(missing) else None
+        off, dst, src = 0, [], []
+        for i, p in enumerate(params):
+            k = p.numel()
+            g = grads[off:off + k].view_as(p)
+            off += k
+            if p.grad is None:
+                if present[i] > 0:
+                    p.grad = g.clone()
+            else:
+                dst.append(p.grad)
+                src.append(g)
+        if dst:
+            torch._foreach_copy_(dst, src)
 
     # ------------------------------------------------------------------ data
     def process_data_dict(self, data):

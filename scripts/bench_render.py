@@ -6,7 +6,7 @@ assembled by one RCCL all-gather (model/render_dist.py).  Prints one JSON line:
 rays/s (whole job), frames/s, ms per frame.
 
     python scripts/bench_render.py [--frames K --warmup W]
-    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 scripts/bench_render.py
+    python scripts/bench_render.py --gpus N      (spawns N ranks, one per GPU)
 """
 import argparse
 import json
@@ -29,8 +29,14 @@ def main():
     ap.add_argument("--frames", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--gemm-precision", choices=["f32", "bf16x6", "f16x3"], default="f16x3")
+    ap.add_argument("--gpus", type=int, default=1)
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        from bench import spawn_ranks        # N ranks as a child torch.distributed.run
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:], script=os.path.abspath(__file__)))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench_render: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -75,7 +81,7 @@ def main():
     if rank == 0:
         n = H * W
         print(json.dumps({"metric": "full-frame eval render rays/s (188x621, 128 samples/ray, D=256)",
-                          "value": args.frames * n / el, "unit": "rays/s", "n_gpus": world,
+                          "value": args.frames * n / el, "unit": "rays/s", "n_gpus": dist.get_world_size() if world > 1 else 1,
                           "frames": args.frames, "warmup": args.warmup, "ms_per_frame": 1e3 * el / args.frames,
                           "frames_per_s": args.frames / el, "higher_is_better": True, "scaling": "strong",
                           "dtype": "f32", "gemm_arithmetic": args.gemm_precision, "data": "synthetic",

@@ -123,3 +123,67 @@ def test_full_frame_render_sharded_all_gather():
         assert torch.allclose(res[r][0], o["rgb"].reshape(-1, 3), atol=1e-6)
         assert torch.allclose(res[r][1], o["depth_pred"].reshape(-1), atol=1e-5)
         assert torch.equal(res[r][0], res[0][0])
+
+
+def _missing_grad_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(4, 3), torch.nn.Linear(3, 2))
+    cfg = make_cfg(hidden=16)
+    tr = mdl.Trainer(net, None, cfg["training"], device=torch.device("cpu"))
+    ps = tr.bucket_params()
+    # parameter 0: only rank 0 has a gradient; parameter 2: no rank has one; rest: all
+    for i, p in enumerate(ps):
+        if i == 2 or (i == 0 and rank == 1):
+            p.grad = None
+        else:
+            p.grad = torch.full_like(p, float(10 * rank + i))
+    tr.allreduce_grads()
+    q.put((rank, [None if p.grad is None else p.grad.clone().numpy() for p in ps]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_allreduce_fixed_layout_with_missing_gradient():
+    """A rank without a gradient for some parameter still sends the same bucket size (no
+    hang, zeros counted in the average); a parameter no rank has a gradient for stays None
+    on every rank (torch Adam skips it everywhere alike)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_missing_grad_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        g = res[r]
+        assert g[2] is None
+        assert torch.allclose(torch.from_numpy(g[0]), torch.full(g[0].shape, 0.0 / 2))      # (0 + missing) / 2
+        assert torch.allclose(torch.from_numpy(g[1]), torch.full(g[1].shape, (1 + 11) / 2))
+        assert torch.allclose(torch.from_numpy(g[3]), torch.full(g[3].shape, (3 + 13) / 2))
+
+
+def test_bench_launcher_spawns_ranks():
+    """`bench.py --gpus 2` without WORLD_SIZE launches its own two ranks (a child
+    torch.distributed.run) and reports n_gpus from the process group; --plumbing swaps the
+    GPU step for a CPU gloo check of the fixed-layout gradient all-reduce."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--plumbing", "--gpus", "2"],
+                         capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["plumbing"] and line["n_gpus"] == 2 and line["world_size"] == 2
+    assert line["bucket_elems"] > 595_000            # NeRF (595 844) + pose + distortion parameters
+    bad = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--plumbing", "--gpus", "3"],
+                         capture_output=True, text=True, timeout=120, env=dict(env, WORLD_SIZE="2"), cwd=root)
+    assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr
