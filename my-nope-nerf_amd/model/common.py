@@ -7,6 +7,7 @@ once per call into a single camera-to-world matrix.
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -159,3 +160,135 @@ def mse2psnr(mse):
     """common.py:623-630."""
     mse = np.maximum(mse, 1e-10)
     return (-10.0 * np.log10(mse)).astype(np.float32)
+
+
+# ---------------------------------------------------------------------------
+# the rest of the reference module's public helpers (host-side utilities the drivers
+# import: train.py:17, vis/render.py:12, evaluation/*): not on the hot path
+# ---------------------------------------------------------------------------
+from .camera_paths import (create_spheric_poses, generate_spiral_nerf, get_poses_at_times,  # noqa: E402,F401
+                           interp_poses, interp_poses_bspline, interp_t, normalize, poses_avg,
+                           render_path_spiral, scipy_bspline, viewmatrix)
+
+
+def backup(out_dir, config):
+    """common.py:492-508: snapshot the run's config and sources into <out_dir>/backup
+    (config.yaml, train.py, configs/default.yaml and the files of ./model and
+    ./dataloading, relative to the working directory as the reference resolves them).
+    Sources absent from the working directory are skipped instead of raising."""
+    import shutil
+    dst = os.path.join(out_dir, "backup")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copyfile(config, os.path.join(dst, "config.yaml"))
+    for f in ("train.py", os.path.join("configs", "default.yaml")):
+        if os.path.isfile(f):
+            shutil.copy(f, dst)
+    for d in ("model", "dataloading"):
+        if not os.path.isdir(d):
+            continue
+        sub = os.path.join(dst, d)
+        os.makedirs(sub, exist_ok=True)
+        for f in sorted(os.listdir(d)):
+            if os.path.isfile(os.path.join(d, f)):
+                shutil.copy(os.path.join(d, f), sub)
+
+
+def to_pytorch(tensor, return_type=False):
+    """common.py:42-57: numpy -> torch (and whether the input was numpy)."""
+    was_np = isinstance(tensor, np.ndarray)
+    if was_np:
+        tensor = torch.from_numpy(tensor)
+    return (tensor, was_np) if return_type else tensor
+
+
+def transform_to_camera_space(p_world, camera_mat, world_mat, scale_mat):
+    """common.py:163-183: K @ world @ scale applied to world points [B,N,3]."""
+    hom = torch.cat([p_world, torch.ones_like(p_world[..., :1])], dim=-1).transpose(1, 2)
+    return (camera_mat @ world_mat @ scale_mat @ hom)[:, :3].transpose(1, 2)
+
+
+def check_weights(params):
+    """common.py:240-248: warn about NaN parameters."""
+    import logging
+    for k, v in params.items():
+        if torch.isnan(v).any():
+            logging.getLogger(__name__).warning("NaN Values detected in model weight %s.", k)
+
+
+def check_tensor(tensor, tensorname="", input_tensor=None):
+    """common.py:251-262."""
+    import logging
+    if torch.isnan(tensor).any():
+        log = logging.getLogger(__name__)
+        log.warning("Tensor %s contains nan values.", tensorname)
+        if input_tensor is not None:
+            log.warning("Input was: %s", input_tensor)
+
+
+def normalize_tensor(tensor, min_norm=1e-5, feat_dim=-1):
+    """common.py:265-275."""
+    return tensor / tensor.norm(dim=feat_dim, keepdim=True).clamp_min(min_norm)
+
+
+def reprojection(pixels, depth, Rt_ref, world_mat, camera_mat):
+    """common.py:405-434: pixels [B,N,2] at depth -> the reference camera's image plane;
+    returns (xy [B,N,2], valid [B,N,1] float)."""
+    pixels, was_np = to_pytorch(pixels, True)
+    depth, camera_mat, Rt_ref = to_pytorch(depth), to_pytorch(camera_mat), to_pytorch(Rt_ref)
+    d = depth.reshape(1, -1, 1)
+    hom = torch.cat([pixels * d, d, torch.ones_like(d)], dim=-1).transpose(1, 2)
+    M = camera_mat @ Rt_ref @ torch.inverse(world_mat) @ torch.inverse(camera_mat)
+    xyz = (M @ hom)[:, :3].transpose(1, 2)
+    xy = xyz[..., :2] / xyz[..., 2:]
+    valid = (xy.abs().max(dim=-1)[0] <= 1).unsqueeze(-1).float()
+    return (xy.numpy() if was_np else xy), valid
+
+
+def skew_symmetric(w):
+    """common.py:459-465: batched [.., 3] -> [.., 3, 3]."""
+    w0, w1, w2 = w.unbind(dim=-1)
+    o = torch.zeros_like(w0)
+    return torch.stack([torch.stack([o, -w2, w1], -1), torch.stack([w2, o, -w0], -1),
+                        torch.stack([-w1, w0, o], -1)], -2)
+
+
+def _taylor(x, nth, step):
+    """sum_i (-1)^i x^(2i) / prod(...) with the reference's running denominators."""
+    out = torch.zeros_like(x)
+    den = 1.0
+    for i in range(nth + 1):
+        den = step(i, den)
+        out = out + (-1) ** i * x ** (2 * i) / den
+    return out
+
+
+def taylor_A(x, nth=10):
+    """common.py:467-473: sin(x)/x."""
+    return _taylor(x, nth, lambda i, d: d * (2 * i) * (2 * i + 1) if i > 0 else d)
+
+
+def taylor_B(x, nth=10):
+    """common.py:475-481: (1-cos(x))/x^2."""
+    return _taylor(x, nth, lambda i, d: d * (2 * i + 1) * (2 * i + 2))
+
+
+def taylor_C(x, nth=10):
+    """common.py:483-490: (x-sin(x))/x^3."""
+    return _taylor(x, nth, lambda i, d: d * (2 * i + 2) * (2 * i + 3))
+
+
+def convert2mip(pts):
+    """common.py:616-621: contract points outside the unit ball to radius < 2."""
+    n = pts.norm(dim=-1, keepdim=True)
+    return torch.where(n >= 1.0, (2 - 1.0 / n) * (pts / n), pts)
+
+
+def compute_errors(gt, pred):
+    """common.py:676-694: depth error metrics (abs_rel, sq_rel, rmse, rmse_log, a1, a2, a3)."""
+    ratio = np.maximum(gt / pred, pred / gt)
+    a1, a2, a3 = ((ratio < 1.25 ** k).mean() for k in (1, 2, 3))
+    rmse = np.sqrt(((gt - pred) ** 2).mean())
+    rmse_log = np.sqrt(((np.log(gt) - np.log(pred)) ** 2).mean())
+    abs_rel = np.mean(np.abs(gt - pred) / gt)
+    sq_rel = np.mean((gt - pred) ** 2 / gt)
+    return abs_rel, sq_rel, rmse, rmse_log, a1, a2, a3

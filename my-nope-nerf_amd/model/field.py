@@ -451,6 +451,41 @@ class FieldRawFn(torch.autograd.Function):
         return (None, g_p, g_d, *grads)
 
 
+class FieldTrunkFn(torch.autograd.Function):
+    """OfficialStaticNerf.infer_occ (official_nerf.py:60-67) in one HIP forward: points
+    p [n,3] -> (x [n,D] the trunk output h8, sigma_raw [n,1] = fc_density(x)).  sigma_raw
+    is differentiable w.r.t. the points and the parameters (the head backward of the
+    runner); x is returned as a non-differentiable tensor -- the reference only consumes it
+    inside forward(), which runs the fused path instead."""
+
+    @staticmethod
+    def forward(ctx, runner: FieldRunner, p, *params):
+        n = p.shape[0]
+        zeros = torch.zeros_like(p)
+        raw4, _, _, _, st = runner.forward(p, zeros, zeros, None, 0.0, 0.0, 1, 0, keep=True, composite=False)
+        h8 = st["acts"][7][:n, :runner.D].clone()
+        ctx.mark_non_differentiable(h8)
+        ctx.runner, ctx.state, ctx.n = runner, st, n
+        ctx.ray_grad = ctx.needs_input_grad[1]
+        return h8, raw4[:n, 0:1].clone()
+
+    @staticmethod
+    def backward(ctx, g_h8, g_sigma):
+        st = ctx.state
+        graw4 = torch.zeros(st["Np"], 4, device=g_sigma.device)
+        graw4[:ctx.n, 0:1] = g_sigma
+        grads, ray = ctx.runner.backward(st, None, None, ctx.ray_grad, graw4=graw4)
+        ctx.state = None
+        g_p = ray[0] if ray is not None else None
+        return (None, g_p, *grads)
+
+
+def trunk_points(module, p):
+    """(x [n,D], sigma_raw [n,1]) of points p [n,3] (infer_occ)."""
+    runner = module.hip_runner()
+    return FieldTrunkFn.apply(runner, p.contiguous(), *runner.param_list())
+
+
 def eval_points(module, p, d):
     """raw head outputs for arbitrary points (autograd-aware)."""
     runner = module.hip_runner()

@@ -13,7 +13,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .field import FieldRunner, eval_points
+from .field import FieldRunner, eval_points, trunk_points
 
 
 class OfficialStaticNerf(nn.Module):
@@ -62,9 +62,12 @@ class OfficialStaticNerf(nn.Module):
         return sigma
 
     def infer_occ(self, p):
-        raise NotImplementedError(
-            "infer_occ returns the 256-wide trunk activations; the MI355X path keeps them inside "
-            "the fused kernels. Use forward(p, ray_d, only_occupancy=True) for occupancy.")
+        """official_nerf.py:60-67: (x, density) = (trunk output [..,D], fc_density(x) [..,1],
+        before the activation), from one HIP forward.  density is differentiable w.r.t. p
+        and the parameters; x carries no gradient (see field.FieldTrunkFn)."""
+        shape = p.shape[:-1]
+        x, density = trunk_points(self, p.reshape(-1, 3).float())
+        return x.reshape(*shape, self.hidden_dim), density.reshape(*shape, 1)
 
     def forward(self, p, ray_d=None, only_occupancy=False, return_logits=False, return_addocc=False,
                 noise=False, it=100000, **kwargs):

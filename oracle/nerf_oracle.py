@@ -390,19 +390,66 @@ def weight_dist_loss(t_list):
     return dist.mean(), dd.pow(2.0).mean()
 
 
+def depth_invariant_loss(pred, gt, weight=None):
+    """losses.py:35-58 (depth_loss_type 'invariant', via get_depth_loss :67-68): both depths
+    normalised by their median t and mean absolute deviation s, (d - t) / s, then the MSE
+    (optionally weighted: sum(w * se) / (sum(w) + 1e-8)).  torch.median of an even count
+    is the lower middle value."""
+    def norm(d):
+        t = torch.median(d)
+        return (d - t) / torch.mean(torch.abs(d - t))
+    se = (norm(pred) - norm(gt)) ** 2
+    if weight is None:
+        return se.mean()
+    return (se * weight).sum() / (weight.sum() + 1e-8)
+
+
+def depth_consistency_loss(d1_proj, d2, d2_proj=None, d1=None):
+    """losses.py:124-128: sum |d1_proj - d2| / shape[1], averaged with the reverse term when
+    d2_proj is given."""
+    loss = (d1_proj - d2).abs().sum() / float(d1_proj.shape[1])
+    if d2_proj is not None:
+        loss = 0.5 * loss + 0.5 * (d2_proj - d1).abs().sum() / float(d2_proj.shape[1])
+    return loss
+
+
+def t_cycle_loss(rt_pred, rt_gt):
+    """losses.py:161-162: Frobenius norm of I - inverse(Rt_gt) @ Rt_pred (relative pose of
+    the image pair, training.py:329-358)."""
+    eye = torch.eye(4, dtype=rt_gt.dtype)
+    return torch.linalg.norm(eye - torch.inverse(rt_gt) @ rt_pred)
+
+
 def total_loss(rgb_pred, rgb_gt, depth_pred, depth_gt, weights: dict, rgb_loss_type="l2",
-               pc=None, rgb_s=None):
-    """losses.py:164-228 (the terms the V_KITTI configs switch on)."""
-    z = torch.zeros((), dtype=rgb_pred.dtype)
-    l_rgb = rgb_full_loss(rgb_pred, rgb_gt, rgb_loss_type) if weights.get("rgb_weight", 0) != 0 else z
-    l_depth = depth_l1_loss(depth_pred, depth_gt) if weights.get("depth_weight", 0) != 0 else z
-    l_pc = pc if (pc is not None and weights.get("pc_weight", 0) != 0) else z
-    l_rgbs = rgb_s if (rgb_s is not None and weights.get("rgb_s_weight", 0) != 0) else z
-    l2_mean = F.mse_loss(rgb_pred, rgb_gt)
-    loss = (weights.get("rgb_weight", 0) * l_rgb + weights.get("depth_weight", 0) * l_depth
-            + weights.get("pc_weight", 0) * l_pc + weights.get("rgb_s_weight", 0) * l_rgbs)
+               pc=None, rgb_s=None, t_list=None, t_cycle=None, depth_loss_type="l1", d_consistency=None):
+    """losses.py:164-228: the weighted sum of every term the trainer can switch on, with
+    the reference's output keys; a term is evaluated only when its weight is non-zero."""
+    dt = rgb_pred.dtype if rgb_pred is not None else torch.float32
+    z = torch.zeros((), dtype=dt)
+    w = {k: weights.get(k, 0.0) for k in ("rgb_weight", "depth_weight", "pc_weight", "rgb_s_weight",
+                                          "weight_dist_1st_loss", "weight_dist_2nd_loss",
+                                          "depth_consistency_weight", "t_cycle_weight")}
+    l_rgb = rgb_full_loss(rgb_pred, rgb_gt, rgb_loss_type) if w["rgb_weight"] != 0 else z
+    if w["depth_weight"] != 0:
+        l_depth = (depth_l1_loss(depth_pred, depth_gt) if depth_loss_type == "l1"
+                   else depth_invariant_loss(depth_pred, depth_gt))
+    else:
+        l_depth = z
+    if w["weight_dist_1st_loss"] != 0 or w["weight_dist_2nd_loss"] != 0:
+        l_d1, l_d2 = weight_dist_loss(t_list)
+    else:
+        l_d1 = l_d2 = z
+    l_pc = pc if (pc is not None and w["pc_weight"] != 0) else z
+    l_rgbs = rgb_s if (rgb_s is not None and w["rgb_s_weight"] != 0) else z
+    l_dc = d_consistency if (d_consistency is not None and w["depth_consistency_weight"] != 0) else z
+    l_tc = t_cycle if (t_cycle is not None and w["t_cycle_weight"] != 0) else z
+    l2_mean = F.mse_loss(rgb_pred, rgb_gt) if (w["rgb_weight"] != 0 or w["depth_weight"] != 0) else z
+    loss = (w["rgb_weight"] * l_rgb + w["depth_weight"] * l_depth + w["weight_dist_1st_loss"] * l_d1
+            + w["weight_dist_2nd_loss"] * l_d2 + w["pc_weight"] * l_pc + w["rgb_s_weight"] * l_rgbs
+            + w["depth_consistency_weight"] * l_dc + w["t_cycle_weight"] * l_tc)
     return {"loss": loss, "loss_rgb": l_rgb, "loss_depth": l_depth, "l2_mean": l2_mean,
-            "loss_pc": l_pc, "loss_rgb_s": l_rgbs}
+            "loss_dist_1st": l_d1, "loss_dist_2nd": l_d2, "loss_pc": l_pc, "loss_rgb_s": l_rgbs,
+            "loss_depth_consistency": l_dc, "loss_t_cycle": l_tc}
 
 
 def anneal(start, end, anneal_start_epoch, anneal_epochs, current):
@@ -582,12 +629,15 @@ def compute_loss_full(model, pose, distortion, data, tcfg, rcfg, epoch, scheduli
         X = pc1 @ R_rel_12.transpose(1, 2) + t_rel_12
         if w["pc_weight"] != 0.0:
             terms["pc"] = pc_loss(X, pc2)
+        if w["t_cycle_weight"] != 0.0:                                        # losses.py:161-162
+            terms["t_cycle"] = t_cycle_loss(Rt_rel_12, Rt_rel_12_gt)
     rgb_pred = out.get("rgb")
     dgt = out.get("depth_gt")
     if render_model and tcfg["detach_gt_depth"]:
         dgt = dgt.detach()
     ld = total_loss(rgb_pred, rgb_gt, out.get("depth_pred"), dgt, w, rgb_loss_type, pc=terms.get("pc"),
-                    rgb_s=terms.get("rgb_s"))
+                    rgb_s=terms.get("rgb_s"), t_list=pose["t"], t_cycle=terms.get("t_cycle"),
+                    depth_loss_type=tcfg.get("depth_loss_type", "l1"))
     ld["scale"], ld["shift"] = scale_input, shift_input
     return ld
 

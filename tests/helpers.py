@@ -69,3 +69,30 @@ def synthetic_rays(R=1024, S=128, H=188, W=621, seed=0, zero_frac=0.05, fx=362.5
     return {"pixels": pixels, "depth": depth, "K": camera_K(H, W, fx, fx), "c2w": c2w,
             "w2c": torch.inverse(c2w).unsqueeze(0), "scale": torch.eye(4).unsqueeze(0),
             "noise": torch.rand(1, R, S, generator=g), "ray_idx": idx}
+
+
+# ---- parity bar (BASELINE.json north_star: 1e-4 rel on rendered RGB / depth) -----------
+RENDER_RTOL = 1e-4     # elementwise, relative to the oracle value
+RENDER_ATOL = 1e-6     # absolute floor for values near zero (dark pixels, masked depths)
+
+
+def elementwise_excess(a, b, rtol=RENDER_RTOL, atol=RENDER_ATOL):
+    """max over elements of |a - b| / (rtol |b| + atol): <= 1 passes the elementwise bar
+    |a - b| <= rtol |b| + atol."""
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).abs() / (rtol * b.abs() + atol)).max().item()
+
+
+def assert_elementwise(a, b, rtol=RENDER_RTOL, atol=RENDER_ATOL, what=""):
+    """|a - b| <= rtol |b| + atol for every element; the message carries the worst element
+    and, as a diagnostic, the max-normalised error max|a-b| / max|b|."""
+    a_, b_ = a.detach().double().cpu(), b.detach().double().cpu()
+    assert a_.shape == b_.shape, (what, a_.shape, b_.shape)
+    err = (a_ - b_).abs()
+    lim = rtol * b_.abs() + atol
+    ratio = err / lim
+    if ratio.numel() and ratio.max().item() > 1.0:
+        i = int(ratio.argmax())
+        raise AssertionError(f"{what}: element {i}: |{a_.flatten()[i].item():.9g} - {b_.flatten()[i].item():.9g}| = "
+                             f"{err.flatten()[i].item():.3g} > {rtol:g}*|b| + {atol:g} "
+                             f"(max-normalised error {(err.max() / b_.abs().max().clamp_min(1e-30)).item():.3g})")

@@ -50,9 +50,9 @@ def test_hip_matches_fixture(dev, f):
     noise = fx["noise"].to(dev) if fx["noise"] is not None else None
     out = rnd.nope_nerf(i["pixels"], i["depth"], i["K"], i["w2c"], i["scale"], add_noise=noise is not None,
                         noise=noise)
-    rel = lambda a, b: ((a.cpu() - b).abs().max() / b.abs().max()).item()
-    assert rel(out["rgb"].detach(), fx["rgb"]) < 1e-4
-    assert rel(out["depth_pred"].detach(), fx["depth_pred"]) < 1e-4
+    from tests.helpers import assert_elementwise
+    assert_elementwise(out["rgb"], fx["rgb"], what="rgb")                  # |a-b| <= 1e-4 |b| + 1e-6
+    assert_elementwise(out["depth_pred"], fx["depth_pred"], what="depth")
     loss = orc.rgb_full_loss(out["rgb"], fx["gt"].to(dev)) + 0.04 * orc.depth_l1_loss(out["depth_pred"], out["depth_gt"])
     assert abs(loss.item() - fx["loss"].item()) < 1e-4 * abs(fx["loss"].item())
     loss.backward()

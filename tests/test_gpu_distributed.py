@@ -39,9 +39,9 @@ def _setup(dev):
     img = torch.stack([0.5 + 0.4 * torch.sin(5 * xx + yy), 0.5 + 0.3 * torch.cos(4 * yy), 0.2 + 0.6 * xx * yy])
     depth = 1.5 + 4.0 * torch.rand(1, H, W, generator=g)       # no holes: every rank masks 0 rays
     c2w = torch.stack([rigid_c2w(3, 0.2), rigid_c2w(4, 0.2)])
-    data = {"img": img.unsqueeze(0).to(dev), "img.idx": torch.tensor([1]), "img.depth": depth.to(dev),
+    data = {"img": img.unsqueeze(0).to(dev), "img.idx": torch.tensor([0]), "img.depth": depth.to(dev),
             "img.depth_mask": torch.ones(1, H, W, dtype=torch.bool), "img.camera_mat": camera_K(H, W, FX, FX).to(dev),
-            "img.scale_mat": torch.eye(4).unsqueeze(0).to(dev), "img.pose_gt": c2w[1:2].to(dev)}
+            "img.scale_mat": torch.eye(4).unsqueeze(0).to(dev), "img.pose_gt": c2w[0:1].to(dev)}
     torch.manual_seed(42)
     net = mdl.OfficialStaticNerf(cfg)
     model = mdl.get_model(mdl.Renderer(net, cfg["rendering"], device=dev), cfg, device=dev)
@@ -53,7 +53,7 @@ def _setup(dev):
     opt_pose = torch.optim.Adam(pose.parameters(), lr=1e-3)
     distn = mdl.Learn_Distortion(2, True, True, cfg).to(dev)
     with torch.no_grad():
-        distn.scales.copy_(torch.tensor([[1.1], [0.95]]))
+        distn.global_scales.copy_(torch.tensor([[1.1], [0.95]]))
     opt_dist = torch.optim.Adam(distn.parameters(), lr=1e-3)
     tr = mdl.Trainer(model, opt, t, device=dev, optimizer_pose=opt_pose, pose_param_net=pose,
                      optimizer_distortion=opt_dist, distortion_net=distn)
@@ -68,6 +68,15 @@ def _grads(tr):
 
 
 def _rank(rank, world, port, q):
+    try:
+        _rank_body(rank, world, port, q)
+    except BaseException:                    # report instead of leaving the parent waiting
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+        raise
+
+
+def _rank_body(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -96,9 +105,18 @@ def test_hip_train_step_under_process_group_matches_full_batch(dev):
     procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = {}
-    for _ in range(world):
-        r, g, pr = q.get(timeout=300)
+    import queue
+    import time
+    res, t0 = {}, time.time()
+    while len(res) < world:
+        try:
+            r, g, pr = q.get(timeout=5)
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"a rank exited with {dead} before reporting"
+            assert time.time() - t0 < 240, "ranks did not report within 240 s"
+            continue
+        assert g != "error", f"rank {r} failed:\n{pr}"
         res[r] = (g, pr)
     for p in procs:
         p.join(timeout=120)

@@ -19,11 +19,21 @@ from tests.helpers import camera_K, make_cfg, rigid_c2w
 
 pytestmark = pytest.mark.gpu
 
-H, W, FX = 48, 72, 60.0
-R, S, D = 256, 32, 64
+# (name, H, W, fx, rays, samples, hidden, cameras, (camera, reference) per step, training overrides)
+CASES = [
+    ("small", 48, 72, 60.0, 256, 32, 64, 2, ((0, 1), (1, 0), (0, 1)), {}),
+    # config 3 at its bench shape: 188x621 (P = 47 x 155 = 7 285 points per cloud), 1024 x 128, D = 256
+    ("cfg3", 188, 621, 362.5, 1024, 128, 256, 2, ((0, 1), (1, 0)), {}),
+    # configs/V_KITTI/*_d9.yaml:39 (t_cycle_weight [1.0, 0.0]) plus the camera-path regularisers
+    # (losses.py:105-114) on a 3-camera path
+    ("d9_tcycle_dist", 48, 72, 60.0, 256, 32, 64, 3, ((0, 1), (1, 2), (2, 1)),
+     {"t_cycle_weight": [1.0, 0.0], "weight_dist_1st_loss": [0.2, 0.0], "weight_dist_2nd_loss": [0.3, 0.0]}),
+    # depth_loss_type 'invariant' (losses.py:35-58, 67-68)
+    ("invariant_depth", 48, 72, 60.0, 256, 32, 64, 2, ((0, 1), (1, 0)), {"depth_loss_type": "invariant"}),
+]
 
 
-def _scene(seed):
+def _scene(seed, H, W):
     g = torch.Generator().manual_seed(seed)
     yy, xx = torch.meshgrid(torch.linspace(0, 1, H), torch.linspace(0, 1, W), indexing="ij")
     img = torch.stack([0.5 + 0.4 * torch.sin(7 * xx + 3 * yy + seed), 0.5 + 0.4 * torch.cos(6 * yy - 2 * xx),
@@ -33,8 +43,7 @@ def _scene(seed):
     return img, depth.unsqueeze(0)
 
 
-def _data(cam, imgs, depths, c2w_gt, K):
-    ref = 1 - cam
+def _data(cam, ref, imgs, depths, c2w_gt, K):
     return {"img": imgs[cam], "img.depth": depths[cam], "img.depth_mask": depths[cam] > 0,
             "img.camera_mat": K, "img.scale_mat": torch.eye(4).unsqueeze(0), "img.pose_gt": c2w_gt[cam].unsqueeze(0),
             "img.idx": torch.tensor([cam]), "img.ref_imgs": imgs[ref], "img.ref_depths": depths[ref],
@@ -57,15 +66,20 @@ def _nrel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-def test_full_nope_nerf_step_matches_oracle(dev, gemm_precision):
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_full_nope_nerf_step_matches_oracle(dev, gemm_precision, case):
+    name, H, W, FX, R, S, D, n_cams, steps, over = case
     cfg = make_cfg(hidden=D, S=S)
     tcfg = dict(cfg["training"])
+    tcfg.update(over)
     tcfg["n_training_points"] = R
     tcfg["annealing_epochs"], tcfg["scheduling_start"] = 0, 0
+    cfg["training"] = tcfg
     rcfg = cfg["rendering"]
-    imgs, depths = zip(*[_scene(s) for s in (0, 1)])
-    c2w_gt = torch.stack([rigid_c2w(11, 0.2), rigid_c2w(12, 0.2)])
-    c2w_gt[1, :3, 3] = c2w_gt[0, :3, 3] + torch.tensor([0.05, 0.0, -0.1])   # overlapping views
+    imgs, depths = zip(*[_scene(s, H, W) for s in range(n_cams)])
+    c2w_gt = torch.stack([rigid_c2w(11, 0.2)] * n_cams)
+    for c in range(1, n_cams):                                  # overlapping views along a path
+        c2w_gt[c, :3, 3] = c2w_gt[0, :3, 3] + c * torch.tensor([0.05, 0.0, -0.1])
     K = camera_K(H, W, FX, FX)
 
     # ---- parameters shared by both sides
@@ -75,14 +89,15 @@ def test_full_nope_nerf_step_matches_oracle(dev, gemm_precision):
                          occ_activation=cfg["model"]["occ_activation"])
     ref.load_state_dict(net.state_dict())
     g = torch.Generator().manual_seed(3)
-    r0, t0 = 0.01 * torch.randn(2, 3, generator=g), 0.02 * torch.randn(2, 3, generator=g)
-    scales0, shifts0 = torch.tensor([[1.15], [1.0]]), torch.tensor([[0.05], [-0.03]])
+    r0, t0 = 0.01 * torch.randn(n_cams, 3, generator=g), 0.02 * torch.randn(n_cams, 3, generator=g)
+    scales0 = torch.tensor([[1.15], [0.9], [1.0]])[-n_cams:]
+    shifts0 = torch.tensor([[0.05], [0.02], [-0.03]])[-n_cams:]
 
     # ---- HIP side: the drop-in Trainer
     renderer = mdl.Renderer(net, rcfg, device=dev)
     nn_model = mdl.get_model(renderer, cfg, device=dev)
-    pose = mdl.LearnPose(2, True, True, cfg, init_c2w=c2w_gt.clone()).to(dev)
-    dist = mdl.Learn_Distortion(2, True, True, cfg).to(dev)
+    pose = mdl.LearnPose(n_cams, True, True, cfg, init_c2w=c2w_gt.clone()).to(dev)
+    dist = mdl.Learn_Distortion(n_cams, True, True, cfg).to(dev)
     with torch.no_grad():
         pose.r.copy_(r0); pose.t.copy_(t0)
         dist.global_scales.copy_(scales0); dist.global_shifts.copy_(shifts0)
@@ -101,9 +116,10 @@ def test_full_nope_nerf_step_matches_oracle(dev, gemm_precision):
     o_opt_dist = torch.optim.Adam([o_dist["scales"], o_dist["shifts"]], lr=5e-4)
 
     gdraw = torch.Generator().manual_seed(5)
-    keys = ("loss", "loss_rgb", "loss_depth", "loss_pc", "loss_rgb_s", "l2_mean")
-    for step, cam in enumerate((0, 1, 0)):
-        data = _data(cam, imgs, depths, c2w_gt, K)
+    keys = ("loss", "loss_rgb", "loss_depth", "loss_pc", "loss_rgb_s", "l2_mean", "loss_dist_1st", "loss_dist_2nd",
+            "loss_t_cycle")
+    for step, (cam, refc) in enumerate(steps):
+        data = _data(cam, refc, imgs, depths, c2w_gt, K)
         ray_idx = torch.randperm(H * W, generator=gdraw)[:R]
         noise = torch.rand(1, R, S, generator=gdraw)
         # oracle

@@ -7,7 +7,7 @@ import torch
 from model.official_nerf import OfficialStaticNerf
 from model.rendering import Renderer
 from oracle import nerf_oracle as orc
-from tests.helpers import make_cfg, synthetic_rays
+from tests.helpers import assert_elementwise, make_cfg, synthetic_rays
 
 pytestmark = pytest.mark.gpu
 
@@ -25,6 +25,7 @@ def _pair(cfg, seed=0):
 
 
 def _rel(a, b):
+    """max-normalised error (diagnostic; the bar is assert_elementwise)."""
     return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
 
 
@@ -51,8 +52,8 @@ def test_render_forward_matches_oracle(dev, gemm_precision, hidden, S, R, opts):
                             b["scale"].to(dev), add_noise=True, noise=b["noise"].to(dev))
         o = orc.render_nope_nerf(ref, b["pixels"], b["depth"], b["K"], b["w2c"], b["scale"], cfg["rendering"],
                                  noise=b["noise"])
-    assert _rel(out["rgb"].cpu(), o["rgb"]) < RTOL
-    assert _rel(out["depth_pred"].cpu(), o["depth_pred"]) < RTOL
+    assert_elementwise(out["rgb"], o["rgb"], what="rgb")
+    assert_elementwise(out["depth_pred"], o["depth_pred"], what="depth")
     assert torch.equal(out["depth_gt"].cpu(), o["depth_gt"]) or _rel(out["depth_gt"].cpu(), o["depth_gt"]) < 1e-6
     assert (out["alpha"].cpu() - o["alpha"]).abs().max().item() < 1e-4
     assert _rel(out["z_vals"].cpu(), o["z_vals"]) < 1e-6
@@ -69,8 +70,8 @@ def test_render_eval_mode_full_frame_tile(dev, gemm_precision):
                             b["w2c"].to(dev), b["scale"].to(dev), add_noise=False, eval_=True)
         o = orc.render_nope_nerf(ref, b["pixels"], torch.ones(1, 2048, 1), b["K"], b["w2c"], b["scale"],
                                  cfg["rendering"], noise=None, eval_=True)
-    assert _rel(out["rgb"].cpu(), o["rgb"]) < RTOL
-    assert _rel(out["depth_pred"].cpu(), o["depth_pred"]) < RTOL
+    assert_elementwise(out["rgb"], o["rgb"], what="rgb")
+    assert_elementwise(out["depth_pred"], o["depth_pred"], what="depth")
 
 
 def test_render_backward_matches_oracle(dev, gemm_precision):
@@ -130,8 +131,8 @@ def test_points_forward_api(dev, gemm_precision):
     net = net.to(dev)
     rgb, dens = net(p.to(dev), d.to(dev), return_addocc=True)
     rgb_r, dens_r = ref(p, d)
-    assert _rel(rgb.cpu(), rgb_r) < RTOL
-    assert _rel(dens.cpu(), dens_r) < RTOL
+    assert_elementwise(rgb, rgb_r, what="rgb")
+    assert_elementwise(dens, dens_r, what="density")
 
 
 def test_render_image_full_frame(dev, gemm_precision):
@@ -152,5 +153,5 @@ def test_render_image_full_frame(dev, gemm_precision):
         o = orc.render_nope_nerf(ref, pix, torch.ones(1, H * W, 1), K, w2c, scale, cfg["rendering"], noise=None,
                                  eval_=True)
     assert rgb.shape == (H * W, 3) and depth.shape == (H * W,)
-    assert _rel(rgb.cpu(), o["rgb"].reshape(-1, 3)) < RTOL
-    assert _rel(depth.cpu(), o["depth_pred"].reshape(-1)) < RTOL
+    assert_elementwise(rgb, o["rgb"].reshape(-1, 3), what="rgb")
+    assert_elementwise(depth, o["depth_pred"].reshape(-1), what="depth")
