@@ -232,7 +232,7 @@ int nerf_encode_bwd(const float* pts_o, const float* pts_d, const float* view, c
  * row r scaled by 2^e_r (row max -> [2^14, 2^15)), planes 0 / 1 = fp16 hi / lo, and e_r as
  * an int32 in the first word of plane 2's chunk 0 of that row (u16 index
  * ((2*K/8)*rows + r)*8). */
-#define NERF_MAX_PACK 16
+#define NERF_MAX_PACK 24
 typedef struct {
     const float* src;
     float* dst;    /* [rows][ld_dst] */

@@ -454,6 +454,8 @@ extern "C" int nerf_mlp_chain_fwd(const float* enc_p, const float* enc_d, const 
     for (int l = 0; l < CNL; ++l) {
         const nerf_chain_layer& L = layers[l];
         NERF_CHECK(L.img && L.bias, "%s: layer %d needs its weight image and bias", __func__, l);
+        NERF_CHECK((((uintptr_t)L.bias) & 15u) == 0, "%s: layer %d: bias not 16-byte aligned (16-byte LDS-DMA)",
+                   __func__, l);
         NERF_CHECK(L.img_rows >= L_OUT[l] && (((uintptr_t)L.img) & 15u) == 0,
                    "%s: layer %d: image rows %d < %d or image not 16-byte aligned", __func__, l, L.img_rows, L_OUT[l]);
         NERF_CHECK(L.out == nullptr || (L.ldo >= L_OUT[l] && L.ldo % 4 == 0 && (((uintptr_t)L.out) & 15u) == 0),

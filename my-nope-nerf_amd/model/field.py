@@ -91,7 +91,10 @@ class FieldRunner:
         # bf16x3 split images of w / wt: the B operands of GEMM precision mode 1
         self.ws = {l.name: _hip.split_image(l.out_p, l.kp, device) for l in self.layers}
         self.wts = {l.name: _hip.split_image(l.kp, l.out_p, device) for l in self.layers}
-        self.b_r = z(HR)           # padded colour-layer bias
+        # padded, 16-byte-aligned copies of every layer bias (the chain kernel loads them by
+        # 16-byte LDS-DMA; HipAdam's flat parameter buffer leaves biases 4-byte aligned)
+        self.bias_p = {l.name: z(l.out_p) for l in self.layers}
+        self.b_r = self.bias_p["lr"]
         self.wc = z(3, HR)         # padded fc_rgb weight
         self.device = device
 
@@ -114,14 +117,15 @@ class FieldRunner:
             wts = self.wts[l.name].data_ptr() if self.split else None
             descs.append(_hip.PackDesc(W.data_ptr(), self.w[l.name].data_ptr(), self.wt[l.name].data_ptr(),
                                        W.shape[0], W.shape[1], l.kp, l.kp, l.out_p, ws, wts, l.out_p))
-        br = self.m.rgb_layers[0].bias
-        descs.append(_hip.PackDesc(br.data_ptr(), self.b_r.data_ptr(), None, 1, br.shape[0], self.HR, 0, 0))
+        for l in self.layers:
+            b = l.linear.bias
+            descs.append(_hip.PackDesc(b.data_ptr(), self.bias_p[l.name].data_ptr(), None, 1, b.shape[0], l.out_p, 0, 0))
         wc = self.m.fc_rgb.weight
         descs.append(_hip.PackDesc(wc.data_ptr(), self.wc.data_ptr(), None, 3, wc.shape[1], self.HR, 0, 0))
         _hip.pack_weights(descs)
 
     def bias(self, l: LayerSpec):
-        return self.b_r if l.name == "lr" else l.linear.bias
+        return self.bias_p[l.name]
 
     # ------------------------------------------------------------------ forward
     def forward(self, pts_o, pts_d, view, noise, near, far, S: int, flags: int, keep: bool,
