@@ -34,7 +34,7 @@ extern "C" {
 /* Row tile of every per-sample GEMM: sample buffers are padded to a multiple of it. */
 #define NERF_ROW_TILE 128
 
-/* ABI version: 5 added nerf_prof_read_kinds (round 2). */
+/* ABI version: 5 added nerf_prof_read_kinds and nerf_render_eval_fused (round 2). */
 #define NERF_HIP_ABI_VERSION 5
 int nerf_hip_abi_version(void);
 const char* nerf_hip_last_error(void);
@@ -172,6 +172,25 @@ typedef struct {
 } nerf_chain_layer;
 int nerf_mlp_chain_fwd(const float* enc_p, const float* enc_d, const float* enc_p_rmax,
                        const float* enc_d_rmax, int n_pad, const nerf_chain_layer* layers, void* stream);
+/* The fused per-ray eval render (BASELINE.json north_star; rendering.py:36-168 with eval_ /
+ * no noise, official_nerf.py:60-119): ONE launch per ray chunk computes, per 128-row block
+ * of S-sample rays (S divides 128), the stratified sample positions and both positional
+ * encodings in-kernel, runs the ten linears of nerf_mlp_chain_fwd with the activations in
+ * registers, the density / colour heads in the layer epilogues and the sigma -> alpha ->
+ * exclusive-product composite of the block's rays -- no per-sample tensor touches HBM
+ * except alpha [R][S] and z [R*S] (outputs of the reference's out-dict).
+ * pts_o / pts_d / view: [R][3] ray origins, sample directions, view directions; layers: the
+ * ten chain descriptors with out / mask / cmax NULL; wd [256], bd [1]: fc_density; wc [3][128]
+ * (padded), bc [3]: fc_rgb.  flags as nerf_composite_fwd.  Outputs rgb [R][3], dist [R]
+ * (ray distance; the caller applies the eval z-depth division), alpha [R][S], z [R*S].
+ * GEMM precision mode 2, hidden width 256.  Replaces rendering.py:89-141 +
+ * official_nerf.py:60-96 for the render callers (extracting_images.py:65-76,
+ * training.py:103-165). */
+int nerf_render_eval_fused(const float* pts_o, const float* pts_d, const float* view, int n_rays, int n_samples,
+                           float near_z, float far_z, int flags, const nerf_chain_layer* layers, const float* wd,
+                           const float* bd, const float* wc, const float* bc, float* rgb, float* dist, float* alpha,
+                           float* z, void* stream);
+
 /* Diagnostics only: per-block phase cycles of nerf_mlp_chain_fwd into buf[(n_pad/128)*6]
  * uint64 (DMA wait, barrier, MFMA section, epilogue, total, end time); NULL switches off. */
 int nerf_chain_debug_stamps(void* buf);

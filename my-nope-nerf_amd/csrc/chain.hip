@@ -23,6 +23,7 @@
 // (134 MB per 256-wide layer at 1024 x 128 samples), every per-layer prologue, launch gap
 // and tail, and keeps the weight stream off the critical path.
 #include "gemm.hpp"
+#include "samples.hpp"
 
 namespace nerf {
 namespace {
@@ -88,6 +89,15 @@ struct ChainFwdArgs {
     int n_pad;
     nerf_chain_layer L[CNL];
     unsigned long long* stamps;   // diagnostics (nerf_chain_debug_stamps): per-block phase cycles or NULL
+    // the fused per-ray eval render (nerf_render_eval_fused): samples + encodings in the
+    // prologue, density / colour heads in the l7 / colour-layer epilogues, sigma -> alpha ->
+    // composite of the block's rays at the end
+    const float* po; const float* pd; const float* view;   // [R][3]
+    int R, S, flags;
+    float near_z, far_z;
+    const float* wd; const float* bd;   // fc_density weight [256], bias [1]
+    const float* wc; const float* bc;   // fc_rgb weight padded [3][128], bias [3]
+    float* rgb; float* dist; float* alpha; float* z;   // [R][3], [R], [R][S], [R*S]
 };
 
 constexpr int kbase(int l) { return l == 0 ? 0 : kbase(l - 1) + L_KS[l - 1]; }
@@ -98,6 +108,7 @@ struct ChainState {
     char* ring; char* leb16; float* lbias; uint32_t* lcm;   // leb16: [2][256 rows][16 B], exponent in word 0
     char* lenc; float* lrp; float* lrd;                      // encoding tile [128][64], row maxima [128] x 2
     float* stage;                                            // this wave's [32][STG_LD] epilogue tile
+    float* fx;                                               // fused eval: wd [256], wc [3][128], raw [128][4], z [128]
     int tid, lane, sl, hf;
     size_t m0, row;
     int er;                          // row exponent of the current A operand
@@ -125,13 +136,16 @@ constexpr int ENC_D_STEP = 4 + 16 * 3 + 20;   // kbase(5): the enc_d tile replac
 // LDS-DMA instructions every wave issues with global k-step tt (uniform across waves):
 // 4 for the weight ring, +2 at a layer's first step (weight-row exponents, biases), +10 at
 // step 0 (enc_p tile 8, enc_p / enc_d row maxima 1 + 1), +8 at ENC_D_STEP (enc_d tile)
-constexpr int dma_count(int tt) {
-    return tt >= CT ? 0 : DMA_PER_STEP + (first_step(tt) ? 2 : 0) + (tt == 0 ? 10 : 0) + (tt == ENC_D_STEP ? 8 : 0);
+// (fused eval: the encodings are computed in-kernel, so step 0 and ENC_D_STEP carry no extras)
+constexpr int dma_count(int tt, bool fused = false) {
+    return tt >= CT ? 0
+                    : DMA_PER_STEP + (first_step(tt) ? 2 : 0) + (tt == 0 && !fused ? 10 : 0) +
+                          (tt == ENC_D_STEP && !fused ? 8 : 0);
 }
 // DMAs issued after those of step tt by the time step tt is consumed (steps tt+1 .. tt+NSLOT-2)
-constexpr int dma_after(int tt) {
+constexpr int dma_after(int tt, bool fused = false) {
     int n = 0;
-    for (int u = tt + 1; u <= tt + NSLOT - 2; ++u) n += dma_count(u);
+    for (int u = tt + 1; u <= tt + NSLOT - 2; ++u) n += dma_count(u, fused);
     return n;
 }
 
@@ -147,7 +161,7 @@ __device__ __forceinline__ void chain_dma_enc(const float* enc, ChainState& st) 
 }
 
 // global k-step TT -> ring slot TT % NSLOT, plus the extras of dma_count(TT)
-template <int TT>
+template <int TT, bool F>
 __device__ __forceinline__ void chain_dma(const ChainFwdArgs& p, ChainState& st) {
     if constexpr (TT < CT) {
         constexpr int l = [] { int i = 0; while (kbase(i + 1) <= TT) ++i; return i; }();
@@ -174,29 +188,29 @@ __device__ __forceinline__ void chain_dma(const ChainFwdArgs& p, ChainState& st)
             if (st.lane < 16)
                 cdma16(L.bias, (uint32_t)((64 * wr + 4 * st.lane) * 4), reinterpret_cast<char*>(st.lbias + (l & 1) * 256 + 64 * wr));
         }
-        if constexpr (TT == 0) {
+        if constexpr (TT == 0 && !F) {
             chain_dma_enc(p.enc_p, st);
             if (st.lane < 8) {   // 32 row maxima per wave
                 cdma16(p.rp + st.m0, (uint32_t)((32 * w + 4 * st.lane) * 4), reinterpret_cast<char*>(st.lrp + 32 * w));
                 cdma16(p.rd + st.m0, (uint32_t)((32 * w + 4 * st.lane) * 4), reinterpret_cast<char*>(st.lrd + 32 * w));
             }
         }
-        if constexpr (TT == ENC_D_STEP) chain_dma_enc(p.enc_d, st);
+        if constexpr (TT == ENC_D_STEP && !F) chain_dma_enc(p.enc_d, st);
     }
 }
 
 // one k-step of layer l: wait for its slot, publish, refill the ring, MFMAs
-template <int l, int s>
+template <int l, int s, bool F>
 __device__ __forceinline__ void chain_kstep(const ChainFwdArgs& p, ChainState& st) {
     constexpr int TT = kbase(l) + s;
     constexpr int nreg = l == 0 ? 0 : 16;
     constexpr int ntj = L_OUT[l] / 32;
     chain_tick(p, st, st.t_mma);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(dma_after(TT)) : "memory");   // this step's DMAs landed
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(dma_after(TT, F)) : "memory");   // this step's DMAs landed
     chain_tick(p, st, st.t_wait);
     __syncthreads();
     chain_tick(p, st, st.t_bar);
-    chain_dma<TT + NSLOT - 1>(p, st);
+    chain_dma<TT + NSLOT - 1, F>(p, st);
     if constexpr (s == 0) {
         // layer prologue (behind a barrier): the previous layer's column maxima out, this
         // layer's column-max accumulators zeroed (its exponents and biases arrived by DMA)
@@ -229,7 +243,7 @@ __device__ __forceinline__ void chain_kstep(const ChainFwdArgs& p, ChainState& s
         st.acc[j] = cmfma(bh[j % 3], al, st.acc[j]);   // hi . lo
         st.acc[j] = cmfma(bl[j % 3], ah, st.acc[j]);   // lo . hi
         st.acc[j] = cmfma(bh[j % 3], ah, st.acc[j]);   // hi . hi
-        if constexpr (l > 0 && s < nreg) {
+        if constexpr (l > 0 && s < nreg && !F) {
             if (j == 1 && p.L[l - 1].out) {
                 // the previous layer's output, stored beside this layer's MFMAs instead of in a
                 // burst at its epilogue: this k-step's 8 features of the row, rebuilt from the
@@ -252,11 +266,11 @@ __device__ __forceinline__ void chain_kstep(const ChainFwdArgs& p, ChainState& s
     }
 }
 
-template <int l, int s>
+template <int l, int s, bool F>
 __device__ __forceinline__ void chain_ksteps(const ChainFwdArgs& p, ChainState& st) {
     if constexpr (s < L_KS[l]) {
-        chain_kstep<l, s>(p, st);
-        chain_ksteps<l, s + 1>(p, st);
+        chain_kstep<l, s, F>(p, st);
+        chain_ksteps<l, s + 1, F>(p, st);
     }
 }
 
@@ -269,8 +283,54 @@ __device__ __forceinline__ void enc_frags(ChainState& st, int rl) {
         frag_from8(src[4 * s + 2 * st.hf], src[4 * s + 2 * st.hf + 1], st.er, st.enc_hi[s], st.enc_lo[s]);
 }
 
+// fused eval: the view-direction encodings of the block's rays (27 values of
+// encode_position L = 4, official_nerf.py:87, 99-119, zero padded to 32) and their maxima
+// live in LDS, one 36-float record per ray (fx + FX_ENCD): the view direction is per ray,
+// so 128 / S records serve the block's 128 rows
+constexpr int FX_RAW = 640, FX_Z = 1152, FX_ENCD = 1280, ENCD_REC = 36;
+__device__ __forceinline__ void fused_encode_d(const ChainFwdArgs& p, ChainState& st) {
+    const int nr = CROWS / p.S;
+    if (st.tid >= nr) return;
+    const size_t ray = st.m0 / (size_t)p.S + st.tid;
+    float d[3] = {0.f, 0.f, 0.f};
+    if (ray < (size_t)p.R) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) d[c] = p.view[3 * ray + c];
+    }
+    float* rec = st.fx + FX_ENCD + ENCD_REC * st.tid;
+    float m = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { rec[c] = d[c]; m = fmaxf(m, fabsf(d[c])); }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float f = (float)(1 << i);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float sn, cs;
+            sincosf(f * d[c], &sn, &cs);
+            rec[3 + 6 * i + c] = sn;
+            rec[6 + 6 * i + c] = cs;
+            m = fmaxf(m, fmaxf(fabsf(sn), fabsf(cs)));
+        }
+    }
+#pragma unroll
+    for (int c = 27; c < 32; ++c) rec[c] = 0.f;
+    rec[32] = m;
+}
+// this lane's 4 encoding k-steps (8-feature chunks 16 s + 8 hf .. + 7; columns >= 32 zero)
+__device__ __forceinline__ void enc_d_frags(ChainState& st, const float* rec) {
+    const float4* src = reinterpret_cast<const float4*>(rec);
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const float4 u = s < 2 ? src[4 * s + 2 * st.hf] : z4;
+        const float4 v = s < 2 ? src[4 * s + 2 * st.hf + 1] : z4;
+        frag_from8(u, v, st.er, st.enc_hi[s], st.enc_lo[s]);
+    }
+}
+
 // layer l: k-loop, epilogue (features f = 32 j + 8 q + 4 hf + c of row st.row), next A
-template <int l>
+template <int l, bool F>
 __device__ __forceinline__ void chain_layer(const ChainFwdArgs& p, ChainState& st) {
     constexpr int ntj = L_OUT[l] / 32;
     constexpr bool relu = l != 8;
@@ -279,8 +339,13 @@ __device__ __forceinline__ void chain_layer(const ChainFwdArgs& p, ChainState& s
     for (int j = 0; j < 8; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) st.acc[j][r] = 0.f;
-    chain_ksteps<l, 0>(p, st);
+    chain_ksteps<l, 0, F>(p, st);
     chain_tick(p, st, st.t_mma);
+    // fused eval heads: sigma_raw = fc_density(h8) in l7's epilogue, the colour logits
+    // fc_rgb(hr) in the colour layer's (official_nerf.py:66, 91), partial dots over this
+    // lane's features, the lane halves summed below
+    constexpr bool head_d = F && l == 7, head_c = F && l == CNL - 1;
+    float hs0 = 0.f, hs1 = 0.f, hs2 = 0.f;
 
     // the colour layer stores its output here; every other layer's output is stored by the
     // next layer's k-steps (chain_kstep)
@@ -303,6 +368,7 @@ __device__ __forceinline__ void chain_layer(const ChainFwdArgs& p, ChainState& s
             x.z = __builtin_amdgcn_ldexpf(st.acc[j][4 * q + 2], -(st.er + e4.z)) + b4.z;
             x.w = __builtin_amdgcn_ldexpf(st.acc[j][4 * q + 3], -(st.er + e4.w)) + b4.w;
             if (relu) x = make_float4(fmaxf(x.x, 0.f), fmaxf(x.y, 0.f), fmaxf(x.z, 0.f), fmaxf(x.w, 0.f));
+
             st.acc[j][4 * q + 0] = x.x; st.acc[j][4 * q + 1] = x.y;
             st.acc[j][4 * q + 2] = x.z; st.acc[j][4 * q + 3] = x.w;
             w |= ((x.x > 0.f ? 1u : 0u) | (x.y > 0.f ? 2u : 0u) | (x.z > 0.f ? 4u : 0u) | (x.w > 0.f ? 8u : 0u))
@@ -348,14 +414,55 @@ __device__ __forceinline__ void chain_layer(const ChainFwdArgs& p, ChainState& s
             }
         }
     }
+    if constexpr (head_d || head_c) {
+        // the head dots over the epilogue's results (acc now holds the layer output), one
+        // feature quad at a time: the scheduling barriers keep the weight reads from being
+        // hoisted into one 128-register burst
+#pragma unroll
+        for (int j = 0; j < ntj; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                __builtin_amdgcn_sched_barrier(0);
+                const int f0 = 32 * j + 8 * q + 4 * st.hf;
+                const float x0 = st.acc[j][4 * q], x1 = st.acc[j][4 * q + 1];
+                const float x2 = st.acc[j][4 * q + 2], x3 = st.acc[j][4 * q + 3];
+                if constexpr (head_d) {
+                    const float4 wv = *reinterpret_cast<const float4*>(st.fx + f0);
+                    hs0 += x0 * wv.x + x1 * wv.y + x2 * wv.z + x3 * wv.w;
+                } else {
+                    const float4 w0 = *reinterpret_cast<const float4*>(st.fx + 256 + f0);
+                    const float4 w1 = *reinterpret_cast<const float4*>(st.fx + 384 + f0);
+                    const float4 w2 = *reinterpret_cast<const float4*>(st.fx + 512 + f0);
+                    hs0 += x0 * w0.x + x1 * w0.y + x2 * w0.z + x3 * w0.w;
+                    hs1 += x0 * w1.x + x1 * w1.y + x2 * w1.z + x3 * w1.w;
+                    hs2 += x0 * w2.x + x1 * w2.y + x2 * w2.z + x3 * w2.w;
+                }
+            }
+        __builtin_amdgcn_sched_barrier(0);
+        // raw4 row (sigma_raw, rgb logits) of this sample into the block's LDS rows
+        float* raw = st.fx + FX_RAW + 4 * ((st.tid >> 6) * 32 + st.sl);
+        hs0 += __shfl_xor(hs0, 32, 64);
+        if constexpr (head_d) {
+            if (st.hf == 0) raw[0] = hs0 + p.bd[0];
+        } else {
+            hs1 += __shfl_xor(hs1, 32, 64);
+            hs2 += __shfl_xor(hs2, 32, 64);
+            if (st.hf == 0) {
+                raw[1] = hs0 + p.bc[0];
+                raw[2] = hs1 + p.bc[1];
+                raw[3] = hs2 + p.bc[2];
+            }
+        }
+    }
     chain_tick(p, st, st.t_epi);
     if constexpr (l < CNL - 1) {
         // next layer's A operand: row exponent over the row's 256 features (and the encoding
         // joined in the next layer), fp16 pairs, quad exchange between the lane halves
         float m = fmaxf(rmx, __shfl_xor(rmx, 32, 64));
         const int rl = (st.tid >> 6) * 32 + st.sl;   // row inside the block
-        if constexpr (l == 3) m = fmaxf(m, st.lrp[rl]);
-        if constexpr (l == 8) m = fmaxf(m, st.lrd[rl]);
+        const float* drec = F ? st.fx + FX_ENCD + ENCD_REC * (rl / (F ? p.S : 1)) : nullptr;
+        if constexpr (l == 3) m = fmaxf(m, F ? fmaxf(st.lrp[rl], st.lrd[rl]) : st.lrp[rl]);
+        if constexpr (l == 8) m = fmaxf(m, F ? drec[32] : st.lrd[rl]);
         st.er = row_exp(m);
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
@@ -379,14 +486,110 @@ __device__ __forceinline__ void chain_layer(const ChainFwdArgs& p, ChainState& s
             st.act_hi[s] = make_uint4(h0[0], h1[0], h0[1], h1[1]);
             st.act_lo[s] = make_uint4(l0[0], l1[0], l0[1], l1[1]);
         }
-        if constexpr (l == 3 || l == 8) enc_frags(st, rl);   // the enc_p / enc_d tile in LDS
+        if constexpr (l == 3 || (l == 8 && !F)) enc_frags(st, rl);   // the enc_p / enc_d tile in LDS
+        if constexpr (l == 8 && F) enc_d_frags(st, drec);
         chain_tick(p, st, st.t_epi);
     }
 }
 
+// fused eval prologue: samples (rendering.py:183-198, no jitter) and the position encoding
+// (official_nerf.py:61, 99-119) of the block's 128 rows into the LDS tile the chain reads
+// (the layout nerf_encode_samples writes), with row maxima and z.  Waves 0-1 write columns
+// 0..32 (x, levels 0-4), waves 2-3 columns 33..63 (levels 5-9, zero pad): no divergence.
+__device__ __forceinline__ void fused_encode_p(const ChainFwdArgs& p, ChainState& st) {
+    const int row = st.tid & 127, half = st.tid >> 7;
+    const size_t g = st.m0 + row;
+    float* dst = reinterpret_cast<float*>(st.lenc + row * 256);
+    float x[3] = {0.f, 0.f, 0.f}, z = 0.f;
+    const bool live = g < (size_t)p.R * p.S;
+    if (live) {
+        const size_t ray = g / (size_t)p.S;
+        const int i = (int)(g - ray * (size_t)p.S);
+        z = lerp_z(linspace01(i, p.S), p.near_z, p.far_z);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) x[c] = ray_point(p.po[3 * ray + c], p.pd[3 * ray + c], z);
+    }
+    float m = 0.f;
+    if (half == 0) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { dst[c] = x[c]; m = fmaxf(m, fabsf(x[c])); }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const float f = (float)(1 << i);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                float sn, cs;
+                sincosf(f * x[c], &sn, &cs);
+                dst[3 + 6 * i + c] = sn;
+                dst[6 + 6 * i + c] = cs;
+                m = fmaxf(m, fmaxf(fabsf(sn), fabsf(cs)));
+            }
+        }
+        st.fx[FX_Z + row] = z;
+        if (live) p.z[g] = z;
+    } else {
+#pragma unroll
+        for (int i = 5; i < 10; ++i) {
+            const float f = (float)(1 << i);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                float sn, cs;
+                sincosf(f * x[c], &sn, &cs);
+                dst[3 + 6 * i + c] = sn;
+                dst[6 + 6 * i + c] = cs;
+                m = fmaxf(m, fmaxf(fabsf(sn), fabsf(cs)));
+            }
+        }
+        dst[63] = 0.f;
+    }
+    // the two halves' maxima of a row: lrp (columns 0..32) and lrd (33..63; lrd holds no
+    // enc_d maxima in the fused kernel); readers take the max of both
+    (half == 0 ? st.lrp : st.lrd)[row] = m;
+}
+
+// fused eval epilogue: sigma -> alpha -> exclusive-product compositing of the block's
+// 128 / S rays (rendering.py:113-141, the arithmetic of k_composite16_fwd), one thread per
+// ray walking its S samples in order
+__device__ __forceinline__ void fused_composite(const ChainFwdArgs& p, const ChainState& st) {
+    const int nr = CROWS / p.S;
+    if (st.tid >= nr) return;
+    const size_t ray = st.m0 / (size_t)p.S + st.tid;
+    if (ray >= (size_t)p.R) return;
+    const float* raw = st.fx + FX_RAW + 4 * st.tid * p.S;
+    const float* zl = st.fx + FX_Z + st.tid * p.S;
+    float T = 1.f, s0 = 0.f, s1 = 0.f, s2 = 0.f, sd = 0.f, sw = 0.f;
+    float* al = p.alpha + ray * (size_t)p.S;
+    for (int i = 0; i < p.S; ++i) {
+        const float sg = f_density(raw[4 * i], p.flags);
+        float a;
+        if (p.flags & F_DIST_ALPHA)
+            a = i == p.S - 1 ? 1.f : 1.f - __expf(-1.0f * sg * (zl[i + 1] - zl[i]));
+        else
+            a = 1.f - __expf(-1.0f * sg);
+        const float w = a * T;
+        s0 += w * f_sigmoid(raw[4 * i + 1]);
+        s1 += w * f_sigmoid(raw[4 * i + 2]);
+        s2 += w * f_sigmoid(raw[4 * i + 3]);
+        sd += w * zl[i];
+        sw += w;
+        T *= 1.f - a + kEps;
+        al[i] = a;
+    }
+    if (p.flags & F_WHITE_BKGD) {
+        const float bg = 1.f - sw;
+        s0 += bg; s1 += bg; s2 += bg;
+    }
+    p.rgb[3 * ray + 0] = s0;
+    p.rgb[3 * ray + 1] = s1;
+    p.rgb[3 * ray + 2] = s2;
+    p.dist[ray] = sd;
+}
+
+template <bool F>
 __global__ __launch_bounds__(256) void k_mlp_chain_fwd(ChainFwdArgs p) {
     constexpr int RING = NSLOT * SBYTES, LEB = 2 * 4096, LBIAS = 2 * 256 * 4, LCM = 2 * 256 * 4, LENC = 128 * 256;
     constexpr int LSTG = 4 * 32 * STG_LD * 4;
+    static_assert(LSTG >= (FX_ENCD + ENCD_REC * 64) * 4, "the fused eval buffers live in the staging region");
     __shared__ __attribute__((aligned(16))) char smem[RING + LEB + LBIAS + LCM + LENC + 2 * 512 + LSTG];
     ChainState st;
     st.ring = smem;
@@ -397,6 +600,7 @@ __global__ __launch_bounds__(256) void k_mlp_chain_fwd(ChainFwdArgs p) {
     st.lrp = reinterpret_cast<float*>(st.lenc + LENC);
     st.lrd = st.lrp + 128;
     st.stage = reinterpret_cast<float*>(st.lenc + LENC + 2 * 512) + (threadIdx.x >> 6) * 32 * STG_LD;
+    st.fx = reinterpret_cast<float*>(st.lenc + LENC + 2 * 512);
     st.tid = threadIdx.x;
     st.lane = st.tid & 63; st.sl = st.lane & 31; st.hf = st.lane >> 5;
     st.m0 = (size_t)blockIdx.x * CROWS;
@@ -405,29 +609,40 @@ __global__ __launch_bounds__(256) void k_mlp_chain_fwd(ChainFwdArgs p) {
     st.t_last = __builtin_amdgcn_s_memtime();
     const unsigned long long t_start = st.t_last;
 
-    chain_dma<0>(p, st);
-    chain_dma<1>(p, st);
-    chain_dma<2>(p, st);
-    chain_dma<3>(p, st);
+    chain_dma<0, F>(p, st);
+    chain_dma<1, F>(p, st);
+    chain_dma<2, F>(p, st);
+    chain_dma<3, F>(p, st);
     static_assert(NSLOT == 5, "prologue issues NSLOT - 1 k-steps");
+    if constexpr (F) {
+        // head weights into LDS, then the samples and position encodings (beside the DMAs)
+        st.fx[st.tid] = p.wd[st.tid];
+        for (int e = st.tid; e < 384; e += 256) st.fx[256 + e] = p.wc[e];
+        fused_encode_p(p, st);
+        fused_encode_d(p, st);
+    }
     // step 0's group (with the enc_p tile and the row maxima) landed, published to the block
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(dma_count(1) + dma_count(2) + dma_count(3)) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(dma_count(1, F) + dma_count(2, F) + dma_count(3, F)) : "memory");
     __syncthreads();
     const int rl = (st.tid >> 6) * 32 + st.sl;
-    st.er = row_exp(st.lrp[rl]);
+    st.er = row_exp(F ? fmaxf(st.lrp[rl], st.lrd[rl]) : st.lrp[rl]);
     enc_frags(st, rl);
 
-    chain_layer<0>(p, st);
-    chain_layer<1>(p, st);
-    chain_layer<2>(p, st);
-    chain_layer<3>(p, st);
-    chain_layer<4>(p, st);
-    chain_layer<5>(p, st);
-    chain_layer<6>(p, st);
-    chain_layer<7>(p, st);
-    chain_layer<8>(p, st);
-    chain_layer<9>(p, st);
+    chain_layer<0, F>(p, st);
+    chain_layer<1, F>(p, st);
+    chain_layer<2, F>(p, st);
+    chain_layer<3, F>(p, st);
+    chain_layer<4, F>(p, st);
+    chain_layer<5, F>(p, st);
+    chain_layer<6, F>(p, st);
+    chain_layer<7, F>(p, st);
+    chain_layer<8, F>(p, st);
+    chain_layer<9, F>(p, st);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every DMA landed before the LDS is released
+    if constexpr (F) {
+        __syncthreads();   // every row's raw4 in LDS
+        fused_composite(p, st);
+    }
     if (p.stamps && st.tid == 0) {
         unsigned long long* o = p.stamps + (size_t)blockIdx.x * 6;
         o[0] = st.t_wait; o[1] = st.t_bar; o[2] = st.t_mma; o[3] = st.t_epi;
@@ -465,7 +680,43 @@ extern "C" int nerf_mlp_chain_fwd(const float* enc_p, const float* enc_d, const 
         a.L[l] = L;
     }
     a.stamps = g_chain_stamps;
-    hipLaunchKernelGGL(k_mlp_chain_fwd, dim3(n_pad / CROWS), dim3(256), 0, as_stream(stream), a);
+    hipLaunchKernelGGL(k_mlp_chain_fwd<false>, dim3(n_pad / CROWS), dim3(256), 0, as_stream(stream), a);
+    return check_launch(__func__);
+}
+
+extern "C" int nerf_render_eval_fused(const float* pts_o, const float* pts_d, const float* view, int n_rays,
+                                      int n_samples, float near_z, float far_z, int flags,
+                                      const nerf_chain_layer* layers, const float* wd, const float* bd,
+                                      const float* wc, const float* bc, float* rgb, float* dist, float* alpha,
+                                      float* z, void* stream) {
+    NERF_CHECK_PTR(pts_o); NERF_CHECK_PTR(pts_d); NERF_CHECK_PTR(view); NERF_CHECK_PTR(layers);
+    NERF_CHECK_PTR(wd); NERF_CHECK_PTR(bd); NERF_CHECK_PTR(wc); NERF_CHECK_PTR(bc);
+    NERF_CHECK_PTR(rgb); NERF_CHECK_PTR(dist); NERF_CHECK_PTR(alpha); NERF_CHECK_PTR(z);
+    NERF_CHECK(n_rays > 0 && n_samples >= 2 && CROWS % n_samples == 0,
+               "%s: n_rays=%d, n_samples=%d: the samples of a ray must tile the %d-row block (S >= 2 divides %d)",
+               __func__, n_rays, n_samples, CROWS, CROWS);
+    NERF_CHECK((int64_t)n_rays * n_samples <= (int64_t)1 << 30, "%s: too many samples", __func__);
+    NERF_CHECK(gemm_precision() == 2, "%s: the fused chain runs in GEMM precision mode 2 (fp16 pair images)", __func__);
+    NERF_CHECK((flags & ~7) == 0, "%s: unknown flags %d", __func__, flags);
+    ChainFwdArgs a{};
+    const int64_t n = (int64_t)n_rays * n_samples;
+    a.n_pad = (int)((n + CROWS - 1) / CROWS * CROWS);
+    for (int l = 0; l < CNL; ++l) {
+        const nerf_chain_layer& L = layers[l];
+        NERF_CHECK(L.img && L.bias, "%s: layer %d needs its weight image and bias", __func__, l);
+        NERF_CHECK((((uintptr_t)L.bias) & 15u) == 0 && (((uintptr_t)L.img) & 15u) == 0 && L.img_rows >= L_OUT[l],
+                   "%s: layer %d: image / bias not 16-byte aligned or image rows %d < %d", __func__, l, L.img_rows,
+                   L_OUT[l]);
+        NERF_CHECK(L.out == nullptr && L.mask == nullptr && L.cmax == nullptr,
+                   "%s: layer %d: the eval render saves no activations, masks or column maxima", __func__, l);
+        a.L[l] = L;
+    }
+    a.po = pts_o; a.pd = pts_d; a.view = view;
+    a.R = n_rays; a.S = n_samples; a.flags = flags; a.near_z = near_z; a.far_z = far_z;
+    a.wd = wd; a.bd = bd; a.wc = wc; a.bc = bc;
+    a.rgb = rgb; a.dist = dist; a.alpha = alpha; a.z = z;
+    a.stamps = g_chain_stamps;
+    hipLaunchKernelGGL(k_mlp_chain_fwd<true>, dim3(a.n_pad / CROWS), dim3(256), 0, as_stream(stream), a);
     return check_launch(__func__);
 }
 

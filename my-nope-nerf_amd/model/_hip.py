@@ -78,6 +78,8 @@ _SIGS = {
     "nerf_pack_weights": ([ctypes.POINTER(PackDesc), _c_i, _c_p], _c_i),
     "nerf_mlp_chain_fwd": ([_c_p, _c_p, _c_p, _c_p, _c_i, ctypes.POINTER(ChainLayer), _c_p], _c_i),
     "nerf_chain_debug_stamps": ([_c_p], _c_i),
+    "nerf_render_eval_fused": ([_c_p, _c_p, _c_p, _c_i, _c_i, _c_f, _c_f, _c_i, ctypes.POINTER(ChainLayer), _c_p, _c_p,
+                                _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_adam_step": ([_c_p, _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p], _c_i),
     "nerf_chamfer_nn": ([_c_p, _c_i, _c_p, _c_i, _c_p, _c_p], _c_i),
     "nerf_gemm_set_policy": ([_c_i, _c_i], _c_i),
@@ -268,6 +270,21 @@ def encode_bwd(pts_o, pts_d, view, z, genc_p, genc_d, n_rays, n_samples, g_po, g
 def pack_weights(descs: Sequence[PackDesc]):
     arr = (PackDesc * len(descs))(*descs)
     _call("nerf_pack_weights", arr, len(descs), _stream())
+
+
+def render_eval_fused(pts_o, pts_d, view, R, S, near, far, flags, layers: Sequence[ChainLayer], wd, bd, wc, bc,
+                      rgb, dist, alpha, z):
+    """The fused per-ray eval render (one launch: samples, encodings, ten linears, heads,
+    composite; GEMM precision mode 2, hidden 256, S >= 2 dividing 128)."""
+    if len(layers) != 10:
+        raise ValueError("render_eval_fused: needs the 10 layer descriptors")
+    for t in (pts_o, pts_d, view, wd, bd, wc, bc, rgb, dist, alpha, z):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise RuntimeError("render_eval_fused: float32 contiguous tensors expected")
+    arr = (ChainLayer * 10)(*layers)
+    _call("nerf_render_eval_fused", _ptr(pts_o), _ptr(pts_d), _ptr(view), int(R), int(S), float(near), float(far),
+          int(flags), arr, _ptr(wd), _ptr(bd), _ptr(wc), _ptr(bc), _ptr(rgb), _ptr(dist), _ptr(alpha), _ptr(z),
+          _stream())
 
 
 def mlp_chain_fwd(enc_p, enc_d, enc_p_rmax, enc_d_rmax, n_pad, layers: Sequence[ChainLayer]):

@@ -228,6 +228,29 @@ class FieldRunner:
         env = os.environ.get("NERF_CHAIN")
         return env == "1" if env is not None else not keep
 
+    def use_fused_eval(self, S: int) -> bool:
+        """The fused per-ray eval kernel (nerf_render_eval_fused: samples, encodings, the
+        layer chain, heads and composite in one launch) covers the chain's configurations
+        when a ray's samples tile the 128-row block (S >= 2 divides 128).  NERF_FUSED=0
+        falls back to the chain + separate encode / heads / composite launches."""
+        if os.environ.get("NERF_FUSED") == "0":
+            return False
+        return self.use_chain(False) and S >= 2 and 128 % S == 0
+
+    def render_eval_fused(self, pts_o, pts_d, view, near, far, S: int, flags: int):
+        """-> rgb [R,3], dist [R], alpha [R,S], z [R,S] in one launch (no saved state)."""
+        R = pts_o.shape[0]
+        dev = pts_o.device
+        self.pack()
+        descs = [_hip.ChainLayer(self.ws[l.name].data_ptr(), self.ws[l.name].shape[2], self.bias(l).data_ptr(),
+                                 None, l.out_p, None, l.out_p // 32, None) for l in self.layers]
+        e = lambda *sh: torch.empty(*sh, device=dev, dtype=torch.float32)
+        rgb, dist, alpha, z = e(R, 3), e(R), e(R, S), e(R, S)
+        m = self.m
+        _hip.render_eval_fused(pts_o, pts_d, view, R, S, near, far, flags, descs, m.fc_density.weight,
+                               m.fc_density.bias, self.wc, m.fc_rgb.bias, rgb, dist, alpha, z)
+        return rgb, dist, alpha, z
+
     def _rmax_alloc(self, Np: int, dev):
         """Row-max buffer factory for precision mode 2 (None otherwise): a buffer for an
         operand of `width` columns; wider than one 256-column GEMM block it is max-accumulated
@@ -418,6 +441,10 @@ def render_field_eval(module, pts_o, pts_d, view, near, far, S, flags, ray_chunk
     few, large launches on a 288 GB device."""
     runner = module.hip_runner()
     R = pts_o.shape[0]
+    if runner.use_fused_eval(S):
+        # one launch for the whole frame: nothing per-sample is materialised but alpha / z
+        return runner.render_eval_fused(pts_o.contiguous(), pts_d.contiguous(), view.contiguous(), near, far, S,
+                                        flags)
     outs = []
     for r0 in range(0, R, ray_chunk):
         r1 = min(R, r0 + ray_chunk)
