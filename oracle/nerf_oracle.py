@@ -375,7 +375,7 @@ def mean_on_mask(diff, valid_mask):
     mask = valid_mask.expand_as(diff)
     if mask.sum() > 0:
         return diff[mask].sum() / mask.sum()
-    return torch.tensor(0.0, dtype=diff.dtype)
+    return torch.tensor(0.0, dtype=diff.dtype, device=diff.device)
 
 
 def rgb_s_loss(rgb1, rgb2, valid_points):
@@ -416,7 +416,7 @@ def depth_consistency_loss(d1_proj, d2, d2_proj=None, d1=None):
 def t_cycle_loss(rt_pred, rt_gt):
     """losses.py:161-162: Frobenius norm of I - inverse(Rt_gt) @ Rt_pred (relative pose of
     the image pair, training.py:329-358)."""
-    eye = torch.eye(4, dtype=rt_gt.dtype)
+    eye = torch.eye(4, dtype=rt_gt.dtype, device=rt_gt.device)
     return torch.linalg.norm(eye - torch.inverse(rt_gt) @ rt_pred)
 
 
@@ -425,7 +425,7 @@ def total_loss(rgb_pred, rgb_gt, depth_pred, depth_gt, weights: dict, rgb_loss_t
     """losses.py:164-228: the weighted sum of every term the trainer can switch on, with
     the reference's output keys; a term is evaluated only when its weight is non-zero."""
     dt = rgb_pred.dtype if rgb_pred is not None else torch.float32
-    z = torch.zeros((), dtype=dt)
+    z = torch.zeros((), dtype=dt, device=rgb_pred.device if rgb_pred is not None else "cpu")
     w = {k: weights.get(k, 0.0) for k in ("rgb_weight", "depth_weight", "pc_weight", "rgb_s_weight",
                                           "weight_dist_1st_loss", "weight_dist_2nd_loss",
                                           "depth_consistency_weight", "t_cycle_weight")}
@@ -486,7 +486,7 @@ def train_step_render(model: OracleNerf, optimizer, img, depth_img, camera_mat, 
     world_mat = torch.inverse(c2w).unsqueeze(0)                           # training.py:257
     img_flat = img.view(1, 3, h * w).permute(0, 2, 1)
     rgb_gt = img_flat[:, ray_idx]                                          # training.py:285-286
-    p = arange_pixels(h, w, dtype=img.dtype)[1][:, ray_idx]               # training.py:287-288
+    p = arange_pixels(h, w, device=img.device, dtype=img.dtype)[1][:, ray_idx]   # training.py:287-288
     depth = F.interpolate(depth_img, (h, w), mode="area").view(1, 1, -1).permute(0, 2, 1)[:, ray_idx]
     out = render_nope_nerf(model, p, depth, camera_mat, world_mat, scale_mat, cfg_render, noise)
     ld = total_loss(out["rgb"], rgb_gt, out["depth_pred"], out["depth_gt"],
@@ -572,7 +572,7 @@ def compute_loss_full(model, pose, distortion, data, tcfg, rcfg, epoch, scheduli
     depth_input = depth_input * scale_input + shift_input                    # shift_first False
     img_flat = img.view(B, 3, h * w_).permute(0, 2, 1)
     rgb_gt = img_flat[:, ray_idx]                                             # :285-286
-    p = arange_pixels(h, w_, dtype=img.dtype)[1][:, ray_idx]                 # :287-288
+    p = arange_pixels(h, w_, device=img.device, dtype=img.dtype)[1][:, ray_idx]   # :287-288
     out = {}
     if render_model:                                                          # :290-303
         depth = F.interpolate(depth_input, (h, w_), mode="area").reshape(1, -1, 1)[:, ray_idx]
@@ -604,7 +604,7 @@ def compute_loss_full(model, pose, distortion, data, tcfg, rcfg, epoch, scheduli
             scale1 = scale_ref
         R_rel_12, t_rel_12 = Rt_rel_12[:, :3, :3], Rt_rel_12[:, :3, 3]
         res = (int(h_depth / tcfg["pc_ratio"]), int(w_depth / tcfg["pc_ratio"]))   # :360-361
-        p_pc = arange_pixels(res[0], res[1], dtype=img.dtype)[1]
+        p_pc = arange_pixels(res[0], res[1], device=img.device, dtype=img.dtype)[1]
         d1 = F.interpolate(d1, res, mode="nearest")
         d2 = F.interpolate(d2, res, mode="nearest")
         d1 = torch.where(d1 < nl, torch.full_like(d1, nl), d1)              # d1[d1 < nl] = nl
