@@ -255,9 +255,12 @@ def composite(alpha: torch.Tensor, rgb: torch.Tensor, z: torch.Tensor, dist_alph
 
 def render_nope_nerf(model: OracleNerf, pixels, depth, camera_mat, world_mat, scale_mat,
                      cfg: Optional[dict] = None, noise: Optional[torch.Tensor] = None,
-                     eval_: bool = False) -> Dict[str, torch.Tensor]:
+                     eval_: bool = False, chunk: Optional[int] = None) -> Dict[str, torch.Tensor]:
     """Renderer.nope_nerf, rendering.py:36-168 (uniform and ndc sampling).
-    ``noise`` is the injected U[0,1) (1,R,S) tensor; None == add_noise False."""
+    ``noise`` is the injected U[0,1) (1,R,S) tensor; None == add_noise False.  ``chunk``:
+    evaluate the network in chunks of that many samples, as rendering.py:102-111 does with
+    n_max_network_queries (a no-op in exact arithmetic; on a GPU it changes the GEMM
+    shapes and so their rounding -- the convergence study's reference-vs-reference control)."""
     c = dict(DEFAULT_RENDER_CFG)
     c.update(cfg or {})
     S = c["num_points"] - c["outside_steps"]
@@ -276,7 +279,11 @@ def render_nope_nerf(model: OracleNerf, pixels, depth, camera_mat, world_mat, sc
     dirs = -1 * ray.unsqueeze(-2).repeat(1, S, 1).reshape(-1, 3)
     if not c["use_ray_dir"]:
         dirs = torch.ones_like(dirs)
-    rgb_s, alpha_s = model(pts, dirs)               # rendering.py:100-111 (chunking is a no-op)
+    if chunk:                                       # rendering.py:100-111
+        outs = [model(pts[i:i + chunk], dirs[i:i + chunk]) for i in range(0, pts.shape[0], chunk)]
+        rgb_s, alpha_s = torch.cat([o[0] for o in outs]), torch.cat([o[1] for o in outs])
+    else:
+        rgb_s, alpha_s = model(pts, dirs)           # (chunking is a no-op in exact arithmetic)
     rgb_out, dist, alpha, _ = composite(alpha_s.view(R, S), rgb_s.view(R, S, 3), z.view(R, S),
                                         c["dist_alpha"], c["white_background"])
     if eval_ and c["normalise_ray"]:                # rendering.py:144-148
@@ -477,7 +484,7 @@ def camera_K(h: int, w: int, fx: float, fy: float, dtype=torch.float32):
 
 def train_step_render(model: OracleNerf, optimizer, img, depth_img, camera_mat, c2w, scale_mat,
                       ray_idx, noise, cfg_render=None, rgb_weight=1.0, depth_weight=0.04,
-                      rgb_loss_type="l2"):
+                      rgb_loss_type="l2", chunk=None):
     """training.py:70-100 with compute_loss restricted to the render branch
     (training.py:277-303; losses rgb + depth as configured for epoch 0 of straight_d1
     minus the reference-image branch).  ``ray_idx``/``noise`` are injected."""
@@ -488,7 +495,7 @@ def train_step_render(model: OracleNerf, optimizer, img, depth_img, camera_mat, 
     rgb_gt = img_flat[:, ray_idx]                                          # training.py:285-286
     p = arange_pixels(h, w, device=img.device, dtype=img.dtype)[1][:, ray_idx]   # training.py:287-288
     depth = F.interpolate(depth_img, (h, w), mode="area").view(1, 1, -1).permute(0, 2, 1)[:, ray_idx]
-    out = render_nope_nerf(model, p, depth, camera_mat, world_mat, scale_mat, cfg_render, noise)
+    out = render_nope_nerf(model, p, depth, camera_mat, world_mat, scale_mat, cfg_render, noise, chunk=chunk)
     ld = total_loss(out["rgb"], rgb_gt, out["depth_pred"], out["depth_gt"],
                     {"rgb_weight": rgb_weight, "depth_weight": depth_weight}, rgb_loss_type)
     ld["loss"].backward()

@@ -5,9 +5,18 @@ backward, fused loss, HipAdam) and the oracle (CPU restatement of training.py:70
 by torch on the GPU as the checker: it is device-agnostic and gfx950 has no TF32, so its
 fp32 GEMMs are true fp32) train the same initial field on the same synthetic V_KITTI-shaped
 scene with identical ray draws and stratified noise every step.  The HIP side is trained
-once per GEMM arithmetic (exact-f32 MFMA, bf16x6, f16x3).  Every --every steps all sides
-render every pixel without noise and report PSNR (common.py:623-630); the run continues
-to --steps (default 2000).  One JSON line per (width, seed) and a summary line.
+once per GEMM arithmetic (exact-f32 MFMA, bf16x6, f16x3).
+
+Training is chaotic: after a few hundred Adam steps two fp32 runs that differ only in
+rounding follow different trajectories, and a single snapshot PSNR swings by dB from one
+step to the next.  So the study compares the PLATEAU: the PSNR of the mean full-frame MSE
+over the evaluations in the last --window steps (every --every-late steps), per seed and
+averaged over seeds.  As a control it trains a second oracle whose network runs in the
+reference's own 64 000-sample chunks (rendering.py:102-111: exact arithmetic is unchanged,
+the GEMM rounding is not) -- the reference-vs-reference spread is the floor any port can be
+held to.  The scene has fine texture (a blurred noise layer over smooth gradients) so the
+fields plateau below the noise-free 45-50 dB regime.  One JSON line per (width, seed) and a
+summary line.
 
     python scripts/convergence.py [--steps 2000 --seeds 0 1 2 --widths 64 256]
 """
@@ -32,12 +41,16 @@ H, W, FX = 94, 310, 181.25                       # half the V_KITTI frame (188 x
 
 
 def scene(seed, dev):
-    """A smooth synthetic image + depth prior (U-shaped road-like ramp, 5 % holes)."""
+    """Smooth gradients + a blurred noise texture (correlation ~3 px), depth prior a road-like
+    ramp with 5 % holes."""
     g = torch.Generator().manual_seed(1000 + seed)
     yy, xx = torch.meshgrid(torch.linspace(0, 1, H), torch.linspace(0, 1, W), indexing="ij")
     ph = torch.rand(3, generator=g) * 6.28
-    img = torch.stack([0.5 + 0.35 * torch.sin(5 * xx + 2 * yy + ph[0]), 0.5 + 0.35 * torch.cos(4 * yy - 3 * xx + ph[1]),
-                       0.35 + 0.3 * torch.sin(3 * xx * yy + ph[2])], 0).unsqueeze(0)
+    img = torch.stack([0.5 + 0.3 * torch.sin(5 * xx + 2 * yy + ph[0]), 0.5 + 0.3 * torch.cos(4 * yy - 3 * xx + ph[1]),
+                       0.35 + 0.25 * torch.sin(3 * xx * yy + ph[2])], 0).unsqueeze(0)
+    tex = torch.nn.functional.avg_pool2d(torch.rand(1, 3, H, W, generator=g) - 0.5, 3, stride=1, padding=1,
+                                         count_include_pad=False)
+    img = (img + 0.5 * tex).clamp(0, 1)
     depth = 1.5 + 5.0 * yy + 0.5 * torch.sin(4 * xx) + 0.05 * torch.rand(H, W, generator=g)
     holes = torch.rand(H, W, generator=g) < 0.05
     depth[holes] = 0.0
@@ -52,6 +65,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--every", type=int, default=250)
+    ap.add_argument("--window", type=int, default=500, help="plateau window (last steps)")
+    ap.add_argument("--every-late", type=int, default=50, help="evaluation spacing inside the window")
+    ap.add_argument("--chunk", type=int, default=64000,
+                    help="control oracle's network chunk (the reference's n_max_network_queries); capped at half a "
+                         "step's samples so the control always splits its GEMMs")
     ap.add_argument("--seeds", type=int, nargs="+", default=[0, 1, 2])
     ap.add_argument("--widths", type=int, nargs="+", default=[64, 256])
     ap.add_argument("--modes", nargs="+", default=list(MODES))
@@ -89,6 +107,9 @@ def main():
             ref = orc.OracleNerf(hidden_dim=D).to(dev)
             ref.load_state_dict(init)
             opt_o = torch.optim.Adam(ref.parameters(), lr=1e-3)
+            ref_b = orc.OracleNerf(hidden_dim=D).to(dev)       # control: the reference's chunked network
+            ref_b.load_state_dict(init)
+            opt_b = torch.optim.Adam(ref_b.parameters(), lr=1e-3)
             # HIP sides
             sides = {}
             for name in args.modes:
@@ -107,25 +128,27 @@ def main():
                                                    dense_depth=True)
                 return psnr(((out["rgb"] - img_flat) ** 2).mean().item())
 
-            def eval_oracle():
+            def eval_oracle(net):
                 with torch.no_grad():
                     rgb = []
                     for r0 in range(0, H * W, 8192):
-                        o = orc.render_nope_nerf(ref, pix[:, r0:r0 + 8192], depth.reshape(1, -1, 1)[:, r0:r0 + 8192],
+                        o = orc.render_nope_nerf(net, pix[:, r0:r0 + 8192], depth.reshape(1, -1, 1)[:, r0:r0 + 8192],
                                                  K, w2c, scale, cfg["rendering"], noise=None)
                         rgb.append(o["rgb"])
                     rgb = torch.cat(rgb, 1)
                 return psnr(((rgb - img_flat) ** 2).mean().item())
 
-            curve = {"step": [], "oracle": [], **{m: [] for m in args.modes}}
+            sides_all = ["oracle", "oracle_chunked"] + list(args.modes)
+            curve = {"step": [], **{m: [] for m in sides_all}}
 
             def record(step):
                 curve["step"].append(step)
-                curve["oracle"].append(eval_oracle())
+                curve["oracle"].append(eval_oracle(ref))
+                curve["oracle_chunked"].append(eval_oracle(ref_b))
                 for m in args.modes:
                     curve[m].append(eval_hip(m))
-                print(f"D={D} seed={seed} step {step}: oracle {curve['oracle'][-1]:.4f} dB  " +
-                      "  ".join(f"{m} {curve[m][-1]:.4f}" for m in args.modes), file=sys.stderr, flush=True)
+                print(f"D={D} seed={seed} step {step}: " + "  ".join(f"{m} {curve[m][-1]:.4f}" for m in sides_all),
+                      file=sys.stderr, flush=True)
 
             record(0)
             g = torch.Generator().manual_seed(77 + seed)
@@ -136,25 +159,46 @@ def main():
                 noise = torch.rand(1, R, S, generator=g)
                 ri, nz = ray_idx.to(dev), noise.to(dev)
                 orc.train_step_render(ref, opt_o, img, depth.unsqueeze(1), K, c2w, scale, ri, nz, cfg["rendering"])
+                orc.train_step_render(ref_b, opt_b, img, depth.unsqueeze(1), K, c2w, scale, ri, nz, cfg["rendering"],
+                                      chunk=min(args.chunk, R * S // 2))
                 for m in args.modes:
                     _hip.gemm_set_precision(MODES[m])
                     tr = sides[m][0]
                     tr.inject = (ri, nz)
                     tr.train_step(data, it=step, epoch=0, scheduling_start=0)
-                if step % args.every == 0 or step == args.steps:
+                late = step > args.steps - args.window
+                if step % args.every == 0 or step == args.steps or (late and step % args.every_late == 0):
                     record(step)
-            final = {m: curve[m][-1] for m in args.modes}
-            last = curve["oracle"][-1]
-            k = max(0, len(curve["step"]) - 3)                      # ~500 steps before the end
+            # plateau: PSNR of the mean MSE over the evaluations inside the window
+            win = [i for i, st in enumerate(curve["step"]) if st >= args.steps - args.window]
+            plateau = {m: -10.0 * math.log10(sum(10 ** (-curve[m][i] / 10) for i in win) / len(win)) for m in sides_all}
+            early = [i for i, st in enumerate(curve["step"]) if args.steps - 2 * args.window <= st < args.steps - args.window]
+            prev = (-10.0 * math.log10(sum(10 ** (-curve["oracle"][i] / 10) for i in early) / len(early))
+                    if early else None)
             line = {"width": D, "samples": S, "rays": R, "seed": seed, "steps": args.steps, "image": [H, W],
-                    "psnr_oracle": last, "psnr_hip": final, "delta_db": {m: final[m] - last for m in args.modes},
-                    "oracle_gain_last_500_steps_db": last - curve["oracle"][k],
+                    "plateau_window_steps": args.window, "plateau_evals": len(win), "plateau_psnr": plateau,
+                    "delta_db": {m: plateau[m] - plateau["oracle"] for m in sides_all if m != "oracle"},
+                    "oracle_plateau_gain_over_previous_window_db": (plateau["oracle"] - prev) if prev else None,
                     "curve": curve, "seconds": time.time() - t0}
             print(json.dumps(line), flush=True)
             summary.append(line)
-    worst = {m: max(abs(l["delta_db"][m]) for l in summary) for m in args.modes}
-    print(json.dumps({"summary": True, "max_abs_delta_db": worst, "runs": len(summary),
-                      "bar_db": 0.1, "pass": all(v <= 0.1 for v in worst.values())}), flush=True)
+    keys = [m for m in summary[0]["delta_db"]]
+    agg = {}
+    for D in args.widths:
+        runs = [l for l in summary if l["width"] == D]
+        agg[D] = {}
+        for m in keys + ["oracle"]:
+            v = [l["plateau_psnr"][m] for l in runs]
+            agg[D][m] = {"mean_plateau_psnr": sum(v) / len(v)}
+        for m in keys:
+            d = [l["delta_db"][m] for l in runs]
+            mu = sum(d) / len(d)
+            sd = (sum((x - mu) ** 2 for x in d) / max(1, len(d) - 1)) ** 0.5
+            agg[D][m].update({"mean_delta_db": mu, "std_delta_db": sd, "max_abs_delta_db": max(abs(x) for x in d)})
+    ok = all(abs(agg[D][m]["mean_delta_db"]) <= 0.1 for D in args.widths for m in args.modes)
+    print(json.dumps({"summary": True, "per_width": agg, "seeds": args.seeds, "bar_db": 0.1,
+                      "bar": "|mean over seeds of plateau PSNR(HIP) - plateau PSNR(oracle)| <= 0.1 dB",
+                      "pass": ok}), flush=True)
 
 
 if __name__ == "__main__":
