@@ -123,17 +123,22 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 KIND_NAMES = {
     "fwd": "forward NT (nerf_linear_fwd)",
     "dx": "input-gradient NT (nerf_linear_bwd_data)",
-    "dw": "weight-gradient TN (nerf_linear_bwd_weight; algorithmic bytes exclude the split-K slabs)",
+    "dw": "weight-gradient TN on 256x256 tiles (nerf_linear_bwd_weight; algorithmic bytes exclude the split-K "
+          "slabs)",
+    "dw_narrow": "narrow weight-gradient TN (encoding segments, colour layer; nerf_linear_bwd_weight)",
 }
 KERNEL = {
     "f16x3": {"fwd": "k_gemm_nt_x6<128,256,2,2,0,true,true,2> (fp16 pair, 3 products)",
               "dx": "k_gemm_nt_x6<128,256,2,2,1,true,true,2> (fp16 pair, 3 products)",
-              "dw": "k_gemm_tn_x6<256,256,2,2,true> (fp16 pair, 3 products)"},
+              "dw": "k_gemm_tn_x6<256,256,2,2,true> (fp16 pair, 3 products)",
+              "dw_narrow": "k_gemm_tn_x6<128,64|128,2,2,true> (fp16 pair, 3 products)"},
     "bf16x6": {"fwd": "k_gemm_nt_x6<256,256,2,2,0,true> (bf16x3 split, 6 products)",
                "dx": "k_gemm_nt_x6<256,256,2,2,1,true> (bf16x3 split, 6 products)",
-               "dw": "k_gemm_tn_x6<256,256,2,2,false> (bf16x3 split, 6 products)"},
+               "dw": "k_gemm_tn_x6<256,256,2,2,false> (bf16x3 split, 6 products)",
+               "dw_narrow": "k_gemm_tn_x6<128,64|128,2,2,false> (bf16x3 split, 6 products)"},
     "f32": {"fwd": "k_gemm_nt<256,256,2,4,0> (f32 MFMA 32x32x2)", "dx": "k_gemm_nt<256,256,2,4,1> (f32 MFMA 32x32x2)",
-            "dw": "k_gemm_tn<256,256,2,4> (f32 MFMA 32x32x2)"},
+            "dw": "k_gemm_tn<256,256,2,4> (f32 MFMA 32x32x2)",
+            "dw_narrow": "k_gemm_tn<128,64|128,...> (f32 MFMA 32x32x2)"},
 }
 
 

@@ -378,7 +378,8 @@ int nerf_prof_read(double* gemm_ms, int64_t* gemm_launches, double* gemm_flops, 
 
 /* Per-kind breakdown of the same records (call before nerf_prof_read, which resets them):
  * kind 0 = forward NT (nerf_linear_fwd), 1 = input gradient NT (nerf_linear_bwd_data),
- * 2 = weight gradient TN (nerf_linear_bwd_weight).  flops: algorithmic f32 FLOPs of the
+ * 2 = weight gradient TN (nerf_linear_bwd_weight) on 256 x 256 output tiles, 3 = the narrow
+ * weight gradients (an output or K side below 256: the encoding segments, the colour layer).  flops: algorithmic f32 FLOPs of the
  * launches (2*m*n*k, padded shapes); bytes: their algorithmic HBM bytes (operands read
  * once, outputs written once: A, B, C and the ReLU bit masks; for the weight gradient the
  * dY and X panels plus ONE nout x kin gradient, not the split-K slabs); mfma_flops: flops
@@ -389,7 +390,8 @@ int nerf_prof_read(double* gemm_ms, int64_t* gemm_launches, double* gemm_flops, 
 #define NERF_PROF_FWD 0
 #define NERF_PROF_DX 1
 #define NERF_PROF_DW 2
-#define NERF_PROF_KINDS 3
+#define NERF_PROF_DW_NARROW 3
+#define NERF_PROF_KINDS 4
 typedef struct nerf_prof_kind {
     double ms;
     int64_t launches;

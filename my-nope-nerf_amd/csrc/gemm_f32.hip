@@ -446,7 +446,8 @@ extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const
     const double fl = 2.0 * m * nout * (double)kin;
     // algorithmic bytes: the dy and x panels and one nout x kin gradient (+ bias); the
     // split-K slabs are structural traffic of this design, not algorithmic
-    prof_next(NERF_PROF_DW, 4.0 * m * (double)(nout + kin) + 4.0 * nout * (double)kin + (bslab ? 4.0 * nout : 0.0));
+    prof_next(nout % 256 == 0 && kin % 256 == 0 ? NERF_PROF_DW : NERF_PROF_DW_NARROW,
+              4.0 * m * (double)(nout + kin) + 4.0 * nout * (double)kin + (bslab ? 4.0 * nout : 0.0));
     const int pol = g_tn_policy ? g_tn_policy : 3;
     if (g_precision >= 1) return dispatch_tn_x6(a, nout, kin, splits, pol, s, fl, h16);
     prof_begin(s);

@@ -45,7 +45,7 @@ class ProfKind(ctypes.Structure):
                 ("bytes", ctypes.c_double), ("mfma_flops", ctypes.c_double), ("exact_f32", _c_i)]
 
 
-PROF_KINDS = ("fwd", "dx", "dw")   # NERF_PROF_FWD / _DX / _DW
+PROF_KINDS = ("fwd", "dx", "dw", "dw_narrow")   # NERF_PROF_FWD / _DX / _DW / _DW_NARROW
 ABI_VERSION = 5                    # NERF_HIP_ABI_VERSION
 
 
@@ -393,7 +393,7 @@ def prof_enable(on: bool):
 
 def prof_read_kinds():
     """Per-kind GEMM records since prof_enable (call before prof_read, which resets them):
-    {"fwd"|"dx"|"dw": {ms, launches, flops, bytes, mfma_flops, exact_f32}}."""
+    {"fwd"|"dx"|"dw"|"dw_narrow": {ms, launches, flops, bytes, mfma_flops, exact_f32}}."""
     arr = (ProfKind * len(PROF_KINDS))()
     _call("nerf_prof_read_kinds", arr, len(PROF_KINDS))
     return {name: {f: getattr(arr[i], f) for f, _ in ProfKind._fields_} for i, name in enumerate(PROF_KINDS)}
