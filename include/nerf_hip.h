@@ -127,6 +127,9 @@ int nerf_slab_reduce(const float* slab, int splits, int nout, int ldslab, int no
  * 2 = 128x256 / 8 waves, 3 = 256x256 / 8 waves;  tn (weight gradient): 1 = 128x128,
  * 3 = 256x256 / 8 waves. */
 int nerf_gemm_set_policy(int nt_policy, int tn_policy);
+/* Weight-gradient split-K target (tuning knob; 0 = built-in default): about this many
+ * blocks per nerf_linear_bwd_weight launch, as nerf_linear_bwd_weight_splits picks them. */
+int nerf_gemm_set_dw_blocks(int target_blocks);
 
 /* f32 arithmetic of the GEMM family (process-wide; default 0):
  *   0  exact-f32 v_mfma_f32_32x32x2_f32 (a k-ordered f32 fma chain);

@@ -328,6 +328,7 @@ static int launch_nt(const NTArgs& a, hipStream_t s, double flops) {
 // 3 = 256x256/8 waves
 static int g_nt_policy = 0;
 static int g_tn_policy = 0;
+static int g_dw_blocks = 0;   // nerf_gemm_set_dw_blocks: target blocks per weight-gradient launch (0 = default)
 
 // f32 arithmetic (nerf_gemm_set_precision): 0 = exact-f32 MFMA, 1 = split-bf16 emulation
 static int g_precision = 0;
@@ -487,6 +488,12 @@ extern "C" int nerf_slab_reduce(const float* slab, int splits, int nout, int lds
     return check_launch(__func__);
 }
 
+extern "C" int nerf_gemm_set_dw_blocks(int target_blocks) {
+    NERF_CHECK(target_blocks >= 0 && target_blocks <= 1 << 16, "%s: target %d", __func__, target_blocks);
+    g_dw_blocks = target_blocks;
+    return NERF_OK;
+}
+
 extern "C" int nerf_gemm_set_policy(int nt_policy, int tn_policy) {
     NERF_CHECK(nt_policy >= 0 && nt_policy <= 3 && tn_policy >= 0 && tn_policy <= 3,
                "%s: policies are 0..3", __func__);
@@ -505,6 +512,7 @@ extern "C" int nerf_linear_bwd_weight_splits(int nout, int kin, int m) {
     else { tiles = ((nout + 127) / 128) * ((kin + 127) / 128); target = 512; }
     static const int env_target = [] { const char* e = getenv("NERF_DW_BLOCKS"); return e ? atoi(e) : 0; }();
     if (env_target > 0) target = env_target;   // experiment hook: blocks per dW launch
+    if (g_dw_blocks > 0) target = g_dw_blocks;  // nerf_gemm_set_dw_blocks
     int splits = 1;
     while (splits * 2 * tiles <= target && m % (splits * 2 * BK) == 0 && m / (splits * 2) >= 256) splits *= 2;
     return splits;

@@ -83,6 +83,7 @@ _SIGS = {
     "nerf_adam_step": ([_c_p, _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p], _c_i),
     "nerf_chamfer_nn": ([_c_p, _c_i, _c_p, _c_i, _c_p, _c_p], _c_i),
     "nerf_gemm_set_policy": ([_c_i, _c_i], _c_i),
+    "nerf_gemm_set_dw_blocks": ([_c_i], _c_i),
     "nerf_gemm_set_precision": ([_c_i], _c_i),
     "nerf_gemm_get_precision": ([], _c_i),
     "nerf_gemm_debug_ablate": ([_c_i], _c_i),
@@ -381,6 +382,11 @@ def gemm_set_precision(mode):
     2 = f32 emulated on fp16 MFMA for the forward / backward-data GEMMs (row-scaled 2-word
     split, 3 products; weight gradients as mode 1)."""
     _call("nerf_gemm_set_precision", int(mode))
+
+
+def gemm_set_dw_blocks(target: int):
+    """Weight-gradient split-K target blocks per launch (0 = default)."""
+    _call("nerf_gemm_set_dw_blocks", int(target))
 
 
 def gemm_get_precision():

@@ -1,0 +1,71 @@
+"""A/B of GEMM tuning knobs on the real cfg2 training step (bench.py's workload), one
+trainer, settings interleaved over rounds; prints ms/step per setting (median of rounds).
+
+    python scripts/step_ab.py [--steps 20 --rounds 3]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "my-nope-nerf_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+# name -> (nt policy, tn policy, dW target blocks); 0 = default
+SETTINGS = {
+    "default": (0, 0, 0),
+    "tn128_b256": (0, 1, 256),
+    "tn128_b512": (0, 1, 512),
+    "tn128_b1024": (0, 1, 1024),
+    "tn256_b128": (0, 0, 128),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--settings", nargs="+", default=list(SETTINGS))
+    args = ap.parse_args()
+    from model import _hip
+    _hip.load_library()
+    _hip.gemm_set_precision(2)
+    dev = torch.device("cuda", 0)
+    cfg = bench.make_cfg()
+    data, c2w = bench.synthetic_scene(dev)
+    trainer, _ = bench.build_trainer(dev, c2w, cfg)
+    it = 0
+    res = {k: [] for k in args.settings}
+    for _ in range(args.rounds):
+        for name in args.settings:
+            nt, tn, blocks = SETTINGS[name]
+            _hip.gemm_set_policy(nt, tn)
+            _hip.gemm_set_dw_blocks(blocks)
+            for _ in range(3):
+                trainer.train_step(data, it=it, epoch=0, scheduling_start=0)
+                it += 1
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                ld = trainer.train_step(data, it=it, epoch=0, scheduling_start=0)
+                it += 1
+            torch.cuda.synchronize()
+            res[name].append(1e3 * (time.perf_counter() - t0) / args.steps)
+            if not torch.isfinite(ld["loss"]).item():
+                raise RuntimeError(f"{name}: non-finite loss")
+    _hip.gemm_set_policy(0, 0)
+    _hip.gemm_set_dw_blocks(0)
+    print(json.dumps({k: {"ms_per_step_median": statistics.median(v), "rounds": v} for k, v in res.items()}))
+
+
+if __name__ == "__main__":
+    main()
