@@ -130,6 +130,9 @@ int nerf_gemm_set_policy(int nt_policy, int tn_policy);
 /* Weight-gradient split-K target (tuning knob; 0 = built-in default): about this many
  * blocks per nerf_linear_bwd_weight launch, as nerf_linear_bwd_weight_splits picks them. */
 int nerf_gemm_set_dw_blocks(int target_blocks);
+/* Output-tile store hint of the split NT GEMMs (tuning knob; default 0 = plain stores,
+ * 1 = non-temporal).  NERF_STORE_NT in the environment sets the initial value. */
+int nerf_gemm_set_store_hint(int nontemporal);
 
 /* f32 arithmetic of the GEMM family (process-wide; default 0):
  *   0  exact-f32 v_mfma_f32_32x32x2_f32 (a k-ordered f32 fma chain);

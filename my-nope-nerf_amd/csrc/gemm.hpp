@@ -48,7 +48,20 @@ struct NTArgs {
     const float* ar1; const float* ar2;
     float* c_rmax;
     float* c_cmax; int ldcm;
+    int store_nt;   // tuning (nerf_gemm_set_store_hint): output tiles stored with the non-temporal hint
 };
+
+typedef float nt_f32x4 __attribute__((ext_vector_type(4)));
+// a float4 of the output tile: plain store, or non-temporal (streaming: the tile is not
+// read back by this kernel, the next layer reads it from HBM / the infinity cache)
+__device__ __forceinline__ void store_out4(float* dst, const float4& x, bool nt) {
+    if (nt) {
+        const nt_f32x4 v = {x.x, x.y, x.z, x.w};
+        __builtin_nontemporal_store(v, reinterpret_cast<nt_f32x4*>(dst));
+    } else {
+        *reinterpret_cast<float4*>(dst) = x;
+    }
+}
 
 // max |a| over row m of the (one or two segment) A operand
 __device__ __forceinline__ float a_rowmax(const NTArgs& p, int m) {
@@ -449,7 +462,7 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
                                            acc[i][j][4 * q + 2] + b4[q].z, acc[i][j][4 * q + 3] + b4[q].w);
                     if (p.relu) x = make_float4(fmaxf(x.x, 0.f), fmaxf(x.y, 0.f), fmaxf(x.z, 0.f), fmaxf(x.w, 0.f));
                     track(i, j, q, x);
-                    *reinterpret_cast<float4*>(p.c + row * p.ldc + fb + 8 * q) = x;
+                    store_out4(p.c + row * p.ldc + fb + 8 * q, x, p.store_nt);
                     const uint32_t nib = (x.x > 0.f ? 1u : 0u) | (x.y > 0.f ? 2u : 0u) | (x.z > 0.f ? 4u : 0u) |
                                          (x.w > 0.f ? 8u : 0u);
                     w |= nib << (8 * q + 4 * hf);
@@ -496,7 +509,7 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
                     x.z = (bits & 4u) ? x.z : 0.f;
                     x.w = (bits & 8u) ? x.w : 0.f;
                     track(i, j, q, x);
-                    *reinterpret_cast<float4*>(p.c + row * p.ldc + fb + 8 * q) = x;
+                    store_out4(p.c + row * p.ldc + fb + 8 * q, x, p.store_nt);
                 }
             }
         }

@@ -328,7 +328,8 @@ static int launch_nt(const NTArgs& a, hipStream_t s, double flops) {
 // 3 = 256x256/8 waves
 static int g_nt_policy = 0;
 static int g_tn_policy = 0;
-static int g_dw_blocks = 0;   // nerf_gemm_set_dw_blocks: target blocks per weight-gradient launch (0 = default)
+static int g_dw_blocks = 0;
+static int g_store_nt = [] { const char* e = getenv("NERF_STORE_NT"); return e ? atoi(e) : 0; }();   // nerf_gemm_set_dw_blocks: target blocks per weight-gradient launch (0 = default)
 
 // f32 arithmetic (nerf_gemm_set_precision): 0 = exact-f32 MFMA, 1 = split-bf16 emulation
 static int g_precision = 0;
@@ -339,6 +340,7 @@ static int dispatch_nt(const NTArgs& a, hipStream_t s, double flops) {
     if (g_precision >= 1 && a.bs != nullptr) {   // the split paths need the weight image
         NTArgs b = a;
         b.ablate = g_ablate;
+        b.store_nt = g_store_nt;
         b.stamps = g_stamps;
         if (g_precision == 2) {
             NERF_CHECK(a.ar1 != nullptr && (a.a2 == nullptr || a.ar2 != nullptr),
@@ -486,6 +488,11 @@ extern "C" int nerf_slab_reduce(const float* slab, int splits, int nout, int lds
     hipLaunchKernelGGL(k_slab_reduce, dim3(blocks), dim3(256), 0, as_stream(stream), slab, splits,
                        nout, ldslab, nout_ref, kin_ref, bslab, gw, gb, accumulate);
     return check_launch(__func__);
+}
+
+extern "C" int nerf_gemm_set_store_hint(int nontemporal) {
+    g_store_nt = nontemporal != 0;
+    return NERF_OK;
 }
 
 extern "C" int nerf_gemm_set_dw_blocks(int target_blocks) {

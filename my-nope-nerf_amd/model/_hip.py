@@ -84,6 +84,7 @@ _SIGS = {
     "nerf_chamfer_nn": ([_c_p, _c_i, _c_p, _c_i, _c_p, _c_p], _c_i),
     "nerf_gemm_set_policy": ([_c_i, _c_i], _c_i),
     "nerf_gemm_set_dw_blocks": ([_c_i], _c_i),
+    "nerf_gemm_set_store_hint": ([_c_i], _c_i),
     "nerf_gemm_set_precision": ([_c_i], _c_i),
     "nerf_gemm_get_precision": ([], _c_i),
     "nerf_gemm_debug_ablate": ([_c_i], _c_i),
@@ -382,6 +383,11 @@ def gemm_set_precision(mode):
     2 = f32 emulated on fp16 MFMA for the forward / backward-data GEMMs (row-scaled 2-word
     split, 3 products; weight gradients as mode 1)."""
     _call("nerf_gemm_set_precision", int(mode))
+
+
+def gemm_set_store_hint(nontemporal: bool):
+    """Output-tile store hint of the split NT GEMMs (tuning knob)."""
+    _call("nerf_gemm_set_store_hint", int(bool(nontemporal)))
 
 
 def gemm_set_dw_blocks(target: int):

@@ -20,13 +20,14 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-# name -> (nt policy, tn policy, dW target blocks); 0 = default
+# name -> (nt policy, tn policy, dW target blocks, non-temporal NT stores); 0 = default
 SETTINGS = {
-    "default": (0, 0, 0),
-    "tn128_b256": (0, 1, 256),
-    "tn128_b512": (0, 1, 512),
-    "tn128_b1024": (0, 1, 1024),
-    "tn256_b128": (0, 0, 128),
+    "default": (0, 0, 0, 0),
+    "store_nt": (0, 0, 0, 1),
+    "tn128_b256": (0, 1, 256, 0),
+    "tn128_b512": (0, 1, 512, 0),
+    "tn128_b1024": (0, 1, 1024, 0),
+    "tn256_b128": (0, 0, 128, 0),
 }
 
 
@@ -47,9 +48,10 @@ def main():
     res = {k: [] for k in args.settings}
     for _ in range(args.rounds):
         for name in args.settings:
-            nt, tn, blocks = SETTINGS[name]
+            nt, tn, blocks, snt = SETTINGS[name]
             _hip.gemm_set_policy(nt, tn)
             _hip.gemm_set_dw_blocks(blocks)
+            _hip.gemm_set_store_hint(snt)
             for _ in range(3):
                 trainer.train_step(data, it=it, epoch=0, scheduling_start=0)
                 it += 1
@@ -64,6 +66,7 @@ def main():
                 raise RuntimeError(f"{name}: non-finite loss")
     _hip.gemm_set_policy(0, 0)
     _hip.gemm_set_dw_blocks(0)
+    _hip.gemm_set_store_hint(0)
     print(json.dumps({k: {"ms_per_step_median": statistics.median(v), "rounds": v} for k, v in res.items()}))
 
 
