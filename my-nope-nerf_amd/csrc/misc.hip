@@ -112,8 +112,9 @@ __global__ __launch_bounds__(256) void k_pack_h(PackBatch pb) {
 //   g += wd*p; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2
 //   denom = sqrt(v)/sqrt(bc2) + eps;  p -= (lr/bc1) * m / denom
 // Hyper-parameters and the step count live in device memory (hyper = {step, lr, b1, b2,
-// eps, wd, -, ticket}) so a captured hipGraph replays correct bias corrections and picks up
-// lr changes.  Every workgroup uses step + 1; the last one to finish (ticket) stores it.
+// eps, wd, -, ticket}) so a captured hipGraph replays correct bias corrections; an lr change
+// reaches a replay once the host pushes it into the device block (HipAdam.sync_hyper()
+// between replays).  Every workgroup uses step + 1; the last one to finish (ticket) stores it.
 __device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v, float b1, float b2, float eps,
                                           float wd, float sbc2, float step_size) {
     if (wd != 0.f) g = g + wd * p;

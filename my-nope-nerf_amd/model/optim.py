@@ -42,6 +42,13 @@ class HipAdam(torch.optim.Optimizer):
         self._hyper_host = None
         self._sync_hyper()
 
+    def sync_hyper(self):
+        """Push the param-group hyper-parameters (lr, betas, eps, weight decay) into the
+        device block k_adam reads.  step() does this itself when run eagerly; a captured
+        hipGraph replays the launch without the host, so a caller whose LR scheduler edits
+        param_groups between replays calls sync_hyper() after the scheduler step."""
+        self._sync_hyper()
+
     def _sync_hyper(self):
         g = self.param_groups[0]
         h = (float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]), float(g["weight_decay"]))

@@ -225,6 +225,12 @@ class Trainer(object):
             else:
                 n_invalid = n_pix - int(depth_mask.sum())
                 risky = n_invalid > 0 and (n_invalid / n_pix) ** R > 1e-9
+            if risky and self.seed_counter is not None:
+                # graph-capture mode: the resample-until-valid loop needs the host to look at
+                # the draw (a sync inside capture) and a replay could never re-decide it
+                raise RuntimeError(
+                    "Trainer: graph-capture mode (enable_graph_rng) needs a depth mask on the host whose "
+                    "valid-pixel count rules out an all-invalid draw (training.py:280-283 resampling)")
             if risky:
                 m = depth_mask.flatten().to(dev)
                 while not m[ray_idx].any():

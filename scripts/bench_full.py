@@ -5,7 +5,13 @@ point-cloud (chamfer) and reprojection (rgb_s) losses on a V_KITTI-shaped two-vi
 Steps alternate the two cameras (both branches of training.py:329-358).  Inputs resident
 in HBM; synthetic data (no dataset offline).  Prints one JSON line.
 
-    python scripts/bench_full.py [--steps K --warmup W]
+    python scripts/bench_full.py [--steps K --warmup W] [--eager]
+
+By default every step replays a hipGraph of the captured train_step (one per view): the
+eager step's host enqueue (~4.4 ms: pose / distortion autograd, two torch Adams, ~150
+launches) exceeds its GPU time.  The ray sampler keys on a device step counter and the
+pose / distortion Adams are capturable (single fused kernels), so each replay trains on
+fresh rays with correct bias corrections.  --eager times the same step without graphs.
 """
 from __future__ import annotations
 
@@ -70,8 +76,10 @@ def setup(dev, capturable=False):
     opt = HipAdam(nn_model.parameters(), lr=1e-3)
     pose = mdl.LearnPose(2, True, True, cfg, init_c2w=c2w.clone()).to(dev)
     distn = mdl.Learn_Distortion(2, True, True, cfg).to(dev)
-    opt_pose = torch.optim.Adam(pose.parameters(), lr=5e-4, capturable=capturable)   # train.py:100, :118
-    opt_dist = torch.optim.Adam(distn.parameters(), lr=5e-4, capturable=capturable)
+    # train.py:100, :118; one fused kernel per optimiser (torch's fused Adam), capturable in graphs
+    fused = {"fused": True} if capturable else {}
+    opt_pose = torch.optim.Adam(pose.parameters(), lr=5e-4, capturable=capturable, **fused)
+    opt_dist = torch.optim.Adam(distn.parameters(), lr=5e-4, capturable=capturable, **fused)
     tr = mdl.Trainer(nn_model, opt, t, device=dev, optimizer_pose=opt_pose, pose_param_net=pose,
                      optimizer_distortion=opt_dist, distortion_net=distn)
     return tr, datas
@@ -82,9 +90,10 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--gemm-precision", choices=["f32", "bf16x6", "f16x3"], default="f16x3")
-    ap.add_argument("--graph", action="store_true",
-                    help="replay hipGraphs of the two views' captured train_steps (the ray draw keys on a "
-                         "device counter, so every replay trains on new rays) instead of eager enqueue")
+    ap.add_argument("--eager", dest="graph", action="store_false",
+                    help="enqueue every step eagerly instead of replaying the hipGraphs of the two views' "
+                         "captured train_steps (default: graphs; the ray draw keys on a device counter, so every "
+                         "replay trains on new rays)")
     args = ap.parse_args()
     from model import _hip
     dev = torch.device("cuda", 0)

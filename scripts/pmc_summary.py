@@ -1,38 +1,67 @@
-"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes of `gemm_bench.py --quick --x6` into
-per-launch HBM bytes (MI355X_MICROARCH.md HBM section: FETCH_SIZE is in KiB and counts
-half of the bytes of 16-B-per-lane streaming reads on gfx950 -> x2; WRITE_SIZE exact).
+"""Summarise rocprofv3 PMC passes of the GEMM launches into per-launch HBM bytes per GEMM
+kind (MI355X_MICROARCH.md HBM section: FETCH_SIZE is in KiB and counts half of the bytes
+of 16-B-per-lane streaming reads on gfx950 -> x2; WRITE_SIZE exact).  The passes are
+separate runs of the same command (`bench.py --steps 3 --warmup 2 --no-alt
+--no-cpu-baseline` under `--kernel-include-regex 'k_gemm_(nt|tn)_x6'`); launches of one
+kernel are summarised by their median.
 
-    python scripts/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/r01/gemm_traffic.json
+    python scripts/pmc_summary.py gpurun_out/r02g/pmc_fetch gpurun_out/r02g/pmc_write \\
+        [gpurun_out/r02g/pmc_sq] > profiles/r02/gemm_traffic.json
 """
+import collections
 import csv
 import json
+import statistics
 import sys
 
+M = 131072          # samples per cfg2 step (1024 rays x 128)
+D = 256
+# kernel template -> (GEMM kind of bench.py's roofline, algorithmic bytes per launch, note)
+KINDS = {
+    "k_gemm_nt_x6<128, 256, 2, 2, 0, true, true, 2>": (
+        "fwd", 4 * M * D * 2 + 4 * D * D + M * D / 8, "x 134.2 MB + y 134.2 MB + W 0.26 MB + ReLU bits 4.2 MB "
+        "(256-wide layers; the skip layer reads 320 columns)"),
+    "k_gemm_nt_x6<128, 256, 2, 2, 1, true, true, 2>": (
+        "dx", 4 * M * D * 2 + 4 * D * D + M * D / 8, "dy 134.2 MB + dx 134.2 MB + W^T 0.26 MB + ReLU bits 4.2 MB"),
+    "k_gemm_tn_x6<256, 256, 2, 2, true>": (
+        "dw", 4 * M * D * 2 + 4 * D * D, "dy 134.2 MB + x 134.2 MB + dW 0.26 MB; measured writes are the 256 "
+        "split-K slabs (67 MB)"),
+}
 
-def load(d, counter):
-    agg = {}
+
+def load(d):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
-        if r["Counter_Name"] != counter:
-            continue
-        key = (int(r["Dispatch_Id"]), r["Kernel_Name"])
-        agg[key] = agg.get(key, 0.0) + float(r["Counter_Value"])
+        agg[r["Kernel_Name"].replace("void nerf::", "").split("(")[0]][r["Counter_Name"]].append(
+            float(r["Counter_Value"]))
     return agg
 
 
 def main():
-    fetch, write = load(sys.argv[1], "FETCH_SIZE"), load(sys.argv[2], "WRITE_SIZE")
-    # the two passes run the same launch sequence: pair them by order
-    fk, wk = sorted(fetch), sorted(write)
+    fetch, write = load(sys.argv[1]), load(sys.argv[2])
+    sq = load(sys.argv[3]) if len(sys.argv) > 3 else {}
     out = []
-    for (fd, fn), (wd, wn) in zip(fk, wk):
-        if "gemm" not in fn:
-            continue
-        assert fn == wn, (fn, wn)
-        rd = 2 * fetch[(fd, fn)] * 1024
-        wr = write[(wd, wn)] * 1024
-        out.append({"kernel": fn.split("(")[0], "read_bytes": rd, "write_bytes": wr, "bytes": rd + wr})
-    print(json.dumps({"source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) "
-                                "of scripts/gemm_bench.py --quick --x6; FETCH_SIZE x2 (gfx950 correction)",
+    for k in sorted(fetch):
+        rd = 2 * statistics.median(fetch[k]["FETCH_SIZE"]) * 1024
+        wr = statistics.median(write[k]["WRITE_SIZE"]) * 1024
+        e = {"kernel": k, "launches_profiled": len(fetch[k]["FETCH_SIZE"]), "read_bytes": rd, "write_bytes": wr,
+             "bytes": rd + wr}
+        if k in KINDS:
+            kind, alg, note = KINDS[k]
+            e.update({"kind": kind, "algorithmic_bytes": alg, "traffic_over_algorithmic": (rd + wr) / alg,
+                      "note": f"in-step launches, median over the profiled steps; algorithmic: {note}"})
+        if k in sq:
+            s = {c: statistics.median(v) for c, v in sq[k].items()}
+            waves = s.get("SQ_WAVES", 0) or 1
+            # SQ_WAVE_CYCLES / _WAIT_INST_ANY / _ACTIVE_INST_ANY count quad-cycles (guide)
+            e["per_wave_cycles"] = {"lifetime": 4 * s.get("SQ_WAVE_CYCLES", 0) / waves,
+                                    "waiting_on_dependencies": 4 * s.get("SQ_WAIT_INST_ANY", 0) / waves,
+                                    "issuing": 4 * s.get("SQ_ACTIVE_INST_ANY", 0) / waves,
+                                    "mfma_busy": s.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / waves}
+        out.append(e)
+    print(json.dumps({"source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / --pmc WRITE_SIZE / SQ counters "
+                                "(separate passes) of `bench.py --steps 3 --warmup 2 --no-alt --no-cpu-baseline`, "
+                                "--kernel-include-regex 'k_gemm_(nt|tn)_x6'; FETCH_SIZE x2 (gfx950 correction)",
                       "launches": out}, indent=1))
 
 
