@@ -146,117 +146,6 @@ __device__ __forceinline__ float tn_colmax(const float* cm, int ld, size_t s0, i
     return m;
 }
 
-// ---------------------------------------------------------------------------
-// Main loop shared by the NT and TN kernels (one wave per SIMD, accumulators in AGPRs).
-//
-// 16-deep K tiles alternate between two split-image LDS buffers.  Iteration kt reads
-// the B fragments of tile kt (all TN) and its A fragments one 32-row tile ahead from
-// buffer kt&1 and issues the MFMAs; beside them the stager
-//   issue_early(kt)  starts asynchronous copies at the top of the iteration;
-//   split(kt)        puts tile kt+1 into buffer (kt+1)&1 -- interleaved with row tile
-//                    0's MFMAs (<= 3 VALU per 32-cycle MFMA gap);
-//   issue(kt)        starts the register loads its later iterations need;
-//   before_barrier() waits for whatever the barrier publishes;
-// then one barrier.  Stager::prologue leaves tile 0 in buffer 0.
-// ---------------------------------------------------------------------------
-template <int TM, int TN, int BM, int BN, typename Stager>
-__device__ __forceinline__ void x6_mainloop(char* smem, int nkt, int wm0, int wn0, f32x16 (&acc)[TM][TN],
-                                            Stager& st, unsigned long long* stamps = nullptr) {
-    constexpr bool H = Stager::H;          // fp16 pair (3 products) instead of bf16 triple (6)
-    constexpr int NP = H ? 2 : 3;
-    using IA = XImg<BM, NP>;
-    using IB = XImg<BN, NP>;
-    constexpr int BUF = IA::BYTES + IB::BYTES;
-    const int lane = lane_id();
-    const int l32 = lane & 31, hi = lane >> 5;
-    const int aoff = hi * IA::HALF + (wm0 + l32) * 16;
-    const int boff = IA::BYTES + hi * IB::HALF + (wn0 + l32) * 16;
-    auto rd = [&](const char* q, int plane, uint4 (&f)[NP]) {
-#pragma unroll
-        for (int p = 0; p < NP; ++p) f[p] = *reinterpret_cast<const uint4*>(q + p * plane);
-    };
-    auto mm = [&](int i, const uint4 (&a)[NP], const uint4 (&b)[TN][NP]) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            f32x16 c = acc[i][j];
-            if constexpr (H) {
-                c = mfma_f16(a[0], b[j][1], c);    // hi.lo
-                c = mfma_f16(a[1], b[j][0], c);    // lo.hi
-                c = mfma_f16(a[0], b[j][0], c);    // hi.hi
-            } else {
-                c = mfma_bf16(a[1], b[j][1], c);   // mid.mid
-                c = mfma_bf16(a[0], b[j][2], c);   // hi.lo
-                c = mfma_bf16(a[2], b[j][0], c);   // lo.hi
-                c = mfma_bf16(a[0], b[j][1], c);   // hi.mid
-                c = mfma_bf16(a[1], b[j][0], c);   // mid.hi
-                c = mfma_bf16(a[0], b[j][0], c);   // hi.hi
-            }
-            acc[i][j] = c;
-        }
-    };
-    if constexpr (H) {
-        // three products per tile leave too few MFMA gaps in one row tile for the split:
-        // every fragment is read up front and the split VALU spreads over all row tiles
-        st.prologue(smem, nkt);
-        for (int kt = 0; kt < nkt; ++kt) {
-            const char* cur = smem + (kt & 1) * BUF;
-            char* wimg = smem + ((kt + 1) & 1) * BUF;
-            uint4 b[TN][NP], a[TM][NP];
-#pragma unroll
-            for (int j = 0; j < TN; ++j) rd(cur + boff + 32 * 16 * j, IB::PLANE, b[j]);
-#pragma unroll
-            for (int i = 0; i < TM; ++i) rd(cur + aoff + 32 * 16 * i, IA::PLANE, a[i]);
-            st.split(kt, nkt, wimg, wimg + IA::BYTES);
-            st.issue(kt, nkt, wimg + IA::BYTES);
-#pragma unroll
-            for (int i = 0; i < TM; ++i) mm(i, a[i], b);
-#pragma unroll
-            for (int q = 0; q < 3 * TN * TM; ++q) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            st.before_barrier();
-            __syncthreads();
-        }
-        return;
-    } else {
-    st.prologue(smem, nkt);
-    stamp(stamps, 1);
-    for (int kt = 0; kt < nkt; ++kt) {
-        const char* cur = smem + (kt & 1) * BUF;
-        char* wimg = smem + ((kt + 1) & 1) * BUF;
-        uint4 b[TN][3], a0[3], a1[3];
-        st.issue_early(kt, nkt, wimg + IA::BYTES);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) rd(cur + boff + 32 * 16 * j, IB::PLANE, b[j]);
-        rd(cur + aoff, IA::PLANE, a0);
-        if (TM > 1) rd(cur + aoff + 32 * 16, IA::PLANE, a1);
-        st.split(kt, nkt, wimg, wimg + IA::BYTES);
-        mm(0, a0, b);
-#pragma unroll
-        for (int q = 0; q < 6 * TN; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        st.issue(kt, nkt, wimg + IA::BYTES);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 1; i < TM; ++i) {
-            uint4 (&ac)[3] = (i & 1) ? a1 : a0;
-            uint4 (&an)[3] = (i & 1) ? a0 : a1;
-            if (i + 1 < TM) rd(cur + aoff + 32 * 16 * (i + 1), IA::PLANE, an);
-            mm(i, ac, b);
-        }
-        st.before_barrier();
-        __syncthreads();
-    }
-    }
-}
-
-
-
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 // 16 bytes per lane global -> LDS (global_load_lds_dwordx4): lane l lands at
@@ -580,70 +469,82 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void k_gemm_nt_x6(NTArgs p) {
 // are sample-major: 8-row column strips, split in the kernel; the bias gradient (column
 // sums of dy) is accumulated from the same registers.
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int NT, bool HH = false>
+// The strips of a k-tile can be loaded NS tiles ahead of the split that consumes them (NS
+// register sets; dispatch_tn_x6 picks the depth).
+template <int BM, int BN, int NT, bool HH = false, int NSET = 1>
 struct TNStager {
     static constexpr bool H = HH;       // fp16 pair images with per-column scales (mode 2)
     static constexpr int NP = H ? 2 : 3;
+    static constexpr int NS = NSET;     // register sets (tiles in flight)
     static constexpr int SA = (2 * BM + NT - 1) / NT;
     static constexpr int SB = (2 * BN + NT - 1) / NT;
     const float* dyb; const float* xb;
     int lddy, ldx;
     int offa[SA], offb[SB];
     int ea[SA], eb[SB];                 // H: scale exponents of this thread's columns
-    float va[SA][8], vb[SB][8];
+    float va[NS][SA][8], vb[NS][SB][8];
     float bsum[SA];
     bool do_bias;
     __device__ __forceinline__ bool a_ok(int i) const { return SA * NT == 2 * BM || (int)threadIdx.x + NT * i < 2 * BM; }
     __device__ __forceinline__ bool b_ok(int i) const { return SB * NT == 2 * BN || (int)threadIdx.x + NT * i < 2 * BN; }
 
+    // buffer descriptors over this split's dy / x rows: one 32-bit lane offset per strip
+    // (VGPR) and the row offset of each of its 8 loads in an SGPR, instead of 16 + 16
+    // per-load 64-bit addresses
+    __amdgpu_buffer_rsrc_t rdy, rx;
     __device__ __forceinline__ void init(const TNArgs& p, size_t s0, int o0, int j0, bool bias) {
         lddy = p.lddy; ldx = p.ldx;
         dyb = p.dy + s0 * lddy + o0;
         xb = p.x + s0 * ldx + j0;
+        rdy = __builtin_amdgcn_make_buffer_rsrc((void*)dyb, (short)0, (p.rows_per_split * lddy - o0) * 4, 0x00020000);
+        rx = __builtin_amdgcn_make_buffer_rsrc((void*)xb, (short)0, (p.rows_per_split * ldx - j0) * 4, 0x00020000);
 #pragma unroll
         for (int i = 0; i < SA; ++i) {
             const int idx = threadIdx.x + NT * i;
-            offa[i] = 8 * (idx / BM) * lddy + idx % BM;
+            offa[i] = 4 * (8 * (idx / BM) * lddy + idx % BM);
             bsum[i] = 0.f;
             if (H) ea[i] = row_exp(tn_colmax(p.cm_dy, p.ldcm_dy, s0, p.rows_per_split, o0 + idx % BM));
         }
 #pragma unroll
         for (int i = 0; i < SB; ++i) {
             const int idx = threadIdx.x + NT * i;
-            offb[i] = 8 * (idx / BN) * ldx + idx % BN;
+            offb[i] = 4 * (8 * (idx / BN) * ldx + idx % BN);
             if (H) eb[i] = row_exp(tn_colmax(p.cm_x, p.ldcm_x, s0, p.rows_per_split, j0 + idx % BN));
         }
         do_bias = bias;
     }
+    template <int U>
     __device__ __forceinline__ void load(int kt) {
-        const float* da = dyb + (size_t)kt * XK * lddy;
-        const float* db = xb + (size_t)kt * XK * ldx;
+        const int sa = kt * XK * lddy * 4, sb = kt * XK * ldx * 4;
 #pragma unroll
         for (int i = 0; i < SA; ++i)
             if (a_ok(i)) {
 #pragma unroll
-                for (int t = 0; t < 8; ++t) va[i][t] = da[offa[i] + t * lddy];
+                for (int t = 0; t < 8; ++t)
+                    va[U][i][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rdy, offa[i], sa + t * lddy * 4, 0));
             }
 #pragma unroll
         for (int i = 0; i < SB; ++i)
             if (b_ok(i)) {
 #pragma unroll
-                for (int t = 0; t < 8; ++t) vb[i][t] = db[offb[i] + t * ldx];
+                for (int t = 0; t < 8; ++t)
+                    vb[U][i][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, offb[i], sb + t * ldx * 4, 0));
             }
     }
     // bias sums are taken here, once per real tile (`count` false for the clamped
     // re-stage of the last tile at the end of the main loop)
+    template <int U>
     __device__ __forceinline__ void put(char* Aimg, char* Bimg, bool count) {
 #pragma unroll
         for (int i = 0; i < SA; ++i)
             if (a_ok(i)) {
                 const int idx = threadIdx.x + NT * i;
-                if constexpr (H) put_col8h<BM>(Aimg, idx % BM, idx / BM, va[i], ea[i]);
-                else put_col8<BM>(Aimg, idx % BM, idx / BM, va[i]);
+                if constexpr (H) put_col8h<BM>(Aimg, idx % BM, idx / BM, va[U][i], ea[i]);
+                else put_col8<BM>(Aimg, idx % BM, idx / BM, va[U][i]);
                 if (do_bias && count) {
                     float s = 0.f;
 #pragma unroll
-                    for (int t = 0; t < 8; ++t) s += va[i][t];
+                    for (int t = 0; t < 8; ++t) s += va[U][i][t];
                     bsum[i] += s;
                 }
             }
@@ -651,26 +552,106 @@ struct TNStager {
         for (int i = 0; i < SB; ++i)
             if (b_ok(i)) {
                 const int idx = threadIdx.x + NT * i;
-                if constexpr (H) put_col8h<BN>(Bimg, idx % BN, idx / BN, vb[i], eb[i]);
-                else put_col8<BN>(Bimg, idx % BN, idx / BN, vb[i]);
+                if constexpr (H) put_col8h<BN>(Bimg, idx % BN, idx / BN, vb[U][i], eb[i]);
+                else put_col8<BN>(Bimg, idx % BN, idx / BN, vb[U][i]);
             }
     }
-    // register pipeline: tile 0 in image buffer 0, raw tile 1 in registers
+    template <int U>
+    __device__ __forceinline__ void prologue_load(int nkt) {
+        if constexpr (U < NS) {
+            if (U < nkt) load<U>(U);
+            prologue_load<U + 1>(nkt);
+        }
+    }
+    // register pipeline: tile 0 in image buffer 0, raw tiles 1 .. NS-1 in flight (tile t
+    // lives in register set t % NS)
     __device__ __forceinline__ void prologue(char* smem, int nkt) {
-        load(0);
-        put(smem, smem + XImg<BM, NP>::BYTES, true);
-        load(nkt > 1 ? 1 : 0);
+        prologue_load<0>(nkt);
+        put<0>(smem, smem + XImg<BM, NP>::BYTES, true);
+        if constexpr (NS == 1) {
+            if (1 < nkt) load<0>(1);
+        }
         __syncthreads();
     }
-    __device__ __forceinline__ void split(int kt, int nkt, char* Aimg, char* Bimg) {
-        put(Aimg, Bimg, kt + 1 < nkt);
-    }
-    __device__ __forceinline__ void issue_early(int, int, char*) {}
-    __device__ __forceinline__ void issue(int kt, int nkt, char*) { load(kt + 2 < nkt ? kt + 2 : nkt - 1); }
-    __device__ __forceinline__ void before_barrier() {}
 };
 
-template <int BM, int BN, int WM, int WN, bool H = false>
+// Main loop of the TN kernel (split-bf16 / fp16 pair images, register-staged column strips):
+// iteration kt reads the fragments of tile kt from buffer kt&1, splits tile kt+1 (register
+// set (kt+1) % NS) into the other buffer, issues the loads of tile kt+NS into the set tile kt
+// used (NS == 1: tile kt+2 into the one set, as before), then the MFMAs (VALU of the split
+// interleaved, 3 per MFMA gap) and one barrier.
+template <int TM, int TN, int BM, int BN, typename Stager>
+__device__ __forceinline__ void tn_mainloop(char* smem, int nkt, int wm0, int wn0, f32x16 (&acc)[TM][TN],
+                                            Stager& st) {
+    constexpr bool H = Stager::H;
+    constexpr int NP = H ? 2 : 3;
+    constexpr int NS = Stager::NS;
+    using IA = XImg<BM, NP>;
+    using IB = XImg<BN, NP>;
+    constexpr int BUF = IA::BYTES + IB::BYTES;
+    const int lane = lane_id();
+    const int l32 = lane & 31, hi = lane >> 5;
+    const int aoff = hi * IA::HALF + (wm0 + l32) * 16;
+    const int boff = IA::BYTES + hi * IB::HALF + (wn0 + l32) * 16;
+    auto rd = [&](const char* q, int plane, uint4 (&f)[NP]) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) f[p] = *reinterpret_cast<const uint4*>(q + p * plane);
+    };
+    auto mm = [&](int i, const uint4 (&a)[NP], const uint4 (&b)[TN][NP]) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            f32x16 c = acc[i][j];
+            if constexpr (H) {
+                c = mfma_f16(a[0], b[j][1], c);    // hi.lo
+                c = mfma_f16(a[1], b[j][0], c);    // lo.hi
+                c = mfma_f16(a[0], b[j][0], c);    // hi.hi
+            } else {
+                c = mfma_bf16(a[1], b[j][1], c);   // mid.mid
+                c = mfma_bf16(a[0], b[j][2], c);   // hi.lo
+                c = mfma_bf16(a[2], b[j][0], c);   // lo.hi
+                c = mfma_bf16(a[0], b[j][1], c);   // hi.mid
+                c = mfma_bf16(a[1], b[j][0], c);   // mid.hi
+                c = mfma_bf16(a[0], b[j][0], c);   // hi.hi
+            }
+            acc[i][j] = c;
+        }
+    };
+    constexpr int NPROD = H ? 3 : 6;
+    st.prologue(smem, nkt);
+    auto iter = [&](int kt, auto uc) {
+        constexpr int U = decltype(uc)::value;
+        const char* cur = smem + (kt & 1) * BUF;
+        char* wimg = smem + ((kt + 1) & 1) * BUF;
+        uint4 b[TN][NP], a[TM][NP];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) rd(cur + boff + 32 * 16 * j, IB::PLANE, b[j]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) rd(cur + aoff + 32 * 16 * i, IA::PLANE, a[i]);
+        if (kt + 1 < nkt) st.template put<(U + 1) % NS>(wimg, wimg + IA::BYTES, true);
+        if constexpr (NS == 1) {
+            if (kt + 2 < nkt) st.template load<0>(kt + 2);
+        } else {
+            if (kt + NS < nkt) st.template load<U>(kt + NS);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) mm(i, a[i], b);
+#pragma unroll
+        for (int q = 0; q < NPROD * TN * TM; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();
+    };
+    for (int kt0 = 0; kt0 < nkt; kt0 += NS) {
+        iter(kt0, std::integral_constant<int, 0>{});
+        if constexpr (NS > 1) { if (kt0 + 1 < nkt) iter(kt0 + 1, std::integral_constant<int, 1 % NS>{}); }
+        if constexpr (NS > 2) { if (kt0 + 2 < nkt) iter(kt0 + 2, std::integral_constant<int, 2 % NS>{}); }
+        if constexpr (NS > 3) { if (kt0 + 3 < nkt) iter(kt0 + 3, std::integral_constant<int, 3 % NS>{}); }
+    }
+}
+
+template <int BM, int BN, int WM, int WN, bool H = false, int NS = 1>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_tn_x6(TNArgs p) {
     constexpr int NT = 64 * WM * WN;
     constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -701,11 +682,11 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_tn_x6(TNArgs p) {
         for (int e = tid; e < BM; e += NT) lea[e] = row_exp(tn_colmax(p.cm_dy, p.ldcm_dy, s0, p.rows_per_split, o0 + e));
         for (int e = tid; e < BN; e += NT) leb[e] = row_exp(tn_colmax(p.cm_x, p.ldcm_x, s0, p.rows_per_split, j0 + e));
     }
-    TNStager<BM, BN, NT, H> st;
+    TNStager<BM, BN, NT, H, NS> st;
     st.init(p, s0, o0, j0, do_bias);
     f32x16 acc[TM][TN];
     zero_acc(acc);
-    x6_mainloop<TM, TN, BM, BN>(smem, nkt, wm0, wn0, acc, st);
+    tn_mainloop<TM, TN, BM, BN>(smem, nkt, wm0, wn0, acc, st);
 
     if constexpr (H) tn_store_lds<TM, TN, true>(p, acc, smem, split, o0, j0, wm0, wn0, lea, leb);
     else tn_store_lds(p, acc, smem, split, o0, j0, wm0, wn0);
@@ -764,25 +745,48 @@ int dispatch_nt_x6(const NTArgs& a, int epi, int policy, hipStream_t s, double f
     return check_launch(h16 ? "k_gemm_nt_x6 (fp16 pair)" : "k_gemm_nt_x6");
 }
 
-template <bool H>
+template <bool H, int NS>
 static void pick_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, hipStream_t s) {
     if (policy == 3 && nout % 256 == 0 && kin % 256 == 0)
-        hipLaunchKernelGGL((k_gemm_tn_x6<256, 256, 2, 2, H>), dim3(nout / 256, kin / 256, splits), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_gemm_tn_x6<256, 256, 2, 2, H, NS>), dim3(nout / 256, kin / 256, splits), dim3(256), 0,
+                           s, a);
     else if (nout % 128 == 0 && kin % 128 == 0)
-        hipLaunchKernelGGL((k_gemm_tn_x6<128, 128, 2, 2, H>), dim3(nout / 128, kin / 128, splits), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_gemm_tn_x6<128, 128, 2, 2, H, NS>), dim3(nout / 128, kin / 128, splits), dim3(256), 0,
+                           s, a);
     else if (nout % 128 == 0)
-        hipLaunchKernelGGL((k_gemm_tn_x6<128, 64, 2, 2, H>), dim3(nout / 128, kin / 64, splits), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_gemm_tn_x6<128, 64, 2, 2, H, NS>), dim3(nout / 128, kin / 64, splits), dim3(256), 0, s,
+                           a);
     else if (kin % 128 == 0)
-        hipLaunchKernelGGL((k_gemm_tn_x6<64, 128, 1, 4, H>), dim3(nout / 64, kin / 128, splits), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_gemm_tn_x6<64, 128, 1, 4, H, NS>), dim3(nout / 64, kin / 128, splits), dim3(256), 0, s,
+                           a);
     else
-        hipLaunchKernelGGL((k_gemm_tn_x6<64, 64, 1, 2, H>), dim3(nout / 64, kin / 64, splits), dim3(128), 0, s, a);
+        hipLaunchKernelGGL((k_gemm_tn_x6<64, 64, 1, 2, H, NS>), dim3(nout / 64, kin / 64, splits), dim3(128), 0, s, a);
 }
+
+// register sets of the TN strip pipeline (tiles in flight; NERF_TN_NS overrides for A/B runs).
+// One set: three sets (tiles loaded three k-steps ahead, 251 VGPRs, no spills) measured the
+// same 82-85 us per 131072 x 256 x 256 launch and the same step time (profiles/r02/
+// tn_pipeline_ab.txt) -- the kernel moves ~335 MB (operands + split-K slabs) at ~4.2 TB/s,
+// it is not load-latency bound
+static const int g_tn_ns = [] {
+    const char* e = getenv("NERF_TN_NS");
+    const int v = e ? atoi(e) : 0;
+    return v >= 1 && v <= 3 ? v : 0;
+}();
 
 int dispatch_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, hipStream_t s, double flops,
                    bool h16) {
     prof_begin(s);
-    if (h16) pick_tn_x6<true>(a, nout, kin, splits, policy, s);
-    else pick_tn_x6<false>(a, nout, kin, splits, policy, s);
+    const int ns = g_tn_ns ? g_tn_ns : 1;
+    if (h16) {
+        if (ns == 1) pick_tn_x6<true, 1>(a, nout, kin, splits, policy, s);
+        else if (ns == 2) pick_tn_x6<true, 2>(a, nout, kin, splits, policy, s);
+        else pick_tn_x6<true, 3>(a, nout, kin, splits, policy, s);
+    } else {
+        if (ns == 1) pick_tn_x6<false, 1>(a, nout, kin, splits, policy, s);
+        else if (ns == 2) pick_tn_x6<false, 2>(a, nout, kin, splits, policy, s);
+        else pick_tn_x6<false, 3>(a, nout, kin, splits, policy, s);
+    }
     prof_end(s, flops, h16 ? 3 : 6);
     return check_launch(h16 ? "k_gemm_tn_x6 (fp16 pair)" : "k_gemm_tn_x6");
 }

@@ -316,7 +316,7 @@ class FieldRunner:
         # GEMM phases overlap the memory-bound reductions and each other's prologue/epilogue.
         main = torch.cuda.current_stream(dev)
         if self._side is None or self._side.device != dev:
-            self._side = torch.cuda.Stream(dev)
+            self._side = torch.cuda.Stream(dev, priority=int(os.environ.get("NERF_SIDE_PRIORITY", "0")))
         side = self._side
         dy = dyr
         prev_in = {"l0": st["enc_p"], "l1": h["l0"], "l2": h["l1"], "l3": h["l2"], "l4": h["l3"],

@@ -23,6 +23,7 @@ import bench  # noqa: E402
 # name -> (nt policy, tn policy, dW target blocks, non-temporal NT stores); 0 = default
 SETTINGS = {
     "default": (0, 0, 0, 0),
+    "side_hi": (0, 0, 0, 0),
     "store_nt": (0, 0, 0, 1),
     "tn128_b256": (0, 1, 256, 0),
     "tn128_b512": (0, 1, 512, 0),
@@ -46,8 +47,17 @@ def main():
     trainer, _ = bench.build_trainer(dev, c2w, cfg)
     it = 0
     res = {k: [] for k in args.settings}
+    trainers = {}
+    for name in args.settings:
+        # side_hi: the weight-gradient side stream at high priority (a trainer of its own: the
+        # stream is created on the first backward)
+        os.environ["NERF_SIDE_PRIORITY"] = "-1" if name == "side_hi" else "0"
+        trainers[name] = bench.build_trainer(dev, c2w, cfg)[0] if name == "side_hi" else trainer
+        trainers[name].train_step(data, it=0, epoch=0, scheduling_start=0)
+    os.environ.pop("NERF_SIDE_PRIORITY", None)
     for _ in range(args.rounds):
         for name in args.settings:
+            trainer = trainers[name]
             nt, tn, blocks, snt = SETTINGS[name]
             _hip.gemm_set_policy(nt, tn)
             _hip.gemm_set_dw_blocks(blocks)
