@@ -34,8 +34,9 @@ extern "C" {
 /* Row tile of every per-sample GEMM: sample buffers are padded to a multiple of it. */
 #define NERF_ROW_TILE 128
 
-/* ABI version: 5 added nerf_prof_read_kinds and nerf_render_eval_fused (round 2). */
-#define NERF_HIP_ABI_VERSION 5
+/* ABI version: 5 added nerf_prof_read_kinds and nerf_render_eval_fused, 6 the 4x4-chain
+ * backwards (nerf_pose_c2w_bwd, nerf_mat4_inv_bwd, nerf_mat4_mul(_bwd), nerf_unproject_matrix_bwd). */
+#define NERF_HIP_ABI_VERSION 6
 int nerf_hip_abi_version(void);
 const char* nerf_hip_last_error(void);
 
@@ -315,6 +316,24 @@ int nerf_pose_c2w(const float* r, const float* t, const float* init_c2w, float* 
  * inverses (optional, [3][4][4]) = {inv(K), inv(world), inv(scale)} for the backward. */
 int nerf_unproject_matrix(const float* K, const float* world, const float* scale, float* M,
                           float* inverses, void* stream);
+
+/* Backwards of the 4x4 chain (the autograd of training.py:255-265, 334-343 when poses are
+ * learned), one launch each instead of torch's per-op graph:
+ *  nerf_pose_c2w_bwd: g_c2w [4][4] of nerf_pose_c2w -> g_r [3], g_t [3] (each optional);
+ *    the closed form of the Exp map's derivative (common.py:277-310) in f64, the r = 0
+ *    subgradient of |r| taken as 0 (torch's norm backward).
+ *  nerf_mat4_inv_bwd: g_a = -inv_a^T g inv_a^T for [n][4][4] (inv_a: the forward's output).
+ *  nerf_mat4_mul / _bwd: c = a @ b ([n][4][4]); g_a = g b^T, g_b = a^T g (each optional).
+ *  nerf_unproject_matrix_bwd: g_M of nerf_unproject_matrix -> g_K, g_world, g_scale (each
+ *    optional), from the forward's inverses. */
+int nerf_pose_c2w_bwd(const float* r, const float* init_c2w, const float* g_c2w, float* g_r, float* g_t,
+                      void* stream);
+int nerf_mat4_inv_bwd(const float* inv_a, const float* g, int n, float* g_a, void* stream);
+int nerf_mat4_mul(const float* a, const float* b, int n, float* c, void* stream);
+int nerf_mat4_mul_bwd(const float* a, const float* b, const float* g, int n, float* g_a, float* g_b,
+                      void* stream);
+int nerf_unproject_matrix_bwd(const float* inverses, const float* g_M, float* g_K, float* g_world,
+                              float* g_scale, void* stream);
 
 /* Camera rays of Renderer.nope_nerf (rendering.py:52-80): for pixels [R][2], depth [R]
  * (NULL = no depth prior, d_src = 1): cam [R][3] = M[:3,3]; v = M[:3,:3](x,y,1);

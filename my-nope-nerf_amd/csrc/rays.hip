@@ -175,6 +175,163 @@ __global__ void k_pose_c2w(const float* __restrict__ r, const float* __restrict_
     }
 }
 
+// Backward of k_pose_c2w (the closed form of torch autograd through common.py:277-310):
+// G = g @ init^T is the gradient of [R | t]; g_t = G[:3, 3];
+//   dL/dK = s G_R + c (G_R K^T + K^T G_R),  dL/dth = s'(th) <G_R, K> + c'(th) <G_R, K^2>,
+//   s = sin th / th, c = (1 - cos th) / th^2, dth/dr = r / |r| (0 at r = 0, torch's norm
+//   subgradient), K = [r]x so dL/dx = dK[2][1] - dK[1][2] etc.  Evaluated in f64.
+__global__ void k_pose_c2w_bwd(const float* __restrict__ r, const float* __restrict__ init,
+                               const float* __restrict__ g, float* __restrict__ gr, float* __restrict__ gt) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double G[16];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            double s = 0.0;
+            if (init != nullptr) {
+                for (int k = 0; k < 4; ++k) s += (double)g[4 * i + k] * (double)init[4 * j + k];
+            } else {
+                s = g[4 * i + j];
+            }
+            G[4 * i + j] = s;
+        }
+    if (gt != nullptr)
+        for (int i = 0; i < 3; ++i) gt[i] = (float)G[4 * i + 3];
+    if (gr == nullptr) return;
+    const double x = r[0], y = r[1], z = r[2];
+    const double nr = sqrt(x * x + y * y + z * z);
+    const double th = (double)(float)((float)nr + 1e-15f);
+    const double K[9] = {0.0, -z, y, z, 0.0, -x, -y, x, 0.0};
+    double KK[9], GR[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            KK[3 * i + j] = K[3 * i] * K[j] + K[3 * i + 1] * K[3 + j] + K[3 * i + 2] * K[6 + j];
+            GR[3 * i + j] = G[4 * i + j];
+        }
+    const double sn = sin(th), cs = cos(th);
+    const double s = sn / th, c = (1.0 - cs) / (th * th);
+    const double ds = cs / th - sn / (th * th);
+    const double dc = sn / (th * th) - 2.0 * (1.0 - cs) / (th * th * th);
+    double dK[9], gk = 0.0, gkk = 0.0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double a = 0.0, b = 0.0;   // (G_R K^T)_ij, (K^T G_R)_ij
+            for (int k = 0; k < 3; ++k) {
+                a += GR[3 * i + k] * K[3 * j + k];
+                b += K[3 * k + i] * GR[3 * k + j];
+            }
+            dK[3 * i + j] = s * GR[3 * i + j] + c * (a + b);
+            gk += GR[3 * i + j] * K[3 * i + j];
+            gkk += GR[3 * i + j] * KK[3 * i + j];
+        }
+    const double dth = ds * gk + dc * gkk;
+    const double w = nr > 0.0 ? dth / nr : 0.0;
+    gr[0] = (float)(dK[7] - dK[5] + w * x);
+    gr[1] = (float)(dK[2] - dK[6] + w * y);
+    gr[2] = (float)(dK[3] - dK[1] + w * z);
+}
+
+// d inv(A) = -Y dA Y  ->  gA = -Y^T g Y^T, batched ([n][4][4])
+__global__ void k_mat4_inv_bwd(const float* __restrict__ y, const float* __restrict__ g, int n,
+                               float* __restrict__ ga) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float Y[16], Yt[16], G[16], t[16], o[16];
+    load4(y + 16 * (size_t)i, Y);
+    load4(g + 16 * (size_t)i, G);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) Yt[4 * a + b] = Y[4 * b + a];
+    matmul4(Yt, G, t);
+    matmul4(t, Yt, o);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o[k] = -o[k];
+    store4(ga + 16 * (size_t)i, o);
+}
+
+// C = A @ B (batched [n][4][4]) and its backward gA = g B^T, gB = A^T g (either optional)
+__global__ void k_mat4_mul(const float* __restrict__ a, const float* __restrict__ b, int n, float* __restrict__ c) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float A[16], B[16], C[16];
+    load4(a + 16 * (size_t)i, A);
+    load4(b + 16 * (size_t)i, B);
+    matmul4(A, B, C);
+    store4(c + 16 * (size_t)i, C);
+}
+__global__ void k_mat4_mul_bwd(const float* __restrict__ a, const float* __restrict__ b, const float* __restrict__ g,
+                               int n, float* __restrict__ ga, float* __restrict__ gb) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float A[16], B[16], G[16], T[16], O[16];
+    load4(g + 16 * (size_t)i, G);
+    if (ga != nullptr) {
+        load4(b + 16 * (size_t)i, B);
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) T[4 * p + q] = B[4 * q + p];
+        matmul4(G, T, O);
+        store4(ga + 16 * (size_t)i, O);
+    }
+    if (gb != nullptr) {
+        load4(a + 16 * (size_t)i, A);
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) T[4 * p + q] = A[4 * q + p];
+        matmul4(T, G, O);
+        store4(gb + 16 * (size_t)i, O);
+    }
+}
+
+// Backward of k_unproject: M = Si Wi Ki with Xi = inv(X) and d inv(A) = -Ai dA Ai:
+//   gK = -Ki^T ((Si Wi)^T g) Ki^T,  gW = -Wi^T (Si^T g Ki^T) Wi^T,  gS = -Si^T (g (Wi Ki)^T) Si^T
+// (each output optional; inverses = {Ki, Wi, Si} from the forward)
+__global__ void k_unproject_bwd(const float* __restrict__ inverses, const float* __restrict__ g,
+                                float* __restrict__ gK, float* __restrict__ gW, float* __restrict__ gS) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    float Ki[16], Wi[16], Si[16], G[16], A[16], B[16], T[16], O[16];
+    load4(inverses, Ki);
+    load4(inverses + 16, Wi);
+    load4(inverses + 32, Si);
+    load4(g, G);
+    auto tr = [](const float (&x)[16], float (&y)[16]) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) y[4 * p + q] = x[4 * q + p];
+    };
+    auto neg_sandwich = [&](const float (&Xi)[16], const float (&inner)[16], float* out) {
+        float Xt[16], t1[16], t2[16];
+        tr(Xi, Xt);
+        matmul4(Xt, inner, t1);
+        matmul4(t1, Xt, t2);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) t2[k] = -t2[k];
+        store4(out, t2);
+    };
+    if (gK != nullptr) {
+        matmul4(Si, Wi, A);
+        tr(A, T);
+        matmul4(T, G, O);
+        neg_sandwich(Ki, O, gK);
+    }
+    if (gW != nullptr) {
+        tr(Si, T);
+        matmul4(T, G, A);
+        tr(Ki, T);
+        matmul4(A, T, O);
+        neg_sandwich(Wi, O, gW);
+    }
+    if (gS != nullptr) {
+        matmul4(Wi, Ki, B);
+        tr(B, T);
+        matmul4(G, T, O);
+        neg_sandwich(Si, O, gS);
+    }
+}
+
 // M = (inv(scale) @ inv(world)) @ inv(K)  (common.py:139-141); inverses kept for backward
 __global__ void k_unproject(const float* __restrict__ K, const float* __restrict__ world,
                             const float* __restrict__ scale, float* __restrict__ M, float* __restrict__ inverses) {
@@ -450,6 +607,45 @@ extern "C" int nerf_unproject_matrix(const float* K, const float* world, const f
                                      float* inverses, void* stream) {
     NERF_CHECK_PTR(K); NERF_CHECK_PTR(world); NERF_CHECK_PTR(scale); NERF_CHECK_PTR(M);
     hipLaunchKernelGGL(k_unproject, dim3(1), dim3(64), 0, as_stream(stream), K, world, scale, M, inverses);
+    return check_launch(__func__);
+}
+
+extern "C" int nerf_pose_c2w_bwd(const float* r, const float* init_c2w, const float* g_c2w, float* g_r, float* g_t,
+                                 void* stream) {
+    NERF_CHECK_PTR(r); NERF_CHECK_PTR(g_c2w);
+    hipLaunchKernelGGL(k_pose_c2w_bwd, dim3(1), dim3(64), 0, as_stream(stream), r, init_c2w, g_c2w, g_r, g_t);
+    return check_launch(__func__);
+}
+
+extern "C" int nerf_mat4_inv_bwd(const float* inv_a, const float* g, int n, float* g_a, void* stream) {
+    NERF_CHECK_PTR(inv_a); NERF_CHECK_PTR(g); NERF_CHECK_PTR(g_a);
+    NERF_CHECK(n > 0, "%s: n=%d", __func__, n);
+    hipLaunchKernelGGL(k_mat4_inv_bwd, dim3((n + 63) / 64), dim3(64), 0, as_stream(stream), inv_a, g, n, g_a);
+    return check_launch(__func__);
+}
+
+extern "C" int nerf_mat4_mul(const float* a, const float* b, int n, float* c, void* stream) {
+    NERF_CHECK_PTR(a); NERF_CHECK_PTR(b); NERF_CHECK_PTR(c);
+    NERF_CHECK(n > 0, "%s: n=%d", __func__, n);
+    hipLaunchKernelGGL(k_mat4_mul, dim3((n + 63) / 64), dim3(64), 0, as_stream(stream), a, b, n, c);
+    return check_launch(__func__);
+}
+
+extern "C" int nerf_mat4_mul_bwd(const float* a, const float* b, const float* g, int n, float* g_a, float* g_b,
+                                 void* stream) {
+    NERF_CHECK_PTR(g);
+    NERF_CHECK(n > 0, "%s: n=%d", __func__, n);
+    NERF_CHECK(g_a == nullptr || b != nullptr, "%s: g_a needs b", __func__);
+    NERF_CHECK(g_b == nullptr || a != nullptr, "%s: g_b needs a", __func__);
+    hipLaunchKernelGGL(k_mat4_mul_bwd, dim3((n + 63) / 64), dim3(64), 0, as_stream(stream), a, b, g, n, g_a, g_b);
+    return check_launch(__func__);
+}
+
+extern "C" int nerf_unproject_matrix_bwd(const float* inverses, const float* g_M, float* g_K, float* g_world,
+                                         float* g_scale, void* stream) {
+    NERF_CHECK_PTR(inverses); NERF_CHECK_PTR(g_M);
+    hipLaunchKernelGGL(k_unproject_bwd, dim3(1), dim3(64), 0, as_stream(stream), inverses, g_M, g_K, g_world,
+                       g_scale);
     return check_launch(__func__);
 }
 

@@ -745,24 +745,33 @@ __global__ __launch_bounds__(256) void k_composite16_bwd(const float* __restrict
 // ---------------------------------------------------------------------------
 // gradient back to the ray inputs (pose / ray learning)
 // ---------------------------------------------------------------------------
-// g2 (optional): a second gradient of the same encoding (the skip layer's copy of enc_p),
-// summed on the fly instead of by a separate add over [N][64]
-template <int L, int LD>
-__device__ __forceinline__ void encode3_bwd(const float x[3], const float* __restrict__ g,
-                                            const float* __restrict__ g2, float out[3]) {
-    auto G = [&](int k) { return g2 ? g[k] + g2[k] : g[k]; };
-#pragma unroll
-    for (int c = 0; c < 3; ++c) out[c] = G(c);
-#pragma unroll
-    for (int i = 0; i < L; ++i) {
-        const float f = (float)(1 << i);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            float s, co;
-            sincosf(f * x[c], &s, &co);
-            out[c] += f * (co * G(3 + 6 * i + c) - s * G(6 + 6 * i + c));
-        }
-    }
+// One workgroup per ray, four waves over its samples, lane = encoding column: every load of
+// a gradient row is one coalesced 256-byte wave access (a lane-per-sample layout reads 64
+// lines per instruction).  Column k of encode_position (official_nerf.py:99-119) is x_c
+// (k < 3) or sin / cos(2^i x_c) (k = 3 + 6 i + c, + 3 for cos); its derivative w.r.t. x_c
+// is 1, 2^i cos, -2^i sin.  A lane accumulates G[s][k] d_k(x(s)) over its samples (and the
+// same times z_s for the direction gradient, x = o + d z); the view encoding is constant per
+// ray, so its columns are summed first and scaled once.  The per-component sums meet in LDS.
+struct EncCol {
+    int c;        // input component, -1 for a padding column
+    float f;      // 2^i (1 for the identity columns)
+    int kind;     // 0 identity, 1 sin column, 2 cos column
+};
+__device__ __forceinline__ EncCol enc_col(int k, int L) {
+    EncCol e{-1, 0.f, 0};
+    if (k < 3) { e.c = k; e.f = 1.f; e.kind = 0; return e; }
+    const int q = k - 3;
+    if (q >= 6 * L) return e;
+    const int i = q / 6, r = q - 6 * i;
+    e.c = r % 3; e.f = (float)(1 << i); e.kind = r < 3 ? 1 : 2;
+    return e;
+}
+__device__ __forceinline__ float enc_dfac(const EncCol& e, float x) {
+    if (e.c < 0) return 0.f;
+    if (e.kind == 0) return 1.f;
+    float sn, cs;
+    sincosf(e.f * x, &sn, &cs);
+    return e.kind == 1 ? e.f * cs : -e.f * sn;
 }
 
 __global__ __launch_bounds__(256) void k_encode_bwd(const float* __restrict__ po, const float* __restrict__ pd,
@@ -771,41 +780,39 @@ __global__ __launch_bounds__(256) void k_encode_bwd(const float* __restrict__ po
                                                     const float* __restrict__ gd,
                                                     int R, int S, float* __restrict__ g_po,
                                                     float* __restrict__ g_pd, float* __restrict__ g_view) {
-    const int ray = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (ray >= R) return;
-    const int lane = lane_id();
-    float ao[3] = {0.f, 0.f, 0.f}, ad[3] = {0.f, 0.f, 0.f}, av[3] = {0.f, 0.f, 0.f};
-    const float o[3] = {po[3 * ray], po[3 * ray + 1], po[3 * ray + 2]};
-    const float d[3] = {pd[3 * ray], pd[3 * ray + 1], pd[3 * ray + 2]};
-    const float v[3] = {view[3 * ray], view[3 * ray + 1], view[3 * ray + 2]};
-    for (int i = lane; i < S; i += 64) {
-        const size_t s = (size_t)ray * S + i;
+    __shared__ float red[4][3][3];   // [wave][o / d / view][component]
+    const int ray = blockIdx.x;
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const EncCol ep = enc_col(lane, 10), ed = enc_col(lane, 4);
+    const float o = ep.c >= 0 ? po[3 * ray + ep.c] : 0.f;
+    const float d = ep.c >= 0 ? pd[3 * ray + ep.c] : 0.f;
+    float ao = 0.f, ad = 0.f, sv = 0.f;
+    const size_t base = (size_t)ray * S;
+#pragma unroll 4
+    for (int i = w; i < S; i += 4) {
+        const size_t s = base + i;
         const float z = zv[s];
-        float x[3], gx[3], gv[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) x[c] = ray_point(o[c], d[c], z);
-        encode3_bwd<10, ENC_P>(x, gp + s * ENC_P, gp2 ? gp2 + s * ENC_P : nullptr, gx);
-        encode3_bwd<4, ENC_D>(v, gd + s * ENC_D, nullptr, gv);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            ao[c] += gx[c];
-            ad[c] += gx[c] * z;
-            av[c] += gv[c];
-        }
+        float g = gp[s * ENC_P + lane];
+        if (gp2) g += gp2[s * ENC_P + lane];
+        sv += gd[s * ENC_D + lane];
+        const float t = g * enc_dfac(ep, ray_point(o, d, z));
+        ao += t;
+        ad += t * z;
     }
+    const float av = ed.c >= 0 ? sv * enc_dfac(ed, view[3 * ray + ed.c]) : 0.f;
+    // per-component sums over the wave's lanes
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        ao[c] = wave_sum(ao[c]);
-        ad[c] = wave_sum(ad[c]);
-        av[c] = wave_sum(av[c]);
+        const float so = wave_sum(ep.c == c ? ao : 0.f);
+        const float sd = wave_sum(ep.c == c ? ad : 0.f);
+        const float s2 = wave_sum(ed.c == c ? av : 0.f);
+        if (lane == 0) { red[w][0][c] = so; red[w][1][c] = sd; red[w][2][c] = s2; }
     }
-    if (lane == 0) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            g_po[3 * ray + c] = ao[c];
-            g_pd[3 * ray + c] = ad[c];
-            g_view[3 * ray + c] = av[c];
-        }
+    __syncthreads();
+    if (threadIdx.x < 9) {
+        const int k = threadIdx.x / 3, c = threadIdx.x % 3;
+        const float v = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
+        (k == 0 ? g_po : k == 1 ? g_pd : g_view)[3 * ray + c] = v;
     }
 }
 
@@ -962,8 +969,7 @@ extern "C" int nerf_encode_bwd(const float* pts_o, const float* pts_d, const flo
     NERF_CHECK_PTR(genc_p); NERF_CHECK_PTR(genc_d);
     NERF_CHECK_PTR(g_pts_o); NERF_CHECK_PTR(g_pts_d); NERF_CHECK_PTR(g_view);
     NERF_CHECK(n_rays > 0 && n_samples > 0, "%s: empty input", __func__);
-    const int blocks = (n_rays + 3) / 4;
-    hipLaunchKernelGGL(k_encode_bwd, dim3(blocks), dim3(256), 0, as_stream(stream), pts_o, pts_d, view, z,
+    hipLaunchKernelGGL(k_encode_bwd, dim3(n_rays), dim3(256), 0, as_stream(stream), pts_o, pts_d, view, z,
                        genc_p, genc_p2, genc_d, n_rays, n_samples, g_pts_o, g_pts_d, g_view);
     return check_launch(__func__);
 }

@@ -46,7 +46,7 @@ class ProfKind(ctypes.Structure):
 
 
 PROF_KINDS = ("fwd", "dx", "dw", "dw_narrow")   # NERF_PROF_FWD / _DX / _DW / _DW_NARROW
-ABI_VERSION = 5                    # NERF_HIP_ABI_VERSION
+ABI_VERSION = 6                    # NERF_HIP_ABI_VERSION
 
 
 class ChainLayer(ctypes.Structure):
@@ -93,6 +93,11 @@ _SIGS = {
     "nerf_mat4_inv": ([_c_p, _c_i, _c_p, _c_p], _c_i),
     "nerf_pose_c2w": ([_c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_unproject_matrix": ([_c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_pose_c2w_bwd": ([_c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_mat4_inv_bwd": ([_c_p, _c_p, _c_i, _c_p, _c_p], _c_i),
+    "nerf_mat4_mul": ([_c_p, _c_p, _c_i, _c_p, _c_p], _c_i),
+    "nerf_mat4_mul_bwd": ([_c_p, _c_p, _c_p, _c_i, _c_p, _c_p, _c_p], _c_i),
+    "nerf_unproject_matrix_bwd": ([_c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_camera_rays": ([_c_p, _c_p, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_camera_rays_bwd": ([_c_p, _c_p, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_ray_loss": ([_c_p, _c_p, _c_i, _c_p, _c_p, _c_p, _c_i, _c_i, _c_f, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
@@ -324,6 +329,26 @@ def pose_c2w(r, t, init_c2w, out):
 
 def unproject_matrix(K, world, scale, M, inverses=None):
     _call("nerf_unproject_matrix", _ptr(K), _ptr(world), _ptr(scale), _ptr(M), _ptr(inverses), _stream())
+
+
+def pose_c2w_bwd(r, init_c2w, g_c2w, g_r=None, g_t=None):
+    _call("nerf_pose_c2w_bwd", _ptr(r), _ptr(init_c2w), _ptr(g_c2w), _ptr(g_r), _ptr(g_t), _stream())
+
+
+def mat4_inv_bwd(inv_a, g, g_a):
+    _call("nerf_mat4_inv_bwd", _ptr(inv_a), _ptr(g), inv_a.numel() // 16, _ptr(g_a), _stream())
+
+
+def mat4_mul(a, b, c):
+    _call("nerf_mat4_mul", _ptr(a), _ptr(b), a.numel() // 16, _ptr(c), _stream())
+
+
+def mat4_mul_bwd(a, b, g, g_a=None, g_b=None):
+    _call("nerf_mat4_mul_bwd", _ptr(a), _ptr(b), _ptr(g), g.numel() // 16, _ptr(g_a), _ptr(g_b), _stream())
+
+
+def unproject_matrix_bwd(inverses, g_M, g_K=None, g_world=None, g_scale=None):
+    _call("nerf_unproject_matrix_bwd", _ptr(inverses), _ptr(g_M), _ptr(g_K), _ptr(g_world), _ptr(g_scale), _stream())
 
 
 def camera_rays(M, pixels, depth, n_rays, flags, cam, ray, view, ray_norm, d_src, mask):

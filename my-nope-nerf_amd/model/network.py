@@ -1,6 +1,7 @@
 """Model wrapper (drop-in for model/network.py:7-33)."""
 from __future__ import annotations
 
+import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
@@ -21,6 +22,8 @@ class nope_nerf(nn.Module):
             d = depth_img
             if tuple(d.shape[-2:]) != tuple(img_size):
                 d = F.interpolate(d, img_size, mode="area")     # identity when already H x W
-            depth = d.reshape(1, -1, 1)[:, ray_idx]
+            # index_select, not advanced indexing: its backward is one index_add (the ray
+            # indices are distinct) instead of a sorted index_put (distortion learning)
+            depth = torch.index_select(d.reshape(-1), 0, ray_idx.reshape(-1)).view(1, -1, 1)
         return self.renderer(p, depth, camera_mat, world_mat, scale_mat, rendering_technique,
                              eval_=eval_mode, it=it, add_noise=add_noise, **kw)

@@ -38,9 +38,10 @@ class _Inv4(torch.autograd.Function):
     def backward(ctx, g):
         if g is None:
             return None
-        (y,) = ctx.saved_tensors          # d inv(A) = -Y dA Y  ->  gA = -Y^T g Y^T
-        yt = y.transpose(-1, -2)
-        return -(yt @ g @ yt)
+        (y,) = ctx.saved_tensors          # d inv(A) = -Y dA Y  ->  gA = -Y^T g Y^T (one launch)
+        ga = torch.empty_like(y)
+        _hip.mat4_inv_bwd(y, _f32c(g), ga)
+        return ga
 
 
 def inv(m):
@@ -50,6 +51,38 @@ def inv(m):
     if m.shape[-2:] != (4, 4):
         raise ValueError(f"inv: expected [..., 4, 4], got {tuple(m.shape)}")
     return _Inv4.apply(m)
+
+
+# ------------------------------------------------------------------ 4x4 product
+class _Mat4Mul(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.set_materialize_grads(False)
+        ac, bc = _f32c(a), _f32c(b)
+        out = torch.empty(ac.shape, device=a.device, dtype=torch.float32)
+        _hip.mat4_mul(ac, bc, out)
+        ctx.save_for_backward(ac, bc)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is None:
+            return None, None
+        ac, bc = ctx.saved_tensors
+        want_a, want_b = ctx.needs_input_grad
+        ga = torch.empty_like(ac) if want_a else None
+        gb = torch.empty_like(bc) if want_b else None
+        if want_a or want_b:
+            _hip.mat4_mul_bwd(ac, bc, _f32c(g), ga, gb)
+        return ga, gb
+
+
+def mat4_mul(a, b):
+    """a @ b for equally shaped [..., 4, 4] (training.py:337-343's relative poses): one launch
+    forward and one backward on the device, torch matmul on the host."""
+    if not a.is_cuda or a.shape != b.shape or a.shape[-2:] != (4, 4):
+        return a @ b
+    return _Mat4Mul.apply(a, b)
 
 
 # ------------------------------------------------------------------ pose
@@ -80,14 +113,20 @@ class _PoseC2W(torch.autograd.Function):
         if g is None:
             return None, None, None
         r, t, init = ctx.saved_tensors
-        with torch.enable_grad():
-            rr = r.detach().requires_grad_(ctx.needs_input_grad[0])
-            tt = t.detach().requires_grad_(ctx.needs_input_grad[1])
-            ii = None if init is None else init.detach().requires_grad_(ctx.needs_input_grad[2])
-            out = _pose_torch(rr, tt, ii)
-            ins = [x for x in (rr, tt, ii) if x is not None and x.requires_grad]
-            gs = iter(torch.autograd.grad(out, ins, g)) if ins else iter(())
-        return tuple(next(gs) if (x is not None and x.requires_grad) else None for x in (rr, tt, ii))
+        want_r, want_t, want_i = ctx.needs_input_grad
+        g_init = None
+        if want_i:
+            # a learned init_c2w (never in the reference configs): torch autograd of the expression
+            with torch.enable_grad():
+                ii = init.detach().requires_grad_(True)
+                (g_init,) = torch.autograd.grad(_pose_torch(r.detach(), t.detach(), ii), [ii], g)
+        if not (want_r or want_t):
+            return None, None, g_init
+        # the closed-form derivative of Exp / [R | t] @ init: one launch (nerf_pose_c2w_bwd)
+        g_r = torch.empty(3, device=r.device, dtype=torch.float32) if want_r else None
+        g_t = torch.empty(3, device=r.device, dtype=torch.float32) if want_t else None
+        _hip.pose_c2w_bwd(_f32c(r), None if init is None else _f32c(init), _f32c(g), g_r, g_t)
+        return (g_r.view_as(r) if want_r else None, g_t.view_as(t) if want_t else None, g_init)
 
 
 def pose_c2w(r, t, init=None):
@@ -114,21 +153,14 @@ class _Unproject(torch.autograd.Function):
         if gM is None:
             return None, None, None
         (invs,) = ctx.saved_tensors
-        Ki, Wi, Si = invs[0], invs[1], invs[2]
-        g = gM.reshape(4, 4)
-        T = lambda x: x.transpose(0, 1)
-        gK = gW = gS = None
-        # M = Si Wi Ki and d inv(A) = -inv(A) dA inv(A)
-        if ctx.needs_input_grad[0]:
-            gKi = T(Si @ Wi) @ g
-            gK = (-(T(Ki) @ gKi @ T(Ki))).reshape(ctx.shapes[0])
-        if ctx.needs_input_grad[1]:
-            gWi = T(Si) @ g @ T(Ki)
-            gW = (-(T(Wi) @ gWi @ T(Wi))).reshape(ctx.shapes[1])
-        if ctx.needs_input_grad[2]:
-            gSi = g @ T(Wi @ Ki)
-            gS = (-(T(Si) @ gSi @ T(Si))).reshape(ctx.shapes[2])
-        return gK, gW, gS
+        # M = Si Wi Ki and d inv(A) = -inv(A) dA inv(A): all three in one launch
+        want = ctx.needs_input_grad
+        e = lambda: torch.empty(4, 4, device=invs.device, dtype=torch.float32)
+        gK, gW, gS = (e() if want[0] else None), (e() if want[1] else None), (e() if want[2] else None)
+        _hip.unproject_matrix_bwd(invs, _f32c(gM), gK, gW, gS)
+        sh = ctx.shapes
+        return (gK.reshape(sh[0]) if gK is not None else None, gW.reshape(sh[1]) if gW is not None else None,
+                gS.reshape(sh[2]) if gS is not None else None)
 
 
 def unproject_matrix(camera_mat, world_mat, scale_mat):

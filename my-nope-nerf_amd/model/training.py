@@ -22,7 +22,7 @@ import torch.distributed as dist
 from torch.nn import functional as F
 
 from .common import arange_pixels, get_tensor_values, inv, project_to_cam, transform_to_world
-from .rays import can_sample_on_device
+from .rays import can_sample_on_device, mat4_mul
 from .rays import sample_rays as sample_rays_dev
 from .losses import Loss
 from .pair import pair_losses
@@ -334,13 +334,13 @@ class Trainer(object):
         ref_Rt = inv(c2w_ref).unsqueeze(0)
         if int(img_idx) < num_cams - 1:
             d1, d2, img1, img2 = depth_input, depth_ref, img, ref_img
-            Rt_rel_12 = ref_Rt @ inv(world_mat)
-            Rt_rel_12_gt = ref_Rt_gt @ inv(world_mat_gt) if want_gt else None
+            Rt_rel_12 = mat4_mul(ref_Rt, inv(world_mat))
+            Rt_rel_12_gt = mat4_mul(ref_Rt_gt, inv(world_mat_gt)) if want_gt else None
             scale1 = scale_input
         else:
             d1, d2, img1, img2 = depth_ref, depth_input, ref_img, img
-            Rt_rel_12 = world_mat @ inv(ref_Rt)
-            Rt_rel_12_gt = world_mat_gt @ inv(ref_Rt_gt) if want_gt else None
+            Rt_rel_12 = mat4_mul(world_mat, inv(ref_Rt))
+            Rt_rel_12_gt = mat4_mul(world_mat_gt, inv(ref_Rt_gt)) if want_gt else None
             scale1 = scale_ref
         res = (int(h_depth / self.pc_ratio), int(w_depth / self.pc_ratio))
         d1 = F.interpolate(d1, res, mode="nearest").clamp_min(nl)       # d[d < nl] = nl

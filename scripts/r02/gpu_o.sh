@@ -1,0 +1,12 @@
+# round-2 GPU call O: encode backward rewrite -- kernel + pose-gradient parity tests, cfg3 bench, trace
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R
+OUT=$R/gpurun_out/r02o
+mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread \
+  tests/test_gpu_kernels.py -k "encode" tests/test_gpu_render.py tests/test_gpu_full_step.py > $OUT/tests.log 2>&1; rc=$?
+grep -E "FAILED|ERROR|passed|failed" $OUT/tests.log | tail -15; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python scripts/bench_full.py --steps 40 --warmup 5 > $OUT/bench_full_graph.json 2> $OUT/bench_full_graph.err && cat $OUT/bench_full_graph.json && \
+cd /tmp && export TMPDIR=/tmp && \
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/tr3g -o run -- python3 $R/scripts/bench_full.py --steps 12 --warmup 3 > $OUT/b3g.json 2> $OUT/b3g.err && echo "trace ok"

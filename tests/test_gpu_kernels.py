@@ -444,6 +444,45 @@ def test_encode_samples(dev):
     assert (cd[:, 3:27] == 1).all() and (cd[:, 27:] == 0).all()
 
 
+@pytest.mark.parametrize("with_p2", [False, True])
+def test_encode_bwd_matches_autograd(dev, with_p2):
+    """nerf_encode_bwd (gradient of the encodings back to ray origin, direction and view) vs
+    fp64 autograd of the oracle's encode_position at the same sample points."""
+    R, S = 37, 128
+    g = torch.Generator().manual_seed(17)
+    o = _rand(R, 3, g=g) * 3
+    d = torch.nn.functional.normalize(_rand(R, 3, g=g), dim=-1)
+    view = -d
+    z = 0.01 + 9.99 * torch.rand(R, S, generator=g)
+    Np = ((R * S + 127) // 128) * 128
+    gp = torch.zeros(Np, 64)
+    gp[:R * S, :63] = _rand(R * S, 63, g=g)
+    gp2 = torch.zeros(Np, 64)
+    gp2[:R * S, :63] = _rand(R * S, 63, g=g)
+    gd = torch.zeros(Np, 64)
+    gd[:R * S, :27] = _rand(R * S, 27, g=g)
+    outs = [torch.empty(R, 3, device=dev) for _ in range(3)]
+    zd = torch.zeros(Np)
+    zd[:R * S] = z.reshape(-1)
+    _hip.encode_bwd(o.to(dev), d.to(dev), view.to(dev), zd.to(dev), gp.to(dev), gd.to(dev), R, S, *outs,
+                    genc_p2=gp2.to(dev) if with_p2 else None)
+    # the sample points as the kernel forms them (f32 o + d z), differentiated in fp64 there:
+    # at 2^9 the encoding's phase amplifies a 1-ulp point difference ~500x
+    pts32 = (o.unsqueeze(1) + d.unsqueeze(1) * z.unsqueeze(-1)).reshape(-1, 3)
+    p64 = pts32.double().clone().requires_grad_(True)
+    v64 = view.double().clone().requires_grad_(True)
+    gsum = gp[:R * S, :63] + (gp2[:R * S, :63] if with_p2 else 0)
+    loss = (orc.encode_position(p64, 10) * gsum.double()).sum()
+    loss = loss + (orc.encode_position(v64.unsqueeze(1).expand(R, S, 3).reshape(-1, 3), 4)
+                   * gd[:R * S, :27].double()).sum()
+    loss.backward()
+    gpt = p64.grad.view(R, S, 3)
+    refs = (gpt.sum(1), (gpt * z.double().unsqueeze(-1)).sum(1), v64.grad)
+    for h, r in zip(outs, refs):
+        err = ((h.cpu().double() - r).abs().max() / r.abs().max()).item()
+        assert err < 2e-5, err
+
+
 def test_chamfer_nn(dev):
     g = torch.Generator().manual_seed(11)
     X = torch.rand(3, 1000, generator=g) * 4

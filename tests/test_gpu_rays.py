@@ -106,6 +106,55 @@ def test_pose_c2w_matches_oracle_and_grad(dev):
             assert _rel(r.grad, r64.grad) < 1e-4
 
 
+def test_pose_c2w_grad_at_zero_rotation(dev):
+    """r = 0 (LearnPose's initial value): the closed-form backward equals torch autograd of the
+    reference expression in fp32 (the |r| subgradient is 0, the [r]x terms carry the gradient)."""
+    g = torch.Generator().manual_seed(2)
+    init = rigid_c2w(4)
+    gy = torch.randn(4, 4, generator=g)
+    r = torch.zeros(3, device=dev, requires_grad=True)
+    t = torch.randn(3, generator=g).to(dev).requires_grad_(True)
+    rays.pose_c2w(r, t, init.to(dev)).backward(gy.to(dev))
+    rc = torch.zeros(3, requires_grad=True)
+    tc = t.detach().cpu().clone().requires_grad_(True)
+    rays._pose_torch(rc, tc, init).backward(gy)
+    assert torch.isfinite(r.grad).all()
+    assert _rel(r.grad, rc.grad) < 1e-5 and _rel(t.grad, tc.grad) < 1e-6
+
+
+def test_mat4_mul_and_grad(dev):
+    g = torch.Generator().manual_seed(5)
+    A = torch.randn(1, 4, 4, generator=g, dtype=torch.float64)
+    B = torch.randn(1, 4, 4, generator=g, dtype=torch.float64)
+    gy = torch.randn(1, 4, 4, generator=g, dtype=torch.float64)
+    a = A.float().to(dev).requires_grad_(True)
+    b = B.float().to(dev).requires_grad_(True)
+    c = rays.mat4_mul(a, b)
+    assert _rel(c, A @ B) < 1e-6
+    c.backward(gy.float().to(dev))
+    a64, b64 = A.clone().requires_grad_(True), B.clone().requires_grad_(True)
+    (a64 @ b64).backward(gy)
+    assert _rel(a.grad, a64.grad) < 1e-5 and _rel(b.grad, b64.grad) < 1e-5
+
+
+def test_unproject_matrix_grad_all_inputs(dev):
+    """Gradients of inv(S) inv(W) inv(K) w.r.t. all three matrices (focal, pose and scale
+    learning) against fp64 autograd."""
+    b = synthetic_rays(R=8, seed=6)
+    K, w2c, S = b["K"].double(), b["w2c"].double(), b["scale"].double().clone()
+    S[0, :3, :3] *= 1.3
+    gy = torch.randn(1, 4, 4, generator=torch.Generator().manual_seed(7), dtype=torch.float64)
+    ins64 = [x.clone().requires_grad_(True) for x in (K, w2c, S)]
+    iv = torch.linalg.inv
+    ((iv(ins64[2]) @ iv(ins64[1])) @ iv(ins64[0])).backward(gy)
+    ins = [x.float().to(dev).requires_grad_(True) for x in (K, w2c, S)]
+    M = rays.unproject_matrix(*ins)
+    assert _rel(M, (iv(S) @ iv(w2c)) @ iv(K)) < 1e-5
+    M.backward(gy.float().to(dev))
+    for h, r in zip(ins, ins64):
+        assert _rel(h.grad, r.grad) < 1e-4
+
+
 def test_learnpose_forward_device(dev):
     import model as mdl
     init = torch.stack([rigid_c2w(1), rigid_c2w(2)])
