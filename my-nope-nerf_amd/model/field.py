@@ -315,9 +315,12 @@ class FieldRunner:
         # the saved input, so they run on a side stream beside the dX chain: compute-bound
         # GEMM phases overlap the memory-bound reductions and each other's prologue/epilogue.
         main = torch.cuda.current_stream(dev)
-        if self._side is None or self._side.device != dev:
-            self._side = torch.cuda.Stream(dev, priority=int(os.environ.get("NERF_SIDE_PRIORITY", "0")))
-        side = self._side
+        n_side = int(os.environ.get("NERF_SIDE_STREAMS", "1"))
+        tail_main = int(os.environ.get("NERF_TAIL_MAIN", "0"))
+        if self._side is None or self._side[0].device != dev or len(self._side) != n_side:
+            prio = int(os.environ.get("NERF_SIDE_PRIORITY", "0"))
+            self._side = [torch.cuda.Stream(dev, priority=prio) for _ in range(n_side)]
+        sides = self._side
         dy = dyr
         prev_in = {"l0": st["enc_p"], "l1": h["l0"], "l2": h["l1"], "l3": h["l2"], "l4": h["l3"],
                    "l5": h["l4"], "l6": h["l5"], "l7": h["l6"], "lf": h["l7"], "lr": h["lf"]}
@@ -326,33 +329,43 @@ class FieldRunner:
                      "lf": "l7", "lr": "lf"}
         spec = {l.name: l for l in self.layers}
         seg_buf = {"enc_p": st["enc_p"], "enc_d": st["enc_d"]}
+        def weight_grad(l, dy, dy_cm, x_in):
+            W = l.linear.weight
+            nout_ref, kin_ref = W.shape
+            k1 = l.k1
+            splits = _hip.bwd_weight_splits(l.out_p, k1, Np)
+            slab = e(splits * l.out_p * l.kp)
+            bslab = e(splits * l.out_p)
+            _hip.linear_bwd_weight(dy, l.out_p, x_in, k1, Np, splits, slab, l.kp, 0, bslab, dy_cmax=dy_cm,
+                                   x_cmax=fcm.get(prev_cm[l.name]))
+            if l.seg2:
+                _hip.linear_bwd_weight(dy, l.out_p, seg_buf[l.seg2], 64, Np, splits, slab, l.kp, k1, None,
+                                       dy_cmax=dy_cm, x_cmax=fcm.get(l.seg2))
+            gb = G(l.linear.bias) if l.out_p == nout_ref else e(l.out_p)
+            _hip.slab_reduce(slab, splits, l.out_p, l.kp, nout_ref, kin_ref, bslab, G(W), gb)
+            if l.out_p != nout_ref:
+                G(l.linear.bias).copy_(gb[:nout_ref])
+
+        deferred = []
         for step, name in enumerate(order):
             l = spec[name]
             W = l.linear.weight
-            nout_ref, kin_ref = W.shape
             x_in = prev_in[name]
             k1 = l.k1
-            # --- weight / bias gradient on the side stream: split-K slabs + reduce
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
-            dy.record_stream(side)          # dy_l is freed by the main loop while side reads it
-            if dy_cm is not None:
-                dy_cm.record_stream(side)
-            with torch.cuda.stream(side):
-                splits = _hip.bwd_weight_splits(l.out_p, k1, Np)
-                slab = e(splits * l.out_p * l.kp)
-                bslab = e(splits * l.out_p)
-                _hip.linear_bwd_weight(dy, l.out_p, x_in, k1, Np, splits, slab, l.kp, 0, bslab, dy_cmax=dy_cm,
-                                       x_cmax=fcm.get(prev_cm[name]))
-                if l.seg2:
-                    _hip.linear_bwd_weight(dy, l.out_p, seg_buf[l.seg2], 64, Np, splits, slab, l.kp, k1, None,
-                                           dy_cmax=dy_cm, x_cmax=fcm.get(l.seg2))
-                gb = G(l.linear.bias) if l.out_p == nout_ref else e(l.out_p)
-                gw = G(W)
-                _hip.slab_reduce(slab, splits, l.out_p, l.kp, nout_ref, kin_ref, bslab, gw, gb)
-                if l.out_p != nout_ref:
-                    G(l.linear.bias).copy_(gb[:nout_ref])
+            # --- weight / bias gradient on a side stream: split-K slabs + reduce (the last
+            # NERF_TAIL_MAIN layers' on the main stream once the input-gradient chain is done)
+            if step >= len(order) - tail_main:
+                deferred.append((l, dy, dy_cm, x_in))
+            else:
+                side = sides[step % len(sides)]
+                ev = torch.cuda.Event()
+                ev.record(main)
+                side.wait_event(ev)
+                dy.record_stream(side)          # dy_l is freed by the main loop while side reads it
+                if dy_cm is not None:
+                    dy_cm.record_stream(side)
+                with torch.cuda.stream(side):
+                    weight_grad(l, dy, dy_cm, x_in)
             # --- input gradient
             wt = self.wt[name]
             wts = self.wts[name] if self.split else None
@@ -381,9 +394,12 @@ class FieldRunner:
             dy = dx
             dy_rm, dy_cm = dx_rm, dx_cm
 
-        done = torch.cuda.Event()
-        done.record(side)
-        main.wait_event(done)               # gradients complete before autograd hands them on
+        for args in deferred:
+            weight_grad(*args)
+        for side in sides:
+            done = torch.cuda.Event()
+            done.record(side)
+            main.wait_event(done)           # gradients complete before autograd hands them on
         ray = None
         if want_ray_grad:
             g_po, g_pd, g_view = e(R, 3), e(R, 3), e(R, 3)

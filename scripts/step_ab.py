@@ -24,6 +24,10 @@ import bench  # noqa: E402
 SETTINGS = {
     "default": (0, 0, 0, 0),
     "side_hi": (0, 0, 0, 0),
+    "side2": (0, 0, 0, 0),
+    "tail2": (0, 0, 0, 0),
+    "tail3": (0, 0, 0, 0),
+    "side2_tail2": (0, 0, 0, 0),
     "store_nt": (0, 0, 0, 1),
     "tn128_b256": (0, 1, 256, 0),
     "tn128_b512": (0, 1, 512, 0),
@@ -52,12 +56,15 @@ def main():
         # side_hi: the weight-gradient side stream at high priority (a trainer of its own: the
         # stream is created on the first backward)
         os.environ["NERF_SIDE_PRIORITY"] = "-1" if name == "side_hi" else "0"
-        trainers[name] = bench.build_trainer(dev, c2w, cfg)[0] if name == "side_hi" else trainer
+        trainers[name] = bench.build_trainer(dev, c2w, cfg)[0] if name != "default" else trainer
         trainers[name].train_step(data, it=0, epoch=0, scheduling_start=0)
     os.environ.pop("NERF_SIDE_PRIORITY", None)
+    # backward schedule (field.py): weight-gradient side streams / layers whose dW runs on main
+    SCHED = {"side2": ("2", "0"), "tail2": ("1", "2"), "tail3": ("1", "3"), "side2_tail2": ("2", "2")}
     for _ in range(args.rounds):
         for name in args.settings:
             trainer = trainers[name]
+            os.environ["NERF_SIDE_STREAMS"], os.environ["NERF_TAIL_MAIN"] = SCHED.get(name, ("1", "0"))
             nt, tn, blocks, snt = SETTINGS[name]
             _hip.gemm_set_policy(nt, tn)
             _hip.gemm_set_dw_blocks(blocks)
