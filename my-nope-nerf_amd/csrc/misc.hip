@@ -8,7 +8,7 @@ namespace nerf {
 struct PackBatch {
     nerf_pack_desc d[NERF_MAX_PACK];
     int n;
-    int f16;   // GEMM precision mode 2: images in the fp16 pair form (k_pack_h), not bf16x3
+    int f16;   // GEMM precision mode 2: images in the fp16 pair form (pack_h), not bf16x3
 };
 
 // x -> three bf16 words (RNE each) with x = hi + mid + lo (same split as gemm_x6.hip)
@@ -33,13 +33,13 @@ __device__ __forceinline__ void put_split(uint16_t* img, int N, int K, int r, in
     img[o + 2 * plane] = l;
 }
 
-// blockIdx.y selects the descriptor; grid-stride over the padded destination
-__global__ void k_pack(PackBatch pb) {
+// descriptor d; block bx of nb grid-strides over the padded destination
+__device__ __forceinline__ void pack_f32(const PackBatch& pb, const nerf_pack_desc& d, int bx, int nb) {
 #pragma clang fp contract(off)
-    const nerf_pack_desc& d = pb.d[blockIdx.y];
     const int rows_s = d.rows_s > d.rows ? d.rows_s : d.rows;
     const int total = (d.dst_s != nullptr ? rows_s : d.rows) * d.ld_dst;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int gs = nb * blockDim.x;
+    for (int e = bx * blockDim.x + threadIdx.x; e < total; e += gs) {
         const int r = e / d.ld_dst, c = e % d.ld_dst;
         const float x = (c < d.cols && r < d.rows) ? d.src[(size_t)r * d.cols + c] : 0.f;
         if (r < d.rows) d.dst[e] = x;
@@ -47,14 +47,14 @@ __global__ void k_pack(PackBatch pb) {
     }
     if (d.dst_t != nullptr) {
         const int tt = d.rows_t * d.rows;  // dst_t[c][r], c < rows_t, r < rows
-        for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < tt; e += gridDim.x * blockDim.x) {
+        for (int e = bx * blockDim.x + threadIdx.x; e < tt; e += gs) {
             const int c = e / d.rows, r = e % d.rows;
             d.dst_t[(size_t)c * d.ld_t + r] = c < d.cols ? d.src[(size_t)r * d.cols + c] : 0.f;
         }
     }
     if (d.dst_ts != nullptr && !pb.f16) {
         const int tt = d.rows_t * d.ld_t;  // whole image of dst_t, zero past the source
-        for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < tt; e += gridDim.x * blockDim.x) {
+        for (int e = bx * blockDim.x + threadIdx.x; e < tt; e += gs) {
             const int c = e / d.ld_t, r = e % d.ld_t;   // dst_t row c, column r
             const float x = (c < d.cols && r < d.rows) ? d.src[(size_t)r * d.cols + c] : 0.f;
             put_split(d.dst_ts, d.rows_t, d.ld_t, c, r, x);
@@ -85,14 +85,13 @@ __device__ __forceinline__ void put_row_h(uint16_t* img, int N, int K, int r, F&
     if (lane == 0) *reinterpret_cast<int*>(img + 2 * plane + (size_t)r * 8) = e;
 }
 
-// fp16 pair images of the packed weights (GEMM precision mode 2); blockIdx.y = descriptor,
-// one wave per image row, rows of dst_s then of dst_ts
-__global__ __launch_bounds__(256) void k_pack_h(PackBatch pb) {
-    const nerf_pack_desc& d = pb.d[blockIdx.y];
+// fp16 pair images of the packed weights (GEMM precision mode 2): one wave per image row,
+// rows of dst_s then of dst_ts (block bx of nb)
+__device__ __forceinline__ void pack_h(const nerf_pack_desc& d, int bx, int nb) {
     const int rows_s = d.rows_s > d.rows ? d.rows_s : d.rows;
     const int ns = d.dst_s ? rows_s : 0, nt = d.dst_ts ? d.rows_t : 0;
-    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int nwaves = (gridDim.x * blockDim.x) >> 6;
+    const int wave = (bx * blockDim.x + threadIdx.x) >> 6;
+    const int nwaves = (nb * blockDim.x) >> 6;
     for (int w = wave; w < ns + nt; w += nwaves) {
         if (w < ns) {
             const int r = w;
@@ -106,6 +105,15 @@ __global__ __launch_bounds__(256) void k_pack_h(PackBatch pb) {
             });
         }
     }
+}
+
+// one launch for both packs: blockIdx.y = descriptor; blocks [0, PACK_F32) the padded f32
+// copies (and the bf16x3 images), blocks [PACK_F32, +PACK_H) the fp16 pair images (mode 2)
+constexpr int PACK_F32 = 64, PACK_H = 32;
+__global__ __launch_bounds__(256) void k_pack(PackBatch pb) {
+    const nerf_pack_desc& d = pb.d[blockIdx.y];
+    if ((int)blockIdx.x < PACK_F32) pack_f32(pb, d, blockIdx.x, PACK_F32);
+    else pack_h(d, blockIdx.x - PACK_F32, PACK_H);
 }
 
 // torch.optim.Adam (amsgrad=False, maximize=False), single-tensor formulation:
@@ -215,8 +223,8 @@ extern "C" int nerf_pack_weights(const nerf_pack_desc* descs, int n, void* strea
     pb.f16 = gemm_precision() == 2;
     bool images = false;
     for (int i = 0; i < n; ++i) images = images || descs[i].dst_s != nullptr || descs[i].dst_ts != nullptr;
-    hipLaunchKernelGGL(k_pack, dim3(64, n), dim3(256), 0, as_stream(stream), pb);
-    if (pb.f16 && images) hipLaunchKernelGGL(k_pack_h, dim3(32, n), dim3(256), 0, as_stream(stream), pb);
+    const int bx = PACK_F32 + ((pb.f16 && images) ? PACK_H : 0);
+    hipLaunchKernelGGL(k_pack, dim3(bx, n), dim3(256), 0, as_stream(stream), pb);
     return check_launch(__func__);
 }
 

@@ -7,54 +7,101 @@
 
 namespace nerf {
 
-__global__ __launch_bounds__(256) void k_encode_samples(const float* __restrict__ po, const float* __restrict__ pd,
+// One thread per sample, 128 samples (one 128-row group) per block.  Each row is built in
+// LDS (65-float stride: the per-thread scalar writes are conflict-free) and then copied out
+// as whole 256-byte rows, 16 lanes x float4 per row: a thread-per-row float4 store touches 64
+// rows' lines per wave instruction, which held the 67 MB of encodings at ~1.5 TB/s.
+constexpr int ENC_ROWS = 128, ENC_LD = 65;
+
+// encode_position (official_nerf.py:99-119) of one sample into its LDS row; returns max |.|
+template <int L, int W>
+__device__ __forceinline__ float encode3_lds(const float x[3], float* row) {
+    float m = 0.f;
+    int k = 0;
+    auto put = [&](float v) { row[k++] = v; m = fmaxf(m, fabsf(v)); };
+#pragma unroll
+    for (int c = 0; c < 3; ++c) put(x[c]);
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        const float f = (float)(1 << i);
+        float sn[3], co[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) sincosf(f * x[c], &sn[c], &co[c]);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) put(sn[c]);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) put(co[c]);
+    }
+#pragma unroll
+    for (int c = 3 + 6 * L; c < W; ++c) row[c] = 0.f;
+    return m;
+}
+
+// the block's 128 LDS rows -> rows m0 .. m0 + 127 of a [n][64] encoding, coalesced
+__device__ __forceinline__ void enc_copy_out(const float* lds, float* dst, size_t m0) {
+#pragma unroll 4
+    for (int it = 0; it < ENC_ROWS * 16 / ENC_ROWS; ++it) {
+        const int idx = it * ENC_ROWS + threadIdx.x;
+        const int row = idx >> 4, c4 = (idx & 15) * 4;
+        const float* src = lds + row * ENC_LD + c4;
+        *reinterpret_cast<float4*>(dst + (m0 + row) * 64 + c4) = make_float4(src[0], src[1], src[2], src[3]);
+    }
+}
+
+__global__ __launch_bounds__(ENC_ROWS) void k_encode_samples(const float* __restrict__ po, const float* __restrict__ pd,
                                  const float* __restrict__ view, const float* __restrict__ noise,
                                  int R, int S, int n_pad, float nz, float fz,
                                  float* __restrict__ z_out, float* __restrict__ enc_p,
                                  float* __restrict__ enc_d, float* __restrict__ rmax_p,
                                  float* __restrict__ rmax_d, float* __restrict__ cmax_p,
                                  float* __restrict__ cmax_d) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    static_assert(ENC_P == 64 && ENC_D == 64, "row copies assume 64-wide encodings");
+    __shared__ float rows[ENC_ROWS * ENC_LD];
+    __shared__ float wm[2][6];
+    const size_t m0 = (size_t)blockIdx.x * ENC_ROWS;
+    const int s = (int)m0 + threadIdx.x;
     const int total = R * S;
-    float* rp = enc_p + (size_t)s * ENC_P;
-    float* rd = enc_d + (size_t)s * ENC_D;
+    float* lrow = rows + threadIdx.x * ENC_LD;
     float ax[3] = {0.f, 0.f, 0.f}, av[3] = {0.f, 0.f, 0.f};   // |coordinates| (column bounds)
-    if (s >= n_pad) {
-    } else if (s < total) {
+    float x[3] = {0.f, 0.f, 0.f}, v[3] = {0.f, 0.f, 0.f};
+    const bool live = s < total;
+    float z = 0.f;
+    if (live) {
         const int r = s / S, i = s - r * S;
-        float z = lerp_z(linspace01(i, S), nz, fz);
+        z = lerp_z(linspace01(i, S), nz, fz);
         if (noise != nullptr) {  // rendering.py:187-191
             const float zp = i > 0 ? lerp_z(linspace01(i - 1, S), nz, fz) : z;
             const float zn = i < S - 1 ? lerp_z(linspace01(i + 1, S), nz, fz) : z;
             z = jitter_z(z, zp, zn, i == 0, i == S - 1, noise[s]);
         }
-        float x[3], v[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             x[c] = ray_point(po[3 * r + c], pd[3 * r + c], z);  // rendering.py:193-194
             v[c] = view[3 * r + c];
+            ax[c] = fabsf(x[c]);
+            av[c] = fabsf(v[c]);
         }
-        const float mp = encode3<10, ENC_P>(x, rp);
-        const float md = encode3<4, ENC_D>(v, rd);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) { ax[c] = fabsf(x[c]); av[c] = fabsf(v[c]); }
+    }
+    // position encoding rows (padding rows: zeros, max 0)
+    float mp = 0.f;
+    if (live) mp = encode3_lds<10, ENC_P>(x, lrow);
+    else for (int c = 0; c < ENC_P; ++c) lrow[c] = 0.f;
+    if (s < n_pad) {
         z_out[s] = z;
         if (rmax_p) rmax_p[s] = mp;
-        if (rmax_d) rmax_d[s] = md;
-    } else {
-        const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int q = 0; q < ENC_P / 4; ++q) reinterpret_cast<float4*>(rp)[q] = zero;
-#pragma unroll
-        for (int q = 0; q < ENC_D / 4; ++q) reinterpret_cast<float4*>(rd)[q] = zero;
-        z_out[s] = 0.f;
-        if (rmax_p) rmax_p[s] = 0.f;
-        if (rmax_d) rmax_d[s] = 0.f;
     }
+    __syncthreads();
+    enc_copy_out(rows, enc_p, m0);
+    __syncthreads();
+    float md = 0.f;
+    if (live) md = encode3_lds<4, ENC_D>(v, lrow);
+    else for (int c = 0; c < ENC_D; ++c) lrow[c] = 0.f;
+    if (s < n_pad && rmax_d) rmax_d[s] = md;
+    __syncthreads();
+    enc_copy_out(rows, enc_d, m0);
     if (cmax_p != nullptr) {
-        // per 128-row group: exact max of the coordinate columns (wave max, then the group's
-        // two waves in LDS), 1 for the sin / cos columns (|sin|, |cos| <= 1), 0 for the pad
-        __shared__ float wm[4][6];
+        // per 128-row group (this block): exact max of the coordinate columns (wave max, then
+        // the two waves in LDS), 1 for the sin / cos columns (|sin|, |cos| <= 1), 0 for the pad
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
 #pragma unroll
@@ -68,19 +115,17 @@ __global__ __launch_bounds__(256) void k_encode_samples(const float* __restrict_
 #pragma unroll
             for (int c = 0; c < 3; ++c) { wm[w][c] = ax[c]; wm[w][3 + c] = av[c]; }
         __syncthreads();
-        const size_t grp = (size_t)blockIdx.x * 2 + (w >> 1);
-        if ((w & 1) == 0 && grp * 128 < (size_t)n_pad) {
-            const int w0 = w & ~1;
+        if (w == 0) {
             float vp, vd;
             if (l < 3) {
-                vp = fmaxf(wm[w0][l], wm[w0 + 1][l]);
-                vd = fmaxf(wm[w0][3 + l], wm[w0 + 1][3 + l]);
+                vp = fmaxf(wm[0][l], wm[1][l]);
+                vd = fmaxf(wm[0][3 + l], wm[1][3 + l]);
             } else {
                 vp = l < 63 ? 1.f : 0.f;
                 vd = l < 27 ? 1.f : 0.f;
             }
-            cmax_p[grp * ENC_P + l] = vp;
-            cmax_d[grp * ENC_D + l] = vd;
+            cmax_p[blockIdx.x * ENC_P + l] = vp;
+            cmax_d[blockIdx.x * ENC_D + l] = vd;
         }
     }
 }
@@ -832,8 +877,8 @@ extern "C" int nerf_encode_samples(const float* pts_o, const float* pts_d, const
     NERF_CHECK_ALIGN16(enc_p); NERF_CHECK_ALIGN16(enc_d);
     NERF_CHECK(n_rays > 0 && n_samples > 0 && (int64_t)n_rays * n_samples <= n_pad,
                "%s: n_pad=%d < R*S=%lld", __func__, n_pad, (long long)n_rays * n_samples);
-    const int blocks = (n_pad + 255) / 256;
-    hipLaunchKernelGGL(k_encode_samples, dim3(blocks), dim3(256), 0, as_stream(stream), pts_o, pts_d,
+    NERF_CHECK(n_pad % ENC_ROWS == 0, "%s: n_pad=%d must be a multiple of %d", __func__, n_pad, ENC_ROWS);
+    hipLaunchKernelGGL(k_encode_samples, dim3(n_pad / ENC_ROWS), dim3(ENC_ROWS), 0, as_stream(stream), pts_o, pts_d,
                        view, noise, n_rays, n_samples, n_pad, near_z, far_z, z, enc_p, enc_d, enc_p_rmax,
                        enc_d_rmax, enc_p_cmax, enc_d_cmax);
     return check_launch(__func__);

@@ -40,45 +40,6 @@ __device__ __forceinline__ float ray_point(float o, float d, float z) {
     return o + d * z;
 }
 
-// Streams an encoding row to global memory 16 bytes at a time (keeps few values live).
-template <int W>
-struct RowWriter {
-    float4* dst;
-    float buf[4];
-    int n;
-    float amax;   // max |v| of the row (row scale of GEMM precision mode 2)
-    __device__ __forceinline__ void put(float v) {
-        amax = fmaxf(amax, fabsf(v));
-        buf[n & 3] = v;
-        ++n;
-        if ((n & 3) == 0) dst[(n >> 2) - 1] = make_float4(buf[0], buf[1], buf[2], buf[3]);
-    }
-    __device__ __forceinline__ void finish() {
-        while (n < W) put(0.f);
-    }
-};
-
-// encode_position (official_nerf.py:99-119): [x, sin(2^0 x), cos(2^0 x), ...], zero padded to W
-template <int L, int W>
-__device__ __forceinline__ float encode3(const float x[3], float* row) {
-    RowWriter<W> w{reinterpret_cast<float4*>(row), {0.f, 0.f, 0.f, 0.f}, 0, 0.f};
-#pragma unroll
-    for (int c = 0; c < 3; ++c) w.put(x[c]);
-#pragma unroll
-    for (int i = 0; i < L; ++i) {
-        const float f = (float)(1 << i);
-        float s[3], co[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) sincosf(f * x[c], &s[c], &co[c]);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) w.put(s[c]);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) w.put(co[c]);
-    }
-    w.finish();
-    return w.amax;
-}
-
 enum { F_DIST_ALPHA = 1, F_WHITE_BKGD = 2, F_RELU = 4 };
 constexpr float kEps = 1e-6f;  // rendering.py:9
 

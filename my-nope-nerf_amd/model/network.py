@@ -14,9 +14,10 @@ class nope_nerf(nn.Module):
         self.device = device
 
     def forward(self, p, ray_idx, camera_mat, world_mat, scale_mat, rendering_technique, it=0, eval_mode=False,
-                depth_img=None, add_noise=True, img_size=None, **kw):
+                depth_img=None, add_noise=True, img_size=None, depth_affine=None, **kw):
         """network.py:19-33: area-resize the depth prior to the image size, gather it at
-        the sampled rays, render."""
+        the sampled rays, render.  depth_affine (MI355X build): a function applied to the
+        gathered values (the Trainer's scale / shift, commuted past the gather)."""
         depth = None
         if rendering_technique == "nope_nerf":
             d = depth_img
@@ -25,5 +26,7 @@ class nope_nerf(nn.Module):
             # index_select, not advanced indexing: its backward is one index_add (the ray
             # indices are distinct) instead of a sorted index_put (distortion learning)
             depth = torch.index_select(d.reshape(-1), 0, ray_idx.reshape(-1)).view(1, -1, 1)
+            if depth_affine is not None:    # the Trainer's deferred depth-prior distortion
+                depth = depth_affine(depth)
         return self.renderer(p, depth, camera_mat, world_mat, scale_mat, rendering_technique,
                              eval_=eval_mode, it=it, add_noise=add_noise, **kw)

@@ -265,9 +265,16 @@ class Trainer(object):
         c2w = self.pose_param_net(img_idx) if self.pose_param_net is not None else pose_gt.reshape(4, 4)
         world_mat = inv(c2w).unsqueeze(0)
         scale_input = shift_input = None
+        affine_in = None
         if self.distortion_net is not None:
             scale_input, shift_input = self.distortion_net(img_idx)
-            if self.shift_first:
+            if depth_input.is_cuda and tuple(depth_input.shape[-2:]) == (h, w):
+                # training.py:259-264's elementwise scale / shift commutes with the gathers that
+                # consume the prior (the ray gather of network.py:24-26, the nearest resize of
+                # training.py:346-347): apply it after them, to 1024 + 7285 values instead of the
+                # H x W map, so its backward never materialises a dense gradient of the map
+                affine_in = self._affine(scale_input, shift_input)
+            elif self.shift_first:
                 depth_input = (depth_input + shift_input) * scale_input
             else:
                 depth_input = depth_input * scale_input + shift_input
@@ -293,14 +300,14 @@ class Trainer(object):
         rendered_rgb = rendered_depth = gt_depth = dmask = None
         if render_model:
             out = self.model(p, ray_idx, camera_mat, world_mat, scale_mat, self.rendering_technique, it=it,
-                             eval_mode=eval_mode, depth_img=depth_input, img_size=(h, w),
+                             eval_mode=eval_mode, depth_img=depth_input, img_size=(h, w), depth_affine=affine_in,
                              dense_depth=not eval_mode, **extra)
             rendered_rgb, rendered_depth, gt_depth = out["rgb"], out["depth_pred"], out["depth_gt"]
             dmask = out.get("depth_mask")
 
         if use_ref_imgs:
             kwargs.update(self._reference_terms(weights, img, ref_img, depth_input, depth_ref, img_idx, ref_idx,
-                                                ref_pose_gt, world_mat, world_mat_gt, camera_mat, scale_input,
+                                                ref_pose_gt, world_mat, world_mat_gt, camera_mat, scale_input, affine_in,
                                                 num_cams, h_depth, w_depth, nl, it, out_render_path))
         if render_model and self.detach_gt_depth:
             gt_depth = gt_depth.detach()
@@ -312,8 +319,16 @@ class Trainer(object):
         loss_dict["shift"] = shift_input
         return loss_dict
 
+    def _affine(self, scale, shift):
+        """The depth-prior distortion of training.py:259-264 / :325-329 as a function of the
+        (gathered) prior values."""
+        if self.shift_first:
+            return lambda d: (d + shift) * scale
+        return lambda d: d * scale + shift
+
     def _reference_terms(self, weights, img, ref_img, depth_input, depth_ref, img_idx, ref_idx, ref_pose_gt,
-                         world_mat, world_mat_gt, camera_mat, scale_input, num_cams, h_depth, w_depth, nl, it,
+                         world_mat, world_mat_gt, camera_mat, scale_input, affine_in, num_cams, h_depth, w_depth,
+                         nl, it,
                          out_render_path):
         """training.py:305-405: point clouds of the image pair, relative pose, reprojection."""
         B = img.shape[0]
@@ -321,30 +336,39 @@ class Trainer(object):
         ref_Rt_gt = inv(ref_pose_gt).unsqueeze(0) if want_gt else None
         c2w_ref = self.pose_param_net(ref_idx)
         scale_ref = shift_ref = None
+        affine_ref = None
         if self.distortion_net is not None:
             scale_ref, shift_ref = self.distortion_net(ref_idx)
-            if self.shift_first:
+            if self.detach_ref_img:
+                scale_ref, shift_ref = scale_ref.detach(), shift_ref.detach()
+            if affine_in is not None:
+                affine_ref = self._affine(scale_ref, shift_ref)     # after the resize (see compute_loss)
+            elif self.shift_first:
                 depth_ref = scale_ref * (depth_ref + shift_ref)
             else:
                 depth_ref = scale_ref * depth_ref + shift_ref
         if self.detach_ref_img:
             c2w_ref = c2w_ref.detach()
-            scale_ref = scale_ref.detach() if scale_ref is not None else None
             depth_ref = depth_ref.detach()
         ref_Rt = inv(c2w_ref).unsqueeze(0)
         if int(img_idx) < num_cams - 1:
             d1, d2, img1, img2 = depth_input, depth_ref, img, ref_img
+            a1, a2 = affine_in, affine_ref
             Rt_rel_12 = mat4_mul(ref_Rt, inv(world_mat))
             Rt_rel_12_gt = mat4_mul(ref_Rt_gt, inv(world_mat_gt)) if want_gt else None
             scale1 = scale_input
         else:
             d1, d2, img1, img2 = depth_ref, depth_input, ref_img, img
+            a1, a2 = affine_ref, affine_in
             Rt_rel_12 = mat4_mul(world_mat, inv(ref_Rt))
             Rt_rel_12_gt = mat4_mul(world_mat_gt, inv(ref_Rt_gt)) if want_gt else None
             scale1 = scale_ref
         res = (int(h_depth / self.pc_ratio), int(w_depth / self.pc_ratio))
-        d1 = F.interpolate(d1, res, mode="nearest").clamp_min(nl)       # d[d < nl] = nl
-        d2 = F.interpolate(d2, res, mode="nearest").clamp_min(nl)
+        d1 = F.interpolate(d1, res, mode="nearest")
+        d2 = F.interpolate(d2, res, mode="nearest")
+        if a1 is not None:
+            d1, d2 = a1(d1), a2(d2)
+        d1, d2 = d1.clamp_min(nl), d2.clamp_min(nl)                      # d[d < nl] = nl
         if (img.is_cuda and not camera_mat.requires_grad and not self.loss.cfg.get("with_ssim", False)
                 and self.match_method == "dense"):
             # pair.hip: point clouds, chamfer and reprojection terms in 4 + 4 launches
