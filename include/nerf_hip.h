@@ -35,7 +35,8 @@ extern "C" {
 #define NERF_ROW_TILE 128
 
 /* ABI version: 5 added nerf_prof_read_kinds and nerf_render_eval_fused, 6 the 4x4-chain
- * backwards (nerf_pose_c2w_bwd, nerf_mat4_inv_bwd, nerf_mat4_mul(_bwd), nerf_unproject_matrix_bwd). */
+ * backwards (nerf_pose_c2w_bwd, nerf_mat4_inv_bwd, nerf_mat4_mul(_bwd), nerf_unproject_matrix_bwd)
+ * and the depth-prior distortion (nerf_depth_affine(_bwd)). */
 #define NERF_HIP_ABI_VERSION 6
 int nerf_hip_abi_version(void);
 const char* nerf_hip_last_error(void);
@@ -334,6 +335,16 @@ int nerf_mat4_mul_bwd(const float* a, const float* b, const float* g, int n, flo
                       void* stream);
 int nerf_unproject_matrix_bwd(const float* inverses, const float* g_M, float* g_K, float* g_world,
                               float* g_scale, void* stream);
+
+/* Depth-prior distortion of the gathered prior values d [n] (training.py:259-264, 325-329,
+ * with the nearest_limit clamp of :346-347): y = d*scale + shift (shift_first: (d + shift)*scale),
+ * then y < lo -> lo (lo = -INFINITY: no clamp).  scale, shift: device scalars.  Backward:
+ * g_scale / g_shift (device scalars, each optional) = the sums over the unclamped entries;
+ * one workgroup, deterministic. */
+int nerf_depth_affine(const float* d, int n, const float* scale, const float* shift, int shift_first, float lo,
+                      float* y, void* stream);
+int nerf_depth_affine_bwd(const float* d, int n, const float* scale, const float* shift, int shift_first, float lo,
+                          const float* g, float* g_scale, float* g_shift, void* stream);
 
 /* Camera rays of Renderer.nope_nerf (rendering.py:52-80): for pixels [R][2], depth [R]
  * (NULL = no depth prior, d_src = 1): cam [R][3] = M[:3,3]; v = M[:3,:3](x,y,1);

@@ -332,6 +332,51 @@ __global__ void k_unproject_bwd(const float* __restrict__ inverses, const float*
     }
 }
 
+// Depth-prior distortion on gathered prior values (training.py:259-264, 325-329, 346-347):
+// y = d s + t (or (d + t) s with shift_first), then y < lo -> lo (the pc resize's
+// d[d < nearest_limit] = nearest_limit; lo = -inf for none).  Backward: the clamped entries
+// pass no gradient; g_s = sum g (d [+ t]), g_t = sum g (x s with shift_first) -- one
+// workgroup, a fixed-order tree (deterministic).
+constexpr int AF_THREADS = 1024;
+__global__ __launch_bounds__(AF_THREADS) void k_depth_affine(const float* __restrict__ d, int n,
+                                                             const float* __restrict__ s, const float* __restrict__ t,
+                                                             int shift_first, float lo, float* __restrict__ y) {
+#pragma clang fp contract(off)
+    const float sc = s[0], sh = t[0];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float v = shift_first ? (d[i] + sh) * sc : d[i] * sc + sh;
+        y[i] = v < lo ? lo : v;
+    }
+}
+__global__ __launch_bounds__(AF_THREADS) void k_depth_affine_bwd(const float* __restrict__ d, int n,
+                                                                 const float* __restrict__ s,
+                                                                 const float* __restrict__ t, int shift_first,
+                                                                 float lo, const float* __restrict__ g,
+                                                                 float* __restrict__ gs, float* __restrict__ gt) {
+#pragma clang fp contract(off)
+    __shared__ float red[2][AF_THREADS / 64];
+    const float sc = s[0], sh = t[0];
+    float as = 0.f, at = 0.f;
+    for (int i = threadIdx.x; i < n; i += AF_THREADS) {
+        const float v = shift_first ? (d[i] + sh) * sc : d[i] * sc + sh;
+        if (v < lo) continue;
+        const float gi = g[i];
+        as += shift_first ? gi * (d[i] + sh) : gi * d[i];
+        at += shift_first ? gi * sc : gi;
+    }
+    as = wave_sum(as);
+    at = wave_sum(at);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][w] = as; red[1][w] = at; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float a = 0.f, b = 0.f;
+        for (int k = 0; k < AF_THREADS / 64; ++k) { a += red[0][k]; b += red[1][k]; }
+        if (gs) gs[0] = a;
+        if (gt) gt[0] = b;
+    }
+}
+
 // M = (inv(scale) @ inv(world)) @ inv(K)  (common.py:139-141); inverses kept for backward
 __global__ void k_unproject(const float* __restrict__ K, const float* __restrict__ world,
                             const float* __restrict__ scale, float* __restrict__ M, float* __restrict__ inverses) {
@@ -646,6 +691,25 @@ extern "C" int nerf_unproject_matrix_bwd(const float* inverses, const float* g_M
     NERF_CHECK_PTR(inverses); NERF_CHECK_PTR(g_M);
     hipLaunchKernelGGL(k_unproject_bwd, dim3(1), dim3(64), 0, as_stream(stream), inverses, g_M, g_K, g_world,
                        g_scale);
+    return check_launch(__func__);
+}
+
+extern "C" int nerf_depth_affine(const float* d, int n, const float* scale, const float* shift, int shift_first,
+                                 float lo, float* y, void* stream) {
+    NERF_CHECK_PTR(d); NERF_CHECK_PTR(scale); NERF_CHECK_PTR(shift); NERF_CHECK_PTR(y);
+    NERF_CHECK(n > 0, "%s: n=%d", __func__, n);
+    const int blocks = (n + AF_THREADS - 1) / AF_THREADS;
+    hipLaunchKernelGGL(k_depth_affine, dim3(blocks < 64 ? blocks : 64), dim3(AF_THREADS), 0, as_stream(stream), d,
+                       n, scale, shift, shift_first, lo, y);
+    return check_launch(__func__);
+}
+
+extern "C" int nerf_depth_affine_bwd(const float* d, int n, const float* scale, const float* shift, int shift_first,
+                                     float lo, const float* g, float* g_scale, float* g_shift, void* stream) {
+    NERF_CHECK_PTR(d); NERF_CHECK_PTR(scale); NERF_CHECK_PTR(shift); NERF_CHECK_PTR(g);
+    NERF_CHECK(n > 0, "%s: n=%d", __func__, n);
+    hipLaunchKernelGGL(k_depth_affine_bwd, dim3(1), dim3(AF_THREADS), 0, as_stream(stream), d, n, scale, shift,
+                       shift_first, lo, g, g_scale, g_shift);
     return check_launch(__func__);
 }
 

@@ -98,6 +98,8 @@ _SIGS = {
     "nerf_mat4_mul": ([_c_p, _c_p, _c_i, _c_p, _c_p], _c_i),
     "nerf_mat4_mul_bwd": ([_c_p, _c_p, _c_p, _c_i, _c_p, _c_p, _c_p], _c_i),
     "nerf_unproject_matrix_bwd": ([_c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_depth_affine": ([_c_p, _c_i, _c_p, _c_p, _c_i, _c_f, _c_p, _c_p], _c_i),
+    "nerf_depth_affine_bwd": ([_c_p, _c_i, _c_p, _c_p, _c_i, _c_f, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_camera_rays": ([_c_p, _c_p, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_camera_rays_bwd": ([_c_p, _c_p, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_ray_loss": ([_c_p, _c_p, _c_i, _c_p, _c_p, _c_p, _c_i, _c_i, _c_f, _c_f, _c_p, _c_p, _c_p, _c_p, _c_p,
@@ -345,6 +347,16 @@ def mat4_mul(a, b, c):
 
 def mat4_mul_bwd(a, b, g, g_a=None, g_b=None):
     _call("nerf_mat4_mul_bwd", _ptr(a), _ptr(b), _ptr(g), g.numel() // 16, _ptr(g_a), _ptr(g_b), _stream())
+
+
+def depth_affine(d, scale, shift, shift_first, lo, y):
+    _call("nerf_depth_affine", _ptr(d), d.numel(), _ptr(scale), _ptr(shift), int(shift_first), float(lo), _ptr(y),
+          _stream())
+
+
+def depth_affine_bwd(d, scale, shift, shift_first, lo, g, g_scale=None, g_shift=None):
+    _call("nerf_depth_affine_bwd", _ptr(d), d.numel(), _ptr(scale), _ptr(shift), int(shift_first), float(lo), _ptr(g),
+          _ptr(g_scale), _ptr(g_shift), _stream())
 
 
 def unproject_matrix_bwd(inverses, g_M, g_K=None, g_world=None, g_scale=None):

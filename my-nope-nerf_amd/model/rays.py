@@ -85,6 +85,43 @@ def mat4_mul(a, b):
     return _Mat4Mul.apply(a, b)
 
 
+# ------------------------------------------------------------------ depth-prior distortion
+class _DepthAffine(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, d, scale, shift, shift_first, lo):
+        ctx.set_materialize_grads(False)
+        dc, sc, tc = _f32c(d), _f32c(scale), _f32c(shift)
+        y = torch.empty_like(dc)
+        _hip.depth_affine(dc, sc, tc, shift_first, lo, y)
+        ctx.save_for_backward(dc, sc, tc)
+        ctx.meta = (shift_first, lo, scale.shape, shift.shape)
+        return y.view(d.shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is None:
+            return None, None, None, None, None
+        dc, sc, tc = ctx.saved_tensors
+        shift_first, lo, ssh, tsh = ctx.meta
+        want_s, want_t = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        gs = torch.empty(1, device=dc.device, dtype=torch.float32) if want_s else None
+        gt = torch.empty(1, device=dc.device, dtype=torch.float32) if want_t else None
+        if want_s or want_t:
+            _hip.depth_affine_bwd(dc, sc, tc, shift_first, lo, _f32c(g), gs, gt)
+        return (None, gs.view(ssh) if want_s else None, gt.view(tsh) if want_t else None, None, None)
+
+
+def depth_affine(d, scale, shift, shift_first=False, lo=float("-inf")):
+    """The depth prior's scale / shift (training.py:259-264, 325-329) on prior values d, then
+    the nearest_limit clamp y < lo -> lo (training.py:346-347): one launch forward, one
+    backward (gradients to scale / shift only: the prior is data).  Torch on the host or when
+    the prior itself needs a gradient."""
+    if not d.is_cuda or d.requires_grad or scale.numel() != 1 or shift.numel() != 1:
+        y = (d + shift) * scale if shift_first else d * scale + shift
+        return y.clamp_min(lo) if lo != float("-inf") else y
+    return _DepthAffine.apply(d, scale, shift, int(bool(shift_first)), float(lo))
+
+
 # ------------------------------------------------------------------ pose
 def _pose_torch(r, t, init):
     """common.py:277-310 / poses.py:27-30 in torch (host tensors, and the backward)."""

@@ -22,7 +22,7 @@ import torch.distributed as dist
 from torch.nn import functional as F
 
 from .common import arange_pixels, get_tensor_values, inv, project_to_cam, transform_to_world
-from .rays import can_sample_on_device, mat4_mul
+from .rays import can_sample_on_device, depth_affine, mat4_mul
 from .rays import sample_rays as sample_rays_dev
 from .losses import Loss
 from .pair import pair_losses
@@ -321,10 +321,9 @@ class Trainer(object):
 
     def _affine(self, scale, shift):
         """The depth-prior distortion of training.py:259-264 / :325-329 as a function of the
-        (gathered) prior values."""
-        if self.shift_first:
-            return lambda d: (d + shift) * scale
-        return lambda d: d * scale + shift
+        (gathered) prior values, optionally followed by the nearest_limit clamp (one HIP launch
+        each way, rays.depth_affine)."""
+        return lambda d, lo=float("-inf"): depth_affine(d, scale, shift, self.shift_first, lo)
 
     def _reference_terms(self, weights, img, ref_img, depth_input, depth_ref, img_idx, ref_idx, ref_pose_gt,
                          world_mat, world_mat_gt, camera_mat, scale_input, affine_in, num_cams, h_depth, w_depth,
@@ -366,9 +365,10 @@ class Trainer(object):
         res = (int(h_depth / self.pc_ratio), int(w_depth / self.pc_ratio))
         d1 = F.interpolate(d1, res, mode="nearest")
         d2 = F.interpolate(d2, res, mode="nearest")
-        if a1 is not None:
-            d1, d2 = a1(d1), a2(d2)
-        d1, d2 = d1.clamp_min(nl), d2.clamp_min(nl)                      # d[d < nl] = nl
+        if a1 is not None:                                             # distortion, then d[d < nl] = nl
+            d1, d2 = a1(d1, nl), a2(d2, nl)
+        else:
+            d1, d2 = d1.clamp_min(nl), d2.clamp_min(nl)
         if (img.is_cuda and not camera_mat.requires_grad and not self.loss.cfg.get("with_ssim", False)
                 and self.match_method == "dense"):
             # pair.hip: point clouds, chamfer and reprojection terms in 4 + 4 launches

@@ -155,6 +155,32 @@ def test_unproject_matrix_grad_all_inputs(dev):
         assert _rel(h.grad, r.grad) < 1e-4
 
 
+@pytest.mark.parametrize("shift_first,lo", [(False, float("-inf")), (True, float("-inf")), (False, 0.5),
+                                            (True, 0.5)])
+def test_depth_affine_matches_torch(dev, shift_first, lo):
+    """rays.depth_affine (distortion + nearest_limit clamp, one launch each way) vs the torch
+    expressions of training.py:259-264 / 346-347 and their autograd, incl. clamped entries."""
+    g = torch.Generator().manual_seed(8)
+    d = torch.rand(1, 1, 47, 155, generator=g) * 8
+    d[0, 0, :3, :5] = 0.0                                    # below the clamp after the affine
+    gy = torch.randn(1, 1, 47, 155, generator=g)
+    s0, t0 = torch.tensor([1.3]), torch.tensor([-0.2])
+    pre = (d + t0) * s0 if shift_first else d * s0 + t0
+    ref = pre.clamp_min(lo) if lo != float("-inf") else pre
+    sd, td = s0.to(dev).requires_grad_(True), t0.to(dev).requires_grad_(True)
+    y = rays.depth_affine(d.to(dev), sd, td, shift_first, lo)
+    assert torch.equal(y.cpu(), ref)                         # same fp32 expression, bit-exact
+    y.backward(gy.to(dev))
+    # gradients: fp64 sums over the unclamped entries; the bar is relative to sum |term|
+    # (g sums over ~7 000 entries cancel, so fp32 order differences show against the result)
+    keep = (pre >= lo).double()                              # torch's clamp_min passes x >= lo
+    g64 = gy.double() * keep
+    ts = g64 * ((d.double() + t0.double()) if shift_first else d.double())
+    tt = g64 * (s0.double() if shift_first else 1.0)
+    for h, terms in ((sd.grad, ts), (td.grad, tt)):
+        assert abs(h.item() - terms.sum().item()) <= 1e-6 * terms.abs().sum().item()
+
+
 def test_learnpose_forward_device(dev):
     import model as mdl
     init = torch.stack([rigid_c2w(1), rigid_c2w(2)])
