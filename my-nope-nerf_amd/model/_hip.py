@@ -149,8 +149,14 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
+_fns = {}
+
+
 def _call(name: str, *args):
-    rc = getattr(lib(), name)(*args)
+    fn = _fns.get(name)
+    if fn is None:
+        fn = _fns[name] = getattr(lib(), name)
+    rc = fn(*args)
     if rc != 0:
         msg = lib().nerf_hip_last_error().decode(errors="replace")
         raise RuntimeError(f"{name} failed ({rc}): {msg}")
@@ -166,7 +172,15 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
     return t.data_ptr()
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_cur_dev = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def _stream() -> int:
+    """The current HIP stream of the current device (the raw handle: constructing a
+    torch.cuda.Stream per launch cost ~10 us of host time)."""
+    if _raw_stream is not None and _cur_dev is not None:
+        return _raw_stream(_cur_dev())
     return torch.cuda.current_stream().cuda_stream
 
 

@@ -85,7 +85,8 @@ class Trainer(object):
     def train_step(self, data, it=None, epoch=None, scheduling_start=None, render_path=None):
         """training.py:70-100."""
         for m, o in self._modules_and_optims():
-            m.train()
+            if not all(sub.training for sub in m.modules()):   # train() walks and sets every submodule
+                m.train()
             if o is not None:
                 o.zero_grad()
         loss_dict = self.compute_loss(data, it=it, epoch=epoch, scheduling_start=scheduling_start,

@@ -41,7 +41,8 @@ def main():
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     print(f"enqueue {1e3 * (t1 - t0) / 20:.3f} ms/step (profiled), drained {1e3 * (t2 - t0) / 20:.3f} ms/step")
-    pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+    pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+    pstats.Stats(pr).sort_stats("cumulative").print_stats(40)
 
 
 if __name__ == "__main__":
