@@ -516,6 +516,7 @@ extern "C" int nerf_linear_bwd_weight_splits(int nout, int kin, int m) {
     const int pol = g_tn_policy ? g_tn_policy : 3;
     int tiles, target;
     if (pol == 3 && nout % 256 == 0 && kin % 256 == 0) { tiles = (nout / 256) * (kin / 256); target = 256; }
+    else if (pol == 3 && nout % 256 == 0 && kin == 64 && g_precision >= 1) { tiles = nout / 256; target = 256; }
     else { tiles = ((nout + 127) / 128) * ((kin + 127) / 128); target = 512; }
     static const int env_target = [] { const char* e = getenv("NERF_DW_BLOCKS"); return e ? atoi(e) : 0; }();
     if (env_target > 0) target = env_target;   // experiment hook: blocks per dW launch

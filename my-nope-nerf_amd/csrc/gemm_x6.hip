@@ -753,6 +753,10 @@ static void pick_tn_x6(const TNArgs& a, int nout, int kin, int splits, int polic
     else if (nout % 128 == 0 && kin % 128 == 0)
         hipLaunchKernelGGL((k_gemm_tn_x6<128, 128, 2, 2, H, NS>), dim3(nout / 128, kin / 128, splits), dim3(256), 0,
                            s, a);
+    else if (policy == 3 && nout % 256 == 0 && kin == 64)
+        // a 64-wide input (the encodings: l0, the skip segment of l4) against all 256 outputs in
+        // one tile, so each split's dy rows are read once (128 x 64 tiles read them twice)
+        hipLaunchKernelGGL((k_gemm_tn_x6<256, 64, 2, 2, H, NS>), dim3(nout / 256, 1, splits), dim3(256), 0, s, a);
     else if (nout % 128 == 0)
         hipLaunchKernelGGL((k_gemm_tn_x6<128, 64, 2, 2, H, NS>), dim3(nout / 128, kin / 64, splits), dim3(256), 0, s,
                            a);
