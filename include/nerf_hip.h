@@ -36,8 +36,8 @@ extern "C" {
 
 /* ABI version: 5 added nerf_prof_read_kinds and nerf_render_eval_fused, 6 the 4x4-chain
  * backwards (nerf_pose_c2w_bwd, nerf_mat4_inv_bwd, nerf_mat4_mul(_bwd), nerf_unproject_matrix_bwd)
- * and the depth-prior distortion (nerf_depth_affine(_bwd)). */
-#define NERF_HIP_ABI_VERSION 6
+ * and the depth-prior distortion (nerf_depth_affine(_bwd)), 7 nerf_linear_fwd_heads. */
+#define NERF_HIP_ABI_VERSION 7
 int nerf_hip_abi_version(void);
 const char* nerf_hip_last_error(void);
 
@@ -88,6 +88,18 @@ int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2
                     const float* w, const uint16_t* w_split, int w_split_rows, const float* bias, float* y,
                     int ldy, int m, int n, int relu, uint32_t* mask_out, int ldmo,
                     const float* x1_rmax, const float* x2_rmax, float* y_rmax, float* y_cmax, void* stream);
+/* nerf_linear_fwd with the output heads fused into its epilogue (precision mode 2, n = 128 or
+ * 256 -- one column block holds whole output rows): raw4[r][raw_col + c] = sum_f y[r][f]
+ * head_w[c][f] + head_b[c] for c < n_heads, head_w [n_heads][n] (16-byte aligned) -- the
+ * density head on the trunk output (official_nerf.py:66, n_heads 1, raw_col 0) and the colour
+ * head on the colour layer (official_nerf.py:91, n_heads 3, raw_col 1).  Per-row partial
+ * dots are summed in a fixed order (deterministic). */
+int nerf_linear_fwd_heads(const float* x1, int ldx1, int k1, const float* x2, int ldx2, int k2,
+                          const float* w, const uint16_t* w_split, int w_split_rows, const float* bias,
+                          float* y, int ldy, int m, int n, int relu, uint32_t* mask_out, int ldmo,
+                          const float* x1_rmax, const float* x2_rmax, float* y_rmax, float* y_cmax,
+                          const float* head_w, int n_heads, const float* head_b, float* raw4, int raw_col,
+                          void* stream);
 
 /* Backward w.r.t. the layer input (autograd of official_nerf.py:62-91).
  *   dx[m, j] = ( sum_o dy[m,o] wt[j,o]  + (u ? u[m*ldu] * v[j] : 0) ) * (mask ? bit(m,j) : 1)

@@ -49,6 +49,10 @@ struct NTArgs {
     float* c_rmax;
     float* c_cmax; int ldcm;
     int store_nt;   // tuning (nerf_gemm_set_store_hint): output tiles stored with the non-temporal hint
+    // fused output heads (nerf_linear_fwd_heads, precision mode 2, one column block): raw4[m][raw_col + c]
+    // = sum_f y[m][f] head_w[c][f] + head_b[c] for c < n_heads (official_nerf.py:66, 91)
+    const float* head_w; const float* head_b; float* raw4;
+    int n_heads; int raw_col;
 };
 
 typedef float nt_f32x4 __attribute__((ext_vector_type(4)));
@@ -386,11 +390,12 @@ __device__ __forceinline__ void bfly_max(float (&v)[NV], int sl, int& base) {
 //   H (precision mode 2): the accumulators carry the row scales 2^(ea[row] + eb[feature])
 //        (LDS arrays lea / leb, block-local indices), undone first; the row max of the
 //        stored values is max-accumulated into lrm (LDS, float bits) for NTArgs::c_rmax.
-template <int TM, int TN, int EPI, bool H = false>
+template <int TM, int TN, int EPI, bool H = false, bool HD = false>
 __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0, int wm0,
                                                    int wn0, uint32_t* lmask = nullptr, int mw = 0,
                                                    const int* leb = nullptr, const int* lea = nullptr,
-                                                   uint32_t* lrm = nullptr, uint32_t* lcm = nullptr, int lcm_ld = 0) {
+                                                   uint32_t* lrm = nullptr, uint32_t* lcm = nullptr, int lcm_ld = 0,
+                                                   float* lhs = nullptr, const float* lhw = nullptr, int lhw_ld = 0) {
     const int lane = lane_id();
     const int sl = lane & 31, hf = lane >> 5;
     int er[TM];
@@ -443,6 +448,13 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
         return;
     }
     const int cw0 = (n0 + wn0) >> 5;
+    // fused heads (FWD, H only): this lane's partial dots over its features, per row tile
+    const int nh = (EPI == EPI_FWD && H && HD) ? p.n_heads : 0;   // HD: instantiated for the head layers only
+    float hp[3][TM];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) hp[c][i] = 0.f;
     if (EPI == EPI_FWD) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -461,6 +473,15 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
                     float4 x = make_float4(acc[i][j][4 * q] + b4[q].x, acc[i][j][4 * q + 1] + b4[q].y,
                                            acc[i][j][4 * q + 2] + b4[q].z, acc[i][j][4 * q + 3] + b4[q].w);
                     if (p.relu) x = make_float4(fmaxf(x.x, 0.f), fmaxf(x.y, 0.f), fmaxf(x.z, 0.f), fmaxf(x.w, 0.f));
+                    if constexpr (EPI == EPI_FWD && H && HD) {
+#pragma unroll
+                        for (int c = 0; c < 3; ++c)
+                            if (c < nh) {
+                                // head weights staged in LDS (block-local features)
+                                const float4 hw = *reinterpret_cast<const float4*>(lhw + c * lhw_ld + (fb - n0) + 8 * q);
+                                hp[c][i] += x.x * hw.x + x.y * hw.y + x.z * hw.z + x.w * hw.w;
+                            }
+                    }
                     track(i, j, q, x);
                     store_out4(p.c + row * p.ldc + fb + 8 * q, x, p.store_nt);
                     const uint32_t nib = (x.x > 0.f ? 1u : 0u) | (x.y > 0.f ? 2u : 0u) | (x.z > 0.f ? 4u : 0u) |
@@ -513,6 +534,19 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
                 }
             }
         }
+    }
+    if (HD && nh) {
+        // head partials: the lane pair (lane, lane ^ 32) holds one row's features of this wave;
+        // lhs is this wave's [BM][3] slot (one per wave along N), summed in wave order by the
+        // kernel (deterministic)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                if (c < nh) {
+                    const float v = hp[c][i] + __shfl_xor(hp[c][i], 32, 64);
+                    if (hf == 0) lhs[(wm0 + 32 * i + sl) * 3 + c] = v;
+                }
     }
     if constexpr (H) {
         // the lane pair (lane, lane ^ 32) holds one row's features of this wave; the other

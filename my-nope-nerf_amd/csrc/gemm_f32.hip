@@ -373,12 +373,13 @@ static int check_nt(const NTArgs& a, const char* fn) {
     return NERF_OK;
 }
 
-extern "C" int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2, int k2,
-                               const float* w, const uint16_t* w_split, int w_split_rows, const float* bias,
-                               float* y, int ldy, int m, int n, int relu, uint32_t* mask_out, int ldmo,
-                               const float* x1_rmax, const float* x2_rmax, float* y_rmax, float* y_cmax,
-                               void* stream) {
+static int linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2, int k2, const float* w,
+                      const uint16_t* w_split, int w_split_rows, const float* bias, float* y, int ldy, int m, int n,
+                      int relu, uint32_t* mask_out, int ldmo, const float* x1_rmax, const float* x2_rmax,
+                      float* y_rmax, float* y_cmax, const float* head_w, int n_heads, const float* head_b,
+                      float* raw4, int raw_col, void* stream) {
     NTArgs a{};
+    a.head_w = head_w; a.n_heads = n_heads; a.head_b = head_b; a.raw4 = raw4; a.raw_col = raw_col;
     a.a1 = x1; a.lda1 = ldx1; a.k1 = k1;
     a.a2 = x2; a.lda2 = x2 ? ldx2 : 0; a.k2 = x2 ? k2 : 0;
     a.b = w; a.ldb = k1 + a.k2;
@@ -395,6 +396,32 @@ extern "C" int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x
     prof_next(NERF_PROF_FWD, 4.0 * m * (double)(k1 + a.k2) + 4.0 * n * (double)(k1 + a.k2) + 4.0 * m * (double)n +
                                  (mask_out ? m * (double)n / 8 : 0.0));
     return dispatch_nt<EPI_FWD>(a, as_stream(stream), fl);
+}
+
+extern "C" int nerf_linear_fwd(const float* x1, int ldx1, int k1, const float* x2, int ldx2, int k2,
+                               const float* w, const uint16_t* w_split, int w_split_rows, const float* bias,
+                               float* y, int ldy, int m, int n, int relu, uint32_t* mask_out, int ldmo,
+                               const float* x1_rmax, const float* x2_rmax, float* y_rmax, float* y_cmax,
+                               void* stream) {
+    return linear_fwd(x1, ldx1, k1, x2, ldx2, k2, w, w_split, w_split_rows, bias, y, ldy, m, n, relu, mask_out, ldmo,
+                      x1_rmax, x2_rmax, y_rmax, y_cmax, nullptr, 0, nullptr, nullptr, 0, stream);
+}
+
+extern "C" int nerf_linear_fwd_heads(const float* x1, int ldx1, int k1, const float* x2, int ldx2, int k2,
+                                     const float* w, const uint16_t* w_split, int w_split_rows, const float* bias,
+                                     float* y, int ldy, int m, int n, int relu, uint32_t* mask_out, int ldmo,
+                                     const float* x1_rmax, const float* x2_rmax, float* y_rmax, float* y_cmax,
+                                     const float* head_w, int n_heads, const float* head_b, float* raw4,
+                                     int raw_col, void* stream) {
+    NERF_CHECK_PTR(head_w); NERF_CHECK_PTR(head_b); NERF_CHECK_PTR(raw4);
+    NERF_CHECK(n_heads >= 1 && n_heads <= 3 && raw_col >= 0 && raw_col + n_heads <= 4,
+               "%s: n_heads=%d raw_col=%d (raw4 rows have 4 columns)", __func__, n_heads, raw_col);
+    NERF_CHECK(g_precision == 2 && w_split != nullptr && (n == 256 || n == 128),
+               "%s: fused heads need GEMM precision mode 2, the weight image and one column block (n = 128 or 256)",
+               __func__);
+    NERF_CHECK((((uintptr_t)head_w) & 15u) == 0, "%s: head_w must be 16-byte aligned", __func__);
+    return linear_fwd(x1, ldx1, k1, x2, ldx2, k2, w, w_split, w_split_rows, bias, y, ldy, m, n, relu, mask_out, ldmo,
+                      x1_rmax, x2_rmax, y_rmax, y_cmax, head_w, n_heads, head_b, raw4, raw_col, stream);
 }
 
 extern "C" int nerf_linear_bwd_data(const float* dy, int lddy, int k, const float* wt,

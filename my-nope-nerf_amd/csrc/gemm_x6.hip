@@ -375,7 +375,7 @@ struct NTStager {
 
 // OCC: waves per SIMD the kernel is compiled for (2: two co-resident blocks per CU, one
 // block's epilogue store burst beside the other's MFMAs; <= 256 registers per lane)
-template <int BM, int BN, int WM, int WN, int EPI, bool DIRECT, bool H = false, int OCC = 1>
+template <int BM, int BN, int WM, int WN, int EPI, bool DIRECT, bool H = false, int OCC = 1, bool HD = false>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void k_gemm_nt_x6(NTArgs p) {
     constexpr int NT = 64 * WM * WN;
     constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -424,16 +424,37 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void k_gemm_nt_x6(NTArgs p) {
         stamp(p.stamps, 2);
         constexpr int MW = BN / 32;
         const bool gather = EPI == EPI_FWD && p.mask_out != nullptr && !(p.ablate & 1);
+        // fused heads: per-wave row partials in LDS after the mask rows (one column block only)
+        const bool heads = HD && EPI == EPI_FWD && H && p.n_heads > 0 && !(p.ablate & 1);
+        static_assert(BM * MW * 4 + WN * BM * 3 * 4 + 3 * BN * 4 <= MAIN_BYTES, "heads overflow the staging LDS");
+        float* lhs = heads ? reinterpret_cast<float*>(smem + BM * MW * 4) + (wave % WN) * BM * 3 : nullptr;
+        float* lhw = heads ? reinterpret_cast<float*>(smem + BM * MW * 4 + WN * BM * 3 * 4) : nullptr;
         uint32_t* lmask = nullptr;
-        if (gather) {    // the mask rows reuse the staging LDS once the last (clamped) DMA landed
+        if (gather || heads) {    // the mask rows / head partials reuse the staging LDS once the last DMA landed
             dma_wait();
             __syncthreads();
-            lmask = reinterpret_cast<uint32_t*>(smem);
+            if (gather) lmask = reinterpret_cast<uint32_t*>(smem);
+            if (heads) {          // head weights [n_heads][BN] of this column block, one pass of the block
+                for (int e = threadIdx.x; e < p.n_heads * BN; e += NT)
+                    lhw[e] = p.head_w[(size_t)(e / BN) * p.n + n0 + e % BN];
+                __syncthreads();
+            }
         }
-        nt_epilogue_direct<TM, TN, EPI, H>(p, acc, m0, n0, wm0, wn0, lmask, MW, leb, lea, lrm,
-                                           (H && p.c_cmax) ? lcm : nullptr, BN);
-        if (gather || (H && (p.c_rmax || p.c_cmax))) {
+        nt_epilogue_direct<TM, TN, EPI, H, HD>(p, acc, m0, n0, wm0, wn0, lmask, MW, leb, lea, lrm,
+                                               (H && p.c_cmax) ? lcm : nullptr, BN, lhs, lhw, BN);
+        if (gather || heads || (H && (p.c_rmax || p.c_cmax))) {
             __syncthreads();
+            if (heads) {
+                const float* part = reinterpret_cast<const float*>(smem + BM * MW * 4);
+                for (int e = threadIdx.x; e < BM * 3; e += NT) {
+                    const int r = e / 3, c = e - 3 * r;
+                    if (c >= p.n_heads) continue;
+                    float v = 0.f;
+#pragma unroll
+                    for (int w = 0; w < WN; ++w) v += part[w * BM * 3 + e];
+                    p.raw4[(size_t)(m0 + r) * 4 + p.raw_col + c] = v + p.head_b[c];
+                }
+            }
             if (gather)
                 for (int e = threadIdx.x; e < BM * MW; e += NT)
                     p.mask_out[(size_t)(m0 + e / MW) * p.ldmo + (n0 >> 5) + e % MW] = lmask[e];
@@ -711,6 +732,13 @@ static const bool g_nt_direct = [] {
 template <int BM, int BN, int WM, int WN, int EPI>
 static void launch_nt_x6(const NTArgs& a, hipStream_t s, bool h16) {
     constexpr bool co = BM == 128 && BN == 256;   // fits two co-resident blocks per CU (fp16 pair)
+    if constexpr (EPI == EPI_FWD) {
+        if (h16 && a.n_heads > 0) {   // fused output heads: their own instantiation (registers)
+            hipLaunchKernelGGL((k_gemm_nt_x6<BM, BN, WM, WN, EPI, true, true, co ? 2 : 1, true>),
+                               dim3(a.m / BM, a.n / BN), dim3(64 * WM * WN), 0, s, a);
+            return;
+        }
+    }
     if (h16 && co)
         hipLaunchKernelGGL((k_gemm_nt_x6<BM, BN, WM, WN, EPI, true, true, co ? 2 : 1>), dim3(a.m / BM, a.n / BN),
                            dim3(64 * WM * WN), 0, s, a);

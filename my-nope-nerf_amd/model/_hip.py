@@ -46,7 +46,7 @@ class ProfKind(ctypes.Structure):
 
 
 PROF_KINDS = ("fwd", "dx", "dw", "dw_narrow")   # NERF_PROF_FWD / _DX / _DW / _DW_NARROW
-ABI_VERSION = 6                    # NERF_HIP_ABI_VERSION
+ABI_VERSION = 7                    # NERF_HIP_ABI_VERSION
 
 
 class ChainLayer(ctypes.Structure):
@@ -62,6 +62,8 @@ _SIGS = {
                              _c_p, _c_p, _c_p], _c_i),
     "nerf_linear_fwd": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_p, _c_i, _c_i, _c_i, _c_i,
                          _c_p, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_linear_fwd_heads": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_p, _c_i, _c_i, _c_i, _c_i,
+                               _c_p, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_linear_bwd_data": ([_c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_i,
                               _c_i, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_linear_bwd_weight": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p,
@@ -218,16 +220,22 @@ def split_image(rows: int, k: int, device) -> "torch.Tensor":
 
 
 def linear_fwd(x1, k1, x2, k2, w, bias, y, m, n, relu, mask_out=None, w_split=None, x1_rmax=None, x2_rmax=None,
-               y_rmax=None, y_cmax=None):
+               y_rmax=None, y_cmax=None, heads=None):
     """mask_out: int32 [m][n/32] ReLU mask bits of y (optional).  w_split: optional split
     image of w (used by GEMM precision modes 1 and 2).  x1_rmax / x2_rmax: max |x| per row of
     each input segment (required in mode 2); y_rmax: optional [m] output, max |y| per row;
-    y_cmax: optional [m/128][n] output, max |y| per column and 128-row group (mode 2)."""
+    y_cmax: optional [m/128][n] output, max |y| per column and 128-row group (mode 2).
+    heads: optional (head_w [nh][n], head_b [nh], raw4 [m][4], raw_col) -- the output heads
+    fused into the epilogue (nerf_linear_fwd_heads, mode 2)."""
     wsp, wsr = _split_args(w_split)
-    _call("nerf_linear_fwd", _ptr(x1), _ld(x1), k1, _ptr(x2), _ld(x2) if x2 is not None else 0, k2,
-          _ptr(w), wsp, wsr, _ptr(bias), _ptr(y), _ld(y), m, n, int(relu), _ptr(mask_out),
-          _ld(mask_out) if mask_out is not None else 0, _ptr(x1_rmax), _ptr(x2_rmax), _ptr(y_rmax), _ptr(y_cmax),
-          _stream())
+    args = (_ptr(x1), _ld(x1), k1, _ptr(x2), _ld(x2) if x2 is not None else 0, k2,
+            _ptr(w), wsp, wsr, _ptr(bias), _ptr(y), _ld(y), m, n, int(relu), _ptr(mask_out),
+            _ld(mask_out) if mask_out is not None else 0, _ptr(x1_rmax), _ptr(x2_rmax), _ptr(y_rmax), _ptr(y_cmax))
+    if heads is None:
+        _call("nerf_linear_fwd", *args, _stream())
+    else:
+        hw, hb, raw4, col = heads
+        _call("nerf_linear_fwd_heads", *args, _ptr(hw), hw.shape[0], _ptr(hb), _ptr(raw4), int(col), _stream())
 
 
 def linear_bwd_data(dy, k, wt, dx, m, n, mask=None, u=None, ldu=1, v=None, wt_split=None, dy_rmax=None,

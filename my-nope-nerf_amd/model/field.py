@@ -96,6 +96,7 @@ class FieldRunner:
         self.bias_p = {l.name: z(l.out_p) for l in self.layers}
         self.b_r = self.bias_p["lr"]
         self.wc = z(3, HR)         # padded fc_rgb weight
+        self.wd = z(1, D)          # 16-byte-aligned fc_density weight (the fused density head reads it by float4)
         self.device = device
 
     def pack(self):
@@ -122,6 +123,8 @@ class FieldRunner:
             descs.append(_hip.PackDesc(b.data_ptr(), self.bias_p[l.name].data_ptr(), None, 1, b.shape[0], l.out_p, 0, 0))
         wc = self.m.fc_rgb.weight
         descs.append(_hip.PackDesc(wc.data_ptr(), self.wc.data_ptr(), None, 3, wc.shape[1], self.HR, 0, 0))
+        wd = self.m.fc_density.weight
+        descs.append(_hip.PackDesc(wd.data_ptr(), self.wd.data_ptr(), None, 1, wd.shape[1], self.D, 0, 0))
         _hip.pack_weights(descs)
 
     def bias(self, l: LayerSpec):
@@ -180,6 +183,12 @@ class FieldRunner:
                 acts.append(y if y is not None else outs[i])
             _hip.mlp_chain_fwd(enc_p, enc_d, enc_p_rm, enc_d_rm, Np, descs)
             h8 = acts[7]
+        raw4 = e(Np, 4)
+        m = self.m
+        # precision mode 2 at hidden 256: the density / colour heads run in the l7 / colour-layer
+        # epilogues (nerf_linear_fwd_heads) instead of a separate pass over h8 and hr
+        fuse_heads = self.h16 and D == 256 and HR == 128 and not self.use_chain(keep)
+        head_args = {"l7": (self.wd, m.fc_density.bias, raw4, 0), "lr": (self.wc, m.fc_rgb.bias, raw4, 1)}
         for i, l in enumerate(self.layers if not self.use_chain(keep) else []):
             y = outs[i]
             x2 = segs[l.seg2] if l.seg2 else None
@@ -193,16 +202,16 @@ class FieldRunner:
             cmaxes[l.name] = y_cm
             _hip.linear_fwd(x, k1, x2, _hip.ENC_P if x2 is not None else 0, self.w[l.name], self.bias(l), y,
                             Np, l.out_p, l.relu, mask_out=mo, w_split=self.ws[l.name] if self.split else None,
-                            x1_rmax=x_rm, x2_rmax=seg_rm[l.seg2] if l.seg2 else None, y_rmax=y_rm, y_cmax=y_cm)
+                            x1_rmax=x_rm, x2_rmax=seg_rm[l.seg2] if l.seg2 else None, y_rmax=y_rm, y_cmax=y_cm,
+                            heads=head_args.get(l.name) if fuse_heads else None)
             acts.append(y)
             x = y
             x_rm = y_rm
             if l.name == "l7":
                 h8 = y
         hr = acts[9]
-        raw4 = e(Np, 4)
-        m = self.m
-        _hip.heads_fwd(h8, hr, D, m.fc_density.weight, m.fc_density.bias, self.wc, m.fc_rgb.bias, raw4, Np)
+        if not fuse_heads:
+            _hip.heads_fwd(h8, hr, D, m.fc_density.weight, m.fc_density.bias, self.wc, m.fc_rgb.bias, raw4, Np)
         if composite:
             rgb = e(R, 3)
             dist = e(R)

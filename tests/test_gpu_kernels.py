@@ -73,6 +73,42 @@ def test_linear_fwd(dev, gemm_precision, m, n, k1, k2, relu):
     assert torch.equal(bits.view(m, n).bool(), y.cpu() > 0)          # ReLU bits agree with y
 
 
+@pytest.mark.parametrize("n,k1,k2,nh,col", [(256, 256, 0, 1, 0), (128, 256, 64, 3, 1)])
+def test_linear_fwd_fused_heads(dev, n, k1, k2, nh, col):
+    """nerf_linear_fwd_heads (precision mode 2): the layer output as nerf_linear_fwd's, plus
+    raw4[:, col:col+nh] = relu(x W^T + b) head_w^T + head_b (the density head on the trunk,
+    the colour head on the colour layer) vs fp64, the other raw4 columns untouched."""
+    prev = _hip.gemm_get_precision()
+    _hip.gemm_set_precision(2)
+    try:
+        m = 4096
+        g = torch.Generator().manual_seed(n + nh)
+        x1 = _rand(m, k1, g=g)
+        x2 = _rand(m, k2, g=g) if k2 else None
+        W = _rand(n, k1 + k2, g=g) * 0.1
+        b = _rand(n, g=g)
+        hw = _rand(nh, n, g=g)
+        hb = _rand(nh, g=g)
+        x1d, x2d = x1.to(dev), (x2.to(dev) if k2 else None)
+        Wd = W.to(dev)
+        ws = _images(Wd, dev)[0]
+        y = torch.empty(m, n, device=dev)
+        raw4 = torch.full((m, 4), 7.0, device=dev)
+        _hip.linear_fwd(x1d, k1, x2d, k2, Wd, b.to(dev), y, m, n, True, w_split=ws, x1_rmax=_rm(x1d),
+                        x2_rmax=_rm(x2d) if k2 else None, heads=(hw.to(dev).contiguous(), hb.to(dev), raw4, col))
+        xx = torch.cat([x1, x2], 1) if k2 else x1
+        ref_y = torch.relu(xx.double() @ W.double().t() + b.double())
+        ref_h = ref_y @ hw.double().t() + hb.double()
+        torch.cuda.synchronize()
+        assert (y.cpu().double() - ref_y).abs().max().item() < 2e-5 * ref_y.abs().max().item()
+        r = raw4.cpu().double()
+        assert (r[:, col:col + nh] - ref_h).abs().max().item() < 2e-5 * ref_h.abs().max().item()
+        others = [c for c in range(4) if not col <= c < col + nh]
+        assert bool((r[:, others] == 7.0).all())
+    finally:
+        _hip.gemm_set_precision(prev)
+
+
 def test_linear_fwd_asymmetric_identity(dev, gemm_precision):
     """A = I against an asymmetric B catches a transposed C write (guide section 3)."""
     m = n = k = 128
