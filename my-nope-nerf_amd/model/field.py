@@ -58,6 +58,8 @@ class LayerSpec:
 class FieldRunner:
     """Owns the packed weights of one OfficialStaticNerf and launches the kernels."""
 
+    TAIL_SIDE = 0   # backward schedule default (NERF_TAIL_SIDE overrides; DESIGN.md section 4.1)
+
     def __init__(self, module):
         self.m = module
         D = module.hidden_dim
@@ -325,7 +327,13 @@ class FieldRunner:
         # GEMM phases overlap the memory-bound reductions and each other's prologue/epilogue.
         main = torch.cuda.current_stream(dev)
         n_side = int(os.environ.get("NERF_SIDE_STREAMS", "1"))
-        tail_main = int(os.environ.get("NERF_TAIL_MAIN", "0"))
+        # at the training size the side stream trails the input-gradient chain by ~3 layers, and
+        # the last two layers' weight gradients finish sooner on the main stream behind the chain
+        # than behind two more cross-stream waits (2.60 vs 2.67 ms/step, profiles/r02/
+        # backward_schedule_ab2.json); small batches keep everything beside the chain
+        tail_default = 2 if (D == 256 and Np >= 65536) else 0
+        tail_main = int(os.environ.get("NERF_TAIL_MAIN", str(tail_default)))
+        tail_side = int(os.environ.get("NERF_TAIL_SIDE", str(self.TAIL_SIDE)))
         if self._side is None or self._side[0].device != dev or len(self._side) != n_side:
             prio = int(os.environ.get("NERF_SIDE_PRIORITY", "0"))
             self._side = [torch.cuda.Stream(dev, priority=prio) for _ in range(n_side)]
@@ -355,16 +363,21 @@ class FieldRunner:
             if l.out_p != nout_ref:
                 G(l.linear.bias).copy_(gb[:nout_ref])
 
-        deferred = []
+        deferred, deferred_side = [], []
         for step, name in enumerate(order):
             l = spec[name]
             W = l.linear.weight
             x_in = prev_in[name]
             k1 = l.k1
-            # --- weight / bias gradient on a side stream: split-K slabs + reduce (the last
-            # NERF_TAIL_MAIN layers' on the main stream once the input-gradient chain is done)
+            # --- weight / bias gradient on a side stream: split-K slabs + reduce.  The last
+            # NERF_TAIL_MAIN layers' run on the main stream once the input-gradient chain is done;
+            # the NERF_TAIL_SIDE layers before them are enqueued on the side stream behind ONE
+            # wait for that chain (the side stream trails it by ~3 layers at the tail anyway, and
+            # every cross-stream wait costs ~15 us before the next launch)
             if step >= len(order) - tail_main:
                 deferred.append((l, dy, dy_cm, x_in))
+            elif step >= len(order) - tail_main - tail_side:
+                deferred_side.append((l, dy, dy_cm, x_in))
             else:
                 side = sides[step % len(sides)]
                 ev = torch.cuda.Event()
@@ -395,14 +408,25 @@ class FieldRunner:
             mask = None if name == "lr" else st["masks"][prev_name[name]]
             if name == "lf":   # + density path: d sigma_raw (graw4[:,0]) x w_density
                 _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask, u=graw4, ldu=4,
-                                     v=m.fc_density.weight, wt_split=rows(0, k1), dy_rmax=dy_rm, dx_rmax=dx_rm,
-                                     dx_cmax=dx_cm)
+                                     v=self.wd.view(-1), wt_split=rows(0, k1), dy_rmax=dy_rm, dx_rmax=dx_rm,
+                                     dx_cmax=dx_cm)     # v: the 16-byte-aligned copy (float4 epilogue reads)
             else:
                 _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask, wt_split=rows(0, k1),
                                      dy_rmax=dy_rm, dx_rmax=dx_rm, dx_cmax=dx_cm)
             dy = dx
             dy_rm, dy_cm = dx_rm, dx_cm
 
+        if deferred_side:
+            side = sides[0]
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                for args in deferred_side:
+                    args[1].record_stream(side)
+                    if args[2] is not None:
+                        args[2].record_stream(side)
+                    weight_grad(*args)
         for args in deferred:
             weight_grad(*args)
         for side in sides:

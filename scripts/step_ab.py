@@ -24,10 +24,18 @@ import bench  # noqa: E402
 SETTINGS = {
     "default": (0, 0, 0, 0),
     "side_hi": (0, 0, 0, 0),
+    "old_default": (0, 0, 0, 0),
     "side2": (0, 0, 0, 0),
     "tail2": (0, 0, 0, 0),
     "tail3": (0, 0, 0, 0),
     "side2_tail2": (0, 0, 0, 0),
+    "tside2": (0, 0, 0, 0),
+    "tside3": (0, 0, 0, 0),
+    "tside4": (0, 0, 0, 0),
+    "tail1": (0, 0, 0, 0),
+    "tail2_ts1": (0, 0, 0, 0),
+    "tail2_ts2": (0, 0, 0, 0),
+    "tail1_ts2": (0, 0, 0, 0),
     "store_nt": (0, 0, 0, 1),
     "tn128_b256": (0, 1, 256, 0),
     "tn128_b512": (0, 1, 512, 0),
@@ -60,11 +68,19 @@ def main():
         trainers[name].train_step(data, it=0, epoch=0, scheduling_start=0)
     os.environ.pop("NERF_SIDE_PRIORITY", None)
     # backward schedule (field.py): weight-gradient side streams / layers whose dW runs on main
-    SCHED = {"side2": ("2", "0"), "tail2": ("1", "2"), "tail3": ("1", "3"), "side2_tail2": ("2", "2")}
+    SCHED = {"old_default": ("1", "0", "0"), "side2": ("2", "0", "0"), "tail2": ("1", "2", "0"), "tail3": ("1", "3", "0"),
+             "side2_tail2": ("2", "2", "0"), "tside2": ("1", "0", "2"), "tside3": ("1", "0", "3"),
+             "tside4": ("1", "0", "4"), "tail1": ("1", "1", "0"), "tail2_ts1": ("1", "2", "1"),
+             "tail2_ts2": ("1", "2", "2"), "tail1_ts2": ("1", "1", "2")}
     for _ in range(args.rounds):
         for name in args.settings:
             trainer = trainers[name]
-            os.environ["NERF_SIDE_STREAMS"], os.environ["NERF_TAIL_MAIN"] = SCHED.get(name, ("1", "0"))
+            if name in SCHED:
+                (os.environ["NERF_SIDE_STREAMS"], os.environ["NERF_TAIL_MAIN"],
+                 os.environ["NERF_TAIL_SIDE"]) = SCHED[name]
+            else:   # the library defaults
+                for k in ("NERF_SIDE_STREAMS", "NERF_TAIL_MAIN", "NERF_TAIL_SIDE"):
+                    os.environ.pop(k, None)
             nt, tn, blocks, snt = SETTINGS[name]
             _hip.gemm_set_policy(nt, tn)
             _hip.gemm_set_dw_blocks(blocks)
