@@ -4,5 +4,5 @@ R=$GRAFT_REPO_ROOT
 cd $R
 OUT=$R/gpurun_out/r02y
 mkdir -p $OUT
-timeout -k 10 500 python -u scripts/step_ab.py --steps 20 --rounds 6 --settings default tail1 tail2 tail2_ts1 tail2_ts2 tail1_ts2 tside3 > $OUT/step.json 2> $OUT/step.err; rc=$?
+timeout -k 10 500 python -u scripts/step_ab.py --steps 20 --rounds 6 --settings default slab_stream tail1_ts2 > $OUT/step.json 2> $OUT/step.err; rc=$?
 tail -1 $OUT/step.json; exit $rc
