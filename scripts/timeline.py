@@ -29,6 +29,7 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("--marker", default="k_sample_rays")
     ap.add_argument("--skip", type=int, default=3)
+    ap.add_argument("--gaps", type=float, default=0.0, help="list idle gaps of at least this many us")
     args = ap.parse_args()
     rows = []
     with open(args.csv) as f:
@@ -80,6 +81,20 @@ def main():
     print(f"{'kernel':60s} {'sum us':>9s} {'alone us':>9s}")
     for n in sorted(total, key=lambda k: -med(total[k])):
         print(f"{n:60s} {med(total[n]):9.1f} {med(excl[n]):9.1f}")
+    if args.gaps:
+        # idle intervals of the median step, keyed by (kernel that ended last, kernel that starts next)
+        st = steps[len(steps) // 2]
+        out = []
+        end_max, prev = st[0][1], st[0][2]
+        for s, e, n in st[1:]:
+            if s > end_max:
+                out.append(((s - end_max) / 1e3, prev, n, (end_max - st[0][0]) / 1e3))
+            if e > end_max:
+                end_max, prev = e, n
+        print(f"\nidle gaps of one step (>= {args.gaps} us), in order: at_us  gap_us  after -> before")
+        for g, a, b, at in out:
+            if g >= args.gaps:
+                print(f"{at:9.1f} {g:7.1f}  {a} -> {b}")
 
 
 if __name__ == "__main__":
