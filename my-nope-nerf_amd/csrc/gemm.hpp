@@ -390,12 +390,27 @@ __device__ __forceinline__ void bfly_max(float (&v)[NV], int sl, int& base) {
 //   H (precision mode 2): the accumulators carry the row scales 2^(ea[row] + eb[feature])
 //        (LDS arrays lea / leb, block-local indices), undone first; the row max of the
 //        stored values is max-accumulated into lrm (LDS, float bits) for NTArgs::c_rmax.
+//   lvb (H): the column block's bias (FWD) / v (BWD) staged in LDS by the kernel; a global load
+//        issued between the stores would make its wait retire every earlier store first.
+// Diagnostic builds only (make EXTRA=-DNERF_EPI_ABLATE=...; results are wrong): 8 = no
+// output stores (a checksum per lane instead), 16 = no row / column maxima.
+#ifndef NERF_EPI_ABLATE
+#define NERF_EPI_ABLATE 0
+#endif
+constexpr int kEpiAblate = NERF_EPI_ABLATE;
+// Diagnostic builds only (EXTRA=-DNERF_EPI_STAMPS=1): phase stamps inside the NT epilogue
+#ifndef NERF_EPI_STAMPS
+#define NERF_EPI_STAMPS 0
+#endif
+constexpr bool kEpiStamps = NERF_EPI_STAMPS != 0;
+
 template <int TM, int TN, int EPI, bool H = false, bool HD = false>
 __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0, int wm0,
                                                    int wn0, uint32_t* lmask = nullptr, int mw = 0,
                                                    const int* leb = nullptr, const int* lea = nullptr,
                                                    uint32_t* lrm = nullptr, uint32_t* lcm = nullptr, int lcm_ld = 0,
-                                                   float* lhs = nullptr, const float* lhw = nullptr, int lhw_ld = 0) {
+                                                   float* lhs = nullptr, const float* lhw = nullptr, int lhw_ld = 0,
+                                                   const float* lvb = nullptr) {
     const int lane = lane_id();
     const int sl = lane & 31, hf = lane >> 5;
     int er[TM];
@@ -419,8 +434,13 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
             acc[i][j][4 * q + 3] = __builtin_amdgcn_ldexpf(acc[i][j][4 * q + 3], -(er[i] + eb.w));
         }
     };
+    float chk = 0.f;
+    auto out4 = [&](float* dst, const float4& x) {
+        if constexpr (kEpiAblate & 8) chk += x.x + x.y + x.z + x.w;
+        else store_out4(dst, x, p.store_nt);
+    };
     auto track = [&](int i, int j, int q, const float4& x) {
-        if constexpr (H) {
+        if constexpr (H && !(kEpiAblate & 16)) {
             rmx[i] = fmaxf(rmx[i], fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
             if (lcm) {
 #pragma unroll
@@ -462,7 +482,8 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
             float4 b4[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                b4[q] = p.bias ? *reinterpret_cast<const float4*>(p.bias + fb + 8 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+                b4[q] = H ? *reinterpret_cast<const float4*>(lvb + (fb - n0) + 8 * q)
+                      : p.bias ? *reinterpret_cast<const float4*>(p.bias + fb + 8 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 const size_t row = (size_t)(m0 + wm0 + 32 * i + sl);
@@ -483,7 +504,7 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
                             }
                     }
                     track(i, j, q, x);
-                    store_out4(p.c + row * p.ldc + fb + 8 * q, x, p.store_nt);
+                    out4(p.c + row * p.ldc + fb + 8 * q, x);
                     const uint32_t nib = (x.x > 0.f ? 1u : 0u) | (x.y > 0.f ? 2u : 0u) | (x.z > 0.f ? 4u : 0u) |
                                          (x.w > 0.f ? 8u : 0u);
                     w |= nib << (8 * q + 4 * hf);
@@ -515,7 +536,8 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
             float4 v4[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                v4[q] = p.u ? *reinterpret_cast<const float4*>(p.v + fb + 8 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+                v4[q] = H ? *reinterpret_cast<const float4*>(lvb + (fb - n0) + 8 * q)
+                      : p.u ? *reinterpret_cast<const float4*>(p.v + fb + 8 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 const size_t row = (size_t)(m0 + wm0 + 32 * i + sl);
@@ -530,7 +552,7 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
                     x.z = (bits & 4u) ? x.z : 0.f;
                     x.w = (bits & 8u) ? x.w : 0.f;
                     track(i, j, q, x);
-                    store_out4(p.c + row * p.ldc + fb + 8 * q, x, p.store_nt);
+                    out4(p.c + row * p.ldc + fb + 8 * q, x);
                 }
             }
         }
@@ -548,7 +570,9 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
                     if (hf == 0) lhs[(wm0 + 32 * i + sl) * 3 + c] = v;
                 }
     }
-    if constexpr (H) {
+    if constexpr (kEpiStamps) stamp(p.stamps, 4);
+    if constexpr (kEpiAblate & 8) p.c[(size_t)(m0 + wm0 + sl) * p.ldc + n0 + wn0 + hf] = chk;
+    if constexpr (H && !(kEpiAblate & 16)) {
         // the lane pair (lane, lane ^ 32) holds one row's features of this wave; the other
         // waves along N meet in LDS (non-negative floats order like their bits)
 #pragma unroll
@@ -575,6 +599,7 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
             }
         }
     }
+    if constexpr (kEpiStamps) stamp(p.stamps, 5);
 }
 
 // TN epilogue through the LDS writer: float4 slab stores.  H: undo the scales 2^(ea[row] +

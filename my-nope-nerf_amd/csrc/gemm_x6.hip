@@ -291,18 +291,16 @@ struct NTStager {
     int r0, q0;
     int ea[A_F4];                                   // H: row scale exponents of this thread's rows
     char* raw;
+    const int* lea;                                 // H: the block's row exponents (LDS)
 
-    __device__ __forceinline__ void init(const NTArgs& p, int m0, int n0, int K, char* raw_ring) {
+    __device__ __forceinline__ void init(const NTArgs& p, int m0, int n0, int K, char* raw_ring, const int* lds_ea) {
         lda1 = p.lda1; lda2 = p.lda2; k1 = p.k1; bs_rows = p.bs_rows; Kc = K / 8;
         a1b = p.a1 + (size_t)m0 * lda1;
         a2b = p.a2 ? p.a2 + (size_t)m0 * lda2 : p.a1;
         bsb = p.bs + (size_t)n0 * 8;
         r0 = threadIdx.x >> 2; q0 = threadIdx.x & 3;
         raw = raw_ring;
-        if (H) {
-#pragma unroll
-            for (int i = 0; i < A_F4; ++i) ea[i] = row_exp(a_rowmax(p, m0 + r0 + i * RSTEP));
-        }
+        lea = lds_ea;   // read after the prologue's first barrier (the kernel fills it)
     }
     __device__ __forceinline__ void dma_a(int kt, int slot) {
         const int kk = kt * XK;
@@ -350,6 +348,10 @@ struct NTStager {
         dma_b(clamp(1, nkt), smem + BUF + XImg<BM, NP>::BYTES);
         dma_wait();
         __syncthreads();
+        if (H) {
+#pragma unroll
+            for (int i = 0; i < A_F4; ++i) ea[i] = lea[r0 + i * RSTEP];
+        }
         float4 v[A_F4];
         read_slot(0, v);
         put(v, smem);
@@ -389,7 +391,8 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void k_gemm_nt_x6(NTArgs p) {
     constexpr int EPI_BYTES = DIRECT ? BM * (BN / 32) * 4 : (NT / 64) * TileLds<TN>::BYTES + (BM * (BN / 32) + BM) * 4;
     constexpr int MAIN_BYTES = LOOP_BYTES > EPI_BYTES ? LOOP_BYTES : EPI_BYTES;
     constexpr int NG = BM >= 128 ? BM / 128 : 1;                // 128-row groups of the tile
-    constexpr int SCALE_BYTES = H ? (BN + 2 * BM + NG * BN) * 4 : 0;   // leb[BN], lea[BM], lrm[BM], lcm[NG][BN]
+    // leb[BN], lea[BM], lrm[BM], lcm[NG][BN], lvb[BN] (the epilogue's bias / rank-1 v of this column block)
+    constexpr int SCALE_BYTES = H ? (2 * BN + 2 * BM + NG * BN) * 4 : 0;
     __shared__ __attribute__((aligned(16))) char smem[MAIN_BYTES + SCALE_BYTES];
     const int wave = threadIdx.x >> 6;
     const int wm0 = (wave / WN) * WTM;
@@ -401,22 +404,57 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void k_gemm_nt_x6(NTArgs p) {
     int* lea = leb + BN;
     uint32_t* lrm = reinterpret_cast<uint32_t*>(lea + BM);
     uint32_t* lcm = lrm + BM;
+    float* lvb = H ? reinterpret_cast<float*>(lcm + NG * BN) : nullptr;
 
     stamp(p.stamps, 0);
     if (H) {
-        // weight row exponents (plane 2 of the image, one int per 16-byte row chunk), row
-        // exponents of A and the output row-max accumulators; published by the prologue's
-        // first barrier
+        // Block constants in LDS, published by the prologue's first barrier: weight row
+        // exponents (plane 2 of the image, one int per 16-byte row chunk), bias (forward) / v
+        // (input gradient), row exponents of A, zeroed row / column max accumulators.  bias
+        // and v live here because a global load between the epilogue's stores would wait
+        // for them (loads and stores retire through one vmcnt in order).  All loads are
+        // issued (clamped indices, no per-element branches) before the first LDS write, so
+        // the block pays one load latency here, not one per array.
+        const float* vb = EPI == EPI_FWD ? p.bias : (p.u ? p.v : nullptr);
         const int* eimg = reinterpret_cast<const int*>(p.bs + (size_t)2 * (K / 8) * p.bs_rows * 8);
-        for (int e = threadIdx.x; e < BN; e += NT) leb[e] = eimg[(size_t)(n0 + e) * 4];
-        for (int e = threadIdx.x; e < BM; e += NT) {
-            lea[e] = row_exp(a_rowmax(p, m0 + e));
-            lrm[e] = 0u;
+        constexpr int IB = (BN + NT - 1) / NT, IA = (BM + NT - 1) / NT;
+        int ev[IB];
+        float vv[IB], av[IA];
+#pragma unroll
+        for (int i = 0; i < IB; ++i) {
+            const int e = threadIdx.x + i * NT, ec = e < BN ? e : BN - 1;
+            ev[i] = eimg[(size_t)(n0 + ec) * 4];
+            vv[i] = vb ? vb[n0 + ec] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < IA; ++i) {
+            const int e = threadIdx.x + i * NT;
+            av[i] = a_rowmax(p, m0 + (e < BM ? e : BM - 1));
+        }
+#pragma unroll
+        for (int i = 0; i < IB; ++i) {
+            const int e = threadIdx.x + i * NT;
+            if (e < BN) {
+                leb[e] = ev[i];
+                lvb[e] = vv[i];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < IA; ++i) {
+            const int e = threadIdx.x + i * NT;
+            if (e < BM) {
+                lea[e] = row_exp(av[i]);
+                lrm[e] = 0u;
+            }
         }
         for (int e = threadIdx.x; e < NG * BN; e += NT) lcm[e] = 0u;
+        // vmcnt(0) as the builtin, which the compiler's wait insertion sees (an asm wait it
+        // cannot: it would then re-wait before reusing a load's register -- after the first
+        // operand DMA, which that wait would also drain)
+        __builtin_amdgcn_s_waitcnt(0x0F70);
     }
     St st;
-    st.init(p, m0, n0, K, smem + IMG_BYTES);
+    st.init(p, m0, n0, K, smem + IMG_BYTES, lea);
     f32x16 acc[TM][TN];
     zero_acc(acc);
     if (DIRECT) {
@@ -441,7 +479,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void k_gemm_nt_x6(NTArgs p) {
             }
         }
         nt_epilogue_direct<TM, TN, EPI, H, HD>(p, acc, m0, n0, wm0, wn0, lmask, MW, leb, lea, lrm,
-                                               (H && p.c_cmax) ? lcm : nullptr, BN, lhs, lhw, BN);
+                                               (H && p.c_cmax) ? lcm : nullptr, BN, lhs, lhw, BN, lvb);
         if (gather || heads || (H && (p.c_rmax || p.c_cmax))) {
             __syncthreads();
             if (heads) {
@@ -469,6 +507,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void k_gemm_nt_x6(NTArgs p) {
                 for (int e = threadIdx.x; e < NG * BN; e += NT)
                     p.c_cmax[(size_t)(m0 / 128 + e / BN) * p.ldcm + n0 + e % BN] = __uint_as_float(lcm[e]);
         }
+        if constexpr (kEpiStamps) stamp(p.stamps, 9);
         dma_wait();      // the last (clamped) raw-A DMA lands before the workgroup's LDS is released
     } else {
         NTEpiPrefetch<BM, BN, NT, EPI> pf;
