@@ -379,6 +379,28 @@ __device__ __forceinline__ void bfly_max(float (&v)[NV], int sl, int& base) {
     }
 }
 
+// The same halving step with the partner lane read by DPP instead of ds_bpermute (no LDS
+// round trip; the move folds into the max).  CTRL pairs every lane with one that differs in
+// the STEP bit: row_mirror (r <-> 15 - r) for 8, row_half_mirror for 4, quad_perm [3,2,1,0]
+// for 2, [1,0,3,2] for 1.  A mirror also flips the lower bits, so the steps must run from the
+// high bit down (each partner then agrees on every bit already reduced, hence on the kept
+// feature set); xor 16 keeps the shuffle and can run anywhere.
+template <int HALF, int STEP, int NV>
+__device__ __forceinline__ void bfly_max_dpp(float (&v)[NV], int sl, int& base) {
+    constexpr int CTRL = STEP == 8 ? 0x140 : STEP == 4 ? 0x141 : STEP == 2 ? 0x1B : 0xB1;
+    static_assert(STEP == 8 || STEP == 4 || STEP == 2 || STEP == 1, "DPP pairing for bits 0-3 only");
+    const bool bit = (sl & STEP) != 0;
+#pragma unroll
+    for (int t = 0; t < HALF; ++t) {
+        const float keep = bit ? v[t + HALF] : v[t];
+        const float send = bit ? v[t] : v[t + HALF];
+        const float part = __builtin_bit_cast(
+            float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, send), CTRL, 0xF, 0xF, false));
+        v[t] = fmaxf(keep, part);
+    }
+    base += bit ? HALF : 0;
+}
+
 // Direct NT epilogue for the operand-swapped K loop (the MFMAs compute C^T tiles, so each
 // lane holds one sample row and, per register quad 4q..4q+3, four consecutive output
 // features 8q + 4*(lane>>5) + 0..3): float4 stores straight from the accumulators, no
@@ -584,12 +606,13 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
             // column maxima over this wave's rows: a halving butterfly over the 32 lanes of each
             // half-wave (xor 16 .. 1) leaves lane sl with features base + t; the waves along M
             // of one 128-row group meet in LDS
+            // (bits 3..0 by DPP, high bit first; bit 4 by shuffle once 2 values are left)
             int base = 0;
-            bfly_max<NV / 2, 16>(cmx, sl, base);
-            bfly_max<NV / 4, 8>(cmx, sl, base);
-            bfly_max<NV / 8, 4>(cmx, sl, base);
-            bfly_max<NV / 16, 2>(cmx, sl, base);
-            bfly_max<NV / 32, 1>(cmx, sl, base);
+            bfly_max_dpp<NV / 2, 8>(cmx, sl, base);
+            bfly_max_dpp<NV / 4, 4>(cmx, sl, base);
+            bfly_max_dpp<NV / 8, 2>(cmx, sl, base);
+            bfly_max_dpp<NV / 16, 1>(cmx, sl, base);
+            bfly_max<NV / 32, 16>(cmx, sl, base);
             constexpr int n = NV / 32 > 1 ? NV / 32 : 1;   // features left per lane
             uint32_t* g = lcm + (wm0 / 128) * lcm_ld;
 #pragma unroll
