@@ -36,8 +36,8 @@ extern "C" {
 
 /* ABI version: 5 added nerf_prof_read_kinds and nerf_render_eval_fused, 6 the 4x4-chain
  * backwards (nerf_pose_c2w_bwd, nerf_mat4_inv_bwd, nerf_mat4_mul(_bwd), nerf_unproject_matrix_bwd)
- * and the depth-prior distortion (nerf_depth_affine(_bwd)), 7 nerf_linear_fwd_heads. */
-#define NERF_HIP_ABI_VERSION 7
+ * and the depth-prior distortion (nerf_depth_affine(_bwd)), 7 nerf_linear_fwd_heads, 8 nerf_heads_bwd_mode. */
+#define NERF_HIP_ABI_VERSION 8
 int nerf_hip_abi_version(void);
 const char* nerf_hip_last_error(void);
 
@@ -233,6 +233,13 @@ int nerf_heads_bwd(const float* graw4, const float* h8, int ld8, const float* hr
                    float* dyr_rmax, float* dyr_cmax, void* stream);
 /* dyr_rmax (optional): max |dyr| per row; dyr_cmax (optional, [n_pad/128][hidden/2 padded to
  * 64], n_pad % 128 == 0): max |dyr| per column and 128-row group (mode 2 scales). */
+/* The same backward in parts (ABI 8): mode 1 writes dyr and its maxima only (h8, part unused,
+ * may be NULL), mode 2 the head-weight partials only (dyr and its maxima unused), mode 3 both
+ * (= nerf_heads_bwd).  Modes 1 and 2 together give the same results as mode 3; the training
+ * backward runs mode 2 on a side stream, off the input-gradient chain. */
+int nerf_heads_bwd_mode(int mode, const float* graw4, const float* h8, int ld8, const float* hr, int ldr,
+                        int hidden, const float* wc, float* dyr, int lddyr, float* part, int n_pad,
+                        float* dyr_rmax, float* dyr_cmax, void* stream);
 /* Reduce the heads partials into gwd[hidden], gbd[1], gwc[3][hidden/2], gbc[3]. */
 int nerf_heads_reduce(const float* part, int hidden, int n_pad, float* gwd, float* gbd,
                       float* gwc, float* gbc, int accumulate, void* stream);

@@ -226,7 +226,10 @@ __global__ __launch_bounds__(256) void k_heads_fwd(const float* __restrict__ h8,
 }
 
 // part layout per block: [wd: 64*NH][wc: 3*64*NR][bd, bc0, bc1, bc2]
-template <int NH, int NR>
+// MODE bit 0: dyr and its row / column maxima (the input-gradient chain waits for these);
+// bit 1: the head-weight / bias partials (read h8 and hr; nothing downstream waits for them
+// until the optimizer, so the backward runs them on a side stream)
+template <int NH, int NR, int MODE = 3>
 __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ graw4,
                                                    const float* __restrict__ h8, int ld8,
                                                    const float* __restrict__ hr, int ldr,
@@ -266,34 +269,44 @@ __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ gra
         for (int t = 0; t < 16; ++t) {
             const size_t s = s0 + t;
             const float4 gr = *reinterpret_cast<const float4*>(graw4 + 4 * s);
+            if constexpr (MODE & 2) {
 #pragma unroll
-            for (int q = 0; q < NH; ++q) awd[q] += gr.x * h8[s * ld8 + lane + 64 * q];
+                for (int q = 0; q < NH; ++q) awd[q] = fmaf(gr.x, h8[s * ld8 + lane + 64 * q], awd[q]);
+            }
             float dmax = 0.f;
 #pragma unroll
             for (int q = 0; q < NR; ++q) {
                 const float x = hr[s * ldr + lane + 64 * q];
-                float d = gr.y * wcr[0][q] + gr.z * wcr[1][q] + gr.w * wcr[2][q];
-                d = x > 0.f ? d : 0.f;
-                dyr[s * lddyr + lane + 64 * q] = d;
-                dmax = fmaxf(dmax, fabsf(d));
-                cm[q] = fmaxf(cm[q], fabsf(d));
-                awc[0][q] += gr.y * x;
-                awc[1][q] += gr.z * x;
-                awc[2][q] += gr.w * x;
+                if constexpr (MODE & 1) {
+                    // explicit fmas: every MODE instantiation rounds identically
+                    float d = fmaf(gr.w, wcr[2][q], fmaf(gr.z, wcr[1][q], gr.y * wcr[0][q]));
+                    d = x > 0.f ? d : 0.f;
+                    dyr[s * lddyr + lane + 64 * q] = d;
+                    dmax = fmaxf(dmax, fabsf(d));
+                    cm[q] = fmaxf(cm[q], fabsf(d));
+                }
+                if constexpr (MODE & 2) {
+                    awc[0][q] = fmaf(gr.y, x, awc[0][q]);
+                    awc[1][q] = fmaf(gr.z, x, awc[1][q]);
+                    awc[2][q] = fmaf(gr.w, x, awc[2][q]);
+                }
             }
             dm[t] = dmax;
-            abd += gr.x;
-            abc[0] += gr.y; abc[1] += gr.z; abc[2] += gr.w;
+            if constexpr (MODE & 2) {
+                abd += gr.x;
+                abc[0] += gr.y; abc[1] += gr.z; abc[2] += gr.w;
+            }
         }
-        if (dyr_rmax) {   // row maxima of dyr (row scales of GEMM precision mode 2): one butterfly per group
+        if ((MODE & 1) && dyr_rmax) {   // row maxima of dyr (row scales of GEMM precision mode 2): one butterfly per group
             const float m = reduce16<true>(dm);
             if ((lane & 3) == 0) dyr_rmax[s0 + (lane >> 2)] = m;
         }
       }
-      if (dyr_cmax)
+      if ((MODE & 1) && dyr_cmax)
 #pragma unroll
         for (int q = 0; q < NR; ++q) dyr_cmax[(size_t)ch * HR + lane + 64 * q] = cm[q];
     }
+    if constexpr (!(MODE & 2)) return;
     float* rw = red[wave];
 #pragma unroll
     for (int q = 0; q < NH; ++q) rw[lane + 64 * q] = awd[q];
@@ -918,28 +931,45 @@ extern "C" int nerf_heads_part_size(int hidden, int n_pad) {
     return heads_blocks(n_pad) * (hidden + 3 * hrw + 4);
 }
 
-extern "C" int nerf_heads_bwd(const float* graw4, const float* h8, int ld8, const float* hr, int ldr,
-                              int hidden, const float* wc, float* dyr, int lddyr, float* part,
-                              int n_pad, float* dyr_rmax, float* dyr_cmax, void* stream) {
-    NERF_CHECK_PTR(graw4); NERF_CHECK_PTR(h8); NERF_CHECK_PTR(hr); NERF_CHECK_PTR(wc);
-    NERF_CHECK_PTR(dyr); NERF_CHECK_PTR(part);
+template <int MODE>
+static int heads_bwd(const float* graw4, const float* h8, int ld8, const float* hr, int ldr, int hidden,
+                     const float* wc, float* dyr, int lddyr, float* part, int n_pad, float* dyr_rmax,
+                     float* dyr_cmax, hipStream_t s) {
+    const int hrw = hidden / 2 < 64 ? 64 : hidden / 2;
+    dim3 g(heads_blocks(n_pad)), b(256);
+#define NERF_HEADS_BWD(NH, NR) \
+    hipLaunchKernelGGL((k_heads_bwd<NH, NR, MODE>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, \
+                       n_pad, dyr_rmax, dyr_cmax)
+    if (hidden == 256 && hrw == 128) NERF_HEADS_BWD(4, 2);
+    else if (hidden == 128 && hrw == 64) NERF_HEADS_BWD(2, 1);
+    else if (hidden == 64 && hrw == 64) NERF_HEADS_BWD(1, 1);
+    else if (hidden == 512 && hrw == 256) NERF_HEADS_BWD(8, 4);
+    else NERF_CHECK(false, "heads_bwd: unsupported hidden width %d (64/128/256/512)", hidden);
+#undef NERF_HEADS_BWD
+    return check_launch("nerf_heads_bwd");
+}
+
+extern "C" int nerf_heads_bwd_mode(int mode, const float* graw4, const float* h8, int ld8, const float* hr, int ldr,
+                                   int hidden, const float* wc, float* dyr, int lddyr, float* part,
+                                   int n_pad, float* dyr_rmax, float* dyr_cmax, void* stream) {
+    NERF_CHECK(mode >= 1 && mode <= 3, "%s: mode %d (1: dyr, 2: head-weight partials, 3: both)", __func__, mode);
+    NERF_CHECK_PTR(graw4); NERF_CHECK_PTR(hr); NERF_CHECK_PTR(wc);
+    if (mode & 1) NERF_CHECK_PTR(dyr);
+    if (mode & 2) { NERF_CHECK_PTR(h8); NERF_CHECK_PTR(part); }
     NERF_CHECK_ALIGN16(graw4);
     NERF_CHECK(n_pad % 16 == 0, "%s: n_pad %% 16 != 0", __func__);
     NERF_CHECK(dyr_cmax == nullptr || n_pad % 128 == 0, "%s: dyr_cmax needs n_pad %% 128 == 0", __func__);
-    const int hrw = hidden / 2 < 64 ? 64 : hidden / 2;
     hipStream_t s = as_stream(stream);
-    dim3 g(heads_blocks(n_pad)), b(256);
-    if (hidden == 256 && hrw == 128)
-        hipLaunchKernelGGL((k_heads_bwd<4, 2>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax);
-    else if (hidden == 128 && hrw == 64)
-        hipLaunchKernelGGL((k_heads_bwd<2, 1>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax);
-    else if (hidden == 64 && hrw == 64)
-        hipLaunchKernelGGL((k_heads_bwd<1, 1>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax);
-    else if (hidden == 512 && hrw == 256)
-        hipLaunchKernelGGL((k_heads_bwd<8, 4>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax);
-    else
-        NERF_CHECK(false, "%s: unsupported hidden width %d (64/128/256/512)", __func__, hidden);
-    return check_launch(__func__);
+    if (mode == 1) return heads_bwd<1>(graw4, h8, ld8, hr, ldr, hidden, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax, s);
+    if (mode == 2) return heads_bwd<2>(graw4, h8, ld8, hr, ldr, hidden, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax, s);
+    return heads_bwd<3>(graw4, h8, ld8, hr, ldr, hidden, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax, s);
+}
+
+extern "C" int nerf_heads_bwd(const float* graw4, const float* h8, int ld8, const float* hr, int ldr,
+                              int hidden, const float* wc, float* dyr, int lddyr, float* part,
+                              int n_pad, float* dyr_rmax, float* dyr_cmax, void* stream) {
+    return nerf_heads_bwd_mode(3, graw4, h8, ld8, hr, ldr, hidden, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax,
+                               stream);
 }
 
 extern "C" int nerf_heads_reduce(const float* part, int hidden, int n_pad, float* gwd, float* gbd,

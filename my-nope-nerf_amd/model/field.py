@@ -303,30 +303,55 @@ class FieldRunner:
         if graw4 is None:
             graw4 = e(Np, 4)
             _hip.composite_bwd(st["raw4"], st["z"], R, S, flags, g_rgb, g_dist, graw4, Np)
-        # heads: d(fc_density), d(fc_rgb), dY of the colour layer
-        dyr = e(Np, HR)
-        part = e(_hip.heads_part_size(D, Np))
-        rm, cm = self._rmax_alloc(Np, dev), self._cmax_alloc(Np, dev)
-        dy_rm, dy_cm = rm(HR), cm(HR)
-        _hip.heads_bwd(graw4, h["l7"], h["lr"], D, self.wc, dyr, part, Np, dyr_rmax=dy_rm, dyr_cmax=dy_cm)
-        fcm = st.get("cmaxes", {})
-        prev_cm = {"l0": "enc_p", "l1": "l0", "l2": "l1", "l3": "l2", "l4": "l3", "l5": "l4", "l6": "l5",
-                   "l7": "l6", "lf": "l7", "lr": "lf"}
-        gwc = G(m.fc_rgb.weight) if HR == D // 2 else e(3, HR)
-        _hip.heads_reduce(part, D, Np, G(m.fc_density.weight), G(m.fc_density.bias), gwc, G(m.fc_rgb.bias))
-        if HR != D // 2:
-            G(m.fc_rgb.weight).copy_(gwc[:, :D // 2])
-
-        # encoding gradients (pose learning): enc_p reaches layers l0 and l4 (skip), enc_d the
-        # colour layer; each GEMM writes its own buffer and encode_bwd sums the two enc_p ones
-        genc = {}
-
         # walk the layers backwards; dy = gradient w.r.t. the layer's pre-activation output.
         # The weight gradients (split-K GEMM + slab reduce) of layer l depend only on dy_l and
         # the saved input, so they run on a side stream beside the dX chain: compute-bound
         # GEMM phases overlap the memory-bound reductions and each other's prologue/epilogue.
         main = torch.cuda.current_stream(dev)
         n_side = int(os.environ.get("NERF_SIDE_STREAMS", "1"))
+        if self._side is None or self._side[0].device != dev or len(self._side) != n_side:
+            prio = int(os.environ.get("NERF_SIDE_PRIORITY", "0"))
+            self._side = [torch.cuda.Stream(dev, priority=prio) for _ in range(n_side)]
+        sides = self._side
+
+        # heads: d(fc_density), d(fc_rgb), dY of the colour layer.  Only dyr (+ its maxima) is
+        # on the input-gradient chain; at the training size the head-weight partials (which
+        # re-read h8 and hr) and their reduce run on the side stream, beside dyr and the colour
+        # layer's input gradient, before that stream's first weight gradient needs dyr
+        dyr = e(Np, HR)
+        rm, cm = self._rmax_alloc(Np, dev), self._cmax_alloc(Np, dev)
+        dy_rm, dy_cm = rm(HR), cm(HR)
+        split_heads = int(os.environ.get("NERF_HEADS_SIDE", "1" if (D == 256 and Np >= 65536) else "0")) != 0
+        gw = (G(m.fc_density.weight), G(m.fc_density.bias), G(m.fc_rgb.bias))
+
+        def head_weights(mode):
+            part = e(_hip.heads_part_size(D, Np))
+            gwc = G(m.fc_rgb.weight) if HR == D // 2 else e(3, HR)
+            _hip.heads_bwd(graw4, h["l7"], h["lr"], D, self.wc, dyr if mode == 3 else None, part, Np,
+                           dyr_rmax=dy_rm if mode == 3 else None, dyr_cmax=dy_cm if mode == 3 else None, mode=mode)
+            _hip.heads_reduce(part, D, Np, gw[0], gw[1], gwc, gw[2])
+            if HR != D // 2:
+                G(m.fc_rgb.weight).copy_(gwc[:, :D // 2])
+
+        if split_heads:
+            ev = torch.cuda.Event()
+            ev.record(main)
+            sides[0].wait_event(ev)
+            for t in (graw4, h["l7"], h["lr"]):
+                t.record_stream(sides[0])
+            with torch.cuda.stream(sides[0]):
+                head_weights(2)
+            _hip.heads_bwd(graw4, None, h["lr"], D, self.wc, dyr, None, Np, dyr_rmax=dy_rm, dyr_cmax=dy_cm, mode=1)
+        else:
+            head_weights(3)
+        fcm = st.get("cmaxes", {})
+        prev_cm = {"l0": "enc_p", "l1": "l0", "l2": "l1", "l3": "l2", "l4": "l3", "l5": "l4", "l6": "l5",
+                   "l7": "l6", "lf": "l7", "lr": "lf"}
+
+        # encoding gradients (pose learning): enc_p reaches layers l0 and l4 (skip), enc_d the
+        # colour layer; each GEMM writes its own buffer and encode_bwd sums the two enc_p ones
+        genc = {}
+
         # at the training size the side stream trails the input-gradient chain by ~3 layers, and
         # the last two layers' weight gradients finish sooner on the main stream behind the chain
         # than behind two more cross-stream waits (2.60 vs 2.67 ms/step, profiles/r02/
@@ -334,10 +359,6 @@ class FieldRunner:
         tail_default = 2 if (D == 256 and Np >= 65536) else 0
         tail_main = int(os.environ.get("NERF_TAIL_MAIN", str(tail_default)))
         tail_side = int(os.environ.get("NERF_TAIL_SIDE", str(self.TAIL_SIDE)))
-        if self._side is None or self._side[0].device != dev or len(self._side) != n_side:
-            prio = int(os.environ.get("NERF_SIDE_PRIORITY", "0"))
-            self._side = [torch.cuda.Stream(dev, priority=prio) for _ in range(n_side)]
-        sides = self._side
         dy = dyr
         prev_in = {"l0": st["enc_p"], "l1": h["l0"], "l2": h["l1"], "l3": h["l2"], "l4": h["l3"],
                    "l5": h["l4"], "l6": h["l5"], "l7": h["l6"], "lf": h["l7"], "lr": h["lf"]}

@@ -441,6 +441,17 @@ def test_heads_fwd_bwd(dev, hidden):
     assert (gwc.cpu().double() - G[:, 1:].t() @ hr.double()).abs().max().item() < 1e-4 * Np
     assert (gbd.cpu().double() - G[:, 0].sum()).abs().item() < 1e-3
     assert (gbc.cpu().double() - G[:, 1:].sum(0)).abs().max().item() < 1e-3
+    # the split form the training backward uses (mode 1: dyr + maxima, mode 2: head-weight
+    # partials, h8 / dyr not passed where unused) reproduces mode 3 bit for bit
+    dyr1 = torch.full_like(dyr, 7.0)
+    rm1, cm1 = torch.full_like(dyr_rm, -1.0), torch.full_like(dyr_cm, -1.0)
+    _hip.heads_bwd(graw.to(dev), None, hr.to(dev), hidden, wc.to(dev), dyr1, None, Np, dyr_rmax=rm1, dyr_cmax=cm1,
+                   mode=1)
+    part2 = torch.full_like(part, 3.0)
+    _hip.heads_bwd(graw.to(dev), h8.to(dev), hr.to(dev), hidden, wc.to(dev), None, part2, Np, mode=2)
+    torch.cuda.synchronize()
+    assert torch.equal(dyr1, dyr) and torch.equal(rm1, dyr_rm) and torch.equal(cm1, dyr_cm)
+    assert torch.equal(part2, part)
 
 
 def test_encode_samples(dev):
