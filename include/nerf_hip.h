@@ -236,10 +236,12 @@ int nerf_heads_bwd(const float* graw4, const float* h8, int ld8, const float* hr
 /* The same backward in parts (ABI 8): mode 1 writes dyr and its maxima only (h8, part unused,
  * may be NULL), mode 2 the head-weight partials only (dyr and its maxima unused), mode 3 both
  * (= nerf_heads_bwd).  Modes 1 and 2 together give the same results as mode 3; the training
- * backward runs mode 2 on a side stream, off the input-gradient chain. */
+ * backward runs mode 2 on a side stream, off the input-gradient chain.  hr_mask (mode 1,
+ * optional): the colour layer's ReLU bits [n_pad][ldm] (bit = hr > 0, its forward's mask_out)
+ * gate dyr instead of hr, which may then be NULL (2 MB read instead of 67 MB at cfg2). */
 int nerf_heads_bwd_mode(int mode, const float* graw4, const float* h8, int ld8, const float* hr, int ldr,
-                        int hidden, const float* wc, float* dyr, int lddyr, float* part, int n_pad,
-                        float* dyr_rmax, float* dyr_cmax, void* stream);
+                        const uint32_t* hr_mask, int ldm, int hidden, const float* wc, float* dyr, int lddyr,
+                        float* part, int n_pad, float* dyr_rmax, float* dyr_cmax, void* stream);
 /* Reduce the heads partials into gwd[hidden], gbd[1], gwc[3][hidden/2], gbc[3]. */
 int nerf_heads_reduce(const float* part, int hidden, int n_pad, float* gwd, float* gbd,
                       float* gwc, float* gbc, int accumulate, void* stream);

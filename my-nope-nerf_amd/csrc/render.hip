@@ -229,10 +229,13 @@ __global__ __launch_bounds__(256) void k_heads_fwd(const float* __restrict__ h8,
 // MODE bit 0: dyr and its row / column maxima (the input-gradient chain waits for these);
 // bit 1: the head-weight / bias partials (read h8 and hr; nothing downstream waits for them
 // until the optimizer, so the backward runs them on a side stream)
-template <int NH, int NR, int MODE = 3>
+// MB (mode 1 only): the ReLU gate of dyr from the colour layer's mask bits [n][ldm] (bit =
+// hr > 0, written by its forward) instead of re-reading hr
+template <int NH, int NR, int MODE = 3, bool MB = false>
 __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ graw4,
                                                    const float* __restrict__ h8, int ld8,
                                                    const float* __restrict__ hr, int ldr,
+                                                   const uint32_t* __restrict__ hmask, int ldm,
                                                    const float* __restrict__ wc,
                                                    float* __restrict__ dyr, int lddyr,
                                                    float* __restrict__ part, int n_pad,
@@ -276,11 +279,13 @@ __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ gra
             float dmax = 0.f;
 #pragma unroll
             for (int q = 0; q < NR; ++q) {
-                const float x = hr[s * ldr + lane + 64 * q];
+                static_assert(!MB || MODE == 1, "mask-bit gate: dyr-only mode");
+                const float x = MB ? 0.f : hr[s * ldr + lane + 64 * q];
+                const bool on = MB ? ((hmask[s * ldm + ((lane + 64 * q) >> 5)] >> (lane & 31)) & 1u) != 0 : x > 0.f;
                 if constexpr (MODE & 1) {
                     // explicit fmas: every MODE instantiation rounds identically
                     float d = fmaf(gr.w, wcr[2][q], fmaf(gr.z, wcr[1][q], gr.y * wcr[0][q]));
-                    d = x > 0.f ? d : 0.f;
+                    d = on ? d : 0.f;
                     dyr[s * lddyr + lane + 64 * q] = d;
                     dmax = fmaxf(dmax, fabsf(d));
                     cm[q] = fmaxf(cm[q], fabsf(d));
@@ -931,15 +936,15 @@ extern "C" int nerf_heads_part_size(int hidden, int n_pad) {
     return heads_blocks(n_pad) * (hidden + 3 * hrw + 4);
 }
 
-template <int MODE>
-static int heads_bwd(const float* graw4, const float* h8, int ld8, const float* hr, int ldr, int hidden,
-                     const float* wc, float* dyr, int lddyr, float* part, int n_pad, float* dyr_rmax,
-                     float* dyr_cmax, hipStream_t s) {
+template <int MODE, bool MB = false>
+static int heads_bwd(const float* graw4, const float* h8, int ld8, const float* hr, int ldr, const uint32_t* hmask,
+                     int ldm, int hidden, const float* wc, float* dyr, int lddyr, float* part, int n_pad,
+                     float* dyr_rmax, float* dyr_cmax, hipStream_t s) {
     const int hrw = hidden / 2 < 64 ? 64 : hidden / 2;
     dim3 g(heads_blocks(n_pad)), b(256);
 #define NERF_HEADS_BWD(NH, NR) \
-    hipLaunchKernelGGL((k_heads_bwd<NH, NR, MODE>), g, b, 0, s, graw4, h8, ld8, hr, ldr, wc, dyr, lddyr, part, \
-                       n_pad, dyr_rmax, dyr_cmax)
+    hipLaunchKernelGGL((k_heads_bwd<NH, NR, MODE, MB>), g, b, 0, s, graw4, h8, ld8, hr, ldr, hmask, ldm, wc, dyr, \
+                       lddyr, part, n_pad, dyr_rmax, dyr_cmax)
     if (hidden == 256 && hrw == 128) NERF_HEADS_BWD(4, 2);
     else if (hidden == 128 && hrw == 64) NERF_HEADS_BWD(2, 1);
     else if (hidden == 64 && hrw == 64) NERF_HEADS_BWD(1, 1);
@@ -950,26 +955,39 @@ static int heads_bwd(const float* graw4, const float* h8, int ld8, const float* 
 }
 
 extern "C" int nerf_heads_bwd_mode(int mode, const float* graw4, const float* h8, int ld8, const float* hr, int ldr,
-                                   int hidden, const float* wc, float* dyr, int lddyr, float* part,
-                                   int n_pad, float* dyr_rmax, float* dyr_cmax, void* stream) {
+                                   const uint32_t* hr_mask, int ldm, int hidden, const float* wc, float* dyr,
+                                   int lddyr, float* part, int n_pad, float* dyr_rmax, float* dyr_cmax,
+                                   void* stream) {
     NERF_CHECK(mode >= 1 && mode <= 3, "%s: mode %d (1: dyr, 2: head-weight partials, 3: both)", __func__, mode);
-    NERF_CHECK_PTR(graw4); NERF_CHECK_PTR(hr); NERF_CHECK_PTR(wc);
+    NERF_CHECK(hr_mask == nullptr || mode == 1, "%s: the mask-bit gate (hr_mask) is for mode 1", __func__);
+    NERF_CHECK(hr_mask == nullptr || ldm * 32 >= (hidden / 2 < 64 ? 64 : hidden / 2), "%s: ldm %d too small",
+               __func__, ldm);
+    NERF_CHECK_PTR(graw4); NERF_CHECK_PTR(wc);
+    if (hr_mask == nullptr) NERF_CHECK_PTR(hr);
     if (mode & 1) NERF_CHECK_PTR(dyr);
     if (mode & 2) { NERF_CHECK_PTR(h8); NERF_CHECK_PTR(part); }
     NERF_CHECK_ALIGN16(graw4);
     NERF_CHECK(n_pad % 16 == 0, "%s: n_pad %% 16 != 0", __func__);
     NERF_CHECK(dyr_cmax == nullptr || n_pad % 128 == 0, "%s: dyr_cmax needs n_pad %% 128 == 0", __func__);
     hipStream_t s = as_stream(stream);
-    if (mode == 1) return heads_bwd<1>(graw4, h8, ld8, hr, ldr, hidden, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax, s);
-    if (mode == 2) return heads_bwd<2>(graw4, h8, ld8, hr, ldr, hidden, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax, s);
-    return heads_bwd<3>(graw4, h8, ld8, hr, ldr, hidden, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax, s);
+    if (mode == 1 && hr_mask)
+        return heads_bwd<1, true>(graw4, h8, ld8, hr, ldr, hr_mask, ldm, hidden, wc, dyr, lddyr, part, n_pad, dyr_rmax,
+                                  dyr_cmax, s);
+    if (mode == 1)
+        return heads_bwd<1>(graw4, h8, ld8, hr, ldr, nullptr, 0, hidden, wc, dyr, lddyr, part, n_pad, dyr_rmax,
+                            dyr_cmax, s);
+    if (mode == 2)
+        return heads_bwd<2>(graw4, h8, ld8, hr, ldr, nullptr, 0, hidden, wc, dyr, lddyr, part, n_pad, dyr_rmax,
+                            dyr_cmax, s);
+    return heads_bwd<3>(graw4, h8, ld8, hr, ldr, nullptr, 0, hidden, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax,
+                        s);
 }
 
 extern "C" int nerf_heads_bwd(const float* graw4, const float* h8, int ld8, const float* hr, int ldr,
                               int hidden, const float* wc, float* dyr, int lddyr, float* part,
                               int n_pad, float* dyr_rmax, float* dyr_cmax, void* stream) {
-    return nerf_heads_bwd_mode(3, graw4, h8, ld8, hr, ldr, hidden, wc, dyr, lddyr, part, n_pad, dyr_rmax, dyr_cmax,
-                               stream);
+    return nerf_heads_bwd_mode(3, graw4, h8, ld8, hr, ldr, nullptr, 0, hidden, wc, dyr, lddyr, part, n_pad, dyr_rmax,
+                               dyr_cmax, stream);
 }
 
 extern "C" int nerf_heads_reduce(const float* part, int hidden, int n_pad, float* gwd, float* gbd,

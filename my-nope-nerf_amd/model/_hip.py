@@ -73,8 +73,8 @@ _SIGS = {
     "nerf_heads_fwd": ([_c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_heads_part_size": ([_c_i, _c_i], _c_i),
     "nerf_heads_bwd": ([_c_p, _c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_p, _c_p, _c_p], _c_i),
-    "nerf_heads_bwd_mode": ([_c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_p, _c_p, _c_p],
-                            _c_i),
+    "nerf_heads_bwd_mode": ([_c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_i, _c_p, _c_i, _c_p,
+                             _c_p, _c_p], _c_i),
     "nerf_heads_reduce": ([_c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_composite_fwd": ([_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_composite_bwd": ([_c_p, _c_p, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
@@ -275,15 +275,17 @@ def heads_part_size(hidden, n_pad) -> int:
     return int(lib().nerf_heads_part_size(hidden, n_pad))
 
 
-def heads_bwd(graw4, h8, hr, hidden, wc, dyr, part, n_pad, dyr_rmax=None, dyr_cmax=None, mode=3):
-    """mode 1: dyr (+ maxima) only; 2: head-weight partials only; 3: both (nerf_heads_bwd_mode)."""
-    if mode == 3:
+def heads_bwd(graw4, h8, hr, hidden, wc, dyr, part, n_pad, dyr_rmax=None, dyr_cmax=None, mode=3, hr_mask=None):
+    """mode 1: dyr (+ maxima) only; 2: head-weight partials only; 3: both (nerf_heads_bwd_mode).
+    hr_mask (mode 1): the colour layer's ReLU bits [n][k] int32 gate dyr instead of hr."""
+    if mode == 3 and hr_mask is None:
         _call("nerf_heads_bwd", _ptr(graw4), _ptr(h8), _ld(h8), _ptr(hr), _ld(hr), hidden, _ptr(wc), _ptr(dyr),
               _ld(dyr), _ptr(part), n_pad, _ptr(dyr_rmax), _ptr(dyr_cmax), _stream())
     else:
         _call("nerf_heads_bwd_mode", int(mode), _ptr(graw4), _ptr(h8), _ld(h8) if h8 is not None else 0,
-              _ptr(hr), _ld(hr), hidden, _ptr(wc), _ptr(dyr), _ld(dyr) if dyr is not None else 0, _ptr(part),
-              n_pad, _ptr(dyr_rmax), _ptr(dyr_cmax), _stream())
+              _ptr(hr), _ld(hr) if hr is not None else 0, _ptr(hr_mask), _ld(hr_mask) if hr_mask is not None else 0,
+              hidden, _ptr(wc), _ptr(dyr), _ld(dyr) if dyr is not None else 0, _ptr(part), n_pad, _ptr(dyr_rmax),
+              _ptr(dyr_cmax), _stream())
 
 
 def heads_reduce(part, hidden, n_pad, gwd, gbd, gwc, gbc, accumulate=False):

@@ -196,7 +196,9 @@ class FieldRunner:
             x2 = segs[l.seg2] if l.seg2 else None
             k1 = l.k1
             mo = None
-            if keep and l.relu and l.name != "lr":   # ReLU bits for the backward's input masks
+            # ReLU bits for the backward's input masks (and, with the split heads backward,
+            # the colour layer's own: they gate dyr instead of a re-read of hr)
+            if keep and l.relu and (l.name != "lr" or self.heads_side(Np)):
                 mo = torch.empty(Np, l.out_p // 32, device=dev, dtype=torch.int32)
                 masks[l.name] = mo
             y_rm = rm(l.out_p)
@@ -278,6 +280,13 @@ class FieldRunner:
         return lambda width: torch.empty(Np // 128, width, device=dev, dtype=torch.float32)
 
     # ------------------------------------------------------------------ backward
+    def heads_side(self, Np: int) -> bool:
+        """Split heads backward (nerf_heads_bwd_mode): at the training size dyr alone stays on
+        the input-gradient chain, gated by the colour layer's ReLU bits, and the head-weight
+        partials run on the side stream (profiles/r02/heads_side_step_ab.txt)."""
+        default = "1" if (self.D == 256 and Np >= 65536) else "0"
+        return int(os.environ.get("NERF_HEADS_SIDE", default)) != 0
+
     def param_list(self) -> List[torch.nn.Parameter]:
         return list(self.m.parameters())
 
@@ -321,7 +330,7 @@ class FieldRunner:
         dyr = e(Np, HR)
         rm, cm = self._rmax_alloc(Np, dev), self._cmax_alloc(Np, dev)
         dy_rm, dy_cm = rm(HR), cm(HR)
-        split_heads = int(os.environ.get("NERF_HEADS_SIDE", "1" if (D == 256 and Np >= 65536) else "0")) != 0
+        split_heads = self.heads_side(Np)
         gw = (G(m.fc_density.weight), G(m.fc_density.bias), G(m.fc_rgb.bias))
 
         def head_weights(mode):
@@ -341,7 +350,9 @@ class FieldRunner:
                 t.record_stream(sides[0])
             with torch.cuda.stream(sides[0]):
                 head_weights(2)
-            _hip.heads_bwd(graw4, None, h["lr"], D, self.wc, dyr, None, Np, dyr_rmax=dy_rm, dyr_cmax=dy_cm, mode=1)
+            lr_mask = st["masks"].get("lr")   # absent when the forward ran the chain kernel
+            _hip.heads_bwd(graw4, None, h["lr"] if lr_mask is None else None, D, self.wc, dyr, None, Np,
+                           dyr_rmax=dy_rm, dyr_cmax=dy_cm, mode=1, hr_mask=lr_mask)
         else:
             head_weights(3)
         fcm = st.get("cmaxes", {})

@@ -452,6 +452,16 @@ def test_heads_fwd_bwd(dev, hidden):
     torch.cuda.synchronize()
     assert torch.equal(dyr1, dyr) and torch.equal(rm1, dyr_rm) and torch.equal(cm1, dyr_cm)
     assert torch.equal(part2, part)
+    # mode 1 gated by the colour layer's ReLU bits (bit = hr > 0, the forward's mask_out layout)
+    hb = (hr > 0).to(torch.int64).view(Np, HR // 32, 32) << torch.arange(32)
+    bits = hb.sum(-1).to(torch.int64)
+    bits = torch.where(bits >= 2 ** 31, bits - 2 ** 32, bits).to(torch.int32)
+    dyr3 = torch.full_like(dyr, 7.0)
+    rm3, cm3 = torch.full_like(dyr_rm, -1.0), torch.full_like(dyr_cm, -1.0)
+    _hip.heads_bwd(graw.to(dev), None, None, hidden, wc.to(dev), dyr3, None, Np, dyr_rmax=rm3, dyr_cmax=cm3, mode=1,
+                   hr_mask=bits.to(dev))
+    torch.cuda.synchronize()
+    assert torch.equal(dyr3, dyr) and torch.equal(rm3, dyr_rm) and torch.equal(cm3, dyr_cm)
 
 
 def test_encode_samples(dev):
