@@ -364,10 +364,12 @@ class FieldRunner:
         genc = {}
 
         # at the training size the side stream trails the input-gradient chain by ~3 layers, and
-        # the last two layers' weight gradients finish sooner on the main stream behind the chain
-        # than behind two more cross-stream waits (2.60 vs 2.67 ms/step, profiles/r02/
-        # backward_schedule_ab2.json); small batches keep everything beside the chain
-        tail_default = 2 if (D == 256 and Np >= 65536) else 0
+        # the last layers' weight gradients finish sooner on the main stream behind the chain than
+        # behind more cross-stream waits: 2 of them before the heads split (2.60 vs 2.67 ms/step,
+        # profiles/r02/backward_schedule_ab2.json), 3 since it put the head-weight partials on the
+        # side stream (2.552 vs 2.567, tail_schedule_ab_heads_side.json); small batches keep
+        # everything beside the chain
+        tail_default = 3 if (D == 256 and Np >= 65536) else 0
         tail_main = int(os.environ.get("NERF_TAIL_MAIN", str(tail_default)))
         tail_side = int(os.environ.get("NERF_TAIL_SIDE", str(self.TAIL_SIDE)))
         dy = dyr
