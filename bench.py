@@ -20,6 +20,14 @@ accumulated in f32 (bf16x6), or as a row-scaled 2-word fp16 split with three pro
 (DESIGN.md section 4, tests/test_gpu_kernels.py::test_split_accuracy); the exact-f32
 number of the same run is "value_exact_f32".
 
+Execution (--exec, default auto): on one GPU the K steps are timed twice -- enqueued eagerly
+from Python, and as one captured hipGraph of the whole step replayed K times (new rays every
+replay from the sampler's device step counter) -- and "value" is the faster; "execution",
+"ms_per_step_eager" and "ms_per_step_graph" say which and give both.  Both are the full step
+(nothing is cached or skipped); the graph only removes the host's ~1.9 ms (fast core) to
+> 3 ms (slow core) of Python enqueue per step from the timed region, which on a slow host
+is longer than the GPU's step.  N > 1 runs eager.
+
 "roofline" names the GEMM kind with the most time per step (per_kind lists all three)
 and prices it against BOTH ceilings: its MFMA work at the dense MFMA rate of the
 arithmetic that ran, and its algorithmic HBM bytes at 8 TB/s; "bound" is the ceiling
@@ -290,6 +298,9 @@ def main():
     ap.add_argument("--gemm-precision", choices=list(PRECISION), default="f16x3",
                     help="GEMM arithmetic: f32 emulated by a row-scaled 2-word fp16 split (f16x3, default), by a "
                          "3-word bf16 split (bf16x6), or the exact-f32 MFMA (f32); all f32-accurate")
+    ap.add_argument("--exec", dest="exec_mode", choices=["auto", "eager", "graph"], default="auto",
+                    help="auto (1 GPU): time the step eager AND as one replayed hipGraph, report the faster; "
+                         "N > 1 runs eager (RCCL capture is not exercised on this pool)")
     ap.add_argument("--no-alt", dest="alt", action="store_false",
                     help="skip timing the other GEMM arithmetics (reported as alt_gemm)")
     ap.add_argument("--plumbing", action="store_true",
@@ -356,8 +367,53 @@ def main():
             el_h = stats = kinds = None
         return el, ld, stats, kinds, net, el_h
 
+    def measure_graph(precision):
+        """The same K steps as ONE captured hipGraph replayed (1 GPU): the ray sampler keys on a
+        device step counter (Trainer.enable_graph_rng), so every replay trains on new rays, and
+        the whole step -- sampling, render fwd + bwd, loss, Adam -- is in the graph.  The step's
+        host enqueue (~1.9 ms on a fast host core, > 3 ms on a slow one) drops out of the timed
+        region.  Returns (seconds for K replays, loss dict) or None if capture is not possible."""
+        _hip.gemm_set_precision(precision)
+        trainer, _ = build_trainer(dev, c2w, cfg)
+        trainer.enable_graph_rng()
+        step = lambda i: trainer.train_step(data, it=i, epoch=0, scheduling_start=0)  # noqa: E731
+        try:
+            s = torch.cuda.Stream(dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                for i in range(3):
+                    step(i)
+            torch.cuda.current_stream(dev).wait_stream(s)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                out = step(0)
+        except RuntimeError as exc:    # capture unsupported here: eager only
+            log(f"graph capture failed ({exc}); eager timing only")
+            return None
+        for _ in range(args.warmup):
+            g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            g.replay()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if not math.isfinite(out["loss"].detach().item()):
+            raise RuntimeError("graph replay: non-finite loss")
+        return el, out
+
     main_prec = PRECISION[args.gemm_precision]
     elapsed, ld, (gemm_ms, gemm_launches, _, gemm_union_ms), kinds, net, elapsed_hooks = measure(main_prec)
+    elapsed_eager = elapsed
+    graph = None
+    if world == 1 and args.exec_mode in ("auto", "graph"):
+        graph = measure_graph(main_prec)
+        if graph is not None and (args.exec_mode == "graph" or graph[0] < elapsed):
+            elapsed, ld = graph
+    execution = "graph replay" if (graph is not None and elapsed == graph[0]) else "eager"
+    if args.exec_mode == "graph" and execution != "graph replay":
+        raise RuntimeError("--exec graph: capture failed")
     alt = None
     if args.alt:
         # the other GEMM arithmetics on the same workload, reported beside the headline
@@ -429,6 +485,9 @@ def main():
         exact = next((a for a in (alt or []) if a["gemm_arithmetic"] == "f32"), None)
         out = {"metric": METRIC, "value": world * RAYS / (elapsed / args.steps), "unit": "rays/s",
                "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+               "execution": execution,
+               "ms_per_step_eager": 1e3 * elapsed_eager / args.steps,
+               "ms_per_step_graph": 1e3 * graph[0] / args.steps if graph is not None else None,
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                "dtype": DTYPE[args.gemm_precision], "gemm_arithmetic": args.gemm_precision,
                "value_exact_f32": exact["value"] if exact else None,

@@ -64,20 +64,32 @@ __device__ __forceinline__ void pack_f32(const PackBatch& pb, const nerf_pack_de
 
 // Row r of the fp16 pair image of a [N][K] operand (x(c) = element (r, c)): one wave per
 // row; the row max sets the scale 2^e, planes 0 / 1 get hi / lo of x 2^e (RNE fp16 each),
-// e goes into the first word of the row's plane-2 chunk 0 (gemm_x6.hip, mode 2).
+// e goes into the first word of the row's plane-2 chunk 0 (gemm_x6.hip, mode 2).  The row
+// stays in registers between the max and the split (all its loads in flight at once: one
+// memory latency per row, not one per 64 elements and pass).
+constexpr int PACK_H_MAXK = 16 * kWave;
 template <typename F>
 __device__ __forceinline__ void put_row_h(uint16_t* img, int N, int K, int r, F&& x) {
     const int lane = lane_id();
+    float v[PACK_H_MAXK / kWave];
     float m = 0.f;
-    for (int c = lane; c < K; c += kWave) m = fmaxf(m, fabsf(x(c)));
+#pragma unroll
+    for (int i = 0; i < PACK_H_MAXK / kWave; ++i) {
+        const int c = lane + kWave * i;
+        v[i] = c < K ? x(c) : 0.f;
+        m = fmaxf(m, fabsf(v[i]));
+    }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
     const int e = row_exp(m);
     const size_t plane = (size_t)K * N;
-    for (int c = lane; c < K; c += kWave) {
-        const float v = __builtin_amdgcn_ldexpf(x(c), e);
-        const _Float16 h = (_Float16)v;
-        const _Float16 l = (_Float16)(v - (float)h);
+#pragma unroll
+    for (int i = 0; i < PACK_H_MAXK / kWave; ++i) {
+        const int c = lane + kWave * i;
+        if (c >= K) break;
+        const float y = __builtin_amdgcn_ldexpf(v[i], e);
+        const _Float16 h = (_Float16)y;
+        const _Float16 l = (_Float16)(y - (float)h);
         const size_t o = ((size_t)(c >> 3) * N + r) * 8 + (c & 7);
         img[o] = __builtin_bit_cast(uint16_t, h);
         img[o + plane] = __builtin_bit_cast(uint16_t, l);
@@ -108,8 +120,11 @@ __device__ __forceinline__ void pack_h(const nerf_pack_desc& d, int bx, int nb) 
 }
 
 // one launch for both packs: blockIdx.y = descriptor; blocks [0, PACK_F32) the padded f32
-// copies (and the bf16x3 images), blocks [PACK_F32, +PACK_H) the fp16 pair images (mode 2)
-constexpr int PACK_F32 = 64, PACK_H = 32;
+// copies (and the bf16x3 images), blocks [PACK_F32, +PACK_H) the fp16 pair images (mode 2).
+// Sized for latency, not bandwidth (a 256x256 layer is ~1.5 MB of traffic): ~2 elements per
+// thread of the f32 copies, one image row per wave (512 rows of a 256-wide layer + its
+// transpose); blocks of the small descriptors (biases, head weights) exit at once
+constexpr int PACK_F32 = 128, PACK_H = 128;
 __global__ __launch_bounds__(256) void k_pack(PackBatch pb) {
     const nerf_pack_desc& d = pb.d[blockIdx.y];
     if ((int)blockIdx.x < PACK_F32) pack_f32(pb, d, blockIdx.x, PACK_F32);
@@ -207,6 +222,7 @@ extern "C" int nerf_pack_weights(const nerf_pack_desc* descs, int n, void* strea
     NERF_CHECK(n > 0 && n <= NERF_MAX_PACK, "%s: n=%d outside 1..%d", __func__, n, NERF_MAX_PACK);
     PackBatch pb{};
     pb.n = n;
+    pb.f16 = gemm_precision() == 2;
     for (int i = 0; i < n; ++i) {
         const nerf_pack_desc& d = descs[i];
         NERF_CHECK(d.src && d.dst && d.rows > 0 && d.cols > 0 && d.ld_dst >= d.cols,
@@ -215,12 +231,14 @@ extern "C" int nerf_pack_weights(const nerf_pack_desc* descs, int n, void* strea
                    "%s: descriptor %d: rows_t < cols or ld_t < rows", __func__, i);
         NERF_CHECK(d.dst_s == nullptr || d.ld_dst % 8 == 0, "%s: descriptor %d: split image needs ld_dst %% 8 == 0",
                    __func__, i);
+        NERF_CHECK(!pb.f16 || ((d.dst_s == nullptr || d.ld_dst <= PACK_H_MAXK) &&
+                               (d.dst_ts == nullptr || d.ld_t <= PACK_H_MAXK)),
+                   "%s: descriptor %d: fp16 pair image rows longer than %d", __func__, i, PACK_H_MAXK);
         NERF_CHECK(d.dst_ts == nullptr || (d.rows_t >= d.cols && d.ld_t >= d.rows && d.ld_t % 8 == 0),
                    "%s: descriptor %d: transposed split image needs rows_t >= cols, ld_t >= rows, ld_t %% 8 == 0",
                    __func__, i);
         pb.d[i] = d;
     }
-    pb.f16 = gemm_precision() == 2;
     bool images = false;
     for (int i = 0; i < n; ++i) images = images || descs[i].dst_s != nullptr || descs[i].dst_ts != nullptr;
     const int bx = PACK_F32 + ((pb.f16 && images) ? PACK_H : 0);

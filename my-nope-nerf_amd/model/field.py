@@ -172,7 +172,7 @@ class FieldRunner:
             for i, l in enumerate(self.layers):
                 y = outs[i] if (keep or l.name in ("l7", "lr")) else None
                 mo = None
-                if keep and l.relu and l.name != "lr":
+                if keep and l.relu and (l.name != "lr" or self.heads_side(Np)):   # as the per-layer path
                     mo = torch.empty(Np, l.out_p // 32, device=dev, dtype=torch.int32)
                     masks[l.name] = mo
                 y_cm = cm(l.out_p) if l.name != "lr" else None
@@ -350,7 +350,7 @@ class FieldRunner:
                 t.record_stream(sides[0])
             with torch.cuda.stream(sides[0]):
                 head_weights(2)
-            lr_mask = st["masks"].get("lr")   # absent when the forward ran the chain kernel
+            lr_mask = st["masks"].get("lr")
             _hip.heads_bwd(graw4, None, h["lr"] if lr_mask is None else None, D, self.wc, dyr, None, Np,
                            dyr_rmax=dy_rm, dyr_cmax=dy_cm, mode=1, hr_mask=lr_mask)
         else:

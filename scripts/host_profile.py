@@ -31,6 +31,16 @@ def main():
     for i in range(5):
         step(i)
     torch.cuda.synchronize()
+    if "--plain" in sys.argv:
+        # no profiler: host enqueue time per step vs the drained (GPU-inclusive) time
+        t0 = time.perf_counter()
+        for i in range(40):
+            step(5 + i)
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        print(f"plain: enqueue {1e3 * (t1 - t0) / 40:.3f} ms/step, drained {1e3 * (t2 - t0) / 40:.3f} ms/step")
+        return
     pr = cProfile.Profile()
     t0 = time.perf_counter()
     pr.enable()
