@@ -28,6 +28,10 @@ def main():
         data, c2w = bench.synthetic_scene(dev)
         trainer, net = bench.build_trainer(dev, c2w, cfg)
         step = lambda it: trainer.train_step(data, it=it, epoch=0, scheduling_start=0)
+    if "--same-thread" in sys.argv:
+        # the autograd engine runs CUDA backwards on a worker thread, invisible to cProfile;
+        # run them on this thread so FieldRunner.backward's host time shows up
+        torch.autograd.set_multithreading_enabled(False)
     for i in range(5):
         step(i)
     torch.cuda.synchronize()
@@ -52,7 +56,7 @@ def main():
     t2 = time.perf_counter()
     print(f"enqueue {1e3 * (t1 - t0) / 20:.3f} ms/step (profiled), drained {1e3 * (t2 - t0) / 20:.3f} ms/step")
     pstats.Stats(pr).sort_stats("tottime").print_stats(30)
-    pstats.Stats(pr).sort_stats("cumulative").print_stats(40)
+    pstats.Stats(pr).sort_stats("cumulative").print_stats(60)
 
 
 if __name__ == "__main__":
