@@ -2,7 +2,7 @@
 kind (MI355X_MICROARCH.md HBM section: FETCH_SIZE is in KiB and counts half of the bytes
 of 16-B-per-lane streaming reads on gfx950 -> x2; WRITE_SIZE exact).  The passes are
 separate runs of the same command (`bench.py --steps 3 --warmup 2 --no-alt
---no-cpu-baseline` under `--kernel-include-regex 'k_gemm_(nt|tn)_x6'`); launches of one
+--no-cpu-baseline --exec eager` under `--kernel-include-regex 'k_gemm_(nt|tn)_x6'`); launches of one
 kernel are summarised by their median.
 
     python scripts/pmc_summary.py gpurun_out/r02g/pmc_fetch gpurun_out/r02g/pmc_write \\
@@ -18,12 +18,12 @@ M = 131072          # samples per cfg2 step (1024 rays x 128)
 D = 256
 # kernel template -> (GEMM kind of bench.py's roofline, algorithmic bytes per launch, note)
 KINDS = {
-    "k_gemm_nt_x6<128, 256, 2, 2, 0, true, true, 2>": (
+    "k_gemm_nt_x6<128, 256, 2, 2, 0, true, true, 2, false>": (
         "fwd", 4 * M * D * 2 + 4 * D * D + M * D / 8, "x 134.2 MB + y 134.2 MB + W 0.26 MB + ReLU bits 4.2 MB "
         "(256-wide layers; the skip layer reads 320 columns)"),
-    "k_gemm_nt_x6<128, 256, 2, 2, 1, true, true, 2>": (
+    "k_gemm_nt_x6<128, 256, 2, 2, 1, true, true, 2, false>": (
         "dx", 4 * M * D * 2 + 4 * D * D + M * D / 8, "dy 134.2 MB + dx 134.2 MB + W^T 0.26 MB + ReLU bits 4.2 MB"),
-    "k_gemm_tn_x6<256, 256, 2, 2, true>": (
+    "k_gemm_tn_x6<256, 256, 2, 2, true, 1>": (
         "dw", 4 * M * D * 2 + 4 * D * D, "dy 134.2 MB + x 134.2 MB + dW 0.26 MB; measured writes are the 256 "
         "split-K slabs (67 MB)"),
 }
