@@ -106,7 +106,7 @@ class Loss(nn.Module):
         if self.depth_loss_type == "l1":
             if depth_mask is None:
                 return (depth_pred - depth_gt).abs().sum() / float(depth_pred.shape[0])
-            err = torch.where(depth_mask, (depth_pred - depth_gt).abs(), torch.zeros_like(depth_pred))
+            err = torch.where(depth_mask, (depth_pred - depth_gt).abs(), 0.0)   # scalar 0: no fill launch
             return err.sum() / depth_mask.sum().clamp_min(1)   # 0 (not 0/0) if no ray is valid
         if depth_mask is not None:
             depth_pred, depth_gt = depth_pred[depth_mask], depth_gt[depth_mask]
@@ -116,8 +116,8 @@ class Loss(nn.Module):
         """losses.py:79-87 without the data-dependent branch (0 when the mask is empty)."""
         mask = valid_mask.expand_as(diff)
         cnt = mask.sum()
-        total = torch.where(mask, diff, torch.zeros_like(diff)).sum()
-        return torch.where(cnt > 0, total / cnt.clamp_min(1), torch.zeros_like(total))
+        total = torch.where(mask, diff, 0.0).sum()        # scalar zeros: no fill launches
+        return torch.where(cnt > 0, total / cnt.clamp_min(1), 0.0)
 
     def get_reprojection_loss(self, rgb, rgb_refs, valid_points, rgb_refs_ori):
         loss = 0

@@ -75,10 +75,10 @@ def setup(dev, capturable=False):
     opt = HipAdam(nn_model.parameters(), lr=1e-3)
     pose = mdl.LearnPose(2, True, True, cfg, init_c2w=c2w.clone()).to(dev)
     distn = mdl.Learn_Distortion(2, True, True, cfg).to(dev)
-    # train.py:100, :118; one fused kernel per optimiser (torch's fused Adam), capturable in graphs
-    fused = {"fused": True} if capturable else {}
-    opt_pose = torch.optim.Adam(pose.parameters(), lr=5e-4, capturable=capturable, **fused)
-    opt_dist = torch.optim.Adam(distn.parameters(), lr=5e-4, capturable=capturable, **fused)
+    # train.py:100, :118; one fused kernel per optimiser (torch's fused Adam: the same update as
+    # the default multi-tensor path, ~8 launches fewer per optimiser and step), capturable in graphs
+    opt_pose = torch.optim.Adam(pose.parameters(), lr=5e-4, capturable=capturable, fused=True)
+    opt_dist = torch.optim.Adam(distn.parameters(), lr=5e-4, capturable=capturable, fused=True)
     tr = mdl.Trainer(nn_model, opt, t, device=dev, optimizer_pose=opt_pose, pose_param_net=pose,
                      optimizer_distortion=opt_dist, distortion_net=distn)
     return tr, datas
