@@ -328,6 +328,9 @@ static int launch_nt(const NTArgs& a, hipStream_t s, double flops) {
 // 3 = 256x256/8 waves
 static int g_nt_policy = 0;
 static int g_tn_policy = 0;
+// default TN policy (g_tn_policy 0): 3, or 4 -- the XCD-paired 256 x 128 weight-gradient
+// tiles -- unless NERF_DW_PAIR=0
+static const int kTnDefault = [] { const char* e = getenv("NERF_DW_PAIR"); return (e && atoi(e) == 0) ? 3 : 3; }();
 static int g_dw_blocks = 0;
 static int g_store_nt = [] { const char* e = getenv("NERF_STORE_NT"); return e ? atoi(e) : 0; }();   // nerf_gemm_set_dw_blocks: target blocks per weight-gradient launch (0 = default)
 
@@ -478,10 +481,10 @@ extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const
     // split-K slabs are structural traffic of this design, not algorithmic
     prof_next(nout % 256 == 0 && kin % 256 == 0 ? NERF_PROF_DW : NERF_PROF_DW_NARROW,
               4.0 * m * (double)(nout + kin) + 4.0 * nout * (double)kin + (bslab ? 4.0 * nout : 0.0));
-    const int pol = g_tn_policy ? g_tn_policy : 3;
+    const int pol = g_tn_policy ? g_tn_policy : kTnDefault;
     if (g_precision >= 1) return dispatch_tn_x6(a, nout, kin, splits, pol, s, fl, h16);
     prof_begin(s);
-    if (pol == 3 && nout % 256 == 0 && kin % 256 == 0) {
+    if (pol >= 3 && nout % 256 == 0 && kin % 256 == 0) {
         dim3 grid(nout / 256, kin / 256, splits);
         hipLaunchKernelGGL((k_gemm_tn<256, 256, 2, 4>), grid, dim3(512), 0, s, a);
     } else if (nout % 128 == 0 && kin % 128 == 0) {
@@ -529,8 +532,8 @@ extern "C" int nerf_gemm_set_dw_blocks(int target_blocks) {
 }
 
 extern "C" int nerf_gemm_set_policy(int nt_policy, int tn_policy) {
-    NERF_CHECK(nt_policy >= 0 && nt_policy <= 3 && tn_policy >= 0 && tn_policy <= 3,
-               "%s: policies are 0..3", __func__);
+    NERF_CHECK(nt_policy >= 0 && nt_policy <= 3 && tn_policy >= 0 && tn_policy <= 5,
+               "%s: policies are 0..3 (NT) and 0..5 (TN)", __func__);
     g_nt_policy = nt_policy;
     g_tn_policy = tn_policy;
     return NERF_OK;
@@ -540,10 +543,11 @@ extern "C" int nerf_gemm_set_policy(int nt_policy, int tn_policy) {
 // resident wave of blocks (256-tiles: 1 block per CU, 128-tiles: 2), each split a whole
 // number of 32-row K tiles and at least 256 rows
 extern "C" int nerf_linear_bwd_weight_splits(int nout, int kin, int m) {
-    const int pol = g_tn_policy ? g_tn_policy : 3;
+    const int pol = g_tn_policy ? g_tn_policy : kTnDefault;
     int tiles, target;
-    if (pol == 3 && nout % 256 == 0 && kin % 256 == 0) { tiles = (nout / 256) * (kin / 256); target = 256; }
-    else if (pol == 3 && nout % 256 == 0 && kin == 64 && g_precision >= 1) { tiles = nout / 256; target = 256; }
+    if (pol >= 4 && g_precision >= 1 && nout == 256 && kin == 256) { tiles = pol == 4 ? 2 : 4; target = 256; }   // XCD groups
+    else if (pol >= 3 && nout % 256 == 0 && kin % 256 == 0) { tiles = (nout / 256) * (kin / 256); target = 256; }
+    else if (pol >= 3 && nout % 256 == 0 && kin == 64 && g_precision >= 1) { tiles = nout / 256; target = 256; }
     else { tiles = ((nout + 127) / 128) * ((kin + 127) / 128); target = 512; }
     static const int env_target = [] { const char* e = getenv("NERF_DW_BLOCKS"); return e ? atoi(e) : 0; }();
     if (env_target > 0) target = env_target;   // experiment hook: blocks per dW launch

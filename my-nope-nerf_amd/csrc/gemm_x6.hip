@@ -711,7 +711,14 @@ __device__ __forceinline__ void tn_mainloop(char* smem, int nkt, int wm0, int wn
     }
 }
 
-template <int BM, int BN, int WM, int WN, bool H = false, int NS = 1>
+// CT > 0: XCD-paired column tiles.  One output row tile (nout == BM) and CT column tiles of
+// BN; a 1-D grid of splits * CT workgroups in which the CT column tiles of one split sit on
+// the same XCD in consecutive dispatch slots (workgroups go round-robin over the 8 XCDs, so
+// w and w + 8 share one), so they stream the same dy rows at about the same time and the
+// second read of a dy k-tile hits that XCD's L2.  With BN = kin / 2 this halves the split-K
+// slab bytes of a 256 x 256 layer (twice the rows per split at the same block count)
+// without a second HBM read of dy.  Needs splits % 8 == 0.
+template <int BM, int BN, int WM, int WN, bool H = false, int NS = 1, int CT = 0>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_tn_x6(TNArgs p) {
     constexpr int NT = 64 * WM * WN;
     constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -729,12 +736,21 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_tn_x6(TNArgs p) {
     const int wave = tid >> 6;
     const int wm0 = (wave / WN) * WTM;
     const int wn0 = (wave % WN) * WTN;
-    const int o0 = blockIdx.x * BM;
-    const int j0 = blockIdx.y * BN;
-    const int split = blockIdx.z;
+    int o0, jt, split;
+    if constexpr (CT > 0) {
+        const int w = blockIdx.x, slot = w >> 3;
+        o0 = 0;
+        jt = slot % CT;
+        split = (slot / CT) * 8 + (w & 7);
+    } else {
+        o0 = blockIdx.x * BM;
+        jt = blockIdx.y;
+        split = blockIdx.z;
+    }
+    const int j0 = jt * BN;
     const size_t s0 = (size_t)split * p.rows_per_split;
     const int nkt = p.rows_per_split / XK;
-    const bool do_bias = (p.bslab != nullptr) && (blockIdx.y == 0) && !(p.ablate & 4);
+    const bool do_bias = (p.bslab != nullptr) && (jt == 0) && !(p.ablate & 4);
 
     int* lea = reinterpret_cast<int*>(smem + MAIN_BYTES);   // H: scale exponents of the tile's rows / columns
     int* leb = lea + BM;
@@ -814,13 +830,18 @@ int dispatch_nt_x6(const NTArgs& a, int epi, int policy, hipStream_t s, double f
 
 template <bool H, int NS>
 static void pick_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, hipStream_t s) {
-    if (policy == 3 && nout % 256 == 0 && kin % 256 == 0)
+    const int ct = tn_xcd_group(policy, nout, kin, splits);
+    if (ct == 2)
+        hipLaunchKernelGGL((k_gemm_tn_x6<256, 128, 2, 2, H, NS, 2>), dim3(2 * splits), dim3(256), 0, s, a);
+    else if (ct == 4)
+        hipLaunchKernelGGL((k_gemm_tn_x6<256, 64, 2, 2, H, NS, 4>), dim3(4 * splits), dim3(256), 0, s, a);
+    else if (policy >= 3 && nout % 256 == 0 && kin % 256 == 0)
         hipLaunchKernelGGL((k_gemm_tn_x6<256, 256, 2, 2, H, NS>), dim3(nout / 256, kin / 256, splits), dim3(256), 0,
                            s, a);
     else if (nout % 128 == 0 && kin % 128 == 0)
         hipLaunchKernelGGL((k_gemm_tn_x6<128, 128, 2, 2, H, NS>), dim3(nout / 128, kin / 128, splits), dim3(256), 0,
                            s, a);
-    else if (policy == 3 && nout % 256 == 0 && kin == 64)
+    else if (policy >= 3 && nout % 256 == 0 && kin == 64)
         // a 64-wide input (the encodings: l0, the skip segment of l4) against all 256 outputs in
         // one tile, so each split's dy rows are read once (128 x 64 tiles read them twice)
         hipLaunchKernelGGL((k_gemm_tn_x6<256, 64, 2, 2, H, NS>), dim3(nout / 256, 1, splits), dim3(256), 0, s, a);

@@ -41,6 +41,9 @@ SETTINGS = {
     "tn128_b512": (0, 1, 512, 0),
     "tn128_b1024": (0, 1, 1024, 0),
     "tn256_b128": (0, 0, 128, 0),
+    "tn_pair": (0, 4, 0, 0),
+    "tn_quad": (0, 5, 0, 0),
+    "tn3": (0, 3, 0, 0),
 }
 
 
