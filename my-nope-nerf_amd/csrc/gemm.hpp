@@ -56,10 +56,20 @@ struct NTArgs {
 };
 
 typedef float nt_f32x4 __attribute__((ext_vector_type(4)));
-// a float4 of the output tile: plain store, or non-temporal (streaming: the tile is not
-// read back by this kernel, the next layer reads it from HBM / the infinity cache)
-__device__ __forceinline__ void store_out4(float* dst, const float4& x, bool nt) {
-    if (nt) {
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// output store hints (nerf_gemm_set_store_hint): 0 plain, 1 non-temporal, 2 write-through
+// (sc1).  Plain and nt stores leave the line dirty in the XCD's L2, and the release at the
+// kernel boundary writes every dirty line back before the next launch on the stream may
+// start (~B / 6 TB/s on top of the ~1.8 us boundary: MI355X_MICROARCH.md, "boundary");
+// sc1 stores write through and drop the line, so the boundary has nothing left to write.
+// Mode 2 addresses through a buffer descriptor on `base` (byte offsets < 2^31: the host
+// only selects it for outputs below 2 GB).
+__device__ __forceinline__ void store_out4(float* dst, const float4& x, int hint, const float* base) {
+    if (hint == 2) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7FFFFFFF, 0x00020000);
+        const u32x4 v = {__float_as_uint(x.x), __float_as_uint(x.y), __float_as_uint(x.z), __float_as_uint(x.w)};
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)((dst - base) * 4), 0, 16);
+    } else if (hint == 1) {
         const nt_f32x4 v = {x.x, x.y, x.z, x.w};
         __builtin_nontemporal_store(v, reinterpret_cast<nt_f32x4*>(dst));
     } else {
@@ -82,6 +92,7 @@ struct TNArgs {
     int rows_per_split;
     float* slab; int ldslab; int col0; size_t slab_stride;
     float* bslab; int nout;
+    int store_hint;   // 2: slab tiles stored write-through (sc1, see store_out4), else plain
     int ablate;   // diagnostics: 1 = no slab stores, 2 = no K-loop loads, 4 = no bias column sums
     // precision mode 2: column maxima of dy and x per 128-row group ([m/128][ld]); the
     // fp16 pair kernel scales each split's columns by them
@@ -459,7 +470,7 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
     float chk = 0.f;
     auto out4 = [&](float* dst, const float4& x) {
         if constexpr (kEpiAblate & 8) chk += x.x + x.y + x.z + x.w;
-        else store_out4(dst, x, p.store_nt);
+        else store_out4(dst, x, p.store_nt, p.c);
     };
     auto track = [&](int i, int j, int q, const float4& x) {
         if constexpr (H && !(kEpiAblate & 16)) {
@@ -647,7 +658,7 @@ __device__ __forceinline__ void tn_store_lds(const TNArgs& p, f32x16 (&acc)[TM][
             v.z = __builtin_amdgcn_ldexpf(v.z, -(ea + eb.z));
             v.w = __builtin_amdgcn_ldexpf(v.w, -(ea + eb.w));
         }
-        *reinterpret_cast<float4*>(slab + (size_t)(o0 + wm0 + rl) * p.ldslab + p.col0 + j0 + wn0 + c4) = v;
+        store_out4(slab + (size_t)(o0 + wm0 + rl) * p.ldslab + p.col0 + j0 + wn0 + c4, v, p.store_hint, slab);
     });
 }
 

@@ -328,9 +328,9 @@ static int launch_nt(const NTArgs& a, hipStream_t s, double flops) {
 // 3 = 256x256/8 waves
 static int g_nt_policy = 0;
 static int g_tn_policy = 0;
-// default TN policy (g_tn_policy 0): 3, or 4 -- the XCD-paired 256 x 128 weight-gradient
-// tiles -- unless NERF_DW_PAIR=0
-static const int kTnDefault = [] { const char* e = getenv("NERF_DW_PAIR"); return (e && atoi(e) == 0) ? 3 : 3; }();
+// default TN policy (g_tn_policy 0): 3 (the XCD-grouped policies 4 / 5 measured no faster,
+// profiles/r02/dw_xcd_group_ab.txt)
+static const int kTnDefault = 3;
 static int g_dw_blocks = 0;
 static int g_store_nt = [] { const char* e = getenv("NERF_STORE_NT"); return e ? atoi(e) : 0; }();   // nerf_gemm_set_dw_blocks: target blocks per weight-gradient launch (0 = default)
 
@@ -343,7 +343,8 @@ static int dispatch_nt(const NTArgs& a, hipStream_t s, double flops) {
     if (g_precision >= 1 && a.bs != nullptr) {   // the split paths need the weight image
         NTArgs b = a;
         b.ablate = g_ablate;
-        b.store_nt = g_store_nt;
+        // sc1 stores address through a buffer descriptor: outputs below 2 GB only
+        b.store_nt = (g_store_nt == 2 && (double)a.m * a.ldc * 4.0 >= 2147483647.0) ? 0 : g_store_nt;
         b.stamps = g_stamps;
         if (g_precision == 2) {
             NERF_CHECK(a.ar1 != nullptr && (a.a2 == nullptr || a.ar2 != nullptr),
@@ -470,6 +471,7 @@ extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const
     a.rows_per_split = m / splits;
     a.slab = slab; a.ldslab = ldslab; a.col0 = col0; a.slab_stride = (size_t)nout * ldslab;
     a.bslab = bslab; a.nout = nout;
+    a.store_hint = (g_store_nt == 2 && (double)nout * ldslab * 4.0 < 2147483647.0) ? 2 : 0;   // per-split base
     a.ablate = g_ablate >> 4;
     a.cm_dy = dy_cmax; a.ldcm_dy = nout; a.cm_x = x_cmax; a.ldcm_x = kin;
     // mode 2 runs the fp16 pair kernel when the column maxima are there and every split is
@@ -521,7 +523,8 @@ extern "C" int nerf_slab_reduce(const float* slab, int splits, int nout, int lds
 }
 
 extern "C" int nerf_gemm_set_store_hint(int nontemporal) {
-    g_store_nt = nontemporal != 0;
+    NERF_CHECK(nontemporal >= 0 && nontemporal <= 2, "%s: hint %d (0 plain, 1 nt, 2 sc1)", __func__, nontemporal);
+    g_store_nt = nontemporal;
     return NERF_OK;
 }
 

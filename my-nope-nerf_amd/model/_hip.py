@@ -454,9 +454,10 @@ def gemm_set_precision(mode):
     _call("nerf_gemm_set_precision", int(mode))
 
 
-def gemm_set_store_hint(nontemporal: bool):
-    """Output-tile store hint of the split NT GEMMs (tuning knob)."""
-    _call("nerf_gemm_set_store_hint", int(bool(nontemporal)))
+def gemm_set_store_hint(hint):
+    """Output-tile store hint of the split GEMMs (tuning knob): 0 plain, 1 non-temporal,
+    2 write-through (sc1; also the weight-gradient slabs)."""
+    _call("nerf_gemm_set_store_hint", int(hint))
 
 
 def gemm_set_dw_blocks(target: int):

@@ -37,6 +37,7 @@ SETTINGS = {
     "tail2_ts2": (0, 0, 0, 0),
     "tail1_ts2": (0, 0, 0, 0),
     "store_nt": (0, 0, 0, 1),
+    "store_sc1": (0, 0, 0, 2),
     "tn128_b256": (0, 1, 256, 0),
     "tn128_b512": (0, 1, 512, 0),
     "tn128_b1024": (0, 1, 1024, 0),
