@@ -138,11 +138,11 @@ KIND_NAMES = {
 KERNEL = {
     "f16x3": {"fwd": "k_gemm_nt_x6<128,256,2,2,0,true,true,2> (fp16 pair, 3 products)",
               "dx": "k_gemm_nt_x6<128,256,2,2,1,true,true,2> (fp16 pair, 3 products)",
-              "dw": "k_gemm_tn_x6<256,256,2,2,true> (fp16 pair, 3 products)",
-              "dw_narrow": "k_gemm_tn_x6<256,64|128,128|128,64,2,2,true> (fp16 pair, 3 products)"},
+              "dw": "k_gemm_tn_x6<256,128,4,2,true,1,2> (XCD-paired column tiles, 8 waves; fp16 pair, 3 products)",
+              "dw_narrow": "k_gemm_tn_x6<256,64,4,2|128,128,2,2|128,64,2,2,true> (fp16 pair, 3 products)"},
     "bf16x6": {"fwd": "k_gemm_nt_x6<256,256,2,2,0,true> (bf16x3 split, 6 products)",
                "dx": "k_gemm_nt_x6<256,256,2,2,1,true> (bf16x3 split, 6 products)",
-               "dw": "k_gemm_tn_x6<256,256,2,2,false> (bf16x3 split, 6 products)",
+               "dw": "k_gemm_tn_x6<256,128,4,2,false,1,2> (XCD-paired column tiles; bf16x3 split, 6 products)",
                "dw_narrow": "k_gemm_tn_x6<128,64|128,2,2,false> (bf16x3 split, 6 products)"},
     "f32": {"fwd": "k_gemm_nt<256,256,2,4,0> (f32 MFMA 32x32x2)", "dx": "k_gemm_nt<256,256,2,4,1> (f32 MFMA 32x32x2)",
             "dw": "k_gemm_tn<256,256,2,4> (f32 MFMA 32x32x2)",

@@ -665,10 +665,12 @@ __device__ __forceinline__ void tn_store_lds(const TNArgs& p, f32x16 (&acc)[TM][
 // TN policies 4 / 5 (nerf_gemm_set_policy): a 256 x 256 weight gradient in the split modes runs
 // as XCD-paired 256 x 128 column tiles (k_gemm_tn_x6 CT = 2), with twice the rows per split
 // at the same block count; everything else as policy 3
-// (policy 5: four 256 x 64 column tiles per split, four times the rows per split)
+// (policy 5: four 256 x 64 column tiles per split, four times the rows per split; policy 7:
+// policy 4 with eight waves per block, two per SIMD, and the 256 x 64 tile of the 64-wide
+// inputs with eight waves too)
 inline int tn_xcd_group(int policy, int nout, int kin, int splits) {
     if (nout != 256 || kin != 256 || splits % 8 != 0) return 0;
-    return policy == 4 ? 2 : policy == 5 ? 4 : 0;
+    return (policy == 4 || policy == 7) ? 2 : policy == 5 ? 4 : 0;
 }
 
 // split-bf16 launchers (gemm_x6.hip); policy as nerf_gemm_set_policy

@@ -328,9 +328,11 @@ static int launch_nt(const NTArgs& a, hipStream_t s, double flops) {
 // 3 = 256x256/8 waves
 static int g_nt_policy = 0;
 static int g_tn_policy = 0;
-// default TN policy (g_tn_policy 0): 3 (the XCD-grouped policies 4 / 5 measured no faster,
-// profiles/r02/dw_xcd_group_ab.txt)
-static const int kTnDefault = 3;
+// default TN policy (g_tn_policy 0): 7 -- a 256 x 256 weight gradient in the split modes as
+// XCD-paired 256 x 128 column tiles of eight waves (128 splits, half the slab bytes), the
+// 64-wide inputs' 256 x 64 tile with eight waves; 87 vs 104 us per 131072 x 256 x 256 layer
+// with its slab reduce, 37 vs 44 us per 256 x 64 one (profiles/r02/dw_xcd_group_ab.txt)
+static const int kTnDefault = 7;
 static int g_dw_blocks = 0;
 static int g_store_nt = [] { const char* e = getenv("NERF_STORE_NT"); return e ? atoi(e) : 0; }();   // nerf_gemm_set_dw_blocks: target blocks per weight-gradient launch (0 = default)
 
@@ -535,8 +537,8 @@ extern "C" int nerf_gemm_set_dw_blocks(int target_blocks) {
 }
 
 extern "C" int nerf_gemm_set_policy(int nt_policy, int tn_policy) {
-    NERF_CHECK(nt_policy >= 0 && nt_policy <= 3 && tn_policy >= 0 && tn_policy <= 5,
-               "%s: policies are 0..3 (NT) and 0..5 (TN)", __func__);
+    NERF_CHECK(nt_policy >= 0 && nt_policy <= 3 && tn_policy >= 0 && tn_policy <= 7,
+               "%s: policies are 0..3 (NT) and 0..7 (TN)", __func__);
     g_nt_policy = nt_policy;
     g_tn_policy = tn_policy;
     return NERF_OK;
@@ -548,7 +550,10 @@ extern "C" int nerf_gemm_set_policy(int nt_policy, int tn_policy) {
 extern "C" int nerf_linear_bwd_weight_splits(int nout, int kin, int m) {
     const int pol = g_tn_policy ? g_tn_policy : kTnDefault;
     int tiles, target;
-    if (pol >= 4 && g_precision >= 1 && nout == 256 && kin == 256) { tiles = pol == 4 ? 2 : 4; target = 256; }   // XCD groups
+    if ((pol == 4 || pol == 5 || pol == 7) && g_precision >= 1 && nout == 256 && kin == 256) {   // XCD groups
+        tiles = pol == 5 ? 4 : 2;
+        target = 256;
+    }
     else if (pol >= 3 && nout % 256 == 0 && kin % 256 == 0) { tiles = (nout / 256) * (kin / 256); target = 256; }
     else if (pol >= 3 && nout % 256 == 0 && kin == 64 && g_precision >= 1) { tiles = nout / 256; target = 256; }
     else { tiles = ((nout + 127) / 128) * ((kin + 127) / 128); target = 512; }

@@ -1,6 +1,6 @@
 """Weight gradient of one 131072 x 256 x 256 layer (fp16 pair) + its slab reduce, per TN tile
 policy (3: 256x256 tiles, 256 splits; 4: XCD-paired 256x128 tiles, 128 splits; 5: four
-256x64 tiles per split, 64 splits), standalone and beside an input-gradient NT on a
+256x64 tiles per split, 64 splits; 7: policy 4 with 8 waves), standalone and beside an input-gradient NT on a
 second stream (the step's situation).
 
     python scripts/dw_policy_bench.py
@@ -20,7 +20,13 @@ def main():
     dev = torch.device("cuda")
     _hip.load_library()
     _hip.gemm_set_precision(2)
-    M, nout, kin = 131072, 256, 256
+    for nout, kin, pols in ((256, 256, (3, 4, 5, 7)), (256, 64, (3, 7))):
+        shape(dev, nout, kin, pols)
+    _hip.gemm_set_policy(0, 0)
+
+
+def shape(dev, nout, kin, pols):
+    M = 131072
     g = torch.Generator(device=dev).manual_seed(0)
     dy = torch.rand(M, nout, device=dev, generator=g) - 0.5
     x = torch.rand(M, kin, device=dev, generator=g) - 0.5
@@ -28,7 +34,7 @@ def main():
     dy_cm = dy.abs().view(M // 128, 128, nout).amax(1)
     x_cm = x.abs().view(M // 128, 128, kin).amax(1)
     ref = None
-    for pol in (3, 4, 5):
+    for pol in pols:
         _hip.gemm_set_policy(0, pol)
         sp = _hip.bwd_weight_splits(nout, kin, M)
         slab = torch.empty(sp * nout * kin, device=dev)
@@ -41,9 +47,8 @@ def main():
             ref = gw.clone()
         err = ((gw - ref).norm() / ref.norm()).item()
         slab_mb = sp * nout * kin * 4 / 1e6
-        print(f"policy {pol}: splits {sp:4d}  gemm {t_g:7.1f} us  reduce {t_r:6.1f} us  sum {t_g + t_r:7.1f} us  "
+        print(f"{nout}x{kin} policy {pol}: splits {sp:4d}  gemm {t_g:7.1f} us  reduce {t_r:6.1f} us  sum {t_g + t_r:7.1f} us  "
               f"slab {slab_mb:5.1f} MB  rel-diff vs policy 3 {err:.2e}", flush=True)
-    _hip.gemm_set_policy(0, 0)
 
 
 if __name__ == "__main__":

@@ -23,6 +23,10 @@ KINDS = {
         "(256-wide layers; the skip layer reads 320 columns)"),
     "k_gemm_nt_x6<128, 256, 2, 2, 1, true, true, 2, false>": (
         "dx", 4 * M * D * 2 + 4 * D * D + M * D / 8, "dy 134.2 MB + dx 134.2 MB + W^T 0.26 MB + ReLU bits 4.2 MB"),
+    "k_gemm_tn_x6<256, 128, 4, 2, true, 1, 2>": (
+        "dw", 4 * M * D * 2 + 4 * D * D, "dy 134.2 MB + x 134.2 MB + dW 0.26 MB; one launch is both XCD-paired "
+        "256 x 128 column tiles, so dy is fetched by two blocks of one XCD; measured writes are the 128 split-K "
+        "slabs (33.6 MB)"),
     "k_gemm_tn_x6<256, 256, 2, 2, true, 1>": (
         "dw", 4 * M * D * 2 + 4 * D * D, "dy 134.2 MB + x 134.2 MB + dW 0.26 MB; measured writes are the 256 "
         "split-K slabs (67 MB)"),

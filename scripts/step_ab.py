@@ -44,6 +44,7 @@ SETTINGS = {
     "tn256_b128": (0, 0, 128, 0),
     "tn_pair": (0, 4, 0, 0),
     "tn_quad": (0, 5, 0, 0),
+    "tn_pair8": (0, 7, 0, 0),
     "tn3": (0, 3, 0, 0),
 }
 

@@ -103,8 +103,18 @@ def test_pose_and_distortion_modules_match_oracle():
 def test_dw_split_policy():
     from model import _hip
     _hip.load_library()
-    assert _hip.bwd_weight_splits(256, 256, 131072) == 256
+    assert _hip.bwd_weight_splits(256, 256, 131072) == 256     # exact f32: 256 x 256 tiles
     assert _hip.bwd_weight_splits(128, 256, 131072) == 256
+    # split modes, default TN policy 7: XCD-paired 256 x 128 column tiles, 2 blocks per split
+    _hip.gemm_set_precision(2)
+    try:
+        assert _hip.bwd_weight_splits(256, 256, 131072) == 128
+        assert _hip.bwd_weight_splits(256, 64, 131072) == 256
+        _hip.gemm_set_policy(0, 3)
+        assert _hip.bwd_weight_splits(256, 256, 131072) == 256
+    finally:
+        _hip.gemm_set_policy(0, 0)
+        _hip.gemm_set_precision(0)
     for m in (128, 1024, 16384, 131072, 131072 + 128):
         for nout, kin in ((256, 256), (128, 256), (256, 64), (64, 64)):
             s = _hip.bwd_weight_splits(nout, kin, m)
