@@ -667,10 +667,10 @@ __device__ __forceinline__ void tn_store_lds(const TNArgs& p, f32x16 (&acc)[TM][
 // at the same block count; everything else as policy 3
 // (policy 5: four 256 x 64 column tiles per split, four times the rows per split; policy 7:
 // policy 4 with eight waves per block, two per SIMD, and the 256 x 64 tile of the 64-wide
-// inputs with eight waves too)
+// inputs with eight waves too; policy 8: policy 7 with the 128-output tiles at eight waves)
 inline int tn_xcd_group(int policy, int nout, int kin, int splits) {
     if (nout != 256 || kin != 256 || splits % 8 != 0) return 0;
-    return (policy == 4 || policy == 7) ? 2 : policy == 5 ? 4 : 0;
+    return (policy == 4 || policy == 7 || policy == 8) ? 2 : policy == 5 ? 4 : 0;
 }
 
 // split-bf16 launchers (gemm_x6.hip); policy as nerf_gemm_set_policy

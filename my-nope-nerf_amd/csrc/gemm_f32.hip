@@ -537,8 +537,8 @@ extern "C" int nerf_gemm_set_dw_blocks(int target_blocks) {
 }
 
 extern "C" int nerf_gemm_set_policy(int nt_policy, int tn_policy) {
-    NERF_CHECK(nt_policy >= 0 && nt_policy <= 3 && tn_policy >= 0 && tn_policy <= 7,
-               "%s: policies are 0..3 (NT) and 0..7 (TN)", __func__);
+    NERF_CHECK(nt_policy >= 0 && nt_policy <= 3 && tn_policy >= 0 && tn_policy <= 8,
+               "%s: policies are 0..3 (NT) and 0..8 (TN)", __func__);
     g_nt_policy = nt_policy;
     g_tn_policy = tn_policy;
     return NERF_OK;
@@ -550,7 +550,7 @@ extern "C" int nerf_gemm_set_policy(int nt_policy, int tn_policy) {
 extern "C" int nerf_linear_bwd_weight_splits(int nout, int kin, int m) {
     const int pol = g_tn_policy ? g_tn_policy : kTnDefault;
     int tiles, target;
-    if ((pol == 4 || pol == 5 || pol == 7) && g_precision >= 1 && nout == 256 && kin == 256) {   // XCD groups
+    if (pol >= 4 && g_precision >= 1 && nout == 256 && kin == 256) {   // XCD groups
         tiles = pol == 5 ? 4 : 2;
         target = 256;
     }

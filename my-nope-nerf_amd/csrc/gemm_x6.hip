@@ -831,7 +831,7 @@ int dispatch_nt_x6(const NTArgs& a, int epi, int policy, hipStream_t s, double f
 template <bool H, int NS>
 static void pick_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, hipStream_t s) {
     const int ct = tn_xcd_group(policy, nout, kin, splits);
-    if (ct == 2 && policy == 7)   // eight waves (two per SIMD), 64 x 64 per wave
+    if (ct == 2 && policy >= 7)   // eight waves (two per SIMD), 64 x 64 per wave
         hipLaunchKernelGGL((k_gemm_tn_x6<256, 128, 4, 2, H, NS, 2>), dim3(2 * splits), dim3(512), 0, s, a);
     else if (ct == 2)
         hipLaunchKernelGGL((k_gemm_tn_x6<256, 128, 2, 2, H, NS, 2>), dim3(2 * splits), dim3(256), 0, s, a);
@@ -840,15 +840,21 @@ static void pick_tn_x6(const TNArgs& a, int nout, int kin, int splits, int polic
     else if (policy >= 3 && nout % 256 == 0 && kin % 256 == 0)
         hipLaunchKernelGGL((k_gemm_tn_x6<256, 256, 2, 2, H, NS>), dim3(nout / 256, kin / 256, splits), dim3(256), 0,
                            s, a);
+    else if (policy == 8 && nout % 128 == 0 && kin % 128 == 0)   // eight waves, 32 x 64 per wave
+        hipLaunchKernelGGL((k_gemm_tn_x6<128, 128, 4, 2, H, NS>), dim3(nout / 128, kin / 128, splits), dim3(512), 0,
+                           s, a);
     else if (nout % 128 == 0 && kin % 128 == 0)
         hipLaunchKernelGGL((k_gemm_tn_x6<128, 128, 2, 2, H, NS>), dim3(nout / 128, kin / 128, splits), dim3(256), 0,
                            s, a);
-    else if (policy == 7 && nout % 256 == 0 && kin == 64)   // eight waves, 64 x 32 per wave
+    else if (policy >= 7 && nout % 256 == 0 && kin == 64)   // eight waves, 64 x 32 per wave
         hipLaunchKernelGGL((k_gemm_tn_x6<256, 64, 4, 2, H, NS>), dim3(nout / 256, 1, splits), dim3(512), 0, s, a);
     else if (policy >= 3 && nout % 256 == 0 && kin == 64)
         // a 64-wide input (the encodings: l0, the skip segment of l4) against all 256 outputs in
         // one tile, so each split's dy rows are read once (128 x 64 tiles read them twice)
         hipLaunchKernelGGL((k_gemm_tn_x6<256, 64, 2, 2, H, NS>), dim3(nout / 256, 1, splits), dim3(256), 0, s, a);
+    else if (policy == 8 && nout % 128 == 0)   // eight waves, 32 x 32 per wave
+        hipLaunchKernelGGL((k_gemm_tn_x6<128, 64, 4, 2, H, NS>), dim3(nout / 128, kin / 64, splits), dim3(512), 0, s,
+                           a);
     else if (nout % 128 == 0)
         hipLaunchKernelGGL((k_gemm_tn_x6<128, 64, 2, 2, H, NS>), dim3(nout / 128, kin / 64, splits), dim3(256), 0, s,
                            a);

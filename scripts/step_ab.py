@@ -28,6 +28,7 @@ SETTINGS = {
     "side2": (0, 0, 0, 0),
     "tail2": (0, 0, 0, 0),
     "tail3": (0, 0, 0, 0),
+    "tail4": (0, 0, 0, 0),
     "side2_tail2": (0, 0, 0, 0),
     "tside2": (0, 0, 0, 0),
     "tside3": (0, 0, 0, 0),
@@ -45,6 +46,7 @@ SETTINGS = {
     "tn_pair": (0, 4, 0, 0),
     "tn_quad": (0, 5, 0, 0),
     "tn_pair8": (0, 7, 0, 0),
+    "tn_narrow8": (0, 8, 0, 0),
     "tn3": (0, 3, 0, 0),
 }
 
@@ -73,7 +75,7 @@ def main():
         trainers[name].train_step(data, it=0, epoch=0, scheduling_start=0)
     os.environ.pop("NERF_SIDE_PRIORITY", None)
     # backward schedule (field.py): weight-gradient side streams / layers whose dW runs on main
-    SCHED = {"old_default": ("1", "0", "0"), "side2": ("2", "0", "0"), "tail2": ("1", "2", "0"), "tail3": ("1", "3", "0"),
+    SCHED = {"old_default": ("1", "0", "0"), "side2": ("2", "0", "0"), "tail2": ("1", "2", "0"), "tail3": ("1", "3", "0"), "tail4": ("1", "4", "0"),
              "side2_tail2": ("2", "2", "0"), "tside2": ("1", "0", "2"), "tside3": ("1", "0", "3"),
              "tside4": ("1", "0", "4"), "tail1": ("1", "1", "0"), "tail2_ts1": ("1", "2", "1"),
              "tail2_ts2": ("1", "2", "2"), "tail1_ts2": ("1", "1", "2")}

@@ -153,7 +153,7 @@ def test_linear_bwd_data(dev, gemm_precision):
 @pytest.mark.parametrize("nout,kin,m,splits", [(256, 256, 4096, 8), (128, 320, 2048, 4), (256, 64, 1024, 1),
                                                (256, 320, 32768, 64), (128, 256, 12288, 48),
                                                (64, 128, 2048, 2)])
-@pytest.mark.parametrize("tn_policy", [3, 4, 5, 7])
+@pytest.mark.parametrize("tn_policy", [3, 4, 5, 7, 8])
 def test_linear_bwd_weight_and_reduce(dev, gemm_precision, nout, kin, m, splits, tn_policy):
     """Weight gradient + slab reduce vs fp64; TN policy 4 runs the 256 x 256 cases (the
     256-wide segment of the 320-wide one too) as XCD-paired 256 x 128 column tiles."""
