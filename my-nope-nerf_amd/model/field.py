@@ -375,9 +375,11 @@ class FieldRunner:
         # the last layers' weight gradients finish sooner on the main stream behind the chain than
         # behind more cross-stream waits: 2 of them before the heads split (2.60 vs 2.67 ms/step,
         # profiles/r02/backward_schedule_ab2.json), 3 since it put the head-weight partials on the
-        # side stream (2.552 vs 2.567, tail_schedule_ab_heads_side.json); small batches keep
-        # everything beside the chain
-        tail_default = 3 if (D == 256 and Np >= 65536) else 0
+        # side stream (2.552 vs 2.567, tail_schedule_ab_heads_side.json), 2 again since the faster
+        # XCD-paired weight-gradient tiles (TN policy 7) let the side stream keep up (2.575 vs
+        # 2.602 and 2.535 vs 2.539, tail_schedule_ab_policy7.txt); small batches keep everything
+        # beside the chain
+        tail_default = 2 if (D == 256 and Np >= 65536) else 0
         tail_main = int(os.environ.get("NERF_TAIL_MAIN", str(tail_default)))
         tail_side = int(os.environ.get("NERF_TAIL_SIDE", str(self.TAIL_SIDE)))
         dy = dyr
