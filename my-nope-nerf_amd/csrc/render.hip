@@ -330,6 +330,66 @@ __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ gra
         part[(size_t)blockIdx.x * PART + e] = red[0][e] + red[1][e] + red[2][e] + red[3][e];
 }
 
+// MODE 1 alone (dyr + its maxima, on the input-gradient chain): one block per 128-row chunk,
+// each wave two 16-sample groups, the chunk's column maxima combined over the 4 waves in LDS.
+// k_heads_bwd<.., 1, ..> gives a wave a whole chunk (1024 waves at cfg2, one per SIMD): its
+// store stream then waits on one load latency per group; here 4x the waves are resident.  The
+// arithmetic is k_heads_bwd's (same fmas, maxima are order-free), so dyr is bit-identical.
+template <int NR, bool MB>
+__global__ __launch_bounds__(256) void k_heads_dyr(const float* __restrict__ graw4,
+                                                   const float* __restrict__ hr, int ldr,
+                                                   const uint32_t* __restrict__ hmask, int ldm,
+                                                   const float* __restrict__ wc,
+                                                   float* __restrict__ dyr, int lddyr,
+                                                   float* __restrict__ dyr_rmax, float* __restrict__ dyr_cmax) {
+    constexpr int HR = 64 * NR;
+    __shared__ float lcm[4][HR];
+    const int lane = lane_id();
+    const int wave = threadIdx.x >> 6;
+    const size_t ch = blockIdx.x;
+    float wcr[3][NR], cm[NR];
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+        wcr[0][q] = wc[lane + 64 * q];
+        wcr[1][q] = wc[HR + lane + 64 * q];
+        wcr[2][q] = wc[2 * HR + lane + 64 * q];
+        cm[q] = 0.f;
+    }
+#pragma unroll
+    for (int gg = 0; gg < 2; ++gg) {
+        const size_t s0 = (ch * 8 + 2 * wave + gg) * 16;
+        float dm[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const size_t s = s0 + t;
+            const float4 gr = *reinterpret_cast<const float4*>(graw4 + 4 * s);
+            float dmax = 0.f;
+#pragma unroll
+            for (int q = 0; q < NR; ++q) {
+                const bool on = MB ? ((hmask[s * ldm + ((lane + 64 * q) >> 5)] >> (lane & 31)) & 1u) != 0
+                                   : hr[s * ldr + lane + 64 * q] > 0.f;
+                float d = fmaf(gr.w, wcr[2][q], fmaf(gr.z, wcr[1][q], gr.y * wcr[0][q]));
+                d = on ? d : 0.f;
+                dyr[s * lddyr + lane + 64 * q] = d;
+                dmax = fmaxf(dmax, fabsf(d));
+                cm[q] = fmaxf(cm[q], fabsf(d));
+            }
+            dm[t] = dmax;
+        }
+        if (dyr_rmax) {
+            const float m = reduce16<true>(dm);
+            if ((lane & 3) == 0) dyr_rmax[s0 + (lane >> 2)] = m;
+        }
+    }
+    if (dyr_cmax) {
+#pragma unroll
+        for (int q = 0; q < NR; ++q) lcm[wave][lane + 64 * q] = cm[q];
+        __syncthreads();
+        for (int e = threadIdx.x; e < HR; e += blockDim.x)
+            dyr_cmax[ch * HR + e] = fmaxf(fmaxf(lcm[0][e], lcm[1][e]), fmaxf(lcm[2][e], lcm[3][e]));
+    }
+}
+
 // sum the per-block partials: a block per 64 partial elements, its 4 waves split the block
 // range and combine through LDS
 __global__ __launch_bounds__(256) void k_heads_reduce(const float* __restrict__ part, int nblocks, int H, int HR,
@@ -941,6 +1001,17 @@ static int heads_bwd(const float* graw4, const float* h8, int ld8, const float* 
                      int ldm, int hidden, const float* wc, float* dyr, int lddyr, float* part, int n_pad,
                      float* dyr_rmax, float* dyr_cmax, hipStream_t s) {
     const int hrw = hidden / 2 < 64 ? 64 : hidden / 2;
+    if (MODE == 1 && n_pad % 128 == 0) {   // dyr only: a block per 128-row chunk
+#define NERF_HEADS_DYR(NR) \
+        hipLaunchKernelGGL((k_heads_dyr<NR, MB>), dim3(n_pad / 128), dim3(256), 0, s, graw4, hr, ldr, hmask, ldm, wc, \
+                           dyr, lddyr, dyr_rmax, dyr_cmax)
+        if (hrw == 128) NERF_HEADS_DYR(2);
+        else if (hrw == 64) NERF_HEADS_DYR(1);
+        else if (hrw == 256) NERF_HEADS_DYR(4);
+        else NERF_CHECK(false, "heads_bwd: unsupported hidden width %d (64/128/256/512)", hidden);
+#undef NERF_HEADS_DYR
+        return check_launch("nerf_heads_bwd (dyr)");
+    }
     dim3 g(heads_blocks(n_pad)), b(256);
 #define NERF_HEADS_BWD(NH, NR) \
     hipLaunchKernelGGL((k_heads_bwd<NH, NR, MODE, MB>), g, b, 0, s, graw4, h8, ld8, hr, ldr, hmask, ldm, wc, dyr, \
