@@ -139,13 +139,17 @@ int nerf_slab_reduce(const float* slab, int splits, int nout, int ldslab, int no
 
 /* GEMM tile policy (tuning knob; 0 = built-in default).  nt: 1 = 128x128 / 4 waves,
  * 2 = 128x256 / 8 waves, 3 = 256x256 / 8 waves;  tn (weight gradient): 1 = 128x128,
- * 3 = 256x256 / 8 waves. */
+ * 3 = 256x256 / 8 waves (split modes: 4 waves), and in the split modes for 256 x 256
+ * layers: 4 = XCD-paired 256x128 column tiles (4 waves), 5 = four 256x64 column tiles,
+ * 7 (default) = 4 with 8 waves (+ the 64-wide inputs' 256x64 tile at 8 waves), 8 = 7 with
+ * the 128-output tiles at 8 waves.  The default changes nerf_linear_bwd_weight_splits. */
 int nerf_gemm_set_policy(int nt_policy, int tn_policy);
 /* Weight-gradient split-K target (tuning knob; 0 = built-in default): about this many
  * blocks per nerf_linear_bwd_weight launch, as nerf_linear_bwd_weight_splits picks them. */
 int nerf_gemm_set_dw_blocks(int target_blocks);
 /* Output-tile store hint of the split NT GEMMs (tuning knob; default 0 = plain stores,
- * 1 = non-temporal).  NERF_STORE_NT in the environment sets the initial value. */
+ * 1 = non-temporal, 2 = write-through sc1, the weight-gradient slabs too).  NERF_STORE_NT
+ * in the environment sets the initial value. */
 int nerf_gemm_set_store_hint(int nontemporal);
 
 /* f32 arithmetic of the GEMM family (process-wide; default 0):
