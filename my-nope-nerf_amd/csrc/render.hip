@@ -48,6 +48,25 @@ __device__ __forceinline__ void enc_copy_out(const float* lds, float* dst, size_
     }
 }
 
+// the view-direction encodings of the block's rays (one LDS record per ray, slot r - r0) ->
+// rows m0 .. m0 + 127 of the [n][64] enc_d: every sample row repeats its ray's record, rows
+// past the last sample are zeros
+__device__ __forceinline__ void enc_copy_out_rays(const float* rec, float* dst, size_t m0, int S, int r0,
+                                                  int total) {
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+        const int idx = it * ENC_ROWS + threadIdx.x;
+        const int row = idx >> 4, c4 = (idx & 15) * 4;
+        const int s = (int)m0 + row;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (s < total) {
+            const float* src = rec + (s / S - r0) * ENC_LD + c4;
+            v = make_float4(src[0], src[1], src[2], src[3]);
+        }
+        *reinterpret_cast<float4*>(dst + (m0 + row) * 64 + c4) = v;
+    }
+}
+
 __global__ __launch_bounds__(ENC_ROWS) void k_encode_samples(const float* __restrict__ po, const float* __restrict__ pd,
                                  const float* __restrict__ view, const float* __restrict__ noise,
                                  int R, int S, int n_pad, float nz, float fz,
@@ -58,6 +77,7 @@ __global__ __launch_bounds__(ENC_ROWS) void k_encode_samples(const float* __rest
     static_assert(ENC_P == 64 && ENC_D == 64, "row copies assume 64-wide encodings");
     __shared__ float rows[ENC_ROWS * ENC_LD];
     __shared__ float wm[2][6];
+    __shared__ float lmd[ENC_ROWS];   // max |enc_d| per ray slot
     const size_t m0 = (size_t)blockIdx.x * ENC_ROWS;
     const int s = (int)m0 + threadIdx.x;
     const int total = R * S;
@@ -93,12 +113,19 @@ __global__ __launch_bounds__(ENC_ROWS) void k_encode_samples(const float* __rest
     __syncthreads();
     enc_copy_out(rows, enc_p, m0);
     __syncthreads();
-    float md = 0.f;
-    if (live) md = encode3_lds<4, ENC_D>(v, lrow);
-    else for (int c = 0; c < ENC_D; ++c) lrow[c] = 0.f;
-    if (s < n_pad && rmax_d) rmax_d[s] = md;
+    // the view-direction encoding is per ray (official_nerf.py:87 encodes the ray's direction,
+    // repeated over its samples): the block's first sample of each ray encodes it once into
+    // that ray's LDS record (slot r - r0 < 128), the copy-out repeats it per sample row --
+    // the same sincosf on the same input, so enc_d is bit-identical to a per-sample encode
+    const int r0 = (int)(m0 / (size_t)S);
+    if (live && (s % S == 0 || threadIdx.x == 0)) {
+        const int slot = s / S - r0;
+        lmd[slot] = encode3_lds<4, ENC_D>(v, rows + slot * ENC_LD);
+    }
     __syncthreads();
-    enc_copy_out(rows, enc_d, m0);
+    const float md = live ? lmd[s / S - r0] : 0.f;
+    if (s < n_pad && rmax_d) rmax_d[s] = md;
+    enc_copy_out_rays(rows, enc_d, m0, S, r0, total);
     if (cmax_p != nullptr) {
         // per 128-row group (this block): exact max of the coordinate columns (wave max, then
         // the two waves in LDS), 1 for the sin / cos columns (|sin|, |cos| <= 1), 0 for the pad

@@ -475,8 +475,10 @@ def test_heads_fwd_bwd(dev, hidden):
     assert torch.equal(dyr3, dyr) and torch.equal(rm3, dyr_rm) and torch.equal(cm3, dyr_cm)
 
 
-def test_encode_samples(dev):
-    R, S = 33, 64
+@pytest.mark.parametrize("R,S", [(33, 64), (7, 200), (29, 48)])
+def test_encode_samples(dev, R, S):
+    """Samples / encodings vs the oracle; S = 200 and 48 put ray boundaries inside the
+    128-row blocks (the view-direction encoding is computed once per ray of a block)."""
     g = torch.Generator().manual_seed(7)
     o = _rand(R, 3, g=g) * 3
     d = torch.nn.functional.normalize(_rand(R, 3, g=g), dim=-1)
@@ -502,7 +504,8 @@ def test_encode_samples(dev):
     assert (ep.cpu()[:R * S, :63] - ref_p).abs().max().item() < 2e-6
     assert (ed.cpu()[:R * S, :27] - ref_d).abs().max().item() < 2e-6
     assert ep.cpu()[:, 63].abs().max().item() == 0 and ed.cpu()[:, 27:].abs().max().item() == 0
-    assert ep.cpu()[R * S:].abs().max().item() == 0
+    if Np > R * S:
+        assert ep.cpu()[R * S:].abs().max().item() == 0 and ed.cpu()[R * S:].abs().max().item() == 0
     assert torch.equal(rp, ep.abs().amax(1)) and torch.equal(rd, ed.abs().amax(1))
     # column bounds per 128-row group: exact on the coordinates, >= the sin / cos maxima, 0 on the pad
     for c, e in ((cp, ep), (cd, ed)):
