@@ -394,7 +394,10 @@ class FieldRunner:
             W = l.linear.weight
             nout_ref, kin_ref = W.shape
             k1 = l.k1
-            splits = _hip.bwd_weight_splits(l.out_p, k1, Np)
+            # a layer with a 64-wide second segment (l4's skip input) shares one split count over
+            # both launches; NERF_SEG2_SPLITS=1 sizes it for the 64-wide launch (A/B knob)
+            seg2_splits = l.seg2 and os.environ.get("NERF_SEG2_SPLITS", "0") == "1"
+            splits = _hip.bwd_weight_splits(l.out_p, 64 if seg2_splits else k1, Np)
             slab = e(splits * l.out_p * l.kp)
             bslab = e(splits * l.out_p)
             _hip.linear_bwd_weight(dy, l.out_p, x_in, k1, Np, splits, slab, l.kp, 0, bslab, dy_cmax=dy_cm,

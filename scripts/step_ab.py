@@ -46,6 +46,7 @@ SETTINGS = {
     "tn_pair": (0, 4, 0, 0),
     "tn_quad": (0, 5, 0, 0),
     "tn_pair8": (0, 7, 0, 0),
+    "seg2_splits": (0, 0, 0, 0),
     "tn_narrow8": (0, 8, 0, 0),
     "tn3": (0, 3, 0, 0),
 }
@@ -88,6 +89,10 @@ def main():
             else:   # the library defaults
                 for k in ("NERF_SIDE_STREAMS", "NERF_TAIL_MAIN", "NERF_TAIL_SIDE"):
                     os.environ.pop(k, None)
+            if name == "seg2_splits":
+                os.environ["NERF_SEG2_SPLITS"] = "1"
+            else:
+                os.environ.pop("NERF_SEG2_SPLITS", None)
             nt, tn, blocks, snt = SETTINGS[name]
             _hip.gemm_set_policy(nt, tn)
             _hip.gemm_set_dw_blocks(blocks)
