@@ -537,8 +537,8 @@ extern "C" int nerf_gemm_set_dw_blocks(int target_blocks) {
 }
 
 extern "C" int nerf_gemm_set_policy(int nt_policy, int tn_policy) {
-    NERF_CHECK(nt_policy >= 0 && nt_policy <= 3 && tn_policy >= 0 && tn_policy <= 8,
-               "%s: policies are 0..3 (NT) and 0..8 (TN)", __func__);
+    NERF_CHECK(nt_policy >= 0 && nt_policy <= 3 && tn_policy >= 0 && tn_policy <= 8 && tn_policy != 6,
+               "%s: policies are 0..3 (NT) and 0..5, 7, 8 (TN)", __func__);
     g_nt_policy = nt_policy;
     g_tn_policy = tn_policy;
     return NERF_OK;

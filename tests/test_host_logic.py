@@ -112,6 +112,9 @@ def test_dw_split_policy():
         assert _hip.bwd_weight_splits(256, 64, 131072) == 256
         _hip.gemm_set_policy(0, 3)
         assert _hip.bwd_weight_splits(256, 256, 131072) == 256
+        for bad in (6, 9, -1):
+            with pytest.raises(RuntimeError):
+                _hip.gemm_set_policy(0, bad)
     finally:
         _hip.gemm_set_policy(0, 0)
         _hip.gemm_set_precision(0)
