@@ -41,6 +41,7 @@ import argparse
 import json
 import math
 import os
+import statistics
 import sys
 import time
 
@@ -63,7 +64,7 @@ def log(*a):
 
 
 def make_cfg():
-    from tests.helpers import make_cfg as mk
+    from model.synthetic import make_cfg as mk
     cfg = mk(hidden=HIDDEN, S=SAMPLES)
     t = cfg["training"]
     t["n_training_points"] = RAYS
@@ -74,23 +75,8 @@ def make_cfg():
 
 def synthetic_scene(dev, seed=0):
     """V_KITTI-shaped data dict (dataset.py:281-364 keys), resident on the GPU."""
-    from tests.helpers import camera_K, rigid_c2w
-    g = torch.Generator().manual_seed(seed)
-    yy, xx = torch.meshgrid(torch.linspace(0, 1, H), torch.linspace(0, 1, W), indexing="ij")
-    img = torch.stack([0.5 + 0.4 * torch.sin(6 * xx + 2 * yy), 0.5 + 0.4 * torch.cos(5 * yy),
-                       0.3 + 0.3 * xx * yy], 0).unsqueeze(0)
-    img = (img + 0.02 * torch.rand(img.shape, generator=g)).clamp(0, 1)
-    depth = 1.0 + 7.0 * torch.rand(1, H, W, generator=g)
-    holes = torch.rand(1, H, W, generator=g) < 0.05
-    depth[holes] = 0.0
-    c2w = rigid_c2w(seed)
-    data = {"img": img, "img.idx": torch.tensor([0]), "img.depth": depth, "img.depth_mask": ~holes,
-            "img.camera_mat": camera_K(H, W, FOCAL, FOCAL), "img.scale_mat": torch.eye(4).unsqueeze(0),
-            "img.pose_gt": c2w.unsqueeze(0)}
-    for k, v in list(data.items()):
-        if k not in ("img.idx", "img.depth_mask"):
-            data[k] = v.to(dev)
-    return data, c2w
+    from model.synthetic import vkitti_scene
+    return vkitti_scene(dev, seed, H, W, FOCAL)
 
 
 def build_trainer(dev, c2w, cfg):
@@ -126,6 +112,7 @@ def algorithmic_gemm_flops(net, n_samples, split=False):
 
 
 PRECISION = {"f32": 0, "bf16x6": 1, "f16x3": 2}
+DEFAULT_GEMM = "f16x3"          # the library default (nerf_gemm_get_precision() == 2; tests/test_host_logic.py)
 DTYPE = {"f32": "f32", "bf16x6": "f32 (bf16x6 emulation)", "f16x3": "f32 (f16x3 emulation)"}
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 KIND_NAMES = {
@@ -295,7 +282,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--gemm-precision", choices=list(PRECISION), default="f16x3",
+    ap.add_argument("--gemm-precision", choices=list(PRECISION), default=DEFAULT_GEMM,
                     help="GEMM arithmetic: f32 emulated by a row-scaled 2-word fp16 split (f16x3, default), by a "
                          "3-word bf16 split (bf16x6), or the exact-f32 MFMA (f32); all f32-accurate")
     ap.add_argument("--exec", dest="exec_mode", choices=["auto", "eager", "graph"], default="auto",
@@ -321,6 +308,7 @@ def main():
 
     cfg = make_cfg()
     data, c2w = synthetic_scene(dev)
+    medians = {}      # median per-step milliseconds (hipEvents at the step boundaries) per timed pass
 
     def measure(precision, with_hooks=True):
         """W warm-up + K timed train steps with the GEMMs in `precision` (0 exact-f32 MFMA,
@@ -341,9 +329,12 @@ def main():
             if world > 1:
                 dist.barrier()
             _hip.prof_enable(hooks)
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
             t0 = time.perf_counter()
+            evs[0].record()
             for i in range(args.steps):
                 ld = one(it0 + i)
+                evs[i + 1].record()           # step boundaries on the launch stream (no host sync)
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
@@ -352,15 +343,18 @@ def main():
             stats = _hip.prof_read() if hooks else None
             _hip.prof_enable(False)
             el = t1 - t0
+            med = statistics.median(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
             if world > 1:
-                t = torch.tensor([el], device=dev, dtype=torch.float64)
+                t = torch.tensor([el, med], device=dev, dtype=torch.float64)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                el = t.item()
+                el, med = t[0].item(), t[1].item()
+            timed.median_ms = med
             return el, ld, stats, kinds
 
         for i in range(args.warmup):
             one(i)
         el, ld, _, _ = timed(args.warmup, False)
+        medians[precision] = timed.median_ms
         if with_hooks:
             el_h, _, stats, kinds = timed(args.warmup + args.steps, True)
         else:
@@ -394,11 +388,15 @@ def main():
         for _ in range(args.warmup):
             g.replay()
         torch.cuda.synchronize()
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        evs[0].record()
+        for i in range(args.steps):
             g.replay()
+            evs[i + 1].record()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+        medians["graph"] = statistics.median(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
         if not math.isfinite(out["loss"].detach().item()):
             raise RuntimeError("graph replay: non-finite loss")
         return el, out
@@ -486,6 +484,7 @@ def main():
         out = {"metric": METRIC, "value": world * RAYS / (elapsed / args.steps), "unit": "rays/s",
                "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
                "execution": execution,
+               "ms_per_step_median": medians["graph" if execution == "graph replay" else main_prec],
                "ms_per_step_eager": 1e3 * elapsed_eager / args.steps,
                "ms_per_step_graph": 1e3 * graph[0] / args.steps if graph is not None else None,
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,

@@ -37,7 +37,7 @@ extern "C" {
 /* ABI version: 5 added nerf_prof_read_kinds and nerf_render_eval_fused, 6 the 4x4-chain
  * backwards (nerf_pose_c2w_bwd, nerf_mat4_inv_bwd, nerf_mat4_mul(_bwd), nerf_unproject_matrix_bwd)
  * and the depth-prior distortion (nerf_depth_affine(_bwd)), 7 nerf_linear_fwd_heads, 8 nerf_heads_bwd_mode. */
-#define NERF_HIP_ABI_VERSION 8
+#define NERF_HIP_ABI_VERSION 9
 int nerf_hip_abi_version(void);
 const char* nerf_hip_last_error(void);
 
@@ -138,28 +138,23 @@ int nerf_slab_reduce(const float* slab, int splits, int nout, int ldslab, int no
                      void* stream);
 
 /* GEMM tile policy (tuning knob; 0 = built-in default).  nt: 1 = 128x128 / 4 waves,
- * 2 = 128x256 / 8 waves, 3 = 256x256 / 8 waves;  tn (weight gradient): 1 = 128x128,
- * 3 = 256x256 / 8 waves (split modes: 4 waves), and in the split modes for 256 x 256
- * layers: 4 = XCD-paired 256x128 column tiles (4 waves), 5 = four 256x64 column tiles,
- * 7 (default) = 4 with 8 waves (+ the 64-wide inputs' 256x64 tile at 8 waves), 8 = 7 with
- * the 128-output tiles at 8 waves.  The default changes nerf_linear_bwd_weight_splits. */
+ * 2 = 128x256 / 8 waves, 3 = 256x256 / 8 waves (exact-f32 kernels; the fp16 pair kernels
+ * run 128x256 tiles at 3, and the fused-heads launches always one column block);
+ * tn (weight gradient): 3 = 256x256 tiles, 7 (default) = in the split modes a 256 x 256
+ * layer as XCD-paired 256x128 column tiles of 8 waves, the 64-wide inputs' 256x64 tile
+ * and the colour layer's 128x256 tile at 8 waves.  The policy changes
+ * nerf_linear_bwd_weight_splits. */
 int nerf_gemm_set_policy(int nt_policy, int tn_policy);
-/* Weight-gradient split-K target (tuning knob; 0 = built-in default): about this many
- * blocks per nerf_linear_bwd_weight launch, as nerf_linear_bwd_weight_splits picks them. */
-int nerf_gemm_set_dw_blocks(int target_blocks);
-/* Output-tile store hint of the split NT GEMMs (tuning knob; default 0 = plain stores,
- * 1 = non-temporal, 2 = write-through sc1, the weight-gradient slabs too).  NERF_STORE_NT
- * in the environment sets the initial value. */
-int nerf_gemm_set_store_hint(int nontemporal);
 
-/* f32 arithmetic of the GEMM family (process-wide; default 0):
+/* f32 arithmetic of the GEMM family (process-wide; default 2 since ABI 9):
  *   0  exact-f32 v_mfma_f32_32x32x2_f32 (a k-ordered f32 fma chain);
  *   1  f32 emulated on v_mfma_f32_32x32x16_bf16: operands split into three bf16
  *      words (exact), the six cross products >= 2^-16 |a||b| accumulated in f32.
  *      nerf_linear_fwd / nerf_linear_bwd_data use it when given the weight's split
  *      image (w_split / wt_split), nerf_linear_bwd_weight always.
- *   2  as 1 for nerf_linear_bwd_weight; nerf_linear_fwd / nerf_linear_bwd_data emulate
- *      f32 on v_mfma_f32_32x32x16_f16: every operand row is scaled by a power of two
+ *   2  f32 emulated on v_mfma_f32_32x32x16_f16: every operand row (nerf_linear_fwd,
+ *      nerf_linear_bwd_data; nerf_linear_bwd_weight: every column of a split, from the
+ *      producers' per-128-row-group column maxima, else it runs as 1) is scaled by a power of two
  *      (row max -> [2^14, 2^15)) and split into two fp16 words (exact to 2^-22), the
  *      three products hi.lo + lo.hi + hi.hi accumulated in f32, the scales undone in the
  *      epilogue.  Needs the row maxima of the A operand (x1_rmax, ...) and the fp16 pair

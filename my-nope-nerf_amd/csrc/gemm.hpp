@@ -48,34 +48,13 @@ struct NTArgs {
     const float* ar1; const float* ar2;
     float* c_rmax;
     float* c_cmax; int ldcm;
-    int store_nt;   // tuning (nerf_gemm_set_store_hint): output tiles stored with the non-temporal hint
     // fused output heads (nerf_linear_fwd_heads, precision mode 2, one column block): raw4[m][raw_col + c]
     // = sum_f y[m][f] head_w[c][f] + head_b[c] for c < n_heads (official_nerf.py:66, 91)
     const float* head_w; const float* head_b; float* raw4;
     int n_heads; int raw_col;
 };
 
-typedef float nt_f32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-// output store hints (nerf_gemm_set_store_hint): 0 plain, 1 non-temporal, 2 write-through
-// (sc1).  Plain and nt stores leave the line dirty in the XCD's L2, and the release at the
-// kernel boundary writes every dirty line back before the next launch on the stream may
-// start (~B / 6 TB/s on top of the ~1.8 us boundary: MI355X_MICROARCH.md, "boundary");
-// sc1 stores write through and drop the line, so the boundary has nothing left to write.
-// Mode 2 addresses through a buffer descriptor on `base` (byte offsets < 2^31: the host
-// only selects it for outputs below 2 GB).
-__device__ __forceinline__ void store_out4(float* dst, const float4& x, int hint, const float* base) {
-    if (hint == 2) {
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7FFFFFFF, 0x00020000);
-        const u32x4 v = {__float_as_uint(x.x), __float_as_uint(x.y), __float_as_uint(x.z), __float_as_uint(x.w)};
-        __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)((dst - base) * 4), 0, 16);
-    } else if (hint == 1) {
-        const nt_f32x4 v = {x.x, x.y, x.z, x.w};
-        __builtin_nontemporal_store(v, reinterpret_cast<nt_f32x4*>(dst));
-    } else {
-        *reinterpret_cast<float4*>(dst) = x;
-    }
-}
+__device__ __forceinline__ void store_out4(float* dst, const float4& x) { *reinterpret_cast<float4*>(dst) = x; }
 
 // max |a| over row m of the (one or two segment) A operand
 __device__ __forceinline__ float a_rowmax(const NTArgs& p, int m) {
@@ -92,7 +71,6 @@ struct TNArgs {
     int rows_per_split;
     float* slab; int ldslab; int col0; size_t slab_stride;
     float* bslab; int nout;
-    int store_hint;   // 2: slab tiles stored write-through (sc1, see store_out4), else plain
     int ablate;   // diagnostics: 1 = no slab stores, 2 = no K-loop loads, 4 = no bias column sums
     // precision mode 2: column maxima of dy and x per 128-row group ([m/128][ld]); the
     // fp16 pair kernel scales each split's columns by them
@@ -470,7 +448,7 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
     float chk = 0.f;
     auto out4 = [&](float* dst, const float4& x) {
         if constexpr (kEpiAblate & 8) chk += x.x + x.y + x.z + x.w;
-        else store_out4(dst, x, p.store_nt, p.c);
+        else store_out4(dst, x);
     };
     auto track = [&](int i, int j, int q, const float4& x) {
         if constexpr (H && !(kEpiAblate & 16)) {
@@ -658,19 +636,15 @@ __device__ __forceinline__ void tn_store_lds(const TNArgs& p, f32x16 (&acc)[TM][
             v.z = __builtin_amdgcn_ldexpf(v.z, -(ea + eb.z));
             v.w = __builtin_amdgcn_ldexpf(v.w, -(ea + eb.w));
         }
-        store_out4(slab + (size_t)(o0 + wm0 + rl) * p.ldslab + p.col0 + j0 + wn0 + c4, v, p.store_hint, slab);
+        store_out4(slab + (size_t)(o0 + wm0 + rl) * p.ldslab + p.col0 + j0 + wn0 + c4, v);
     });
 }
 
-// TN policies 4 / 5 (nerf_gemm_set_policy): a 256 x 256 weight gradient in the split modes runs
-// as XCD-paired 256 x 128 column tiles (k_gemm_tn_x6 CT = 2), with twice the rows per split
-// at the same block count; everything else as policy 3
-// (policy 5: four 256 x 64 column tiles per split, four times the rows per split; policy 7:
-// policy 4 with eight waves per block, two per SIMD, and the 256 x 64 tile of the 64-wide
-// inputs with eight waves too; policy 8: policy 7 with the 128-output tiles at eight waves)
+// TN policy 7 (the default, nerf_gemm_set_policy): a 256 x 256 weight gradient in the split modes
+// runs as XCD-paired 256 x 128 column tiles of eight waves (k_gemm_tn_x6 CT = 2), twice the rows
+// per split at the same block count; needs a split count that is a multiple of 8
 inline int tn_xcd_group(int policy, int nout, int kin, int splits) {
-    if (nout != 256 || kin != 256 || splits % 8 != 0) return 0;
-    return (policy == 4 || policy == 7 || policy == 8) ? 2 : policy == 5 ? 4 : 0;
+    return (policy == 7 && nout == 256 && kin == 256 && splits % 8 == 0) ? 2 : 0;
 }
 
 // split-bf16 launchers (gemm_x6.hip); policy as nerf_gemm_set_policy

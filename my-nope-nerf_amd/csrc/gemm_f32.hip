@@ -324,20 +324,23 @@ static int launch_nt(const NTArgs& a, hipStream_t s, double flops) {
     return check_launch("k_gemm_nt");
 }
 
-// tile policy (nerf_gemm_set_policy): 0 = default, 1 = 128x128/4 waves, 2 = 128x256/8 waves,
-// 3 = 256x256/8 waves
+// tile policy (nerf_gemm_set_policy): NT 0 = default, 1 = 128x128/4 waves, 2 = 128x256/8 waves,
+// 3 = 256x256/8 waves (exact-f32 kernels; the split kernels: 128x256 fp16 pair, 256x256 bf16x3)
 static int g_nt_policy = 0;
 static int g_tn_policy = 0;
 // default TN policy (g_tn_policy 0): 7 -- a 256 x 256 weight gradient in the split modes as
 // XCD-paired 256 x 128 column tiles of eight waves (128 splits, half the slab bytes), the
-// 64-wide inputs' 256 x 64 tile with eight waves; 87 vs 104 us per 131072 x 256 x 256 layer
-// with its slab reduce, 37 vs 44 us per 256 x 64 one (profiles/r02/dw_xcd_group_ab.txt)
+// 64-wide inputs' 256 x 64 tile and the colour layer's 128 x 256 tile with eight waves (one
+// column tile: each split reads its dy rows once); 87 vs 104 us per 131072 x 256 x 256 layer
+// with its slab reduce, 37 vs 44 us per 256 x 64 one (profiles/r02/dw_xcd_group_ab.txt).
+// Policy 3 is the round-2 256 x 256 tile at one wave per SIMD (also the fallback when a split
+// count is not a multiple of 8).
 static const int kTnDefault = 7;
-static int g_dw_blocks = 0;
-static int g_store_nt = [] { const char* e = getenv("NERF_STORE_NT"); return e ? atoi(e) : 0; }();   // nerf_gemm_set_dw_blocks: target blocks per weight-gradient launch (0 = default)
 
 // f32 arithmetic (nerf_gemm_set_precision): 0 = exact-f32 MFMA, 1 = split-bf16 emulation
-static int g_precision = 0;
+// (6 products), 2 = row-scaled fp16 pair (3 products; the library default since ABI 9 -- the
+// benchmarked path and the one the fused eval kernel needs; f32-accurate: DESIGN.md section 4.1)
+static int g_precision = 2;
 
 template <int EPI>
 static int dispatch_nt(const NTArgs& a, hipStream_t s, double flops) {
@@ -345,8 +348,6 @@ static int dispatch_nt(const NTArgs& a, hipStream_t s, double flops) {
     if (g_precision >= 1 && a.bs != nullptr) {   // the split paths need the weight image
         NTArgs b = a;
         b.ablate = g_ablate;
-        // sc1 stores address through a buffer descriptor: outputs below 2 GB only
-        b.store_nt = (g_store_nt == 2 && (double)a.m * a.ldc * 4.0 >= 2147483647.0) ? 0 : g_store_nt;
         b.stamps = g_stamps;
         if (g_precision == 2) {
             NERF_CHECK(a.ar1 != nullptr && (a.a2 == nullptr || a.ar2 != nullptr),
@@ -468,12 +469,15 @@ extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const
     NERF_CHECK(lddy % 4 == 0 && ldx % 4 == 0 && ldslab >= col0 + kin, "%s: bad leading dims", __func__);
     NERF_CHECK_ALIGN16(dy);
     NERF_CHECK_ALIGN16(x);
+    // the split kernels address a split's rows through 32-bit buffer descriptors (byte offsets)
+    NERF_CHECK((int64_t)(m / splits) * (lddy > ldx ? lddy : ldx) * 4 < ((int64_t)1 << 31),
+               "%s: %d rows per split x leading dimension %d exceed the 2 GB buffer range; use more splits",
+               __func__, m / splits, lddy > ldx ? lddy : ldx);
     TNArgs a{};
     a.dy = dy; a.lddy = lddy; a.x = x; a.ldx = ldx;
     a.rows_per_split = m / splits;
     a.slab = slab; a.ldslab = ldslab; a.col0 = col0; a.slab_stride = (size_t)nout * ldslab;
     a.bslab = bslab; a.nout = nout;
-    a.store_hint = (g_store_nt == 2 && (double)nout * ldslab * 4.0 < 2147483647.0) ? 2 : 0;   // per-split base
     a.ablate = g_ablate >> 4;
     a.cm_dy = dy_cmax; a.ldcm_dy = nout; a.cm_x = x_cmax; a.ldcm_x = kin;
     // mode 2 runs the fp16 pair kernel when the column maxima are there and every split is
@@ -524,21 +528,9 @@ extern "C" int nerf_slab_reduce(const float* slab, int splits, int nout, int lds
     return check_launch(__func__);
 }
 
-extern "C" int nerf_gemm_set_store_hint(int nontemporal) {
-    NERF_CHECK(nontemporal >= 0 && nontemporal <= 2, "%s: hint %d (0 plain, 1 nt, 2 sc1)", __func__, nontemporal);
-    g_store_nt = nontemporal;
-    return NERF_OK;
-}
-
-extern "C" int nerf_gemm_set_dw_blocks(int target_blocks) {
-    NERF_CHECK(target_blocks >= 0 && target_blocks <= 1 << 16, "%s: target %d", __func__, target_blocks);
-    g_dw_blocks = target_blocks;
-    return NERF_OK;
-}
-
 extern "C" int nerf_gemm_set_policy(int nt_policy, int tn_policy) {
-    NERF_CHECK(nt_policy >= 0 && nt_policy <= 3 && tn_policy >= 0 && tn_policy <= 8 && tn_policy != 6,
-               "%s: policies are 0..3 (NT) and 0..5, 7, 8 (TN)", __func__);
+    NERF_CHECK(nt_policy >= 0 && nt_policy <= 3 && (tn_policy == 0 || tn_policy == 3 || tn_policy == 7),
+               "%s: policies are 0..3 (NT) and 0, 3, 7 (TN)", __func__);
     g_nt_policy = nt_policy;
     g_tn_policy = tn_policy;
     return NERF_OK;
@@ -550,16 +542,11 @@ extern "C" int nerf_gemm_set_policy(int nt_policy, int tn_policy) {
 extern "C" int nerf_linear_bwd_weight_splits(int nout, int kin, int m) {
     const int pol = g_tn_policy ? g_tn_policy : kTnDefault;
     int tiles, target;
-    if (pol >= 4 && g_precision >= 1 && nout == 256 && kin == 256) {   // XCD groups
-        tiles = pol == 5 ? 4 : 2;
-        target = 256;
-    }
+    if (pol == 7 && g_precision >= 1 && nout == 256 && kin == 256) { tiles = 2; target = 256; }   // XCD pairs
+    else if (pol == 7 && g_precision >= 1 && nout == 128 && kin % 256 == 0) { tiles = kin / 256; target = 256; }
     else if (pol >= 3 && nout % 256 == 0 && kin % 256 == 0) { tiles = (nout / 256) * (kin / 256); target = 256; }
     else if (pol >= 3 && nout % 256 == 0 && kin == 64 && g_precision >= 1) { tiles = nout / 256; target = 256; }
     else { tiles = ((nout + 127) / 128) * ((kin + 127) / 128); target = 512; }
-    static const int env_target = [] { const char* e = getenv("NERF_DW_BLOCKS"); return e ? atoi(e) : 0; }();
-    if (env_target > 0) target = env_target;   // experiment hook: blocks per dW launch
-    if (g_dw_blocks > 0) target = g_dw_blocks;  // nerf_gemm_set_dw_blocks
     int splits = 1;
     while (splits * 2 * tiles <= target && m % (splits * 2 * BK) == 0 && m / (splits * 2) >= 256) splits *= 2;
     return splits;

@@ -778,12 +778,6 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 8 ? 2 : 1) void k_gemm_tn_
     }
 }
 
-// NERF_NT_DIRECT=0 selects the LDS-transposed epilogue (A/B experiments)
-static const bool g_nt_direct = [] {
-    const char* e = getenv("NERF_NT_DIRECT");
-    return e == nullptr || atoi(e) != 0;
-}();
-
 template <int BM, int BN, int WM, int WN, int EPI>
 static void launch_nt_x6(const NTArgs& a, hipStream_t s, bool h16) {
     constexpr bool co = BM == 128 && BN == 256;   // fits two co-resident blocks per CU (fp16 pair)
@@ -800,12 +794,9 @@ static void launch_nt_x6(const NTArgs& a, hipStream_t s, bool h16) {
     else if (h16)
         hipLaunchKernelGGL((k_gemm_nt_x6<BM, BN, WM, WN, EPI, true, true>), dim3(a.m / BM, a.n / BN),
                            dim3(64 * WM * WN), 0, s, a);
-    else if (g_nt_direct)
+    else
         hipLaunchKernelGGL((k_gemm_nt_x6<BM, BN, WM, WN, EPI, true>), dim3(a.m / BM, a.n / BN), dim3(64 * WM * WN), 0,
                            s, a);
-    else
-        hipLaunchKernelGGL((k_gemm_nt_x6<BM, BN, WM, WN, EPI, false>), dim3(a.m / BM, a.n / BN), dim3(64 * WM * WN),
-                           0, s, a);
 }
 
 // default policy (3): 256x256 tiles for the bf16x3 kernels; the fp16 pair kernels at 128x256
@@ -813,6 +804,13 @@ static void launch_nt_x6(const NTArgs& a, hipStream_t s, bool h16) {
 // 96 -> 83 us for a 131072 x 256 x 256 forward, profiles/r01/gemm_policy_h16.txt)
 template <int EPI>
 static void pick_nt_x6(const NTArgs& a, int pol, hipStream_t s, bool h16) {
+    // fused output heads: one column block holds the whole output row (its head dot products
+    // are complete per block), whatever the policy
+    if (EPI == EPI_FWD && h16 && a.n_heads > 0) {
+        if (a.n == 256) launch_nt_x6<128, 256, 2, 2, EPI>(a, s, h16);
+        else launch_nt_x6<128, 128, 2, 2, EPI>(a, s, h16);
+        return;
+    }
     if (h16 && pol == 3 && a.n % 256 == 0) launch_nt_x6<128, 256, 2, 2, EPI>(a, s, h16);
     else if (pol == 3 && a.m % 256 == 0 && a.n % 256 == 0) launch_nt_x6<256, 256, 2, 2, EPI>(a, s, h16);
     else if (pol >= 2 && a.n % 256 == 0) launch_nt_x6<128, 256, 2, 2, EPI>(a, s, h16);
@@ -828,33 +826,27 @@ int dispatch_nt_x6(const NTArgs& a, int epi, int policy, hipStream_t s, double f
     return check_launch(h16 ? "k_gemm_nt_x6 (fp16 pair)" : "k_gemm_nt_x6");
 }
 
-template <bool H, int NS>
+template <bool H>
 static void pick_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, hipStream_t s) {
-    const int ct = tn_xcd_group(policy, nout, kin, splits);
-    if (ct == 2 && policy >= 7)   // eight waves (two per SIMD), 64 x 64 per wave
+    constexpr int NS = 1;   // one register set: tiles loaded 3 ahead ran the same (profiles/r02/tn_pipeline_ab.txt)
+    if (tn_xcd_group(policy, nout, kin, splits) == 2)   // eight waves (two per SIMD), 64 x 64 per wave
         hipLaunchKernelGGL((k_gemm_tn_x6<256, 128, 4, 2, H, NS, 2>), dim3(2 * splits), dim3(512), 0, s, a);
-    else if (ct == 2)
-        hipLaunchKernelGGL((k_gemm_tn_x6<256, 128, 2, 2, H, NS, 2>), dim3(2 * splits), dim3(256), 0, s, a);
-    else if (ct == 4)
-        hipLaunchKernelGGL((k_gemm_tn_x6<256, 64, 2, 2, H, NS, 4>), dim3(4 * splits), dim3(256), 0, s, a);
     else if (policy >= 3 && nout % 256 == 0 && kin % 256 == 0)
         hipLaunchKernelGGL((k_gemm_tn_x6<256, 256, 2, 2, H, NS>), dim3(nout / 256, kin / 256, splits), dim3(256), 0,
                            s, a);
-    else if (policy == 8 && nout % 128 == 0 && kin % 128 == 0)   // eight waves, 32 x 64 per wave
-        hipLaunchKernelGGL((k_gemm_tn_x6<128, 128, 4, 2, H, NS>), dim3(nout / 128, kin / 128, splits), dim3(512), 0,
-                           s, a);
+    else if (policy == 7 && nout == 128 && kin % 256 == 0)
+        // the colour layer (128 outputs, 256 feature columns): one column tile per 256 inputs, so
+        // each split reads its dy rows once (two 128 x 128 column tiles read them twice)
+        hipLaunchKernelGGL((k_gemm_tn_x6<128, 256, 2, 4, H, NS>), dim3(1, kin / 256, splits), dim3(512), 0, s, a);
     else if (nout % 128 == 0 && kin % 128 == 0)
         hipLaunchKernelGGL((k_gemm_tn_x6<128, 128, 2, 2, H, NS>), dim3(nout / 128, kin / 128, splits), dim3(256), 0,
                            s, a);
-    else if (policy >= 7 && nout % 256 == 0 && kin == 64)   // eight waves, 64 x 32 per wave
+    else if (policy == 7 && nout % 256 == 0 && kin == 64)   // eight waves, 64 x 32 per wave
         hipLaunchKernelGGL((k_gemm_tn_x6<256, 64, 4, 2, H, NS>), dim3(nout / 256, 1, splits), dim3(512), 0, s, a);
     else if (policy >= 3 && nout % 256 == 0 && kin == 64)
         // a 64-wide input (the encodings: l0, the skip segment of l4) against all 256 outputs in
         // one tile, so each split's dy rows are read once (128 x 64 tiles read them twice)
         hipLaunchKernelGGL((k_gemm_tn_x6<256, 64, 2, 2, H, NS>), dim3(nout / 256, 1, splits), dim3(256), 0, s, a);
-    else if (policy == 8 && nout % 128 == 0)   // eight waves, 32 x 32 per wave
-        hipLaunchKernelGGL((k_gemm_tn_x6<128, 64, 4, 2, H, NS>), dim3(nout / 128, kin / 64, splits), dim3(512), 0, s,
-                           a);
     else if (nout % 128 == 0)
         hipLaunchKernelGGL((k_gemm_tn_x6<128, 64, 2, 2, H, NS>), dim3(nout / 128, kin / 64, splits), dim3(256), 0, s,
                            a);
@@ -865,30 +857,11 @@ static void pick_tn_x6(const TNArgs& a, int nout, int kin, int splits, int polic
         hipLaunchKernelGGL((k_gemm_tn_x6<64, 64, 1, 2, H, NS>), dim3(nout / 64, kin / 64, splits), dim3(128), 0, s, a);
 }
 
-// register sets of the TN strip pipeline (tiles in flight; NERF_TN_NS overrides for A/B runs).
-// One set: three sets (tiles loaded three k-steps ahead, 251 VGPRs, no spills) measured the
-// same 82-85 us per 131072 x 256 x 256 launch and the same step time (profiles/r02/
-// tn_pipeline_ab.txt) -- the kernel moves ~335 MB (operands + split-K slabs) at ~4.2 TB/s,
-// it is not load-latency bound
-static const int g_tn_ns = [] {
-    const char* e = getenv("NERF_TN_NS");
-    const int v = e ? atoi(e) : 0;
-    return v >= 1 && v <= 3 ? v : 0;
-}();
-
 int dispatch_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, hipStream_t s, double flops,
                    bool h16) {
     prof_begin(s);
-    const int ns = g_tn_ns ? g_tn_ns : 1;
-    if (h16) {
-        if (ns == 1) pick_tn_x6<true, 1>(a, nout, kin, splits, policy, s);
-        else if (ns == 2) pick_tn_x6<true, 2>(a, nout, kin, splits, policy, s);
-        else pick_tn_x6<true, 3>(a, nout, kin, splits, policy, s);
-    } else {
-        if (ns == 1) pick_tn_x6<false, 1>(a, nout, kin, splits, policy, s);
-        else if (ns == 2) pick_tn_x6<false, 2>(a, nout, kin, splits, policy, s);
-        else pick_tn_x6<false, 3>(a, nout, kin, splits, policy, s);
-    }
+    if (h16) pick_tn_x6<true>(a, nout, kin, splits, policy, s);
+    else pick_tn_x6<false>(a, nout, kin, splits, policy, s);
     prof_end(s, flops, h16 ? 3 : 6);
     return check_launch(h16 ? "k_gemm_tn_x6 (fp16 pair)" : "k_gemm_tn_x6");
 }

@@ -46,7 +46,7 @@ class ProfKind(ctypes.Structure):
 
 
 PROF_KINDS = ("fwd", "dx", "dw", "dw_narrow")   # NERF_PROF_FWD / _DX / _DW / _DW_NARROW
-ABI_VERSION = 8                    # NERF_HIP_ABI_VERSION
+ABI_VERSION = 9                    # NERF_HIP_ABI_VERSION
 
 
 class ChainLayer(ctypes.Structure):
@@ -87,8 +87,6 @@ _SIGS = {
     "nerf_adam_step": ([_c_p, _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p], _c_i),
     "nerf_chamfer_nn": ([_c_p, _c_i, _c_p, _c_i, _c_p, _c_p], _c_i),
     "nerf_gemm_set_policy": ([_c_i, _c_i], _c_i),
-    "nerf_gemm_set_dw_blocks": ([_c_i], _c_i),
-    "nerf_gemm_set_store_hint": ([_c_i], _c_i),
     "nerf_gemm_set_precision": ([_c_i], _c_i),
     "nerf_gemm_get_precision": ([], _c_i),
     "nerf_gemm_debug_ablate": ([_c_i], _c_i),
@@ -449,20 +447,10 @@ def gemm_set_policy(nt: int = 0, tn: int = 0):
 
 def gemm_set_precision(mode):
     """0 = exact-f32 MFMA, 1 = f32 emulated on bf16 MFMA (3-word split, 6 products),
-    2 = f32 emulated on fp16 MFMA for the forward / backward-data GEMMs (row-scaled 2-word
-    split, 3 products; weight gradients as mode 1)."""
+    2 = f32 emulated on fp16 MFMA (row / column-scaled 2-word split, 3 products; the library
+    default, the benchmarked path and the one the fused eval kernel runs).  All three are
+    f32-accurate."""
     _call("nerf_gemm_set_precision", int(mode))
-
-
-def gemm_set_store_hint(hint):
-    """Output-tile store hint of the split GEMMs (tuning knob): 0 plain, 1 non-temporal,
-    2 write-through (sc1; also the weight-gradient slabs)."""
-    _call("nerf_gemm_set_store_hint", int(hint))
-
-
-def gemm_set_dw_blocks(target: int):
-    """Weight-gradient split-K target blocks per launch (0 = default)."""
-    _call("nerf_gemm_set_dw_blocks", int(target))
 
 
 def gemm_get_precision():

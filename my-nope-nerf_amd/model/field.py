@@ -21,6 +21,7 @@ from dataclasses import dataclass
 from typing import List, Optional, Tuple
 
 import torch
+from torch.autograd.function import once_differentiable
 
 from . import _hip
 
@@ -58,8 +59,6 @@ class LayerSpec:
 class FieldRunner:
     """Owns the packed weights of one OfficialStaticNerf and launches the kernels."""
 
-    TAIL_SIDE = 0   # backward schedule default (NERF_TAIL_SIDE overrides; DESIGN.md section 4.1)
-
     def __init__(self, module):
         self.m = module
         D = module.hidden_dim
@@ -84,6 +83,10 @@ class FieldRunner:
         self.device = None
         self._side = None
         self._plist = None
+        # optional persistent gradient buffer (Trainer.allreduce_grads): when set, the backward
+        # writes the parameter gradients as views of grad_buffer[:n] in param_list() order, so
+        # the data-parallel all-reduce runs in place on it
+        self.grad_buffer = None
 
     # ------------------------------------------------------------------ packing
     def _alloc(self, device):
@@ -298,10 +301,12 @@ class FieldRunner:
             pl = self._plist = list(self.m.parameters())
         return pl
 
-    def backward(self, st, g_rgb, g_dist, want_ray_grad: bool, graw4=None):
+    def backward(self, st, g_rgb, g_dist, want_ray_grad: bool, graw4=None, g_h8=None):
         """Returns (list of parameter gradients in self.param_list() order, ray grads or None).
         Starts from the ray gradients (composite backward) or, when ``graw4`` is given,
-        directly from the gradient of the raw head outputs."""
+        directly from the gradient of the raw head outputs.  ``g_h8`` [Np, D] (optional): an
+        extra gradient w.r.t. the trunk output h8 (infer_occ's x), added where l7's ReLU
+        passes it."""
         R, S, Np, flags = st["R"], st["S"], st["Np"], st["flags"]
         D, HR = self.D, self.HR
         dev = st["z"].device
@@ -310,7 +315,14 @@ class FieldRunner:
         h = {l.name: acts[i] for i, l in enumerate(self.layers)}
         m = self.m
         params = self.param_list()
-        flat = torch.empty(sum(p.numel() for p in params), device=dev, dtype=torch.float32)
+        n_par = sum(p.numel() for p in params)
+        buf = self.grad_buffer
+        if (buf is not None and buf.device == dev and buf.numel() >= n_par
+                and all(p.grad is None for p in params)):
+            # autograd hands these views on as param.grad (no other gradient to accumulate into)
+            flat = buf[:n_par]
+        else:
+            flat = torch.empty(n_par, device=dev, dtype=torch.float32)
         grads, off = {}, 0
         for p in params:
             grads[id(p)] = flat[off:off + p.numel()].view_as(p)
@@ -325,10 +337,8 @@ class FieldRunner:
         # the saved input, so they run on a side stream beside the dX chain: compute-bound
         # GEMM phases overlap the memory-bound reductions and each other's prologue/epilogue.
         main = torch.cuda.current_stream(dev)
-        n_side = int(os.environ.get("NERF_SIDE_STREAMS", "1"))
-        if self._side is None or self._side[0].device != dev or len(self._side) != n_side:
-            prio = int(os.environ.get("NERF_SIDE_PRIORITY", "0"))
-            self._side = [torch.cuda.Stream(dev, priority=prio) for _ in range(n_side)]
+        if self._side is None or self._side[0].device != dev:
+            self._side = [torch.cuda.Stream(dev)]
         sides = self._side
 
         # heads: d(fc_density), d(fc_rgb), dY of the colour layer.  Only dyr (+ its maxima) is
@@ -381,7 +391,6 @@ class FieldRunner:
         # beside the chain
         tail_default = 2 if (D == 256 and Np >= 65536) else 0
         tail_main = int(os.environ.get("NERF_TAIL_MAIN", str(tail_default)))
-        tail_side = int(os.environ.get("NERF_TAIL_SIDE", str(self.TAIL_SIDE)))
         dy = dyr
         prev_in = {"l0": st["enc_p"], "l1": h["l0"], "l2": h["l1"], "l3": h["l2"], "l4": h["l3"],
                    "l5": h["l4"], "l6": h["l5"], "l7": h["l6"], "lf": h["l7"], "lr": h["lf"]}
@@ -395,9 +404,8 @@ class FieldRunner:
             nout_ref, kin_ref = W.shape
             k1 = l.k1
             # a layer with a 64-wide second segment (l4's skip input) shares one split count over
-            # both launches; NERF_SEG2_SPLITS=1 sizes it for the 64-wide launch (A/B knob)
-            seg2_splits = l.seg2 and os.environ.get("NERF_SEG2_SPLITS", "0") == "1"
-            splits = _hip.bwd_weight_splits(l.out_p, 64 if seg2_splits else k1, Np)
+            # both launches, sized for the wide one (profiles/r02/seg2_splits_ab.txt)
+            splits = _hip.bwd_weight_splits(l.out_p, k1, Np)
             slab = e(splits * l.out_p * l.kp)
             bslab = e(splits * l.out_p)
             _hip.linear_bwd_weight(dy, l.out_p, x_in, k1, Np, splits, slab, l.kp, 0, bslab, dy_cmax=dy_cm,
@@ -410,23 +418,19 @@ class FieldRunner:
             if l.out_p != nout_ref:
                 G(l.linear.bias).copy_(gb[:nout_ref])
 
-        deferred, deferred_side = [], []
+        deferred = []
         for step, name in enumerate(order):
             l = spec[name]
             W = l.linear.weight
             x_in = prev_in[name]
             k1 = l.k1
             # --- weight / bias gradient on a side stream: split-K slabs + reduce.  The last
-            # NERF_TAIL_MAIN layers' run on the main stream once the input-gradient chain is done;
-            # the NERF_TAIL_SIDE layers before them are enqueued on the side stream behind ONE
-            # wait for that chain (the side stream trails it by ~3 layers at the tail anyway, and
-            # every cross-stream wait costs ~15 us before the next launch)
+            # NERF_TAIL_MAIN layers' run on the main stream once the input-gradient chain is done
+            # (every cross-stream wait costs ~15 us before the next launch)
             if step >= len(order) - tail_main:
                 deferred.append((l, dy, dy_cm, x_in))
-            elif step >= len(order) - tail_main - tail_side:
-                deferred_side.append((l, dy, dy_cm, x_in))
             else:
-                side = sides[step % len(sides)]
+                side = sides[0]
                 ev = torch.cuda.Event()
                 ev.record(main)
                 side.wait_event(ev)
@@ -457,23 +461,21 @@ class FieldRunner:
                 _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask, u=graw4, ldu=4,
                                      v=self.wd.view(-1), wt_split=rows(0, k1), dy_rmax=dy_rm, dx_rmax=dx_rm,
                                      dx_cmax=dx_cm)     # v: the 16-byte-aligned copy (float4 epilogue reads)
+                if g_h8 is not None:
+                    # infer_occ's x = h8 (post-ReLU): its gradient joins l7's pre-activation gradient
+                    # through the same ReLU; the row / column maxima the next GEMMs scale by are
+                    # re-taken (the epilogue wrote those of dx without it)
+                    dx.add_(g_h8 * (h["l7"] > 0))
+                    if dx_rm is not None:
+                        torch.amax(dx.abs(), 1, out=dx_rm)
+                    if dx_cm is not None:
+                        torch.amax(dx.abs().view(Np // 128, 128, k1), 1, out=dx_cm)
             else:
                 _hip.linear_bwd_data(dy, l.out_p, wt[:k1], dx, Np, k1, mask=mask, wt_split=rows(0, k1),
                                      dy_rmax=dy_rm, dx_rmax=dx_rm, dx_cmax=dx_cm)
             dy = dx
             dy_rm, dy_cm = dx_rm, dx_cm
 
-        if deferred_side:
-            side = sides[0]
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                for args in deferred_side:
-                    args[1].record_stream(side)
-                    if args[2] is not None:
-                        args[2].record_stream(side)
-                    weight_grad(*args)
         for args in deferred:
             weight_grad(*args)
         for side in sides:
@@ -506,6 +508,7 @@ class FieldRenderFn(torch.autograd.Function):
         return rgb, dist, alpha, z
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, g_rgb, g_dist, g_alpha, g_z):
         st = ctx.state
         R = st["R"]
@@ -565,6 +568,7 @@ class FieldRawFn(torch.autograd.Function):
         return raw4[:n]
 
     @staticmethod
+    @once_differentiable      # no second derivatives through the HIP kernels: a double backward raises
     def backward(ctx, g_raw):
         st = ctx.state
         Np = st["Np"]
@@ -580,10 +584,10 @@ class FieldRawFn(torch.autograd.Function):
 
 class FieldTrunkFn(torch.autograd.Function):
     """OfficialStaticNerf.infer_occ (official_nerf.py:60-67) in one HIP forward: points
-    p [n,3] -> (x [n,D] the trunk output h8, sigma_raw [n,1] = fc_density(x)).  sigma_raw
-    is differentiable w.r.t. the points and the parameters (the head backward of the
-    runner); x is returned as a non-differentiable tensor -- the reference only consumes it
-    inside forward(), which runs the fused path instead."""
+    p [n,3] -> (x [n,D] the trunk output h8, sigma_raw [n,1] = fc_density(x)), both
+    differentiable w.r.t. the points and the parameters (one runner backward that starts from
+    d sigma_raw and adds dL/dx at the trunk output).  First order only: a double backward
+    (create_graph=True, e.g. a loss on gradient()'s normals) raises."""
 
     @staticmethod
     def forward(ctx, runner: FieldRunner, p, *params):
@@ -591,17 +595,24 @@ class FieldTrunkFn(torch.autograd.Function):
         zeros = torch.zeros_like(p)
         raw4, _, _, _, st = runner.forward(p, zeros, zeros, None, 0.0, 0.0, 1, 0, keep=True, composite=False)
         h8 = st["acts"][7][:n, :runner.D].clone()
-        ctx.mark_non_differentiable(h8)
         ctx.runner, ctx.state, ctx.n = runner, st, n
         ctx.ray_grad = ctx.needs_input_grad[1]
         return h8, raw4[:n, 0:1].clone()
 
     @staticmethod
+    @once_differentiable
     def backward(ctx, g_h8, g_sigma):
         st = ctx.state
-        graw4 = torch.zeros(st["Np"], 4, device=g_sigma.device)
-        graw4[:ctx.n, 0:1] = g_sigma
-        grads, ray = ctx.runner.backward(st, None, None, ctx.ray_grad, graw4=graw4)
+        Np, n = st["Np"], ctx.n
+        dev = st["z"].device
+        graw4 = torch.zeros(Np, 4, device=dev)
+        if g_sigma is not None:
+            graw4[:n, 0:1] = g_sigma
+        gx = None
+        if g_h8 is not None:
+            gx = torch.zeros(Np, ctx.runner.D, device=dev)
+            gx[:n] = g_h8
+        grads, ray = ctx.runner.backward(st, None, None, ctx.ray_grad, graw4=graw4, g_h8=gx)
         ctx.state = None
         g_p = ray[0] if ray is not None else None
         return (None, g_p, *grads)

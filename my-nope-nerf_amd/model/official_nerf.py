@@ -63,8 +63,8 @@ class OfficialStaticNerf(nn.Module):
 
     def infer_occ(self, p):
         """official_nerf.py:60-67: (x, density) = (trunk output [..,D], fc_density(x) [..,1],
-        before the activation), from one HIP forward.  density is differentiable w.r.t. p
-        and the parameters; x carries no gradient (see field.FieldTrunkFn)."""
+        before the activation), from one HIP forward.  Both are differentiable w.r.t. p and
+        the parameters (first order; see field.FieldTrunkFn)."""
         shape = p.shape[:-1]
         x, density = trunk_points(self, p.reshape(-1, 3).float())
         return x.reshape(*shape, self.hidden_dim), density.reshape(*shape, 1)
@@ -87,10 +87,13 @@ class OfficialStaticNerf(nn.Module):
         return rgb
 
     def gradient(self, p, it):
-        """official_nerf.py:46-58: -d(density_raw)/dp, through the HIP backward."""
+        """official_nerf.py:46-58: -d(density_raw)/dp, through the HIP backward.  As in the
+        reference the result is built with create_graph=True; the HIP backward is first order
+        only, so backpropagating a loss through these normals (a second derivative) raises
+        instead of returning a silently wrong gradient."""
         with torch.enable_grad():
             p = p.detach().requires_grad_(True)
             raw = eval_points(self, p.reshape(-1, 3), torch.zeros_like(p).reshape(-1, 3))
             y = raw[:, 0:1]
-            g = torch.autograd.grad(y, p, torch.ones_like(y), create_graph=False, retain_graph=True)[0]
+            g = torch.autograd.grad(y, p, torch.ones_like(y), create_graph=True, retain_graph=True)[0]
             return -g.unsqueeze(1)

@@ -179,12 +179,29 @@ class Renderer(nn.Module):
             f |= F_RELU
         return f
 
+    def normal_diff(self, cam, ray, d_src, mask, it, noise=None):
+        """rendering.py:127-135 (the ``normal_loss`` branch): at the rays' depth-prior surface
+        points and a jittered copy of each (U[-0.005, 0.005) per coordinate), the normals
+        -d sigma_raw/dp / (|.| + 1e-5) from the HIP field backward; returns |n - n_jitter| per
+        surface point.  ``noise`` injects the U[0,1) jitter (N,3).  The reference builds the
+        normals with create_graph=True; here they are first order (OfficialStaticNerf.gradient):
+        a loss backpropagated through the result raises."""
+        surface = (cam + ray * d_src.unsqueeze(-1))[mask]
+        n = surface.shape[0]
+        if noise is None:
+            noise = torch.rand_like(surface)
+        neighbours = surface + (noise - 0.5) * 0.01
+        g = self.model.gradient(torch.cat([surface, neighbours], 0), it)[:, 0, :]
+        normals = g / (g.norm(2, dim=1).unsqueeze(-1) + 10 ** (-5))
+        return torch.norm(normals[:n] - normals[n:], dim=-1)
+
     def nope_nerf(self, pixels, depth, camera_mat, world_mat, scale_mat, add_noise=False, it=100000,
-                  eval_=False, noise=None, dense_depth=False):
+                  eval_=False, noise=None, dense_depth=False, normal_noise=None):
         """rendering.py:36-168.  Extra keyword arguments of the MI355X build:
         ``noise`` injects the stratified U[0,1) tensor (1,R,S) instead of torch.rand;
         ``dense_depth`` returns unmasked depth_pred/depth_gt plus 'depth_mask' (R,) so the
-        training step never needs the boolean-index host sync (rendering.py:151-153)."""
+        training step never needs the boolean-index host sync (rendering.py:151-153);
+        ``normal_noise`` injects the (N,3) jitter of the normal_loss branch."""
         cfg = self.cfg
         S = cfg["num_points"] - cfg.get("outside_steps", 0)
         near, far = float(self.depth_range[0]), float(self.depth_range[1])
@@ -219,7 +236,10 @@ class Renderer(nn.Module):
             d_src = d_src / ray_norm
         if cfg["sample_option"] == "ndc":
             d_src = 1 - 1 / d_src
-        out = {"rgb": rgb.reshape(1, -1, 3), "z_vals": z, "normal": None, "alpha": alpha}
+        normal = None
+        if not eval_ and cfg.get("normal_loss", False):          # rendering.py:127-137
+            normal = self.normal_diff(cam, ray, d_src, mask, it, normal_noise)
+        out = {"rgb": rgb.reshape(1, -1, 3), "z_vals": z, "normal": normal, "alpha": alpha}
         if eval_:
             out["depth_pred"], out["depth_gt"] = dist, d_src
         elif dense_depth:

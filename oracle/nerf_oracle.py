@@ -112,6 +112,19 @@ class OracleNerf(nn.Module):
         return -g.unsqueeze(1)
 
 
+def normal_diff(model: "OracleNerf", cam, ray, d_src, obj_mask, noise):
+    """rendering.py:127-135 (normal_loss branch): surface points cam + ray d at the masked
+    rays (rendering.py:76-88), a jittered copy (noise: the injected U[0,1) (N,3) of
+    torch.rand_like), normals g / (|g| + 1e-5) of g = gradient() (official_nerf.py:46-58),
+    -> |n - n_jitter| per surface point."""
+    surface = (cam + ray * d_src.unsqueeze(-1))[obj_mask]
+    n = surface.shape[0]
+    neighbours = surface + (noise - 0.5) * 0.01
+    g = model.gradient(torch.cat([surface, neighbours], 0))[:, 0, :]
+    normals = g / (g.norm(2, dim=1).unsqueeze(-1) + 10 ** (-5))
+    return torch.norm(normals[:n] - normals[n:], dim=-1)
+
+
 # ----------------------------------------------------------------------------
 # camera helpers  (model/common.py)
 # ----------------------------------------------------------------------------

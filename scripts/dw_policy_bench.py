@@ -1,6 +1,6 @@
 """Weight gradient of one 131072 x 256 x 256 layer (fp16 pair) + its slab reduce, per TN tile
-policy (3: 256x256 tiles, 256 splits; 4: XCD-paired 256x128 tiles, 128 splits; 5: four
-256x64 tiles per split, 64 splits; 7: policy 4 with 8 waves), standalone and beside an input-gradient NT on a
+policy (3: 256x256 tiles, 256 splits; 7: XCD-paired 256x128 tiles of 8 waves, 128 splits, the
+colour layer as one 128x256 tile), standalone and beside an input-gradient NT on a
 second stream (the step's situation).
 
     python scripts/dw_policy_bench.py
@@ -20,7 +20,7 @@ def main():
     dev = torch.device("cuda")
     _hip.load_library()
     _hip.gemm_set_precision(2)
-    for nout, kin, pols in ((256, 256, (3, 4, 5, 7)), (256, 64, (3, 7)), (128, 256, (7, 8)), (128, 64, (7, 8))):
+    for nout, kin, pols in ((256, 256, (3, 7)), (256, 64, (3, 7)), (128, 256, (3, 7)), (128, 64, (3, 7))):
         shape(dev, nout, kin, pols)
     _hip.gemm_set_policy(0, 0)
 

@@ -148,7 +148,7 @@ def main():
     res = {}
     for rnd in range(3):
         for pol in (1, 2, 3):
-            _hip.gemm_set_policy(pol, pol)
+            _hip.gemm_set_policy(pol, 0)
             for name, (fn, fl) in cases.items():
                 us = timeit(fn)
                 res.setdefault((name, pol), []).append(us)

@@ -29,3 +29,21 @@ def gemm_precision(request, dev):
     _hip.gemm_set_precision(request.param)
     yield request.param
     _hip.gemm_set_precision(old)
+
+
+@pytest.fixture(autouse=True)
+def _restore_gemm_state(request):
+    """Every GPU test leaves the process-wide GEMM precision and tile policy as it found them
+    (the library default is precision mode 2, the fp16 pair)."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import torch
+    if not torch.cuda.is_available():
+        yield
+        return
+    from model import _hip
+    old = _hip.gemm_get_precision()
+    yield
+    _hip.gemm_set_precision(old)
+    _hip.gemm_set_policy(0, 0)

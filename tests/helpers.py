@@ -1,57 +1,9 @@
 """Shared test fixtures: configs and seeded synthetic V_KITTI-shaped inputs."""
 from __future__ import annotations
 
-import copy
-import math
-
 import torch
 
-BASE_CFG = {
-    "model": {"hidden_dim": 256, "pos_enc_levels": 10, "dir_enc_levels": 4, "occ_activation": "softplus",
-              "num_layers": 8},
-    "rendering": {"type": "nope_nerf", "n_max_network_queries": 64000, "white_background": False,
-                  "radius": 4.0, "num_points": 128, "depth_range": [0.01, 10.0], "dist_alpha": False,
-                  "use_ray_dir": True, "normalise_ray": True, "normal_loss": False,
-                  "sample_option": "uniform", "outside_steps": 0},
-    "depth": {"type": None},
-    "distortion": {"learn_distortion": True, "fix_scaleN": True, "learn_scale": True, "learn_shift": True},
-    "training": {"type": "nope_nerf", "n_training_points": 1024, "detach_gt_depth": False, "pc_ratio": 4,
-                 "match_method": "dense", "shift_first": False, "detach_ref_img": True, "scale_pcs": True,
-                 "detach_rgbs_scale": False, "vis_reprojection_every": 5000, "nearest_limit": 0.01,
-                 "annealing_epochs": 0, "scheduling_start": 0, "rgb_weight": [1.0, 1.0],
-                 "depth_weight": [0.04, 0.0], "weight_dist_2nd_loss": [0.0, 0.0],
-                 "weight_dist_1st_loss": [0.0, 0.0], "pc_weight": [1.0, 0.0], "rgb_s_weight": [1.0, 0.0],
-                 "depth_consistency_weight": [0.0, 0.0], "t_cycle_weight": [0.0, 0.0],
-                 "depth_loss_type": "l1", "with_auto_mask": False, "with_ssim": False, "vis_geo": False,
-                 "learning_rate": 0.001},
-}
-
-
-def make_cfg(hidden=256, S=128, **render):
-    cfg = copy.deepcopy(BASE_CFG)
-    cfg["model"]["hidden_dim"] = hidden
-    cfg["rendering"]["num_points"] = S
-    cfg["rendering"].update(render)
-    return cfg
-
-
-def camera_K(h, w, fx, fy):
-    """dataset.py:83-86."""
-    return torch.tensor([[2 * fx / w, 0, 0, 0], [0, -2 * fy / h, 0, 0], [0, 0, -1, 0], [0, 0, 0, 1]],
-                        dtype=torch.float32).unsqueeze(0)
-
-
-def rigid_c2w(seed=0, scale=0.3):
-    g = torch.Generator().manual_seed(seed)
-    r = (torch.rand(3, generator=g) - 0.5) * scale
-    th = r.norm()
-    k = r / th
-    K = torch.tensor([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
-    Rm = torch.eye(3) + math.sin(th) * K + (1 - math.cos(th)) * (K @ K)
-    c2w = torch.eye(4)
-    c2w[:3, :3] = Rm
-    c2w[:3, 3] = (torch.rand(3, generator=g) - 0.5)
-    return c2w
+from model.synthetic import BASE_CFG, camera_K, make_cfg, rigid_c2w  # noqa: F401  (the package's builders)
 
 
 def synthetic_rays(R=1024, S=128, H=188, W=621, seed=0, zero_frac=0.05, fx=362.5):

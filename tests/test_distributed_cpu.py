@@ -187,3 +187,66 @@ def test_bench_launcher_spawns_ranks():
     bad = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--plumbing", "--gpus", "3"],
                          capture_output=True, text=True, timeout=120, env=dict(env, WORLD_SIZE="2"), cwd=root)
     assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr
+
+
+def _inplace_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = make_cfg(hidden=64, S=16)
+    torch.manual_seed(0)
+    net = mdl.OfficialStaticNerf(cfg)
+    model = mdl.get_model(mdl.Renderer(net, cfg["rendering"]), cfg)
+    pose = mdl.LearnPose(2, True, True, cfg)
+    distn = mdl.Learn_Distortion(2, True, True, cfg)
+    tr = mdl.Trainer(model, None, cfg["training"], device=torch.device("cpu"), pose_param_net=pose,
+                     distortion_net=distn)
+    flat = tr._bucket_buffer(torch.device("cpu"))
+    runner = net.hip_runner()
+    assert runner.grad_buffer is not None and runner.grad_buffer.data_ptr() == flat.data_ptr()
+    field = runner.param_list()
+    # what FieldRunner.backward does: the field gradients are views of grad_buffer in
+    # param_list() order (autograd hands them on as param.grad); the pose / distortion
+    # gradients are ordinary autograd tensors
+    off = 0
+    for i, p in enumerate(field):
+        p.grad = runner.grad_buffer[off:off + p.numel()].view_as(p)
+        p.grad.fill_(float(rank + i))
+        off += p.numel()
+    ptrs = [p.grad.data_ptr() for p in field]
+    extra = [p for p in tr.bucket_params() if all(p is not f for f in field)]
+    for i, p in enumerate(extra):
+        p.grad = torch.full_like(p, float(100 * rank + i))
+    tr.allreduce_grads()
+    base, end = flat.data_ptr(), flat.data_ptr() + flat.numel() * 4
+    ok_inplace = [p.grad.data_ptr() == ptr for p, ptr in zip(field, ptrs)]      # reduced where they lie
+    ok_views = [base <= p.grad.data_ptr() < end for p in extra]                  # no copy back: bucket views
+    vals = [float(p.grad.flatten()[0]) for p in field] + [float(p.grad.flatten()[0]) for p in extra]
+    q.put((rank, ok_inplace, ok_views, vals, len(field)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_allreduce_in_place_on_field_gradient_buffer():
+    """The NeRF field's gradients are written by the runner into the Trainer's persistent
+    bucket and all-reduced there: after allreduce_grads every field p.grad still points at
+    the same storage (no torch.cat, no copy back), the pose / distortion gradients are views
+    of the same bucket, and every value is the average over the ranks."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_inplace_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        ok_inplace, ok_views, vals, n_field = res[r]
+        assert all(ok_inplace) and all(ok_views)
+        for i, v in enumerate(vals[:n_field]):
+            assert v == (0 + i + 1 + i) / 2
+        for i, v in enumerate(vals[n_field:]):
+            assert v == (i + 100 + i) / 2

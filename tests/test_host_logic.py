@@ -100,24 +100,39 @@ def test_pose_and_distortion_modules_match_oracle():
         assert torch.allclose(s.reshape(()), so.reshape(()).float()) and torch.allclose(sh, sho)
 
 
+def test_library_default_is_benchmarked_path():
+    """The library's default GEMM arithmetic is the one bench.py headlines (the fp16 pair,
+    mode 2), so a drop-in caller of the reference API gets the benchmarked kernels and the
+    fused per-ray eval kernel without any set-up call."""
+    import bench
+    from model import _hip
+    lib = _hip.load_library()
+    assert lib.nerf_gemm_get_precision() == 2
+    assert bench.PRECISION[bench.DEFAULT_GEMM] == lib.nerf_gemm_get_precision()
+
+
 def test_dw_split_policy():
     from model import _hip
     _hip.load_library()
-    assert _hip.bwd_weight_splits(256, 256, 131072) == 256     # exact f32: 256 x 256 tiles
-    assert _hip.bwd_weight_splits(128, 256, 131072) == 256
-    # split modes, default TN policy 7: XCD-paired 256 x 128 column tiles, 2 blocks per split
-    _hip.gemm_set_precision(2)
+    prev = _hip.gemm_get_precision()
+    _hip.gemm_set_precision(0)
     try:
+        assert _hip.bwd_weight_splits(256, 256, 131072) == 256     # exact f32: 256 x 256 tiles
+        assert _hip.bwd_weight_splits(128, 256, 131072) == 256
+        # split modes, default TN policy 7: XCD-paired 256 x 128 column tiles, 2 blocks per split;
+        # the colour layer's 128 x 256 tile, one block per split
+        _hip.gemm_set_precision(2)
         assert _hip.bwd_weight_splits(256, 256, 131072) == 128
         assert _hip.bwd_weight_splits(256, 64, 131072) == 256
+        assert _hip.bwd_weight_splits(128, 256, 131072) == 256
         _hip.gemm_set_policy(0, 3)
         assert _hip.bwd_weight_splits(256, 256, 131072) == 256
-        for bad in (6, 9, -1):
+        for bad in (1, 4, 5, 6, 8, 9, -1):
             with pytest.raises(RuntimeError):
                 _hip.gemm_set_policy(0, bad)
     finally:
         _hip.gemm_set_policy(0, 0)
-        _hip.gemm_set_precision(0)
+        _hip.gemm_set_precision(prev)
     for m in (128, 1024, 16384, 131072, 131072 + 128):
         for nout, kin in ((256, 256), (128, 256), (256, 64), (64, 64)):
             s = _hip.bwd_weight_splits(nout, kin, m)
