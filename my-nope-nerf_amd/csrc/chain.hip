@@ -548,41 +548,86 @@ __device__ __forceinline__ void fused_encode_p(const ChainFwdArgs& p, ChainState
 }
 
 // fused eval epilogue: sigma -> alpha -> exclusive-product compositing of the block's
-// 128 / S rays (rendering.py:113-141, the arithmetic of k_composite16_fwd), one thread per
-// ray walking its S samples in order
+// 128 / S rays (rendering.py:113-141), from the raw4 / z rows in LDS, with the arithmetic of
+// k_composite16_fwd (so the fused and the unfused render agree bit for bit): one 16-lane DPP
+// row per ray, lane l owning samples [l J, l J + J) (J = max(1, S / 16)); transmittance by a
+// row prefix-product scan, the sums by row butterflies; each lane stores its J alphas as
+// contiguous float4s (a ray's S alphas are one contiguous run across its row)
+template <int J>
+__device__ __forceinline__ void fused_composite16(const ChainFwdArgs& p, const ChainState& st) {
+    const int S = p.S;
+    const int nr = CROWS / S;
+    const int l16 = st.tid & 15;
+    for (int rb = 0; rb < nr; rb += 16) {          // 16 rays per pass of the block
+        const int rloc = rb + (st.tid >> 4);
+        const size_t ray = st.m0 / (size_t)S + rloc;
+        const bool active = rloc < nr && ray < (size_t)p.R;   // whole 16-lane rows are (in)active
+        const int i0 = l16 * J;
+        float al[J], T[J], c[J][3], z[J];
+        bool valid[J];
+        float pl = 1.f;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int i = i0 + j;
+            valid[j] = active && i < S;
+            float a = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f, zz = 0.f;
+            if (valid[j]) {
+                const int e = rloc * S + i;
+                const float4 r = *reinterpret_cast<const float4*>(st.fx + FX_RAW + 4 * e);
+                zz = st.fx[FX_Z + e];
+                const float sg = f_density(r.x, p.flags);
+                if (p.flags & F_DIST_ALPHA)
+                    a = i == S - 1 ? 1.f : 1.f - __expf(-1.0f * sg * (st.fx[FX_Z + e + 1] - zz));   // rendering.py:116-122
+                else
+                    a = 1.f - __expf(-1.0f * sg);
+                c0 = f_sigmoid(r.y); c1 = f_sigmoid(r.z); c2 = f_sigmoid(r.w);
+            }
+            al[j] = a; z[j] = zz;
+            c[j][0] = c0; c[j][1] = c1; c[j][2] = c2;
+            T[j] = pl;
+            pl *= valid[j] ? (1.f - a + kEps) : 1.f;
+        }
+        const float excl = dpp_f<0x111>(1.f, row_scan_mul(pl));   // product over the lanes before this one
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, sd = 0.f, sw = 0.f;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const float w = al[j] * (T[j] * excl);
+            s0 += w * c[j][0];
+            s1 += w * c[j][1];
+            s2 += w * c[j][2];
+            sd += w * z[j];
+            sw += w;
+        }
+        float* ao = p.alpha + ray * (size_t)S + i0;
+        if (J % 4 == 0 && active) {
+#pragma unroll
+            for (int q = 0; q < J / 4; ++q)
+                *reinterpret_cast<float4*>(ao + 4 * q) = make_float4(al[4 * q], al[4 * q + 1], al[4 * q + 2], al[4 * q + 3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < J; ++j)
+                if (valid[j]) ao[j] = al[j];
+        }
+        s0 = row_sum(s0); s1 = row_sum(s1); s2 = row_sum(s2); sd = row_sum(sd);
+        if (p.flags & F_WHITE_BKGD) sw = row_sum(sw);
+        if (active && l16 == 0) {
+            if (p.flags & F_WHITE_BKGD) {          // rendering.py:139-141
+                const float bg = 1.f - sw;
+                s0 += bg; s1 += bg; s2 += bg;
+            }
+            p.rgb[3 * ray + 0] = s0;
+            p.rgb[3 * ray + 1] = s1;
+            p.rgb[3 * ray + 2] = s2;
+            p.dist[ray] = sd;
+        }
+    }
+}
+
 __device__ __forceinline__ void fused_composite(const ChainFwdArgs& p, const ChainState& st) {
-    const int nr = CROWS / p.S;
-    if (st.tid >= nr) return;
-    const size_t ray = st.m0 / (size_t)p.S + st.tid;
-    if (ray >= (size_t)p.R) return;
-    const float* raw = st.fx + FX_RAW + 4 * st.tid * p.S;
-    const float* zl = st.fx + FX_Z + st.tid * p.S;
-    float T = 1.f, s0 = 0.f, s1 = 0.f, s2 = 0.f, sd = 0.f, sw = 0.f;
-    float* al = p.alpha + ray * (size_t)p.S;
-    for (int i = 0; i < p.S; ++i) {
-        const float sg = f_density(raw[4 * i], p.flags);
-        float a;
-        if (p.flags & F_DIST_ALPHA)
-            a = i == p.S - 1 ? 1.f : 1.f - __expf(-1.0f * sg * (zl[i + 1] - zl[i]));
-        else
-            a = 1.f - __expf(-1.0f * sg);
-        const float w = a * T;
-        s0 += w * f_sigmoid(raw[4 * i + 1]);
-        s1 += w * f_sigmoid(raw[4 * i + 2]);
-        s2 += w * f_sigmoid(raw[4 * i + 3]);
-        sd += w * zl[i];
-        sw += w;
-        T *= 1.f - a + kEps;
-        al[i] = a;
-    }
-    if (p.flags & F_WHITE_BKGD) {
-        const float bg = 1.f - sw;
-        s0 += bg; s1 += bg; s2 += bg;
-    }
-    p.rgb[3 * ray + 0] = s0;
-    p.rgb[3 * ray + 1] = s1;
-    p.rgb[3 * ray + 2] = s2;
-    p.dist[ray] = sd;
+    if (p.S >= 128) fused_composite16<8>(p, st);
+    else if (p.S >= 64) fused_composite16<4>(p, st);
+    else if (p.S >= 32) fused_composite16<2>(p, st);
+    else fused_composite16<1>(p, st);
 }
 
 template <bool F>

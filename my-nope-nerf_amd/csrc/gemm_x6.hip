@@ -269,6 +269,13 @@ __device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int
     }
 }
 
+// Diagnostic builds only (make EXTRA=-DNERF_NT_ABLATE=...; results are wrong): the NT main
+// loop without its B-image DMAs (2), its raw-A DMAs (4) or the split VALU of A (8)
+#ifndef NERF_NT_ABLATE
+#define NERF_NT_ABLATE 0
+#endif
+constexpr int kNtAblate = NERF_NT_ABLATE;
+
 // ---------------------------------------------------------------------------
 // NT: C[m][n] = epi( sum_k A[m][k] B[n][k] ).
 // A (activations, f32 [m][k]): LDS-DMA into a 2-slot raw ring, 16 B per lane (a wave
@@ -363,11 +370,13 @@ struct NTStager {
     // iteration kt: B image of tile kt+2 into buffer kt&1 (lands this iteration), then raw A
     // of tile kt+4 into slot (kt+4)%3 = (kt+1)%3 (lands next iteration)
     __device__ __forceinline__ void dma3(int kt, int nkt, char* Bimg) {
-        dma_b(clamp(kt + 2, nkt), Bimg);
-        dma_a(clamp(kt + 4, nkt), (kt + 1) % NSLOT);
+        if constexpr (!(kNtAblate & 2)) dma_b(clamp(kt + 2, nkt), Bimg);
+        if constexpr (!(kNtAblate & 4)) dma_a(clamp(kt + 4, nkt), (kt + 1) % NSLOT);
     }
     __device__ __forceinline__ void read_raw3(int kt, float4 (&v)[A_F4]) { read_slot((kt + 2) % NSLOT, v); }
-    __device__ __forceinline__ void split_raw(const float4 (&v)[A_F4], char* Aimg) { put(v, Aimg); }
+    __device__ __forceinline__ void split_raw(const float4 (&v)[A_F4], char* Aimg) {
+        if constexpr (!(kNtAblate & 8)) put(v, Aimg);
+    }
     // everything but this iteration's raw-A DMA (the last A_F4 VM instructions) has landed
     __device__ __forceinline__ void wait3() {
         static_assert(A_F4 <= 63, "vmcnt field");

@@ -636,35 +636,7 @@ __global__ __launch_bounds__(256) void k_composite_bwd(const float* __restrict__
 // wave-per-ray kernels above the kernel was VALU-bound (~40 % of the HBM roofline at
 // 2^20 rays); these keep it on HBM.
 // ---------------------------------------------------------------------------
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float old, float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
-                                                                  CTRL, 0xF, 0xF, false));
-}
-// inclusive product scan over each 16-lane row (row_shr n; lanes without a source keep 1)
-__device__ __forceinline__ float row_scan_mul(float v) {
-    v *= dpp_f<0x111>(1.f, v);
-    v *= dpp_f<0x112>(1.f, v);
-    v *= dpp_f<0x114>(1.f, v);
-    v *= dpp_f<0x118>(1.f, v);
-    return v;
-}
-// inclusive suffix sum over each 16-lane row (row_shl n)
-__device__ __forceinline__ float row_suffix_add(float v) {
-    v += dpp_f<0x101>(0.f, v);
-    v += dpp_f<0x102>(0.f, v);
-    v += dpp_f<0x104>(0.f, v);
-    v += dpp_f<0x108>(0.f, v);
-    return v;
-}
-// sum over each 16-lane row, in every lane (quad_perm [1,0,3,2], [2,3,0,1], half-mirror, mirror)
-__device__ __forceinline__ float row_sum(float v) {
-    v += dpp_f<0xB1>(0.f, v);
-    v += dpp_f<0x4E>(0.f, v);
-    v += dpp_f<0x141>(0.f, v);
-    v += dpp_f<0x140>(0.f, v);
-    return v;
-}
+// (dpp_f, row_scan_mul, row_suffix_add, row_sum: samples.hpp)
 
 template <int J>
 struct Ray16 {

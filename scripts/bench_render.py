@@ -48,8 +48,8 @@ def main():
     from model.official_nerf import OfficialStaticNerf
     from model.render_dist import render_image
     from model.rendering import Renderer
-    from oracle.nerf_oracle import arange_pixels   # pixel grid formula only (common.py:13-40)
-    from tests.helpers import camera_K, make_cfg, rigid_c2w
+    from model.common import arange_pixels
+    from model.synthetic import camera_K, make_cfg, rigid_c2w
     _hip.load_library()
     _hip.gemm_set_precision({"f32": 0, "bf16x6": 1, "f16x3": 2}[args.gemm_precision])
     cfg = make_cfg(hidden=HIDDEN, S=S)
@@ -59,7 +59,7 @@ def main():
     K = camera_K(H, W, FOCAL, FOCAL).to(dev)
     w2c = torch.inverse(rigid_c2w(0)).unsqueeze(0).to(dev)
     scale = torch.eye(4, device=dev).unsqueeze(0)
-    pix = arange_pixels(H, W)[1].to(dev)
+    pix = arange_pixels((H, W), 1, device=dev)[1]
     for _ in range(args.warmup):
         render_image(rnd, pix, K, w2c, scale)
     torch.cuda.synchronize()

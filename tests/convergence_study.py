@@ -18,7 +18,9 @@ held to.  The scene has fine texture (a blurred noise layer over smooth gradient
 fields plateau below the noise-free 45-50 dB regime.  One JSON line per (width, seed) and a
 summary line.
 
-    python scripts/convergence.py [--steps 2000 --seeds 0 1 2 --widths 64 256]
+    python tests/convergence_study.py [--steps 2000 --seeds 0 1 2 --widths 64 256]
+
+(Under tests/: it runs the oracle as the checker, which only tests may do.)
 """
 from __future__ import annotations
 
@@ -73,6 +75,12 @@ def main():
     ap.add_argument("--seeds", type=int, nargs="+", default=[0, 1, 2])
     ap.add_argument("--widths", type=int, nargs="+", default=[64, 256])
     ap.add_argument("--modes", nargs="+", default=list(MODES))
+    ap.add_argument("--lr-milestones", type=float, nargs="*", default=[],
+                    help="fractions of --steps at which every side's Adam learning rate is multiplied by --lr-gamma "
+                         "(the same MultiStepLR on the oracle and the HIP sides; train.py:79-82 uses MultiStepLR too)")
+    ap.add_argument("--lr-gamma", type=float, default=0.3)
+    ap.add_argument("--no-control", dest="control", action="store_false",
+                    help="skip the chunked-oracle control (halves the oracle time)")
     args = ap.parse_args()
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False
@@ -80,7 +88,7 @@ def main():
     from model import _hip
     from model.optim import HipAdam
     from oracle import nerf_oracle as orc
-    from tests.helpers import camera_K, make_cfg, rigid_c2w
+    from model.synthetic import camera_K, make_cfg, rigid_c2w
     _hip.load_library()
     dev = torch.device("cuda:0")
     K = camera_K(H, W, FX, FX).to(dev)
@@ -138,13 +146,16 @@ def main():
                     rgb = torch.cat(rgb, 1)
                 return psnr(((rgb - img_flat) ** 2).mean().item())
 
-            sides_all = ["oracle", "oracle_chunked"] + list(args.modes)
+            sides_all = ["oracle"] + (["oracle_chunked"] if args.control else []) + list(args.modes)
+            milestones = sorted(int(round(f * args.steps)) for f in args.lr_milestones)
+            optims = [opt_o, opt_b] + [sides[m][0].optimizer for m in args.modes]
             curve = {"step": [], **{m: [] for m in sides_all}}
 
             def record(step):
                 curve["step"].append(step)
                 curve["oracle"].append(eval_oracle(ref))
-                curve["oracle_chunked"].append(eval_oracle(ref_b))
+                if args.control:
+                    curve["oracle_chunked"].append(eval_oracle(ref_b))
                 for m in args.modes:
                     curve[m].append(eval_hip(m))
                 print(f"D={D} seed={seed} step {step}: " + "  ".join(f"{m} {curve[m][-1]:.4f}" for m in sides_all),
@@ -153,14 +164,19 @@ def main():
             record(0)
             g = torch.Generator().manual_seed(77 + seed)
             for step in range(1, args.steps + 1):
+                if step - 1 in milestones:                          # MultiStepLR on every side alike
+                    for o in optims:
+                        for grp in o.param_groups:
+                            grp["lr"] *= args.lr_gamma
                 ray_idx = torch.randperm(H * W, generator=g)[:R]
                 while not valid.flatten()[ray_idx].any():          # training.py:280-283
                     ray_idx = torch.randperm(H * W, generator=g)[:R]
                 noise = torch.rand(1, R, S, generator=g)
                 ri, nz = ray_idx.to(dev), noise.to(dev)
                 orc.train_step_render(ref, opt_o, img, depth.unsqueeze(1), K, c2w, scale, ri, nz, cfg["rendering"])
-                orc.train_step_render(ref_b, opt_b, img, depth.unsqueeze(1), K, c2w, scale, ri, nz, cfg["rendering"],
-                                      chunk=min(args.chunk, R * S // 2))
+                if args.control:
+                    orc.train_step_render(ref_b, opt_b, img, depth.unsqueeze(1), K, c2w, scale, ri, nz, cfg["rendering"],
+                                          chunk=min(args.chunk, R * S // 2))
                 for m in args.modes:
                     _hip.gemm_set_precision(MODES[m])
                     tr = sides[m][0]
@@ -177,6 +193,7 @@ def main():
                     if early else None)
             line = {"width": D, "samples": S, "rays": R, "seed": seed, "steps": args.steps, "image": [H, W],
                     "plateau_window_steps": args.window, "plateau_evals": len(win), "plateau_psnr": plateau,
+                    "lr_milestones": milestones, "lr_gamma": args.lr_gamma,
                     "delta_db": {m: plateau[m] - plateau["oracle"] for m in sides_all if m != "oracle"},
                     "oracle_plateau_gain_over_previous_window_db": (plateau["oracle"] - prev) if prev else None,
                     "curve": curve, "seconds": time.time() - t0}

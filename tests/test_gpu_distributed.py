@@ -79,46 +79,55 @@ def _grads(tr):
 
 
 def _spawn(target, world, *args, timeout=300):
+    """Start `world` ranks, collect one report per rank; on any failure the ranks are killed
+    (a rank blocked on a full result pipe would otherwise keep the test process from exiting)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args, daemon=True) for r in range(world)]
     for p in procs:
         p.start()
     import queue
     import time
     res, t0 = {}, time.time()
-    while len(res) < world:
-        try:
-            r, *payload = q.get(timeout=5)
-        except queue.Empty:
-            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
-            assert not dead, f"a rank exited with {dead} before reporting"
-            assert time.time() - t0 < timeout, f"ranks did not report within {timeout} s"
-            continue
-        assert payload[0] != "error", f"rank {r} failed:\n{payload[1]}"
-        res[r] = payload
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    try:
+        while len(res) < world:
+            try:
+                r, *payload = q.get(timeout=5)
+            except queue.Empty:
+                dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+                assert not dead, f"a rank exited with {dead} before reporting"
+                assert time.time() - t0 < timeout, f"ranks did not report within {timeout} s"
+                continue
+            is_err = isinstance(payload[0], str) and payload[0] == "error"
+            assert not is_err, f"rank {r} failed:\n{payload[1]}"
+            res[r] = payload
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
     return res
 
 
-def _guard(body):
-    def run(rank, world, port, q, *args):
-        try:
-            os.environ["MASTER_ADDR"] = "127.0.0.1"
-            os.environ["MASTER_PORT"] = str(port)
-            dist.init_process_group("gloo", rank=rank, world_size=world)
-            torch.cuda.set_device(0)
-            body(rank, world, q, *args)
-            dist.barrier()
-            dist.destroy_process_group()
-        except BaseException:                    # report instead of leaving the parent waiting
-            import traceback
-            q.put((rank, "error", traceback.format_exc()))
-            raise
-    return run
+def _run_rank(rank, world, port, q, body_name, *args):
+    """Rank entry point (module level: spawn pickles it by name): joins the gloo group on
+    127.0.0.1, runs the named body, reports a traceback instead of leaving the parent waiting."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        globals()[body_name](rank, world, q, *args)
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+        raise
 
 
 def _train_body(rank, world, q, case):
@@ -140,8 +149,6 @@ def _train_body(rank, world, q, case):
     q.put((rank, grads, params, in_bucket))
 
 
-_train_rank = _guard(_train_body)
-
 
 def _nrel(a, b):
     a, b = torch.as_tensor(a).double(), torch.as_tensor(b).double()
@@ -154,7 +161,7 @@ def test_hip_train_step_under_process_group_matches_full_batch(dev, case):
     from oracle import nerf_oracle as orc
     _hip.load_library()
     world = 2
-    res = _spawn(_train_rank, world, case)
+    res = _spawn(_run_rank, world, "_train_body", case)
     for r in range(world):
         assert res[r][2], f"rank {r}: NeRF gradients are not views of the all-reduce bucket"
 
@@ -226,12 +233,10 @@ def _render_body(rank, world, q):
     q.put((rank, rgb.cpu().numpy(), depth.cpu().numpy()))
 
 
-_render_rank = _guard(_render_body)
-
 
 def test_full_frame_render_sharded_under_process_group_is_bit_identical(dev):
     world = 2
-    res = _spawn(_render_rank, world)
+    res = _spawn(_run_rank, world, "_render_body")
     from model.render_dist import render_image
     rnd, _, pix, K, w2c, sc, _ = _frame_setup(dev)
     rgb, depth = render_image(rnd, pix, K, w2c, sc)        # no process group: the whole frame in one call

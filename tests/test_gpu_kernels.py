@@ -307,6 +307,7 @@ def test_pack_split_images(dev):
     dst_t = torch.zeros(rows_t, ld_t, device=dev)
     ws = _hip.split_image(rows_s, ld, dev) - 1        # poisoned: every element must be written
     wts = _hip.split_image(rows_t, ld_t, dev) - 1
+    _hip.gemm_set_precision(1)                        # the bf16x3 form (mode 2 writes the fp16 pair)
     _hip.pack_weights([_hip.PackDesc(W.data_ptr(), dst.data_ptr(), dst_t.data_ptr(), rows, cols, ld, rows_t, ld_t,
                                      ws.data_ptr(), wts.data_ptr(), rows_s)])
     torch.cuda.synchronize()
