@@ -401,7 +401,7 @@ __device__ __forceinline__ void bfly_max_dpp(float (&v)[NV], int sl, int& base) 
 //   H (precision mode 2): the accumulators carry the row scales 2^(ea[row] + eb[feature])
 //        (LDS arrays lea / leb, block-local indices), undone first; the row max of the
 //        stored values is max-accumulated into lrm (LDS, float bits) for NTArgs::c_rmax.
-//   lvb (H): the column block's bias (FWD) / v (BWD) staged in LDS by the kernel; a global load
+//   lvb (optional): the column block's bias (FWD) / v (BWD) staged in LDS by the kernel; a global load
 //        issued between the stores would make its wait retire every earlier store first.
 // Diagnostic builds only (make EXTRA=-DNERF_EPI_ABLATE=...; results are wrong): 8 = no
 // output stores (a checksum per lane instead), 16 = no row / column maxima.
@@ -493,7 +493,7 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
             float4 b4[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                b4[q] = H ? *reinterpret_cast<const float4*>(lvb + (fb - n0) + 8 * q)
+                b4[q] = lvb ? *reinterpret_cast<const float4*>(lvb + (fb - n0) + 8 * q)
                       : p.bias ? *reinterpret_cast<const float4*>(p.bias + fb + 8 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
@@ -547,7 +547,7 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
             float4 v4[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                v4[q] = H ? *reinterpret_cast<const float4*>(lvb + (fb - n0) + 8 * q)
+                v4[q] = lvb ? *reinterpret_cast<const float4*>(lvb + (fb - n0) + 8 * q)
                       : p.u ? *reinterpret_cast<const float4*>(p.v + fb + 8 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int i = 0; i < TM; ++i) {

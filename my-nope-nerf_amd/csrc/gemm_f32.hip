@@ -28,7 +28,9 @@ constexpr int BK = 32;
 // ---------------------------------------------------------------------------
 // shared MFMA block: acc[TM][TN] += As[k][wm0..] x Bs[k][wn0..] over BK
 // ---------------------------------------------------------------------------
-template <int TM, int TN, int LDA, int LDB>
+// SWAP: the weight fragment is the MFMA's A operand, so acc[i][j] holds the transposed tile
+// (lanes along samples, registers along features: nt_epilogue_direct's float4 row stores)
+template <int TM, int TN, int LDA, int LDB, bool SWAP = false>
 __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const float* __restrict__ Bs,
                                           int wm0, int wn0, f32x16 (&acc)[TM][TN]) {
     // operands of k-pair kp+1 are read from LDS before the MFMAs of kp issue, so the
@@ -50,7 +52,8 @@ __device__ __forceinline__ void mfma_tile(const float* __restrict__ As, const fl
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[i], rb[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = SWAP ? __builtin_amdgcn_mfma_f32_32x32x2f32(rb[j], ra[i], acc[i][j], 0, 0, 0)
+                                 : __builtin_amdgcn_mfma_f32_32x32x2f32(ra[i], rb[j], acc[i][j], 0, 0, 0);
     };
     rd(0, a0, b0);
 #pragma unroll
@@ -134,21 +137,30 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_nt(NTArgs p) {
     f32x16 acc[TM][TN];
     zero_acc(acc);
 
-    NTEpiPrefetch<BM, BN, NT, EPI> pf;
-
     load_tile(0);
     store_tile(0);
     __syncthreads();
     for (int kt = 0; kt < nkt; ++kt) {
         const int cur = kt & 1;
-        if (kt + 1 < nkt) { if (!(p.ablate & 2)) load_tile(kt + 1); }
-        else pf.load(p, m0, n0);
-        mfma_tile<TM, TN, LDA, LDB>(As(cur), Bs(cur), wm0, wn0, acc);
+        if (kt + 1 < nkt && !(p.ablate & 2)) load_tile(kt + 1);
+        mfma_tile<TM, TN, LDA, LDB, true>(As(cur), Bs(cur), wm0, wn0, acc);
         if (kt + 1 < nkt) store_tile(cur ^ 1);
         __syncthreads();
     }
 
-    nt_epilogue<BM, BN, NT, TM, TN, EPI>(p, acc, smem, m0, n0, wm0, wn0, pf);
+    // operand-swapped accumulators: every lane owns one sample row, four consecutive features
+    // per register quad -> one float4 store each (4x fewer store instructions than one float
+    // per accumulator register; the row-per-lane store tail is issue-bound).  The column
+    // block's bias (FWD) / rank-1 v (BWD) is staged in LDS first (after the last barrier the
+    // image buffers are free): a global load between the stores would wait for all of them.
+    float* lvb = smem;
+    const float* vb = EPI == EPI_FWD ? p.bias : (p.u ? p.v : nullptr);
+    if (vb) {
+        for (int e = tid; e < BN; e += NT) lvb[e] = vb[n0 + e];
+        __syncthreads();
+    }
+    nt_epilogue_direct<TM, TN, EPI>(p, acc, m0, n0, wm0, wn0, nullptr, 0, nullptr, nullptr, nullptr, nullptr, 0,
+                                    nullptr, nullptr, 0, vb ? lvb : nullptr);
 }
 
 // ---------------------------------------------------------------------------

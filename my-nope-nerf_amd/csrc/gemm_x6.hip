@@ -43,6 +43,19 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int XK = 16;   // K per LDS tile
 
+// Diagnostic builds only (make EXTRA=-DNERF_NT_ABLATE=...; results are wrong): the NT main
+// loop without its B-image DMAs (2), its raw-A DMAs (4) or the split VALU of A (8)
+#ifndef NERF_NT_ABLATE
+#define NERF_NT_ABLATE 0
+#endif
+constexpr int kNtAblate = NERF_NT_ABLATE;
+// Experiment (make EXTRA=-DNERF_NT_SPREAD=1): the DMA / split schedule of the NT main loop
+// spread between the MFMAs (x6_mainloop_pf)
+#ifndef NERF_NT_SPREAD
+#define NERF_NT_SPREAD 0
+#endif
+constexpr bool kNtSpread = NERF_NT_SPREAD != 0;
+
 __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
     f32x2 v = {a, b};
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));   // v_cvt_pk_bf16_f32 (RNE)
@@ -231,6 +244,39 @@ __device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int
     stamp(stamps, 1);
 
     auto iter = [&](int kt, uint4 (&ac)[TM][NP], uint4 (&bc)[TN][NP], uint4 (&an)[TM][NP], uint4 (&bn)[TN][NP]) {
+        if constexpr (kNtSpread && H && TM == 2 && TN == 4 && Stager::B_C == 4 && Stager::A_F4 == 2) {
+            // NERF_NT_SPREAD: the split first, then one LDS-DMA piece before each of the first six
+            // 32x32 output tiles' three MFMAs, so a piece's issue cost overlaps the MFMAs in flight
+            // instead of stalling the wave at the top of the k-step
+            char* wimg = smem + (kt & 1) * BUF;
+            const char* nbuf = smem + ((kt + 1) & 1) * BUF;
+            {
+                float4 raw[Stager::A_F4];
+                st.read_raw3(kt, raw);
+                st.split_raw(raw, wimg);
+            }
+            rdB(nbuf, bn);
+            rdA(nbuf, an, 0, 1);
+            const int ktb = st.clamp(kt + 2, nkt), kta = st.clamp(kt + 4, nkt);
+            auto tile = [&](int i, int j) {
+                f32x16 c = acc[i][j];
+                c = mf(ac[i][0], bc[j][1], c);
+                c = mf(ac[i][1], bc[j][0], c);
+                c = mf(ac[i][0], bc[j][0], c);
+                acc[i][j] = c;
+            };
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                if (t < 4) { if constexpr (!(kNtAblate & 2)) st.dma_b_piece(ktb, wimg + IA::BYTES, t); }
+                else if (t < 6) { if constexpr (!(kNtAblate & 4)) st.dma_a_piece(kta, (kt + 1) % Stager::NSLOT, t - 4); }
+                tile(t / TN, t % TN);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            rdA(nbuf, an, 1, 2);
+            st.wait3();
+            __syncthreads();
+            return;
+        }
         char* wimg = smem + (kt & 1) * BUF;
         const char* nbuf = smem + ((kt + 1) & 1) * BUF;
         constexpr int HT = (TM + 1) / 2;
@@ -269,12 +315,6 @@ __device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int
     }
 }
 
-// Diagnostic builds only (make EXTRA=-DNERF_NT_ABLATE=...; results are wrong): the NT main
-// loop without its B-image DMAs (2), its raw-A DMAs (4) or the split VALU of A (8)
-#ifndef NERF_NT_ABLATE
-#define NERF_NT_ABLATE 0
-#endif
-constexpr int kNtAblate = NERF_NT_ABLATE;
 
 // ---------------------------------------------------------------------------
 // NT: C[m][n] = epi( sum_k A[m][k] B[n][k] ).
@@ -309,26 +349,31 @@ struct NTStager {
         raw = raw_ring;
         lea = lds_ea;   // read after the prologue's first barrier (the kernel fills it)
     }
-    __device__ __forceinline__ void dma_a(int kt, int slot) {
+    __device__ __forceinline__ void dma_a_piece(int kt, int slot, int i) {
         const int kk = kt * XK;
         const bool seg1 = kk < k1;
         const float* abase = seg1 ? a1b + kk : a2b + (kk - k1);
         const int lda = seg1 ? lda1 : lda2;
         const int wrow = (threadIdx.x >> 6) * 16;   // first row of this wave's lanes
-#pragma unroll
-        for (int i = 0; i < A_F4; ++i)
-            dma16(abase + (size_t)(r0 + i * RSTEP) * lda + 4 * q0, raw + slot * RAW + (wrow + i * RSTEP) * 64);
+        dma16(abase + (size_t)(r0 + i * RSTEP) * lda + 4 * q0, raw + slot * RAW + (wrow + i * RSTEP) * 64);
     }
-    __device__ __forceinline__ void dma_b(int kt, char* Bimg) {
+    __device__ __forceinline__ void dma_a(int kt, int slot) {
+#pragma unroll
+        for (int i = 0; i < A_F4; ++i) dma_a_piece(kt, slot, i);
+    }
+    __device__ __forceinline__ void dma_b_piece(int kt, char* Bimg, int i) {
         const uint16_t* bt = bsb + (size_t)kt * 16 * bs_rows;
         const int lane = threadIdx.x & 63;
+        const int idx = threadIdx.x + NT * i;
+        const int n = idx % BN, pk = idx / BN;
+        dma16(bt + (((size_t)(pk >> 1) * Kc + (pk & 1)) * bs_rows + n) * 8,
+              Bimg + (pk >> 1) * XImg<BN, NP>::PLANE + (pk & 1) * XImg<BN, NP>::HALF + (n - lane) * 16);
+    }
+    __device__ __forceinline__ void dma_b(int kt, char* Bimg) {
 #pragma unroll
         for (int i = 0; i < B_C; ++i) {
             if (B_C * NT != B_CH && (int)(threadIdx.x & ~63) + NT * i >= B_CH) break;   // wave-uniform
-            const int idx = threadIdx.x + NT * i;
-            const int n = idx % BN, pk = idx / BN;
-            dma16(bt + (((size_t)(pk >> 1) * Kc + (pk & 1)) * bs_rows + n) * 8,
-                  Bimg + (pk >> 1) * XImg<BN, NP>::PLANE + (pk & 1) * XImg<BN, NP>::HALF + (n - lane) * 16);
+            dma_b_piece(kt, Bimg, i);
         }
     }
     __device__ __forceinline__ void read_slot(int slot, float4 (&v)[A_F4]) {
@@ -376,6 +421,11 @@ struct NTStager {
     __device__ __forceinline__ void read_raw3(int kt, float4 (&v)[A_F4]) { read_slot((kt + 2) % NSLOT, v); }
     __device__ __forceinline__ void split_raw(const float4 (&v)[A_F4], char* Aimg) {
         if constexpr (!(kNtAblate & 8)) put(v, Aimg);
+    }
+    // one float4 of the split (NERF_NT_SPREAD schedule)
+    __device__ __forceinline__ void split_piece(const float4 (&v)[A_F4], char* Aimg, int i) {
+        if constexpr (H) put_row4h<BM>(Aimg, r0 + i * RSTEP, q0, v[i], ea[i]);
+        else put_row4<BM>(Aimg, r0 + i * RSTEP, q0, v[i]);
     }
     // everything but this iteration's raw-A DMA (the last A_F4 VM instructions) has landed
     __device__ __forceinline__ void wait3() {

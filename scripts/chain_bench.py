@@ -16,7 +16,7 @@ import torch  # noqa: E402
 
 from model import _hip  # noqa: E402
 from model.official_nerf import OfficialStaticNerf  # noqa: E402
-from tests.helpers import make_cfg  # noqa: E402
+from model.synthetic import make_cfg  # noqa: E402
 
 
 def main():
@@ -33,6 +33,9 @@ def main():
     def fwd(keep=True):
         return runner.forward(o, d, -d, noise, 0.01, 10.0, S, 0, keep=keep)
 
+    if "--fused" in sys.argv:
+        fused_phases(dev, net, runner)
+        return
     for chain in ("1", "0", "1"):
         os.environ["NERF_CHAIN"] = chain
         for keep in (True, False):
@@ -58,6 +61,34 @@ def main():
         med = np.median(st[:, :5], axis=0)
         print(f"keep={keep}: chain phase cycles per block (median over {len(st)} blocks, wave 0): dma wait {med[0]:.0f}  "
               f"barrier {med[1]:.0f}  mfma section {med[2]:.0f}  epilogue {med[3]:.0f}  total {med[4]:.0f}", flush=True)
+
+
+def fused_phases(dev, net, runner):
+    """Per-block phase cycles of the fused per-ray eval kernel at the cfg4 frame size."""
+    R, S = 116748, 128
+    o = (torch.rand(R, 3, device=dev) - 0.5) * 4
+    d = torch.nn.functional.normalize(torch.rand(R, 3, device=dev) - 0.5, dim=-1)
+    fn = lambda: runner.render_eval_fused(o, d, -d, 0.01, 10.0, S, 0)   # noqa: E731
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(3):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    nb = R * S // 128
+    buf = torch.zeros(nb * 6, dtype=torch.int64, device=dev)
+    _hip.lib().nerf_chain_debug_stamps(ctypes.c_void_p(buf.data_ptr()))
+    fn()
+    torch.cuda.synchronize()
+    _hip.lib().nerf_chain_debug_stamps(None)
+    st = buf.cpu().numpy().reshape(-1, 6).astype(np.float64)
+    med = np.median(st[:, :5], axis=0)
+    print(f"fused eval: {s.elapsed_time(e) / 3:.2f} ms/frame; phase cycles per block (median over {len(st)} blocks, "
+          f"wave 0): dma wait {med[0]:.0f}  barrier {med[1]:.0f}  mfma section {med[2]:.0f}  epilogue {med[3]:.0f}  "
+          f"total {med[4]:.0f}", flush=True)
 
 
 if __name__ == "__main__":
