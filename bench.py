@@ -447,8 +447,9 @@ def main():
                            (d["mfma"]["achieved_tflops_f32eq"], d["mfma"]["peak_tflops_f32eq"],
                             "TFLOP/s (f32-equivalent)"))
         traffic, traffic_note = None, None
-        tpath = os.path.join(ROOT, "profiles", "r02", "gemm_traffic.json")
-        if os.path.exists(tpath) and args.gemm_precision == "f16x3":
+        tpath = next((q for q in (os.path.join(ROOT, "profiles", r, "gemm_traffic.json") for r in ("r03", "r02"))
+                      if os.path.exists(q)), "")
+        if tpath and args.gemm_precision == "f16x3":
             # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC
             # passes (FETCH_SIZE x2 + WRITE_SIZE, the guide's gfx950 correction)
             t = json.load(open(tpath))

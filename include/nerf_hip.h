@@ -37,7 +37,7 @@ extern "C" {
 /* ABI version: 5 added nerf_prof_read_kinds and nerf_render_eval_fused, 6 the 4x4-chain
  * backwards (nerf_pose_c2w_bwd, nerf_mat4_inv_bwd, nerf_mat4_mul(_bwd), nerf_unproject_matrix_bwd)
  * and the depth-prior distortion (nerf_depth_affine(_bwd)), 7 nerf_linear_fwd_heads, 8 nerf_heads_bwd_mode. */
-#define NERF_HIP_ABI_VERSION 9
+#define NERF_HIP_ABI_VERSION 10
 int nerf_hip_abi_version(void);
 const char* nerf_hip_last_error(void);
 
@@ -191,6 +191,18 @@ typedef struct {
 } nerf_chain_layer;
 int nerf_mlp_chain_fwd(const float* enc_p, const float* enc_d, const float* enc_p_rmax,
                        const float* enc_d_rmax, int n_pad, const nerf_chain_layer* layers, void* stream);
+/* The training forward chain (official_nerf.py:60-96 under training.py:70-92): the ten
+ * linears of nerf_mlp_chain_fwd in ONE launch at two waves per SIMD, saving what the per-layer
+ * kernels (nerf_linear_fwd) save for the backward -- every layer output (out, mandatory; the
+ * trunk layers' rebuilt from the fp16 pair the next layer consumed, within 2^-22 relative),
+ * the ReLU words (mask, mandatory except for lf, ldmask even) and the per-128-row-group column
+ * maxima (cmax, mandatory except for the colour layer) -- plus raw4 [n_pad][4] = (sigma_raw,
+ * rgb logits) from the density / colour heads in the l7 / colour-layer epilogues (wd [256],
+ * bd [1], wc [3][128] padded, bc [3], as nerf_render_eval_fused).  Encodings and their row
+ * maxima as nerf_encode_samples writes them.  GEMM precision mode 2, hidden width 256. */
+int nerf_mlp_chain_train(const float* enc_p, const float* enc_d, const float* enc_p_rmax, const float* enc_d_rmax,
+                         int n_pad, const nerf_chain_layer* layers, const float* wd, const float* bd, const float* wc,
+                         const float* bc, float* raw4, void* stream);
 /* The fused per-ray eval render (BASELINE.json north_star; rendering.py:36-168 with eval_ /
  * no noise, official_nerf.py:60-119): ONE launch per ray chunk computes, per 128-row block
  * of S-sample rays (S divides 128), the stratified sample positions and both positional

@@ -25,6 +25,8 @@
 #include "gemm.hpp"
 #include "samples.hpp"
 
+#include <cstdlib>
+
 namespace nerf {
 namespace {
 
@@ -98,6 +100,7 @@ struct ChainFwdArgs {
     const float* wd; const float* bd;   // fc_density weight [256], bias [1]
     const float* wc; const float* bc;   // fc_rgb weight padded [3][128], bias [3]
     float* rgb; float* dist; float* alpha; float* z;   // [R][3], [R], [R][S], [R*S]
+    float* raw4;                                       // training chain: [n_pad][4] head outputs
 };
 
 constexpr int kbase(int l) { return l == 0 ? 0 : kbase(l - 1) + L_KS[l - 1]; }
@@ -288,16 +291,16 @@ __device__ __forceinline__ void enc_frags(ChainState& st, int rl) {
 // live in LDS, one 36-float record per ray (fx + FX_ENCD): the view direction is per ray,
 // so 128 / S records serve the block's 128 rows
 constexpr int FX_RAW = 640, FX_Z = 1152, FX_ENCD = 1280, ENCD_REC = 36;
-__device__ __forceinline__ void fused_encode_d(const ChainFwdArgs& p, ChainState& st) {
+__device__ __forceinline__ void fused_encode_d(const ChainFwdArgs& p, float* fx, int tid, size_t m0) {
     const int nr = CROWS / p.S;
-    if (st.tid >= nr) return;
-    const size_t ray = st.m0 / (size_t)p.S + st.tid;
+    if (tid >= nr) return;
+    const size_t ray = m0 / (size_t)p.S + tid;
     float d[3] = {0.f, 0.f, 0.f};
     if (ray < (size_t)p.R) {
 #pragma unroll
         for (int c = 0; c < 3; ++c) d[c] = p.view[3 * ray + c];
     }
-    float* rec = st.fx + FX_ENCD + ENCD_REC * st.tid;
+    float* rec = fx + FX_ENCD + ENCD_REC * tid;
     float m = 0.f;
 #pragma unroll
     for (int c = 0; c < 3; ++c) { rec[c] = d[c]; m = fmaxf(m, fabsf(d[c])); }
@@ -553,14 +556,14 @@ __device__ __forceinline__ void fused_encode_p(const ChainFwdArgs& p, ChainState
 // row per ray, lane l owning samples [l J, l J + J) (J = max(1, S / 16)); transmittance by a
 // row prefix-product scan, the sums by row butterflies; each lane stores its J alphas as
 // contiguous float4s (a ray's S alphas are one contiguous run across its row)
-template <int J>
-__device__ __forceinline__ void fused_composite16(const ChainFwdArgs& p, const ChainState& st) {
+template <int J, int NTH>
+__device__ __forceinline__ void fused_composite16(const ChainFwdArgs& p, const float* fx, int tid, size_t m0) {
     const int S = p.S;
     const int nr = CROWS / S;
-    const int l16 = st.tid & 15;
-    for (int rb = 0; rb < nr; rb += 16) {          // 16 rays per pass of the block
-        const int rloc = rb + (st.tid >> 4);
-        const size_t ray = st.m0 / (size_t)S + rloc;
+    const int l16 = tid & 15;
+    for (int rb = 0; rb < nr; rb += NTH / 16) {    // NTH / 16 rays per pass of the block
+        const int rloc = rb + (tid >> 4);
+        const size_t ray = m0 / (size_t)S + rloc;
         const bool active = rloc < nr && ray < (size_t)p.R;   // whole 16-lane rows are (in)active
         const int i0 = l16 * J;
         float al[J], T[J], c[J][3], z[J];
@@ -573,11 +576,11 @@ __device__ __forceinline__ void fused_composite16(const ChainFwdArgs& p, const C
             float a = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f, zz = 0.f;
             if (valid[j]) {
                 const int e = rloc * S + i;
-                const float4 r = *reinterpret_cast<const float4*>(st.fx + FX_RAW + 4 * e);
-                zz = st.fx[FX_Z + e];
+                const float4 r = *reinterpret_cast<const float4*>(fx + FX_RAW + 4 * e);
+                zz = fx[FX_Z + e];
                 const float sg = f_density(r.x, p.flags);
                 if (p.flags & F_DIST_ALPHA)
-                    a = i == S - 1 ? 1.f : 1.f - __expf(-1.0f * sg * (st.fx[FX_Z + e + 1] - zz));   // rendering.py:116-122
+                    a = i == S - 1 ? 1.f : 1.f - __expf(-1.0f * sg * (fx[FX_Z + e + 1] - zz));   // rendering.py:116-122
                 else
                     a = 1.f - __expf(-1.0f * sg);
                 c0 = f_sigmoid(r.y); c1 = f_sigmoid(r.z); c2 = f_sigmoid(r.w);
@@ -623,11 +626,12 @@ __device__ __forceinline__ void fused_composite16(const ChainFwdArgs& p, const C
     }
 }
 
-__device__ __forceinline__ void fused_composite(const ChainFwdArgs& p, const ChainState& st) {
-    if (p.S >= 128) fused_composite16<8>(p, st);
-    else if (p.S >= 64) fused_composite16<4>(p, st);
-    else if (p.S >= 32) fused_composite16<2>(p, st);
-    else fused_composite16<1>(p, st);
+template <int NTH>
+__device__ __forceinline__ void fused_composite(const ChainFwdArgs& p, const float* fx, int tid, size_t m0) {
+    if (p.S >= 128) fused_composite16<8, NTH>(p, fx, tid, m0);
+    else if (p.S >= 64) fused_composite16<4, NTH>(p, fx, tid, m0);
+    else if (p.S >= 32) fused_composite16<2, NTH>(p, fx, tid, m0);
+    else fused_composite16<1, NTH>(p, fx, tid, m0);
 }
 
 template <bool F>
@@ -664,7 +668,7 @@ __global__ __launch_bounds__(256) void k_mlp_chain_fwd(ChainFwdArgs p) {
         st.fx[st.tid] = p.wd[st.tid];
         for (int e = st.tid; e < 384; e += 256) st.fx[256 + e] = p.wc[e];
         fused_encode_p(p, st);
-        fused_encode_d(p, st);
+        fused_encode_d(p, st.fx, st.tid, st.m0);
     }
     // step 0's group (with the enc_p tile and the row maxima) landed, published to the block
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(dma_count(1, F) + dma_count(2, F) + dma_count(3, F)) : "memory");
@@ -686,13 +690,590 @@ __global__ __launch_bounds__(256) void k_mlp_chain_fwd(ChainFwdArgs p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every DMA landed before the LDS is released
     if constexpr (F) {
         __syncthreads();   // every row's raw4 in LDS
-        fused_composite(p, st);
+        fused_composite<256>(p, st.fx, st.tid, st.m0);
     }
     if (p.stamps && st.tid == 0) {
         unsigned long long* o = p.stamps + (size_t)blockIdx.x * 6;
         o[0] = st.t_wait; o[1] = st.t_bar; o[2] = st.t_mma; o[3] = st.t_epi;
         o[4] = __builtin_amdgcn_s_memtime() - t_start; o[5] = __builtin_amdgcn_s_memrealtime();
     }
+}
+
+// ---------------------------------------------------------------------------
+// The fused per-ray eval kernel at two waves per SIMD (k_render_fused2, the default of
+// nerf_render_eval_fused).  Same per-ray path as k_mlp_chain_fwd<true> -- samples and
+// encodings in the prologue, the ten linears with the activations resident in registers,
+// the heads in the l7 / colour-layer epilogues, the composite at the end -- but a block's 128
+// rows are 8 waves x 16 rows on v_mfma_f32_16x16x32_f16 instead of 4 waves x 32 rows on
+// 32x32x16: a wave's accumulators (16 rows x 256 outputs) and its A operand (16 rows x 256
+// as fp16 pairs) are 64 + 64 registers, so the kernel fits 256 registers and two waves share
+// each SIMD -- one wave's epilogue (unscale, bias, ReLU, re-split: VALU) runs beside the
+// other wave's MFMAs instead of leaving the matrix pipe idle (the 32-row kernel spends a
+// third of its cycles in epilogues at one wave per SIMD, profiles/r03/fused_eval_phases.txt).
+//
+// Operand-swapped 16x16x32 MFMAs: A = a weight fragment (lane l: feature l & 15, k = 8 (l >> 4)
+// .. + 7), B = an activation fragment (sample l & 15, the same k), so D[feature][sample] puts
+// sample l & 15 in lane l with features 4 (l >> 4) .. + 3 of the 16-feature tile.  The next
+// layer's fragment for k-step t needs features 32 t + 8 (l >> 4) .. + 7 of the lane's sample:
+// tiles 2 t and 2 t + 1 are re-split to fp16 pairs and moved between the 16-lane rows by one
+// v_permlane32_swap and one v_permlane16_swap per word (rows (A0 A1 A2 A3 | B0 B1 B2 B3) ->
+// (A0 A1 | A2 A3 | B0 B1 | B2 B3) pairs).
+// ---------------------------------------------------------------------------
+namespace f2 {
+constexpr int NW = 8;                   // waves per block, two per SIMD
+constexpr int NTH = 64 * NW;            // threads
+constexpr int SHALF = 256 * 16;         // one k-half of a slot: 256 image rows x 16 B, unpadded (the
+                                        // 16x16x32 fragment reads are conflict-free without a pad)
+constexpr int SPLANE = 2 * SHALF;
+constexpr int SBYTES = 2 * SPLANE;      // 16 KB per 16-k step (fp16 hi / lo planes)
+constexpr int FX_WD = 0, FX_WC = 256;   // fc_density weight [256], fc_rgb weight [3][128]
+
+// LDS map.  Eval: a 6-slot weight ring (two 32-k steps in flight) and the position-encoding
+// tile the prologue computes.  Training (TR): the encodings come from HBM, so their 32 KB go
+// to two more ring slots (three 32-k steps in flight: a store issued beside a k-step's
+// MFMAs has three k-steps to complete before a wait counts it, see wait_n) and the column
+// maxima of the block's 128-row group ([2 parities][256] uint, LDS atomics)
+template <bool TR>
+struct LY {
+    static constexpr int NSLOT = TR ? 8 : 6;
+    static constexpr int D = NSLOT / 2 - 1;                   // 32-k steps in flight
+    static constexpr int O_RING = 0;
+    static constexpr int O_LEB = NSLOT * SBYTES;              // [2][256][16 B] weight-row exponent chunks
+    static constexpr int O_EXP = O_LEB + 2 * 256 * 16;        // [2][256] int: the exponents, compact
+    static constexpr int O_BIAS = O_EXP + 2 * 256 * 4;        // [2][256] float
+    static constexpr int O_ENC = O_BIAS + 2 * 256 * 4;        // eval: [128][64] float position encodings
+    static constexpr int O_CMX = O_ENC;                       // training: [2][256] uint column maxima
+    static constexpr int O_RMX = O_ENC + (TR ? 2 * 256 * 4 : 128 * 64 * 4);   // eval: [4][128] row maxima
+    static constexpr int O_FX = O_RMX + 4 * 128 * 4;          // head weights, raw4 / z rows, view records
+    static constexpr int FX_FLOATS = TR ? FX_ENCD : FX_ENCD + (CROWS / 2) * ENCD_REC;
+    static constexpr int BYTES = O_FX + FX_FLOATS * 4;
+    static_assert(BYTES <= 160 * 1024, "LDS");
+};
+
+constexpr int layer_of(int tt) { int i = 0; while (i + 1 < CNL && kbase(i + 1) <= tt) ++i; return i; }
+constexpr int dma_count(int tt) {
+    return tt >= CT ? 0 : (L_OUT[layer_of(tt)] == 256 ? 2 : 1) + (kbase(layer_of(tt)) == tt ? 1 : 0);
+}
+
+#ifndef NERF_TRAIN_ABLATE
+#define NERF_TRAIN_ABLATE 0   // diagnostic builds only: 1 no activation stores, 2 no ReLU words / column maxima
+#endif
+constexpr int kTrAblate = NERF_TRAIN_ABLATE;
+
+// the counted waits.  Every 32-k step k (global over the chain) waits for the DMAs issued D
+// steps earlier; vmcnt counts loads, stores and LDS-DMA together in issue order, so the count
+// is every vector-memory op the wave issued after them: the later steps' DMAs and, in the
+// training kernel, the stores each step issues after its DMAs (the previous layer's
+// activation pieces, its ReLU words at step 7, at a layer's first step the column maxima of
+// the layer before).  Ops left out of the count only make a wait stricter.
+constexpr int nks(int l) { return L_KS[l] / 2; }
+constexpr int kfirst(int l) { return l == 0 ? 0 : kfirst(l - 1) + nks(l - 1); }
+constexpr int layer_of_k(int k) { int l = 0; while (l + 1 < CNL && kfirst(l + 1) <= k) ++l; return l; }
+constexpr int tt_of_k(int k) { return kbase(layer_of_k(k)) + 2 * (k - kfirst(layer_of_k(k))); }
+template <bool TR>
+constexpr int dma_ops_k(int k) {
+    return dma_count(tt_of_k(k) + 2 * LY<TR>::D) + dma_count(tt_of_k(k) + 2 * LY<TR>::D + 1);
+}
+template <bool TR>
+constexpr int st_ops_k(int k) {
+    const int l = layer_of_k(k), u = k - kfirst(l);
+    if (!TR || l == 0) return 0;
+    return (u < 8 && !(kTrAblate & 1) ? 2 : 0) + (u == 7 && l - 1 != 8 && !(kTrAblate & 2) ? 1 : 0) +
+           (u == 0 && l >= 2 && !(kTrAblate & 2) ? 1 : 0);
+}
+template <bool TR>
+constexpr int wait_n(int k) {
+    constexpr int D = LY<TR>::D;
+    int n = k >= D ? st_ops_k<TR>(k - D) : 0;
+    for (int i = (k - D + 1 > 0 ? k - D + 1 : 0); i < k; ++i) n += dma_ops_k<TR>(i) + st_ops_k<TR>(i);
+    if (k < D)
+        for (int t = 2 * k + 2; t < 2 * D; ++t) n += dma_count(t);
+    return n;
+}
+static_assert(wait_n<false>(5) == dma_count(kbase(1) + 6 + 2) + dma_count(kbase(1) + 6 + 3), "eval waits");
+static_assert(wait_n<false>(0) == dma_count(2) + dma_count(3), "eval waits");
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma16(const uint4& w, const uint4& a, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(ch16x8, w), __builtin_bit_cast(ch16x8, a), c,
+                                                  0, 0, 0);
+}
+// pins a value's computation here (the compiler may not sink it past the LDS-DMA issue)
+__device__ __forceinline__ void opaque(uint4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+// OR over the four 16-lane rows
+__device__ __forceinline__ uint32_t rows_or(uint32_t v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    const uint32_t r = a[0] | a[1];
+    const auto b = __builtin_amdgcn_permlane32_swap(r, r, false, false);
+    return b[0] | b[1];
+}
+
+struct State {
+    char* lds;
+    float* fx;
+    int tid, wave, lane, n, g;          // n = lane & 15 (the lane's sample in the wave), g = lane >> 4
+    size_t m0;
+    int rl;                             // the lane's row in the block (16 wave + n)
+    int er;                             // row exponent of the current A operand
+    uint32_t mk0, mk1;                  // training: the lane's two ReLU words of the previous layer
+    uint4 act_hi[8], act_lo[8];         // A operand: 8 k-steps of 32 (the 256 activations)
+    uint4 enc_hi[2], enc_lo[2];         // encoding segment (64 columns) of the current layer
+    f32x4 acc[16];                      // 16 rows x 256 outputs
+};
+
+// global 16-k step TT -> ring slot TT % NSLOT (2 pieces per wave; 1 for the 128-row colour
+// layer) + at a layer's first step one piece per wave: waves 0-3 the weight-row exponents
+// (64 image rows each), waves 4-7 the biases (16 lanes x 4 floats each); the 128-wide layer's
+// extra waves repeat the first ones (same bytes to the same place), so every wave issues the
+// same count (its vmcnt waits are compile-time)
+template <int TT, bool TR>
+__device__ __forceinline__ void dma(const ChainFwdArgs& p, State& st) {
+    using Y = LY<TR>;
+    if constexpr (TT < CT) {
+        constexpr int l = layer_of(TT);
+        constexpr int s = TT - kbase(l);
+        constexpr int ks = L_KS[l];
+        constexpr int NO = L_OUT[l];
+        const nerf_chain_layer& L = p.L[l];
+        char* slot = st.lds + Y::O_RING + (TT % Y::NSLOT) * SBYTES;
+#pragma unroll
+        for (int i = 0; i < (NO == 256 ? 2 : 1); ++i) {
+            const int c = st.tid + NTH * i;              // 16-byte chunk of the step's image rows
+            const int ph = c / NO, n = c % NO;           // plane * 2 + k-half (wave-uniform), image row
+            const uint32_t off = (uint32_t)(((ph >> 1) * (2 * ks) + 2 * s + (ph & 1)) * L.img_rows + n) * 16;
+            cdma16(L.img, off, slot + ph * SHALF + (n - st.lane) * 16);
+        }
+        if constexpr (s == 0) {
+            if (st.wave < 4) {
+                const int wr = NO == 256 ? st.wave : (st.wave & 1);
+                const int n = 64 * wr + st.lane;
+                cdma16(L.img, (uint32_t)((2 * (2 * ks) * L.img_rows + n) * 16),
+                       st.lds + Y::O_LEB + (l & 1) * 4096 + 64 * wr * 16);
+            } else if (st.lane < 16) {                   // one instruction, lanes 0-15 active
+                const int wb = NO == 256 ? st.wave - 4 : ((st.wave - 4) & 1);
+                cdma16(L.bias, (uint32_t)((64 * wb + 4 * st.lane) * 4),
+                       st.lds + Y::O_BIAS + ((l & 1) * 256 + 64 * wb) * 4);
+            } else {
+                // the other lanes of the bias instruction: masked off (the instruction is one
+                // vmcnt op for the wave either way)
+            }
+        }
+    }
+}
+
+template <int T0, int N, bool TR>
+__device__ __forceinline__ void dma_n(const ChainFwdArgs& p, State& st) {
+    if constexpr (N > 0) {
+        dma<T0, TR>(p, st);
+        dma_n<T0 + 1, N - 1, TR>(p, st);
+    }
+}
+
+// the 8 consecutive encoding columns of this lane's k-chunk for k-step t (32 columns) of a
+// row, at exponent er -> fragment planes
+__device__ __forceinline__ void enc_frag(const float* row, int t, int g, int er, uint4& hi, uint4& lo) {
+    const float4* src = reinterpret_cast<const float4*>(row + 32 * t + 8 * g);
+    frag_from8(src[0], src[1], er, hi, lo);
+}
+
+// training: the previous layer's output features 32 u + 8 g .. + 7 of the lane's row, rebuilt
+// from the fp16 pair this k-step feeds the MFMAs ((hi + lo) 2^-e: the value this layer
+// consumed, within 2^-22 relative of the f32 epilogue result) -> stored, its ReLU bits (word u,
+// bits 8 g ..) and its column maxima over the wave's 16 rows (a quad max by DPP, then LDS
+// atomics from the quads' first lanes).  The work is spread over the step's MFMA tiles (piece
+// j after tile j's MFMAs): the two waves of a SIMD reach their k-steps together, so short VALU
+// pieces between MFMA groups keep the matrix pipe fed where one block of VALU would not
+__device__ __forceinline__ float rebuilt(const uint4& ah, const uint4& al, int k, int er) {
+    const ch16x2 h = __builtin_bit_cast(ch16x2, (&ah.x)[k >> 1]);
+    const ch16x2 o = __builtin_bit_cast(ch16x2, (&al.x)[k >> 1]);
+    return __builtin_amdgcn_ldexpf((float)h[k & 1] + (float)o[k & 1], -er);
+}
+template <int l, int u, int j, int ntj>
+__device__ __forceinline__ void save_piece(const ChainFwdArgs& p, State& st, const uint4& ah, const uint4& al,
+                                           uint32_t& bits) {
+    using Y = LY<true>;
+    const nerf_chain_layer& P = p.L[l - 1];
+    if constexpr (j == 1 || j == 2) {           // 4 features: store, ReLU bits
+        constexpr int k0 = 4 * (j - 1);
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = rebuilt(ah, al, k0 + k, st.er);
+        if constexpr (!(kTrAblate & 1))
+            *reinterpret_cast<float4*>(P.out + (st.m0 + st.rl) * P.ldo + 32 * u + 8 * st.g + k0) =
+                make_float4(v[0], v[1], v[2], v[3]);
+        if constexpr (!(kTrAblate & 2) && l - 1 != 8) {   // lf has no ReLU
+#pragma unroll
+            for (int k = 0; k < 4; ++k) bits |= (v[k] > 0.f ? 1u : 0u) << (k0 + k);
+            if constexpr (j == 2) {
+                const uint32_t w = rows_or(bits << (8 * st.g));
+                if constexpr (u & 1) st.mk1 = st.g == (u >> 1) ? w : st.mk1;
+                else st.mk0 = st.g == (u >> 1) ? w : st.mk0;
+                if constexpr (u == 7)
+                    *reinterpret_cast<uint2*>(P.mask + (st.m0 + st.rl) * P.ldmask + 2 * st.g) =
+                        make_uint2(st.mk0, st.mk1);
+            }
+        }
+    }
+    if constexpr (!(kTrAblate & 2) && j >= 3) {   // column maxima: one feature per tile (two for 8 tiles)
+        constexpr int per = ntj >= 11 ? 1 : 2;
+        constexpr int k0 = (j - 3) * per;
+        uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + Y::O_CMX) + ((l - 1) & 1) * 256 + 32 * u + 8 * st.g;
+#pragma unroll
+        for (int k = k0; k < k0 + per && k < 8; ++k) {
+            float c = fabsf(rebuilt(ah, al, k, st.er));
+            c = fmaxf(c, dpp_f<0xB1>(0.f, c));
+            c = fmaxf(c, dpp_f<0x4E>(0.f, c));
+            if ((st.n & 3) == 0) atomicMax(cm + k, __float_as_uint(c));
+        }
+    }
+}
+
+// tile j of a k-step (compile-time j, so the save pieces are placed between MFMA groups)
+template <int l, int u, bool TR, int j, int ntj, int nact>
+__device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, const uint4& ah, const uint4& al,
+                                            const char* base, uint4 (&wh)[2], uint4 (&wl)[2], uint32_t& bits) {
+    if constexpr (j < ntj) {
+        if constexpr (j + 1 < ntj) {
+            wh[(j + 1) & 1] = *reinterpret_cast<const uint4*>(base + 256 * (j + 1));
+            wl[(j + 1) & 1] = *reinterpret_cast<const uint4*>(base + 256 * (j + 1) + SPLANE);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        st.acc[j] = mfma16(wh[j & 1], al, st.acc[j]);   // hi . lo
+        st.acc[j] = mfma16(wl[j & 1], ah, st.acc[j]);   // lo . hi
+        st.acc[j] = mfma16(wh[j & 1], ah, st.acc[j]);   // hi . hi
+        if constexpr (TR && u < nact) save_piece<l, u, j, ntj>(p, st, ah, al, bits);
+        __builtin_amdgcn_sched_barrier(0);
+        mstep_tiles<l, u, TR, j + 1, ntj, nact>(p, st, ah, al, base, wh, wl, bits);
+    }
+}
+
+// one 32-k MFMA step u of layer l (16-k steps TT, TT + 1): wait for its two slots, publish
+// them, refill the two slots step u - 1 read, 16 or 8 feature tiles x 3 products; training:
+// at the first step the column maxima of layer l - 2 leave LDS, and the steps from the
+// register tile save the previous layer's output (save_prev) beside the MFMAs
+template <int l, int u, bool TR>
+__device__ __forceinline__ void kstep(const ChainFwdArgs& p, State& st) {
+    using Y = LY<TR>;
+    constexpr int TT = kbase(l) + 2 * u;
+    constexpr int nact = l == 0 ? 0 : 8;         // k-steps from the register tile, then the encoding
+    constexpr int ntj = L_OUT[l] / 16;
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_n<TR>(kfirst(l) + u)) : "memory");
+    __syncthreads();
+    dma<TT + 2 * Y::D, TR>(p, st);
+    dma<TT + 2 * Y::D + 1, TR>(p, st);
+    if constexpr (u == 0) {
+        // this layer's exponents (landed with step TT) into the compact array; published to the
+        // epilogue by the next step's barrier (every layer has at least two 32-k steps)
+        if (st.tid < L_OUT[l])
+            reinterpret_cast<int*>(st.lds + Y::O_EXP)[(l & 1) * 256 + st.tid] =
+                *reinterpret_cast<const int*>(st.lds + Y::O_LEB + (l & 1) * 4096 + st.tid * 16);
+        if constexpr (TR && l >= 2 && !(kTrAblate & 2)) {
+            // layer l - 2's column maxima over the block's 128 rows (its 128-row group), complete
+            // since layer l - 1's last step: wave w stores features 32 w .. + 31 and clears them
+            if (st.lane < 32) {
+                uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + Y::O_CMX) + (l & 1) * 256 + 32 * st.wave + st.lane;
+                p.L[l - 2].cmax[(st.m0 / CROWS) * L_OUT[l - 2] + 32 * st.wave + st.lane] = __uint_as_float(*cm);
+                *cm = 0u;
+            }
+        }
+    }
+    const uint4& ah = u < nact ? st.act_hi[u < nact ? u : 0] : st.enc_hi[u < nact ? 0 : u - nact];
+    const uint4& al = u < nact ? st.act_lo[u < nact ? u : 0] : st.enc_lo[u < nact ? 0 : u - nact];
+    // lane (g, n) reads k-chunk g: slot of step TT + (g >> 1), k-half g & 1, image row 16 j + n
+    const char* s0 = st.lds + Y::O_RING + (TT % Y::NSLOT) * SBYTES;
+    const char* s1 = st.lds + Y::O_RING + ((TT + 1) % Y::NSLOT) * SBYTES;
+    const char* base = ((st.g >> 1) ? s1 : s0) + (st.g & 1) * SHALF + st.n * 16;
+    // weight fragments one tile ahead of their MFMAs (the next tile's reads have the three
+    // MFMAs of this one, ~48 cycles x 2 waves, to land)
+    uint4 wh[2], wl[2];
+    wh[0] = *reinterpret_cast<const uint4*>(base);
+    wl[0] = *reinterpret_cast<const uint4*>(base + SPLANE);
+    uint32_t bits = 0;
+    mstep_tiles<l, u, TR, 0, ntj, nact>(p, st, ah, al, base, wh, wl, bits);
+}
+
+template <int l, int u, bool TR>
+__device__ __forceinline__ void ksteps(const ChainFwdArgs& p, State& st) {
+    if constexpr (2 * u < L_KS[l]) {
+        kstep<l, u, TR>(p, st);
+        ksteps<l, u + 1, TR>(p, st);
+    }
+}
+
+// layer l: k-loop, epilogue (feature f = 16 j + 4 g + i of the lane's sample), heads, next A.
+// Training: the colour layer stores its f32 output and ReLU words here (no later layer
+// consumes it; every other layer's are saved by the next layer's k-steps)
+template <int l, bool TR>
+__device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
+    using Y = LY<TR>;
+    constexpr int ntj = L_OUT[l] / 16;
+    constexpr bool relu = l != 8;
+    constexpr bool head_d = l == 7, head_c = l == CNL - 1;
+    constexpr bool last_tr = TR && l == CNL - 1;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) st.acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    ksteps<l, 0, TR>(p, st);
+    // the lane's feature offset, opaque per layer: otherwise the exponent / bias addresses of
+    // the even (odd) layers are computed once and kept live -- spilled -- across the chain
+    int g4 = 4 * st.g;
+    asm volatile("" : "+v"(g4));
+    const int* le = reinterpret_cast<const int*>(st.lds + Y::O_EXP) + (l & 1) * 256 + g4;
+    const float* lb = reinterpret_cast<const float*>(st.lds + Y::O_BIAS) + (l & 1) * 256 + g4;
+    float rmx = 0.f, hs0 = 0.f, hs1 = 0.f, hs2 = 0.f;
+    uint32_t mw = 0;
+#pragma unroll
+    for (int j = 0; j < ntj; ++j) {
+        // one tile at a time: the barrier keeps the exponent / bias / head-weight reads from
+        // being hoisted into one register burst (two waves per SIMD leave 256 registers)
+        __builtin_amdgcn_sched_barrier(0);
+        const int f0 = 16 * j + g4;
+        const int4 e4 = *reinterpret_cast<const int4*>(le + 16 * j);
+        const float4 b4 = *reinterpret_cast<const float4*>(lb + 16 * j);
+        f32x4 x;
+        x[0] = __builtin_amdgcn_ldexpf(st.acc[j][0], -(st.er + e4.x)) + b4.x;
+        x[1] = __builtin_amdgcn_ldexpf(st.acc[j][1], -(st.er + e4.y)) + b4.y;
+        x[2] = __builtin_amdgcn_ldexpf(st.acc[j][2], -(st.er + e4.z)) + b4.z;
+        x[3] = __builtin_amdgcn_ldexpf(st.acc[j][3], -(st.er + e4.w)) + b4.w;
+        if (relu) {
+            x[0] = fmaxf(x[0], 0.f); x[1] = fmaxf(x[1], 0.f); x[2] = fmaxf(x[2], 0.f); x[3] = fmaxf(x[3], 0.f);
+        }
+        st.acc[j] = x;
+        rmx = fmaxf(rmx, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+        if constexpr (last_tr) {   // hr (the f32 epilogue value, as the per-layer kernel) and its ReLU words
+            const nerf_chain_layer& L = p.L[l];
+            *reinterpret_cast<float4*>(L.out + (st.m0 + st.rl) * L.ldo + f0) = make_float4(x[0], x[1], x[2], x[3]);
+            mw |= ((x[0] > 0.f ? 1u : 0u) | (x[1] > 0.f ? 2u : 0u) | (x[2] > 0.f ? 4u : 0u) | (x[3] > 0.f ? 8u : 0u))
+                  << ((j & 1) * 16 + g4);
+            if (j & 1) {
+                const uint32_t w = rows_or(mw);          // word j / 2 of the row, in every row of lanes
+                if ((j >> 1) & 1) st.mk1 = st.g == (j >> 2) ? w : st.mk1;
+                else st.mk0 = st.g == (j >> 2) ? w : st.mk0;
+                mw = 0;
+            }
+        }
+        if constexpr (head_d) {              // sigma_raw = fc_density(h8) (official_nerf.py:66)
+            const float4 w = *reinterpret_cast<const float4*>(st.fx + FX_WD + f0);
+            hs0 += x[0] * w.x + x[1] * w.y + x[2] * w.z + x[3] * w.w;
+        }
+        if constexpr (head_c) {              // rgb logits = fc_rgb(hr) (official_nerf.py:91)
+            const float4 w0 = *reinterpret_cast<const float4*>(st.fx + FX_WC + f0);
+            const float4 w1 = *reinterpret_cast<const float4*>(st.fx + FX_WC + 128 + f0);
+            const float4 w2 = *reinterpret_cast<const float4*>(st.fx + FX_WC + 256 + f0);
+            hs0 += x[0] * w0.x + x[1] * w0.y + x[2] * w0.z + x[3] * w0.w;
+            hs1 += x[0] * w1.x + x[1] * w1.y + x[2] * w1.z + x[3] * w1.w;
+            hs2 += x[0] * w2.x + x[1] * w2.y + x[2] * w2.z + x[3] * w2.w;
+        }
+    }
+    if constexpr (last_tr && !(kTrAblate & 2)) {
+        const nerf_chain_layer& L = p.L[l];
+        if (2 * st.g < L_OUT[l] / 32)
+            *reinterpret_cast<uint2*>(L.mask + (st.m0 + st.rl) * L.ldmask + 2 * st.g) = make_uint2(st.mk0, st.mk1);
+    }
+    // the four 16-lane rows hold one sample's features: reduce across them (lanes n, n + 16,
+    // n + 32, n + 48)
+    if constexpr (head_d || head_c) {
+        float* raw = st.fx + FX_RAW + 4 * st.rl;
+        hs0 += __shfl_xor(hs0, 16, 64);
+        hs0 += __shfl_xor(hs0, 32, 64);
+        if constexpr (head_d) {
+            if (st.g == 0) raw[0] = hs0 + p.bd[0];
+        } else {
+            hs1 += __shfl_xor(hs1, 16, 64);
+            hs1 += __shfl_xor(hs1, 32, 64);
+            hs2 += __shfl_xor(hs2, 16, 64);
+            hs2 += __shfl_xor(hs2, 32, 64);
+            if (st.g == 0) {
+                raw[1] = hs0 + p.bc[0];
+                raw[2] = hs1 + p.bc[1];
+                raw[3] = hs2 + p.bc[2];
+            }
+        }
+    }
+    if constexpr (l < CNL - 1) {
+        // next layer's A operand: row exponent over the row's 256 features (and the encoding
+        // the next layer joins), fp16 pairs, rows exchanged into the fragment layout
+        float m = fmaxf(rmx, __shfl_xor(rmx, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        const float* drec = st.fx + FX_ENCD + ENCD_REC * (st.rl / p.S);
+        if constexpr (l == 3) {
+            if constexpr (TR) {
+                m = fmaxf(m, p.rp[st.m0 + st.rl]);
+            } else {
+                const float* rp = reinterpret_cast<const float*>(st.lds + Y::O_RMX);
+                m = fmaxf(m, fmaxf(fmaxf(rp[st.rl], rp[128 + st.rl]), fmaxf(rp[256 + st.rl], rp[384 + st.rl])));
+            }
+        }
+        if constexpr (l == 8) m = fmaxf(m, TR ? p.rd[st.m0 + st.rl] : drec[32]);
+        st.er = row_exp(m);
+        const int e = st.er;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            __builtin_amdgcn_sched_barrier(0);
+            const f32x4 A = st.acc[2 * t], B = st.acc[2 * t + 1];
+            uint32_t ha0, la0, ha1, la1, hb0, lb0, hb1, lb1;
+            csplit(__builtin_amdgcn_ldexpf(A[0], e), __builtin_amdgcn_ldexpf(A[1], e), ha0, la0);
+            csplit(__builtin_amdgcn_ldexpf(A[2], e), __builtin_amdgcn_ldexpf(A[3], e), ha1, la1);
+            csplit(__builtin_amdgcn_ldexpf(B[0], e), __builtin_amdgcn_ldexpf(B[1], e), hb0, lb0);
+            csplit(__builtin_amdgcn_ldexpf(B[2], e), __builtin_amdgcn_ldexpf(B[3], e), hb1, lb1);
+            // (A0 A1 A2 A3 | B0 B1 B2 B3) over the 16-lane rows -> permlane32: (A0 A1 B0 B1 | A2 A3 B2 B3)
+            // -> permlane16: (A0 A2 B0 B2 | A1 A3 B1 B3): row r then holds its 8 consecutive features
+            const auto h0 = __builtin_amdgcn_permlane32_swap(ha0, hb0, false, false);
+            const auto h1 = __builtin_amdgcn_permlane32_swap(ha1, hb1, false, false);
+            const auto l0 = __builtin_amdgcn_permlane32_swap(la0, lb0, false, false);
+            const auto l1 = __builtin_amdgcn_permlane32_swap(la1, lb1, false, false);
+            const auto H0 = __builtin_amdgcn_permlane16_swap(h0[0], h0[1], false, false);
+            const auto H1 = __builtin_amdgcn_permlane16_swap(h1[0], h1[1], false, false);
+            const auto L0 = __builtin_amdgcn_permlane16_swap(l0[0], l0[1], false, false);
+            const auto L1 = __builtin_amdgcn_permlane16_swap(l1[0], l1[1], false, false);
+            st.act_hi[t] = make_uint4(H0[0], H1[0], H0[1], H1[1]);
+            st.act_lo[t] = make_uint4(L0[0], L1[0], L0[1], L1[1]);
+        }
+        if constexpr (l == 3) {   // training: the encodings in HBM
+            const float* er_row = TR ? p.enc_p + (st.m0 + st.rl) * 64
+                                     : reinterpret_cast<const float*>(st.lds + Y::O_ENC) + st.rl * 64;
+            enc_frag(er_row, 0, st.g, e, st.enc_hi[0], st.enc_lo[0]);
+            enc_frag(er_row, 1, st.g, e, st.enc_hi[1], st.enc_lo[1]);
+        }
+        if constexpr (l == 8) {   // the view-direction encoding (27 columns + zeros)
+            enc_frag(TR ? p.enc_d + (st.m0 + st.rl) * 64 : drec, 0, st.g, e, st.enc_hi[0], st.enc_lo[0]);
+            st.enc_hi[1] = make_uint4(0u, 0u, 0u, 0u);
+            st.enc_lo[1] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+}
+
+// prologue: samples (rendering.py:183-198, no jitter) and the position encoding
+// (official_nerf.py:61, 99-119) of the block's 128 rows into the LDS tile, four threads per
+// row (x and levels 0-2 | 3-5 | 6-7 | 8-9 and the zero pad), with a row max per part and z
+__device__ __forceinline__ void encode_p(const ChainFwdArgs& p, State& st) {
+    using Y = LY<false>;
+    const int row = st.tid & 127, part = st.tid >> 7;
+    const size_t g = st.m0 + row;
+    float* dst = reinterpret_cast<float*>(st.lds + Y::O_ENC) + row * 64;
+    float x[3] = {0.f, 0.f, 0.f}, z = 0.f;
+    const bool live = g < (size_t)p.R * p.S;
+    if (live) {
+        const size_t ray = g / (size_t)p.S;
+        const int i = (int)(g - ray * (size_t)p.S);
+        z = lerp_z(linspace01(i, p.S), p.near_z, p.far_z);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) x[c] = ray_point(p.po[3 * ray + c], p.pd[3 * ray + c], z);
+    }
+    float m = 0.f;
+    const int lv0 = part == 0 ? 0 : part == 1 ? 3 : part == 2 ? 6 : 8;
+    const int lv1 = part == 0 ? 3 : part == 1 ? 6 : part == 2 ? 8 : 10;
+    if (part == 0) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { dst[c] = x[c]; m = fmaxf(m, fabsf(x[c])); }
+        st.fx[FX_Z + row] = z;
+        if (live) p.z[g] = z;
+    }
+    if (part == 3) dst[63] = 0.f;
+    for (int lv = lv0; lv < lv1; ++lv) {
+        const float f = (float)(1 << lv);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float sn, cs;
+            sincosf(f * x[c], &sn, &cs);
+            dst[3 + 6 * lv + c] = sn;
+            dst[6 + 6 * lv + c] = cs;
+            m = fmaxf(m, fmaxf(fabsf(sn), fabsf(cs)));
+        }
+    }
+    reinterpret_cast<float*>(st.lds + Y::O_RMX)[part * 128 + row] = m;
+}
+
+template <bool TR>
+__device__ __forceinline__ void init_state(State& st, char* smem) {
+    st.lds = smem;
+    st.fx = reinterpret_cast<float*>(smem + LY<TR>::O_FX);
+    st.tid = threadIdx.x;
+    st.wave = __builtin_amdgcn_readfirstlane(st.tid >> 6);
+    st.lane = st.tid & 63; st.n = st.lane & 15; st.g = st.lane >> 4;
+    st.m0 = (size_t)blockIdx.x * CROWS;
+    st.rl = 16 * st.wave + st.n;
+    st.mk0 = st.mk1 = 0u;
+}
+
+template <bool TR>
+__device__ __forceinline__ void chain_layers(const ChainFwdArgs& p, State& st) {
+    layer<0, TR>(p, st);
+    layer<1, TR>(p, st);
+    layer<2, TR>(p, st);
+    layer<3, TR>(p, st);
+    layer<4, TR>(p, st);
+    layer<5, TR>(p, st);
+    layer<6, TR>(p, st);
+    layer<7, TR>(p, st);
+    layer<8, TR>(p, st);
+    layer<9, TR>(p, st);
+}
+
+}  // namespace f2
+
+__global__ __launch_bounds__(512, 2) void k_render_fused2(ChainFwdArgs p) {
+    using namespace f2;
+    using Y = LY<false>;
+    __shared__ __attribute__((aligned(16))) char smem[Y::BYTES];
+    State st;
+    init_state<false>(st, smem);
+    dma_n<0, 2 * Y::D, false>(p, st);
+    // head weights into LDS, then the samples and both encodings (beside the DMAs)
+    if (st.tid < 256) st.fx[FX_WD + st.tid] = p.wd[st.tid];
+    for (int e = st.tid; e < 384; e += NTH) st.fx[FX_WC + e] = p.wc[e];
+    encode_p(p, st);
+    fused_encode_d(p, st.fx, st.tid, st.m0);
+    __syncthreads();
+    {
+        const float* rp = reinterpret_cast<const float*>(smem + Y::O_RMX);
+        st.er = row_exp(fmaxf(fmaxf(rp[st.rl], rp[128 + st.rl]), fmaxf(rp[256 + st.rl], rp[384 + st.rl])));
+        const float* row = reinterpret_cast<const float*>(smem + Y::O_ENC) + st.rl * 64;
+        enc_frag(row, 0, st.g, st.er, st.enc_hi[0], st.enc_lo[0]);
+        enc_frag(row, 1, st.g, st.er, st.enc_hi[1], st.enc_lo[1]);
+    }
+    chain_layers<false>(p, st);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every DMA landed before the LDS is released
+    __syncthreads();   // every row's raw4 in LDS
+    fused_composite<NTH>(p, st.fx, st.tid, st.m0);
+}
+
+// The training forward chain at two waves per SIMD (nerf_mlp_chain_train): the layer walk of
+// k_render_fused2 over the encodings nerf_encode_samples wrote (the backward needs them in
+// HBM anyway), saving what the per-layer kernels save -- every layer's output, the ReLU
+// words, the per-128-row-group column maxima -- and raw4 from the in-epilogue heads.  The
+// stores ride beside the MFMAs and are counted in the k-steps' vmcnt waits (wait_n).
+__global__ __launch_bounds__(512, 2) void k_mlp_chain_train2(ChainFwdArgs p) {
+    using namespace f2;
+    using Y = LY<true>;
+    __shared__ __attribute__((aligned(16))) char smem[Y::BYTES];
+    State st;
+    init_state<true>(st, smem);
+    // l0's A operand straight from HBM, before any LDS-DMA is in flight (the compiler waits
+    // for ordinary loads with vmcnt(0))
+    st.er = row_exp(p.rp[st.m0 + st.rl]);
+    {
+        const float* row = p.enc_p + (st.m0 + st.rl) * 64;
+        enc_frag(row, 0, st.g, st.er, st.enc_hi[0], st.enc_lo[0]);
+        enc_frag(row, 1, st.g, st.er, st.enc_hi[1], st.enc_lo[1]);
+        opaque(st.enc_hi[0]); opaque(st.enc_lo[0]); opaque(st.enc_hi[1]); opaque(st.enc_lo[1]);
+    }
+    if (st.tid < 256) st.fx[FX_WD + st.tid] = p.wd[st.tid];
+    for (int e = st.tid; e < 384; e += NTH) st.fx[FX_WC + e] = p.wc[e];
+    reinterpret_cast<uint32_t*>(smem + Y::O_CMX)[st.tid] = 0u;   // both column-max parities (512 words)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    dma_n<0, 2 * Y::D, true>(p, st);
+    chain_layers<true>(p, st);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // every row's raw4 in LDS, lf's column maxima complete
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));   // re-derived here: nothing of the prologue stays live to the end
+    const size_t m0 = (size_t)blockIdx.x * CROWS;
+    if (tid < CROWS)
+        *reinterpret_cast<float4*>(p.raw4 + (m0 + tid) * 4) = *reinterpret_cast<const float4*>(st.fx + FX_RAW + 4 * tid);
+    else if (tid < CROWS + 256 && !(kTrAblate & 2))
+        p.L[8].cmax[(m0 / CROWS) * L_OUT[8] + tid - CROWS] =
+            __uint_as_float(reinterpret_cast<const uint32_t*>(smem + Y::O_CMX)[(8 & 1) * 256 + tid - CROWS]);
 }
 
 }  // namespace nerf
@@ -729,6 +1310,40 @@ extern "C" int nerf_mlp_chain_fwd(const float* enc_p, const float* enc_d, const 
     return check_launch(__func__);
 }
 
+extern "C" int nerf_mlp_chain_train(const float* enc_p, const float* enc_d, const float* enc_p_rmax,
+                                    const float* enc_d_rmax, int n_pad, const nerf_chain_layer* layers, const float* wd,
+                                    const float* bd, const float* wc, const float* bc, float* raw4, void* stream) {
+    NERF_CHECK_PTR(enc_p); NERF_CHECK_PTR(enc_d); NERF_CHECK_PTR(enc_p_rmax); NERF_CHECK_PTR(enc_d_rmax);
+    NERF_CHECK_PTR(layers); NERF_CHECK_PTR(wd); NERF_CHECK_PTR(bd); NERF_CHECK_PTR(wc); NERF_CHECK_PTR(bc);
+    NERF_CHECK_PTR(raw4);
+    NERF_CHECK(n_pad > 0 && n_pad % CROWS == 0, "%s: n_pad=%d must be a positive multiple of %d", __func__, n_pad,
+               CROWS);
+    NERF_CHECK(gemm_precision() == 2, "%s: the fused chain runs in GEMM precision mode 2 (fp16 pair images)", __func__);
+    NERF_CHECK_ALIGN16(enc_p); NERF_CHECK_ALIGN16(enc_d); NERF_CHECK_ALIGN16(raw4);
+    ChainFwdArgs a{};
+    a.enc_p = enc_p; a.enc_d = enc_d; a.rp = enc_p_rmax; a.rd = enc_d_rmax; a.n_pad = n_pad;
+    for (int l = 0; l < CNL; ++l) {
+        const nerf_chain_layer& L = layers[l];
+        NERF_CHECK(L.img && L.bias, "%s: layer %d needs its weight image and bias", __func__, l);
+        NERF_CHECK((((uintptr_t)L.bias) & 15u) == 0 && (((uintptr_t)L.img) & 15u) == 0 && L.img_rows >= L_OUT[l],
+                   "%s: layer %d: image / bias not 16-byte aligned or image rows %d < %d", __func__, l, L.img_rows,
+                   L_OUT[l]);
+        // every output is mandatory: the k-steps' vmcnt waits count these stores at compile time
+        NERF_CHECK(L.out && L.ldo >= L_OUT[l] && L.ldo % 4 == 0 && (((uintptr_t)L.out) & 15u) == 0,
+                   "%s: layer %d: the training chain saves every layer output (ldo %d)", __func__, l, L.ldo);
+        NERF_CHECK(l == 8 || (L.mask && L.ldmask >= L_OUT[l] / 32 && L.ldmask % 2 == 0 &&
+                              (((uintptr_t)L.mask) & 7u) == 0),
+                   "%s: layer %d: the ReLU words are mandatory (ldmask %d, even, 8-byte aligned)", __func__, l, L.ldmask);
+        NERF_CHECK(l != 8 || L.mask == nullptr, "%s: the feature layer has no ReLU", __func__);
+        NERF_CHECK(l == CNL - 1 ? L.cmax == nullptr : L.cmax != nullptr,
+                   "%s: layer %d: column maxima are mandatory for l0..lf and absent for the colour layer", __func__, l);
+        a.L[l] = L;
+    }
+    a.wd = wd; a.bd = bd; a.wc = wc; a.bc = bc; a.raw4 = raw4;
+    hipLaunchKernelGGL(k_mlp_chain_train2, dim3(n_pad / CROWS), dim3(f2::NTH), 0, as_stream(stream), a);
+    return check_launch(__func__);
+}
+
 extern "C" int nerf_render_eval_fused(const float* pts_o, const float* pts_d, const float* view, int n_rays,
                                       int n_samples, float near_z, float far_z, int flags,
                                       const nerf_chain_layer* layers, const float* wd, const float* bd,
@@ -761,7 +1376,12 @@ extern "C" int nerf_render_eval_fused(const float* pts_o, const float* pts_d, co
     a.wd = wd; a.bd = bd; a.wc = wc; a.bc = bc;
     a.rgb = rgb; a.dist = dist; a.alpha = alpha; a.z = z;
     a.stamps = g_chain_stamps;
-    hipLaunchKernelGGL(k_mlp_chain_fwd<true>, dim3(a.n_pad / CROWS), dim3(256), 0, as_stream(stream), a);
+    // NERF_FUSED_V1=1 (A/B only): the round-2 kernel, 4 waves x 32 rows at one wave per SIMD
+    static const bool v1 = [] { const char* e = getenv("NERF_FUSED_V1"); return e && atoi(e) != 0; }();
+    if (v1 || g_chain_stamps)
+        hipLaunchKernelGGL(k_mlp_chain_fwd<true>, dim3(a.n_pad / CROWS), dim3(256), 0, as_stream(stream), a);
+    else
+        hipLaunchKernelGGL(k_render_fused2, dim3(a.n_pad / CROWS), dim3(f2::NTH), 0, as_stream(stream), a);
     return check_launch(__func__);
 }
 

@@ -46,7 +46,7 @@ class ProfKind(ctypes.Structure):
 
 
 PROF_KINDS = ("fwd", "dx", "dw", "dw_narrow")   # NERF_PROF_FWD / _DX / _DW / _DW_NARROW
-ABI_VERSION = 9                    # NERF_HIP_ABI_VERSION
+ABI_VERSION = 10                   # NERF_HIP_ABI_VERSION
 
 
 class ChainLayer(ctypes.Structure):
@@ -82,6 +82,8 @@ _SIGS = {
     "nerf_pack_weights": ([ctypes.POINTER(PackDesc), _c_i, _c_p], _c_i),
     "nerf_mlp_chain_fwd": ([_c_p, _c_p, _c_p, _c_p, _c_i, ctypes.POINTER(ChainLayer), _c_p], _c_i),
     "nerf_chain_debug_stamps": ([_c_p], _c_i),
+    "nerf_mlp_chain_train": ([_c_p, _c_p, _c_p, _c_p, _c_i, ctypes.POINTER(ChainLayer), _c_p, _c_p, _c_p, _c_p, _c_p,
+                              _c_p], _c_i),
     "nerf_render_eval_fused": ([_c_p, _c_p, _c_p, _c_i, _c_i, _c_f, _c_f, _c_i, ctypes.POINTER(ChainLayer), _c_p, _c_p,
                                 _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_adam_step": ([_c_p, _c_p, _c_p, _c_p, _c_i64, _c_p, _c_p], _c_i),
@@ -333,6 +335,17 @@ def mlp_chain_fwd(enc_p, enc_d, enc_p_rmax, enc_d_rmax, n_pad, layers: Sequence[
     arr = (ChainLayer * 10)(*layers)
     _call("nerf_mlp_chain_fwd", _ptr(enc_p), _ptr(enc_d), _ptr(enc_p_rmax), _ptr(enc_d_rmax), int(n_pad), arr,
           _stream())
+
+
+def mlp_chain_train(enc_p, enc_d, enc_p_rmax, enc_d_rmax, n_pad, layers: Sequence[ChainLayer], wd, bd, wc, bc,
+                    raw4):
+    """The training forward chain (one launch at two waves per SIMD): every layer output,
+    ReLU words and column maxima the backward needs, plus raw4 from the in-epilogue heads."""
+    if len(layers) != 10:
+        raise ValueError("mlp_chain_train: needs the 10 layer descriptors")
+    arr = (ChainLayer * 10)(*layers)
+    _call("nerf_mlp_chain_train", _ptr(enc_p), _ptr(enc_d), _ptr(enc_p_rmax), _ptr(enc_d_rmax), int(n_pad), arr,
+          _ptr(wd), _ptr(bd), _ptr(wc), _ptr(bc), _ptr(raw4), _stream())
 
 
 def adam_step(param, grad, exp_avg, exp_avg_sq, hyper):

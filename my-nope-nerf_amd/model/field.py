@@ -170,15 +170,22 @@ class FieldRunner:
         seg_rm = {"enc_p": enc_p_rm, "enc_d": enc_d_rm}
         masks = {}
         cmaxes = {"enc_p": enc_p_cm, "enc_d": enc_d_cm}
+        raw4 = e(Np, 4)
+        m = self.m
+        chain_heads = False
         if self.use_chain(keep):
-            # all ten linears in one launch, activations resident in registers (chain.hip)
+            # all ten linears in one launch, activations resident in registers (chain.hip);
+            # training (keep): nerf_mlp_chain_train saves every output, ReLU word and column
+            # maximum the per-layer path saves, and computes raw4 in its epilogues
             descs = []
             for i, l in enumerate(self.layers):
                 y = outs[i] if (keep or l.name in ("l7", "lr")) else None
                 mo = None
-                if keep and l.relu and (l.name != "lr" or self.heads_side(Np)):   # as the per-layer path
+                if keep and l.relu:
                     mo = torch.empty(Np, l.out_p // 32, device=dev, dtype=torch.int32)
-                    masks[l.name] = mo
+                    # as the per-layer path: the colour layer's bits only with the split heads backward
+                    if l.name != "lr" or self.heads_side(Np):
+                        masks[l.name] = mo
                 y_cm = cm(l.out_p) if l.name != "lr" else None
                 cmaxes[l.name] = y_cm
                 ws = self.ws[l.name]
@@ -187,10 +194,13 @@ class FieldRunner:
                                              mo.data_ptr() if mo is not None else None, l.out_p // 32,
                                              y_cm.data_ptr() if y_cm is not None else None))
                 acts.append(y if y is not None else outs[i])
-            _hip.mlp_chain_fwd(enc_p, enc_d, enc_p_rm, enc_d_rm, Np, descs)
+            if keep:
+                _hip.mlp_chain_train(enc_p, enc_d, enc_p_rm, enc_d_rm, Np, descs, m.fc_density.weight,
+                                     m.fc_density.bias, self.wc, m.fc_rgb.bias, raw4)
+                chain_heads = True
+            else:
+                _hip.mlp_chain_fwd(enc_p, enc_d, enc_p_rm, enc_d_rm, Np, descs)
             h8 = acts[7]
-        raw4 = e(Np, 4)
-        m = self.m
         # precision mode 2 at hidden 256: the density / colour heads run in the l7 / colour-layer
         # epilogues (nerf_linear_fwd_heads) instead of a separate pass over h8 and hr
         fuse_heads = self.h16 and D == 256 and HR == 128 and not self.use_chain(keep)
@@ -218,7 +228,7 @@ class FieldRunner:
             if l.name == "l7":
                 h8 = y
         hr = acts[9]
-        if not fuse_heads:
+        if not (fuse_heads or chain_heads):
             _hip.heads_fwd(h8, hr, D, m.fc_density.weight, m.fc_density.bias, self.wc, m.fc_rgb.bias, raw4, Np)
         if composite:
             rgb = e(R, 3)

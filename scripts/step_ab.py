@@ -27,8 +27,10 @@ SETTINGS = {
     "tail3": (0, 0, {"NERF_TAIL_MAIN": "3"}),
     "tn3": (0, 3, {}),
     "heads_joint": (0, 0, {"NERF_HEADS_SIDE": "0"}),
+    "chain": (0, 0, {"NERF_CHAIN": "1"}),
+    "per_layer": (0, 0, {"NERF_CHAIN": "0"}),
 }
-ENV_KEYS = ("NERF_TAIL_MAIN", "NERF_HEADS_SIDE")
+ENV_KEYS = ("NERF_TAIL_MAIN", "NERF_HEADS_SIDE", "NERF_CHAIN")
 
 
 def main():
