@@ -739,7 +739,7 @@ struct LY {
     static constexpr int D = NSLOT / 2 - 1;                   // 32-k steps in flight
     static constexpr int O_RING = 0;
     static constexpr int O_LEB = NSLOT * SBYTES;              // [2][256][16 B] weight-row exponent chunks
-    static constexpr int O_EXP = O_LEB + 2 * 256 * 16;        // [2][256] int: the exponents, compact
+    static constexpr int O_EXP = O_LEB + 2 * 256 * 16;        // [2][256] float: 2^-(weight-row exponent)
     static constexpr int O_BIAS = O_EXP + 2 * 256 * 4;        // [2][256] float
     static constexpr int O_ENC = O_BIAS + 2 * 256 * 4;        // eval: [128][64] float position encodings
     static constexpr int O_CMX = O_ENC;                       // training: [2][256] uint column maxima
@@ -759,6 +759,10 @@ constexpr int dma_count(int tt) {
 #define NERF_TRAIN_ABLATE 0   // diagnostic builds only: 1 no activation stores, 2 no ReLU words / column maxima
 #endif
 constexpr int kTrAblate = NERF_TRAIN_ABLATE;
+#ifndef NERF_COLMAX_ROW
+#define NERF_COLMAX_ROW 0     // A/B: column maxima reduced over the whole 16-lane row before the LDS atomic
+#endif
+constexpr bool kColmaxRow = NERF_COLMAX_ROW != 0;
 
 // the counted waits.  Every 32-k step k (global over the chain) waits for the DMAs issued D
 // steps earlier; vmcnt counts loads, stores and LDS-DMA together in issue order, so the count
@@ -794,6 +798,7 @@ static_assert(wait_n<false>(5) == dma_count(kbase(1) + 6 + 2) + dma_count(kbase(
 static_assert(wait_n<false>(0) == dma_count(2) + dma_count(3), "eval waits");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float pf2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f32x4 mfma16(const uint4& w, const uint4& a, const f32x4& c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(ch16x8, w), __builtin_bit_cast(ch16x8, a), c,
@@ -817,10 +822,33 @@ struct State {
     int rl;                             // the lane's row in the block (16 wave + n)
     int er;                             // row exponent of the current A operand
     uint32_t mk0, mk1;                  // training: the lane's two ReLU words of the previous layer
+    unsigned long long t_wait, t_bar, t_epi, t_pro, t_last, t_start;   // diagnostics (stamps): cycles in the
+                                                       // k-step waits, barriers, layer epilogues, prologue
     uint4 act_hi[8], act_lo[8];         // A operand: 8 k-steps of 32 (the 256 activations)
     uint4 enc_hi[2], enc_lo[2];         // encoding segment (64 columns) of the current layer
     f32x4 acc[16];                      // 16 rows x 256 outputs
 };
+
+// diagnostics (nerf_chain_debug_stamps): cycles since the last tick into *bucket
+__device__ __forceinline__ void tick(const ChainFwdArgs& p, State& st, unsigned long long* bucket) {
+    if (p.stamps == nullptr) return;
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    if (bucket) *bucket += t - st.t_last;
+    st.t_last = t;
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// per block (wave 0): k-step waits, barriers, prologue, layer epilogues, total, and the tail
+// (from the last epilogue to here)
+__device__ __forceinline__ void write_stamps(const ChainFwdArgs& p, State& st) {
+    if (p.stamps && threadIdx.x == 0) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        unsigned long long* o = p.stamps + (size_t)blockIdx.x * 6;
+        o[0] = st.t_wait; o[1] = st.t_bar; o[2] = st.t_pro; o[3] = st.t_epi;
+        o[4] = t - st.t_start; o[5] = t - st.t_last;
+    }
+}
 
 // global 16-k step TT -> ring slot TT % NSLOT (2 pieces per wave; 1 for the 128-row colour
 // layer) + at a layer's first step one piece per wave: waves 0-3 the weight-row exponents
@@ -924,7 +952,13 @@ __device__ __forceinline__ void save_piece(const ChainFwdArgs& p, State& st, con
             float c = fabsf(rebuilt(ah, al, k, st.er));
             c = fmaxf(c, dpp_f<0xB1>(0.f, c));
             c = fmaxf(c, dpp_f<0x4E>(0.f, c));
-            if ((st.n & 3) == 0) atomicMax(cm + k, __float_as_uint(c));
+            if constexpr (kColmaxRow) {       // the whole 16-lane row, one atomic per row
+                c = fmaxf(c, dpp_f<0x141>(0.f, c));
+                c = fmaxf(c, dpp_f<0x140>(0.f, c));
+                if (st.n == 0) atomicMax(cm + k, __float_as_uint(c));
+            } else {
+                if ((st.n & 3) == 0) atomicMax(cm + k, __float_as_uint(c));
+            }
         }
     }
 }
@@ -958,16 +992,19 @@ __device__ __forceinline__ void kstep(const ChainFwdArgs& p, State& st) {
     constexpr int TT = kbase(l) + 2 * u;
     constexpr int nact = l == 0 ? 0 : 8;         // k-steps from the register tile, then the encoding
     constexpr int ntj = L_OUT[l] / 16;
+    tick(p, st, nullptr);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_n<TR>(kfirst(l) + u)) : "memory");
+    tick(p, st, &st.t_wait);
     __syncthreads();
+    tick(p, st, &st.t_bar);
     dma<TT + 2 * Y::D, TR>(p, st);
     dma<TT + 2 * Y::D + 1, TR>(p, st);
     if constexpr (u == 0) {
         // this layer's exponents (landed with step TT) into the compact array; published to the
         // epilogue by the next step's barrier (every layer has at least two 32-k steps)
-        if (st.tid < L_OUT[l])
-            reinterpret_cast<int*>(st.lds + Y::O_EXP)[(l & 1) * 256 + st.tid] =
-                *reinterpret_cast<const int*>(st.lds + Y::O_LEB + (l & 1) * 4096 + st.tid * 16);
+        if (st.tid < L_OUT[l])   // as the scale 2^-e of the weight row (exact)
+            reinterpret_cast<float*>(st.lds + Y::O_EXP)[(l & 1) * 256 + st.tid] = __builtin_amdgcn_ldexpf(
+                1.f, -*reinterpret_cast<const int*>(st.lds + Y::O_LEB + (l & 1) * 4096 + st.tid * 16));
         if constexpr (TR && l >= 2 && !(kTrAblate & 2)) {
             // layer l - 2's column maxima over the block's 128 rows (its 128-row group), complete
             // since layer l - 1's last step: wave w stores features 32 w .. + 31 and clears them
@@ -1014,12 +1051,17 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) st.acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     ksteps<l, 0, TR>(p, st);
+    tick(p, st, nullptr);
     // the lane's feature offset, opaque per layer: otherwise the exponent / bias addresses of
     // the even (odd) layers are computed once and kept live -- spilled -- across the chain
     int g4 = 4 * st.g;
     asm volatile("" : "+v"(g4));
-    const int* le = reinterpret_cast<const int*>(st.lds + Y::O_EXP) + (l & 1) * 256 + g4;
+    const float* le = reinterpret_cast<const float*>(st.lds + Y::O_EXP) + (l & 1) * 256 + g4;
     const float* lb = reinterpret_cast<const float*>(st.lds + Y::O_BIAS) + (l & 1) * 256 + g4;
+    // unscale as (acc 2^-er) 2^-ew + b on packed-f32 ops: both scalings exact (powers of two
+    // in range: er <= 140 keeps 2^-er a float), one rounding, as ldexp(acc, -(er + ew)) + b
+    const float sr = __builtin_amdgcn_ldexpf(1.f, -st.er);
+    const pf2 sr2 = {sr, sr};
     float rmx = 0.f, hs0 = 0.f, hs1 = 0.f, hs2 = 0.f;
     uint32_t mw = 0;
 #pragma unroll
@@ -1028,13 +1070,14 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
         // being hoisted into one register burst (two waves per SIMD leave 256 registers)
         __builtin_amdgcn_sched_barrier(0);
         const int f0 = 16 * j + g4;
-        const int4 e4 = *reinterpret_cast<const int4*>(le + 16 * j);
+        const float4 s4 = *reinterpret_cast<const float4*>(le + 16 * j);
         const float4 b4 = *reinterpret_cast<const float4*>(lb + 16 * j);
+        const pf2 x01 = __builtin_elementwise_fma(pf2{st.acc[j][0], st.acc[j][1]} * sr2, pf2{s4.x, s4.y},
+                                                  pf2{b4.x, b4.y});
+        const pf2 x23 = __builtin_elementwise_fma(pf2{st.acc[j][2], st.acc[j][3]} * sr2, pf2{s4.z, s4.w},
+                                                  pf2{b4.z, b4.w});
         f32x4 x;
-        x[0] = __builtin_amdgcn_ldexpf(st.acc[j][0], -(st.er + e4.x)) + b4.x;
-        x[1] = __builtin_amdgcn_ldexpf(st.acc[j][1], -(st.er + e4.y)) + b4.y;
-        x[2] = __builtin_amdgcn_ldexpf(st.acc[j][2], -(st.er + e4.z)) + b4.z;
-        x[3] = __builtin_amdgcn_ldexpf(st.acc[j][3], -(st.er + e4.w)) + b4.w;
+        x[0] = x01[0]; x[1] = x01[1]; x[2] = x23[0]; x[3] = x23[1];
         if (relu) {
             x[0] = fmaxf(x[0], 0.f); x[1] = fmaxf(x[1], 0.f); x[2] = fmaxf(x[2], 0.f); x[3] = fmaxf(x[3], 0.f);
         }
@@ -1141,6 +1184,7 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
             st.enc_lo[1] = make_uint4(0u, 0u, 0u, 0u);
         }
     }
+    tick(p, st, &st.t_epi);
 }
 
 // prologue: samples (rendering.py:183-198, no jitter) and the position encoding
@@ -1194,6 +1238,8 @@ __device__ __forceinline__ void init_state(State& st, char* smem) {
     st.m0 = (size_t)blockIdx.x * CROWS;
     st.rl = 16 * st.wave + st.n;
     st.mk0 = st.mk1 = 0u;
+    st.t_wait = st.t_bar = st.t_epi = st.t_pro = 0;
+    st.t_last = st.t_start = __builtin_amdgcn_s_memtime();
 }
 
 template <bool TR>
@@ -1232,10 +1278,12 @@ __global__ __launch_bounds__(512, 2) void k_render_fused2(ChainFwdArgs p) {
         enc_frag(row, 0, st.g, st.er, st.enc_hi[0], st.enc_lo[0]);
         enc_frag(row, 1, st.g, st.er, st.enc_hi[1], st.enc_lo[1]);
     }
+    tick(p, st, &st.t_pro);
     chain_layers<false>(p, st);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every DMA landed before the LDS is released
     __syncthreads();   // every row's raw4 in LDS
     fused_composite<NTH>(p, st.fx, st.tid, st.m0);
+    write_stamps(p, st);
 }
 
 // The training forward chain at two waves per SIMD (nerf_mlp_chain_train): the layer walk of
@@ -1263,9 +1311,11 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_train2(ChainFwdArgs p) {
     reinterpret_cast<uint32_t*>(smem + Y::O_CMX)[st.tid] = 0u;   // both column-max parities (512 words)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     dma_n<0, 2 * Y::D, true>(p, st);
+    tick(p, st, &st.t_pro);
     chain_layers<true>(p, st);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();   // every row's raw4 in LDS, lf's column maxima complete
+    write_stamps(p, st);
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));   // re-derived here: nothing of the prologue stays live to the end
     const size_t m0 = (size_t)blockIdx.x * CROWS;
@@ -1340,6 +1390,7 @@ extern "C" int nerf_mlp_chain_train(const float* enc_p, const float* enc_d, cons
         a.L[l] = L;
     }
     a.wd = wd; a.bd = bd; a.wc = wc; a.bc = bc; a.raw4 = raw4;
+    a.stamps = g_chain_stamps;
     hipLaunchKernelGGL(k_mlp_chain_train2, dim3(n_pad / CROWS), dim3(f2::NTH), 0, as_stream(stream), a);
     return check_launch(__func__);
 }
@@ -1378,7 +1429,7 @@ extern "C" int nerf_render_eval_fused(const float* pts_o, const float* pts_d, co
     a.stamps = g_chain_stamps;
     // NERF_FUSED_V1=1 (A/B only): the round-2 kernel, 4 waves x 32 rows at one wave per SIMD
     static const bool v1 = [] { const char* e = getenv("NERF_FUSED_V1"); return e && atoi(e) != 0; }();
-    if (v1 || g_chain_stamps)
+    if (v1)
         hipLaunchKernelGGL(k_mlp_chain_fwd<true>, dim3(a.n_pad / CROWS), dim3(256), 0, as_stream(stream), a);
     else
         hipLaunchKernelGGL(k_render_fused2, dim3(a.n_pad / CROWS), dim3(f2::NTH), 0, as_stream(stream), a);

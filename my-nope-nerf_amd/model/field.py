@@ -245,15 +245,15 @@ class FieldRunner:
 
     def use_chain(self, keep: bool = False) -> bool:
         """The fused layer chain (chain.hip) covers precision mode 2 at hidden 256 / colour
-        128.  It is the default where no activation is saved (eval renders: 775 vs 877 us per
-        131072 samples); saving all nine activations for the backward its row-per-lane stores
-        cost more than the per-layer kernels' direct epilogues (1160 vs 923 us,
-        profiles/r01/chain_bench.txt), so training keeps one launch per layer unless
-        NERF_CHAIN=1; NERF_CHAIN=0 disables it everywhere."""
+        128, and is the default there.  Eval renders (keep=False) run nerf_mlp_chain_fwd (or
+        the fused per-ray kernel, use_fused_eval); training (keep=True) runs
+        nerf_mlp_chain_train at two waves per SIMD, which saves every output, ReLU word and
+        column maximum beside its MFMAs: 736-768 vs 877-904 us per 131072-sample forward and
+        2.474 vs 2.550 ms per cfg2 step (profiles/r03/train_chain_ab.txt).  NERF_CHAIN=0
+        runs one launch per layer; NERF_CHAIN=1 forces the chain."""
         if not (_hip.gemm_get_precision() == 2 and self.D == 256 and self.HR == 128):
             return False
-        env = os.environ.get("NERF_CHAIN")
-        return env == "1" if env is not None else not keep
+        return os.environ.get("NERF_CHAIN", "1") != "0"
 
     def use_fused_eval(self, S: int) -> bool:
         """The fused per-ray eval kernel (nerf_render_eval_fused: samples, encodings, the

@@ -58,9 +58,22 @@ def main():
         torch.cuda.synchronize()
         _hip.lib().nerf_chain_debug_stamps(None)
         st = buf.cpu().numpy().reshape(-1, 6).astype(np.float64)
-        med = np.median(st[:, :5], axis=0)
-        print(f"keep={keep}: chain phase cycles per block (median over {len(st)} blocks, wave 0): dma wait {med[0]:.0f}  "
-              f"barrier {med[1]:.0f}  mfma section {med[2]:.0f}  epilogue {med[3]:.0f}  total {med[4]:.0f}", flush=True)
+        med = np.median(st, axis=0)
+        if keep:   # k_mlp_chain_train2 (two waves per SIMD)
+            print(f"keep=True: training chain phase cycles per block (median over {len(st)} blocks, wave 0): "
+                  f"{f2_phases(med)}", flush=True)
+        else:      # k_mlp_chain_fwd<false> (one wave per SIMD)
+            print(f"keep=False: chain phase cycles per block (median over {len(st)} blocks, wave 0): dma wait "
+                  f"{med[0]:.0f}  barrier {med[1]:.0f}  mfma section {med[2]:.0f}  epilogue {med[3]:.0f}  total "
+                  f"{med[4]:.0f}", flush=True)
+
+
+def f2_phases(med):
+    """k_render_fused2 / k_mlp_chain_train2 stamps: k-step waits, barriers, prologue, layer
+    epilogues, total, tail; the rest of the total is the k-steps' MFMA sections."""
+    mma = med[4] - med[0] - med[1] - med[2] - med[3] - med[5]
+    return (f"k-step waits {med[0]:.0f}  barriers {med[1]:.0f}  prologue {med[2]:.0f}  epilogues {med[3]:.0f}  "
+            f"MFMA sections {mma:.0f}  tail {med[5]:.0f}  total {med[4]:.0f}")
 
 
 def fused_phases(dev, net, runner):
@@ -85,10 +98,14 @@ def fused_phases(dev, net, runner):
     torch.cuda.synchronize()
     _hip.lib().nerf_chain_debug_stamps(None)
     st = buf.cpu().numpy().reshape(-1, 6).astype(np.float64)
-    med = np.median(st[:, :5], axis=0)
-    print(f"fused eval: {s.elapsed_time(e) / 3:.2f} ms/frame; phase cycles per block (median over {len(st)} blocks, "
-          f"wave 0): dma wait {med[0]:.0f}  barrier {med[1]:.0f}  mfma section {med[2]:.0f}  epilogue {med[3]:.0f}  "
-          f"total {med[4]:.0f}", flush=True)
+    med = np.median(st, axis=0)
+    if os.environ.get("NERF_FUSED_V1") == "1":
+        print(f"fused eval (one wave per SIMD): {s.elapsed_time(e) / 3:.2f} ms/frame; phase cycles per block (median "
+              f"over {len(st)} blocks, wave 0): dma wait {med[0]:.0f}  barrier {med[1]:.0f}  mfma section "
+              f"{med[2]:.0f}  epilogue {med[3]:.0f}  total {med[4]:.0f}", flush=True)
+    else:
+        print(f"fused eval (k_render_fused2): {s.elapsed_time(e) / 3:.2f} ms/frame; phase cycles per block (median "
+              f"over {len(st)} blocks, wave 0): {f2_phases(med)}", flush=True)
 
 
 if __name__ == "__main__":

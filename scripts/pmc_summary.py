@@ -27,6 +27,11 @@ KINDS = {
         "dw", 4 * M * D * 2 + 4 * D * D, "dy 134.2 MB + x 134.2 MB + dW 0.26 MB; one launch is both XCD-paired "
         "256 x 128 column tiles, so dy is fetched by two blocks of one XCD; measured writes are the 128 split-K "
         "slabs (33.6 MB)"),
+    "nerf::k_mlp_chain_train2": (
+        "chain_train", 4 * M * 64 * 2 + 4 * M * 2 + 4 * M * D * 9 + 4 * M * 128 + 4 * M * 9 * 8 + 4 * M * 4 +
+        4 * (M // 128) * D * 9 + 4 * M * 4,
+        "reads enc_p + enc_d 67.1 MB + their row maxima 1.0 MB (weights stream from L2); writes the nine 256-wide "
+        "outputs 1208 MB + hr 67.1 MB + ReLU words 37.7 MB + column maxima 9.4 MB + raw4 2.1 MB"),
     "k_gemm_tn_x6<256, 256, 2, 2, true, 1>": (
         "dw", 4 * M * D * 2 + 4 * D * D, "dy 134.2 MB + x 134.2 MB + dW 0.26 MB; measured writes are the 256 "
         "split-K slabs (67 MB)"),
@@ -65,7 +70,7 @@ def main():
         out.append(e)
     print(json.dumps({"source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / --pmc WRITE_SIZE / SQ counters "
                                 "(separate passes) of `bench.py --steps 3 --warmup 2 --no-alt --no-cpu-baseline`, "
-                                "--kernel-include-regex 'k_gemm_(nt|tn)_x6'; FETCH_SIZE x2 (gfx950 correction)",
+                                "--kernel-include-regex 'k_gemm_(nt|tn)_x6|k_mlp_chain_train2'; FETCH_SIZE x2 (gfx950 correction)",
                       "launches": out}, indent=1))
 
 
