@@ -763,6 +763,26 @@ constexpr int kTrAblate = NERF_TRAIN_ABLATE;
 #define NERF_COLMAX_ROW 0     // A/B: column maxima reduced over the whole 16-lane row before the LDS atomic
 #endif
 constexpr bool kColmaxRow = NERF_COLMAX_ROW != 0;
+#ifndef NERF_SAVE_FUSED
+#define NERF_SAVE_FUSED 1     // A/B: 0 = the column maxima rebuilt per feature at MFMA tiles 3-10 (slower, r03l)
+#endif
+constexpr bool kSaveFused = NERF_SAVE_FUSED != 0;
+#ifndef NERF_SAVE_DEPHASE
+#define NERF_SAVE_DEPHASE 0   // A/B: 1 = waves 4-7 run their save pieces half a k-step later (slower: the per-tile
+                              // wave-dependent branches break the MFMA issue, chain_phase_stamps.txt)
+#endif
+constexpr bool kSaveDephase = NERF_SAVE_DEPHASE != 0;
+#ifndef NERF_SPLIT_JIT
+#define NERF_SPLIT_JIT 1      // A/B: 0 = the whole next-layer A operand split in the epilogue
+#endif
+constexpr bool kSplitJit = NERF_SPLIT_JIT != 0;
+#ifndef NERF_SPLIT_DEPHASE
+#define NERF_SPLIT_DEPHASE 0  // 1 spills at two waves per SIMD (the wave-dependent placement merges live ranges)
+#endif
+constexpr bool kSplitDephase = NERF_SPLIT_DEPHASE != 0;
+#ifndef NERF_SPLIT_TILE
+#define NERF_SPLIT_TILE 8     // the MFMA tile (of 16) after which a k-step splits the next k-step's fragment
+#endif
 
 // the counted waits.  Every 32-k step k (global over the chain) waits for the DMAs issued D
 // steps earlier; vmcnt counts loads, stores and LDS-DMA together in issue order, so the count
@@ -827,6 +847,8 @@ struct State {
     uint4 act_hi[8], act_lo[8];         // A operand: 8 k-steps of 32 (the 256 activations)
     uint4 enc_hi[2], enc_lo[2];         // encoding segment (64 columns) of the current layer
     f32x4 acc[16];                      // 16 rows x 256 outputs
+    f32x4 xs[16];                       // the previous layer's outputs not yet split into act (k-step
+                                        // t + 1's tiles are split during k-step t: split_pieces)
 };
 
 // diagnostics (nerf_chain_debug_stamps): cycles since the last tick into *bucket
@@ -922,14 +944,31 @@ __device__ __forceinline__ void save_piece(const ChainFwdArgs& p, State& st, con
                                            uint32_t& bits) {
     using Y = LY<true>;
     const nerf_chain_layer& P = p.L[l - 1];
+    int rl = st.rl;
+    asm volatile("" : "+v"(rl));   // the row's address is rebuilt per piece, not kept live across layers
+    const size_t row = st.m0 + rl;
     if constexpr (j == 1 || j == 2) {           // 4 features: store, ReLU bits
         constexpr int k0 = 4 * (j - 1);
         float v[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = rebuilt(ah, al, k0 + k, st.er);
         if constexpr (!(kTrAblate & 1))
-            *reinterpret_cast<float4*>(P.out + (st.m0 + st.rl) * P.ldo + 32 * u + 8 * st.g + k0) =
+            *reinterpret_cast<float4*>(P.out + row * P.ldo + 32 * u + 8 * st.g + k0) =
                 make_float4(v[0], v[1], v[2], v[3]);
+        if constexpr (kSaveFused && !(kTrAblate & 2)) {   // column maxima of these 4 features, from v
+            uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + Y::O_CMX) + ((l - 1) & 1) * 256 + 32 * u + 8 * st.g + k0;
+            float c[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                c[k] = fabsf(v[k]);
+                c[k] = fmaxf(c[k], dpp_f<0xB1>(0.f, c[k]));
+                c[k] = fmaxf(c[k], dpp_f<0x4E>(0.f, c[k]));
+            }
+            if ((st.n & 3) == 0) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) atomicMax(cm + k, __float_as_uint(c[k]));
+            }
+        }
         if constexpr (!(kTrAblate & 2) && l - 1 != 8) {   // lf has no ReLU
 #pragma unroll
             for (int k = 0; k < 4; ++k) bits |= (v[k] > 0.f ? 1u : 0u) << (k0 + k);
@@ -938,12 +977,11 @@ __device__ __forceinline__ void save_piece(const ChainFwdArgs& p, State& st, con
                 if constexpr (u & 1) st.mk1 = st.g == (u >> 1) ? w : st.mk1;
                 else st.mk0 = st.g == (u >> 1) ? w : st.mk0;
                 if constexpr (u == 7)
-                    *reinterpret_cast<uint2*>(P.mask + (st.m0 + st.rl) * P.ldmask + 2 * st.g) =
-                        make_uint2(st.mk0, st.mk1);
+                    *reinterpret_cast<uint2*>(P.mask + row * P.ldmask + 2 * st.g) = make_uint2(st.mk0, st.mk1);
             }
         }
     }
-    if constexpr (!(kTrAblate & 2) && j >= 3) {   // column maxima: one feature per tile (two for 8 tiles)
+    if constexpr (!kSaveFused && !(kTrAblate & 2) && j >= 3) {   // column maxima: one feature per tile (two for 8 tiles)
         constexpr int per = ntj >= 11 ? 1 : 2;
         constexpr int k0 = (j - 3) * per;
         uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + Y::O_CMX) + ((l - 1) & 1) * 256 + 32 * u + 8 * st.g;
@@ -963,10 +1001,53 @@ __device__ __forceinline__ void save_piece(const ChainFwdArgs& p, State& st, con
     }
 }
 
+// the next layer's A fragment for k-step t from the f32 tiles 2t, 2t + 1 at exponent st.er:
+// fp16 pairs, rows exchanged into the fragment layout ((A0 A1 A2 A3 | B0 B1 B2 B3) over the
+// 16-lane rows -> permlane32: (A0 A1 B0 B1 | A2 A3 B2 B3) -> permlane16: (A0 A2 B0 B2 | A1 A3
+// B1 B3): row r then holds its 8 consecutive features).  Two halves (split; exchange) so the
+// k-step can place them at two MFMA tiles
+struct SplitTmp { uint32_t ha0, la0, ha1, la1, hb0, lb0, hb1, lb1; };
+template <int t>
+__device__ __forceinline__ void split_a(State& st, SplitTmp& q) {
+    const int e = st.er;
+    const f32x4 A = st.xs[2 * t], B = st.xs[2 * t + 1];
+    csplit(__builtin_amdgcn_ldexpf(A[0], e), __builtin_amdgcn_ldexpf(A[1], e), q.ha0, q.la0);
+    csplit(__builtin_amdgcn_ldexpf(A[2], e), __builtin_amdgcn_ldexpf(A[3], e), q.ha1, q.la1);
+    csplit(__builtin_amdgcn_ldexpf(B[0], e), __builtin_amdgcn_ldexpf(B[1], e), q.hb0, q.lb0);
+    csplit(__builtin_amdgcn_ldexpf(B[2], e), __builtin_amdgcn_ldexpf(B[3], e), q.hb1, q.lb1);
+}
+template <int t>
+__device__ __forceinline__ void split_b(State& st, const SplitTmp& q) {
+    const auto h0 = __builtin_amdgcn_permlane32_swap(q.ha0, q.hb0, false, false);
+    const auto h1 = __builtin_amdgcn_permlane32_swap(q.ha1, q.hb1, false, false);
+    const auto l0 = __builtin_amdgcn_permlane32_swap(q.la0, q.lb0, false, false);
+    const auto l1 = __builtin_amdgcn_permlane32_swap(q.la1, q.lb1, false, false);
+    const auto H0 = __builtin_amdgcn_permlane16_swap(h0[0], h0[1], false, false);
+    const auto H1 = __builtin_amdgcn_permlane16_swap(h1[0], h1[1], false, false);
+    const auto L0 = __builtin_amdgcn_permlane16_swap(l0[0], l0[1], false, false);
+    const auto L1 = __builtin_amdgcn_permlane16_swap(l1[0], l1[1], false, false);
+    st.act_hi[t] = make_uint4(H0[0], H1[0], H0[1], H1[1]);
+    st.act_lo[t] = make_uint4(L0[0], L1[0], L0[1], L1[1]);
+}
+// MFMA tiles of a k-step that carry the two split halves for the next k-step: the waves
+// sharing a SIMD (w, w + 4) take them half a step apart
+template <int ntj, bool second>
+constexpr int split_tile(int half) {
+    return ((second ? ntj / 2 : 0) + (ntj >= 16 ? NERF_SPLIT_TILE : NERF_SPLIT_TILE / 2) + half) % ntj;
+}
+template <int l, int u, int j, int ntj, bool second>
+__device__ __forceinline__ void split_piece(State& st, SplitTmp& q) {
+    if constexpr (kSplitJit && l > 0 && u + 1 < 8) {
+        if constexpr (j == split_tile<ntj, second>(0)) split_a<u + 1>(st, q);
+        if constexpr (j == split_tile<ntj, second>(1)) split_b<u + 1>(st, q);
+    }
+}
+
 // tile j of a k-step (compile-time j, so the save pieces are placed between MFMA groups)
 template <int l, int u, bool TR, int j, int ntj, int nact>
 __device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, const uint4& ah, const uint4& al,
-                                            const char* base, uint4 (&wh)[2], uint4 (&wl)[2], uint32_t& bits) {
+                                            const char* base, uint4 (&wh)[2], uint4 (&wl)[2], uint32_t& bits,
+                                            SplitTmp& q) {
     if constexpr (j < ntj) {
         if constexpr (j + 1 < ntj) {
             wh[(j + 1) & 1] = *reinterpret_cast<const uint4*>(base + 256 * (j + 1));
@@ -976,9 +1057,16 @@ __device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, co
         st.acc[j] = mfma16(wh[j & 1], al, st.acc[j]);   // hi . lo
         st.acc[j] = mfma16(wl[j & 1], ah, st.acc[j]);   // lo . hi
         st.acc[j] = mfma16(wh[j & 1], ah, st.acc[j]);   // hi . hi
-        if constexpr (TR && u < nact) save_piece<l, u, j, ntj>(p, st, ah, al, bits);
+        if constexpr (TR && u < nact) {
+            // waves w and w + 4 share a SIMD: the second half runs its pieces half a step later,
+            // so one wave's VALU piece meets the other wave's MFMAs, not its VALU piece
+            if (!kSaveDephase || st.wave < 4) save_piece<l, u, j, ntj>(p, st, ah, al, bits);
+            else save_piece<l, u, (j + ntj / 2) % ntj, ntj>(p, st, ah, al, bits);
+        }
+        if (!kSplitDephase || st.wave < 4) split_piece<l, u, j, ntj, false>(st, q);
+        else split_piece<l, u, j, ntj, true>(st, q);
         __builtin_amdgcn_sched_barrier(0);
-        mstep_tiles<l, u, TR, j + 1, ntj, nact>(p, st, ah, al, base, wh, wl, bits);
+        mstep_tiles<l, u, TR, j + 1, ntj, nact>(p, st, ah, al, base, wh, wl, bits, q);
     }
 }
 
@@ -1027,7 +1115,8 @@ __device__ __forceinline__ void kstep(const ChainFwdArgs& p, State& st) {
     wh[0] = *reinterpret_cast<const uint4*>(base);
     wl[0] = *reinterpret_cast<const uint4*>(base + SPLANE);
     uint32_t bits = 0;
-    mstep_tiles<l, u, TR, 0, ntj, nact>(p, st, ah, al, base, wh, wl, bits);
+    SplitTmp q;
+    mstep_tiles<l, u, TR, 0, ntj, nact>(p, st, ah, al, base, wh, wl, bits, q);
 }
 
 template <int l, int u, bool TR>
@@ -1081,7 +1170,7 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
         if (relu) {
             x[0] = fmaxf(x[0], 0.f); x[1] = fmaxf(x[1], 0.f); x[2] = fmaxf(x[2], 0.f); x[3] = fmaxf(x[3], 0.f);
         }
-        st.acc[j] = x;
+        st.xs[j] = x;
         rmx = fmaxf(rmx, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
         if constexpr (last_tr) {   // hr (the f32 epilogue value, as the per-layer kernel) and its ReLU words
             const nerf_chain_layer& L = p.L[l];
@@ -1150,27 +1239,18 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
         if constexpr (l == 8) m = fmaxf(m, TR ? p.rd[st.m0 + st.rl] : drec[32]);
         st.er = row_exp(m);
         const int e = st.er;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            __builtin_amdgcn_sched_barrier(0);
-            const f32x4 A = st.acc[2 * t], B = st.acc[2 * t + 1];
-            uint32_t ha0, la0, ha1, la1, hb0, lb0, hb1, lb1;
-            csplit(__builtin_amdgcn_ldexpf(A[0], e), __builtin_amdgcn_ldexpf(A[1], e), ha0, la0);
-            csplit(__builtin_amdgcn_ldexpf(A[2], e), __builtin_amdgcn_ldexpf(A[3], e), ha1, la1);
-            csplit(__builtin_amdgcn_ldexpf(B[0], e), __builtin_amdgcn_ldexpf(B[1], e), hb0, lb0);
-            csplit(__builtin_amdgcn_ldexpf(B[2], e), __builtin_amdgcn_ldexpf(B[3], e), hb1, lb1);
-            // (A0 A1 A2 A3 | B0 B1 B2 B3) over the 16-lane rows -> permlane32: (A0 A1 B0 B1 | A2 A3 B2 B3)
-            // -> permlane16: (A0 A2 B0 B2 | A1 A3 B1 B3): row r then holds its 8 consecutive features
-            const auto h0 = __builtin_amdgcn_permlane32_swap(ha0, hb0, false, false);
-            const auto h1 = __builtin_amdgcn_permlane32_swap(ha1, hb1, false, false);
-            const auto l0 = __builtin_amdgcn_permlane32_swap(la0, lb0, false, false);
-            const auto l1 = __builtin_amdgcn_permlane32_swap(la1, lb1, false, false);
-            const auto H0 = __builtin_amdgcn_permlane16_swap(h0[0], h0[1], false, false);
-            const auto H1 = __builtin_amdgcn_permlane16_swap(h1[0], h1[1], false, false);
-            const auto L0 = __builtin_amdgcn_permlane16_swap(l0[0], l0[1], false, false);
-            const auto L1 = __builtin_amdgcn_permlane16_swap(l1[0], l1[1], false, false);
-            st.act_hi[t] = make_uint4(H0[0], H1[0], H0[1], H1[1]);
-            st.act_lo[t] = make_uint4(L0[0], L1[0], L0[1], L1[1]);
+        // k-step 0's fragment now; the others during the next layer's k-steps (split_piece)
+        SplitTmp q;
+        split_a<0>(st, q);
+        split_b<0>(st, q);
+        if constexpr (!kSplitJit) {
+            split_a<1>(st, q); split_b<1>(st, q);
+            split_a<2>(st, q); split_b<2>(st, q);
+            split_a<3>(st, q); split_b<3>(st, q);
+            split_a<4>(st, q); split_b<4>(st, q);
+            split_a<5>(st, q); split_b<5>(st, q);
+            split_a<6>(st, q); split_b<6>(st, q);
+            split_a<7>(st, q); split_b<7>(st, q);
         }
         if constexpr (l == 3) {   // training: the encodings in HBM
             const float* er_row = TR ? p.enc_p + (st.m0 + st.rl) * 64
