@@ -36,8 +36,9 @@ extern "C" {
 
 /* ABI version: 5 added nerf_prof_read_kinds and nerf_render_eval_fused, 6 the 4x4-chain
  * backwards (nerf_pose_c2w_bwd, nerf_mat4_inv_bwd, nerf_mat4_mul(_bwd), nerf_unproject_matrix_bwd)
- * and the depth-prior distortion (nerf_depth_affine(_bwd)), 7 nerf_linear_fwd_heads, 8 nerf_heads_bwd_mode. */
-#define NERF_HIP_ABI_VERSION 10
+ * and the depth-prior distortion (nerf_depth_affine(_bwd)), 7 nerf_linear_fwd_heads, 8 nerf_heads_bwd_mode,
+ * 9 precision mode 2 as the default, 10 nerf_mlp_chain_train, 11 nerf_linear_bwd_weight_seg. */
+#define NERF_HIP_ABI_VERSION 11
 int nerf_hip_abi_version(void);
 const char* nerf_hip_last_error(void);
 
@@ -126,6 +127,18 @@ int nerf_linear_bwd_data(const float* dy, int lddy, int k, const float* wt, cons
 int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const float* x, int ldx,
                            int kin, int m, int splits, float* slab, int ldslab, int col0,
                            float* bslab, const float* dy_cmax, const float* x_cmax, void* stream);
+
+/* The weight gradient of a layer whose input is two segments [x1 | x2] (l4's [h3 | enc_p],
+ * official_nerf.py:62-64; the colour layer's [f | enc_d], :88-90): the same slab as
+ *   nerf_linear_bwd_weight(dy, .., x1, k1, .., col0 = 0, bslab, dy_cmax, x1_cmax) followed by
+ *   nerf_linear_bwd_weight(dy, .., x2, k2, .., col0 = k1, NULL, dy_cmax, x2_cmax)
+ * bit for bit.  In precision mode 2 under TN policy 7 with nout 256 or 128, k1 = 256, k2 = 64
+ * and splits % 8 == 0 it is ONE launch whose column tiles of a split share an XCD, so dy is
+ * read from HBM once (two launches read it twice); any other case runs the two calls. */
+int nerf_linear_bwd_weight_seg(const float* dy, int lddy, int nout, const float* x1, int ldx1, int k1,
+                               const float* x2, int ldx2, int k2, int m, int splits, float* slab, int ldslab,
+                               float* bslab, const float* dy_cmax, const float* x1_cmax, const float* x2_cmax,
+                               void* stream);
 
 /* Recommended `splits` for nerf_linear_bwd_weight at this shape and tile policy. */
 int nerf_linear_bwd_weight_splits(int nout, int kin, int m);

@@ -651,5 +651,8 @@ inline int tn_xcd_group(int policy, int nout, int kin, int splits) {
 int dispatch_nt_x6(const NTArgs& a, int epi, int policy, hipStream_t s, double flops, bool h16 = false);
 int dispatch_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, hipStream_t s, double flops,
                    bool h16 = false);
+// the two-segment weight gradient in one launch (fp16 pair, TN policy 7 shapes only)
+bool tn_seg_supported(int nout, int k1, int k2, int splits);
+int dispatch_tn_x6_seg(const TNArgs& pm, const TNArgs& ps, int nout, int splits, hipStream_t s, double flops);
 
 }  // namespace nerf

@@ -258,23 +258,29 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_tn(TNArgs p) {
 // (bslab) ride along in the last row of blocks.
 constexpr int SR_COLS = 64;
 constexpr int SR_GROUPS = 16;
-__global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ slab, int splits, int nout,
-                                                     int ldslab, int nout_ref, int kin_ref,
-                                                     const float* __restrict__ bslab, float* __restrict__ gw,
-                                                     float* __restrict__ gb, int accumulate) {
-    __shared__ float4 part[SR_GROUPS][16];
+struct SlabJob {
+    const float* slab;
+    int splits, nout, ldslab, nout_ref, kin_ref;
+    const float* bslab;
+    float* gw;
+    float* gb;
+    int accumulate;
+};
+// one block of the reduce: block `blk` of job j (weight blocks, then bias blocks)
+__device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int blk, float4 (&part)[SR_GROUPS][16]) {
     const int l16 = threadIdx.x & 15, grp = threadIdx.x >> 4;
-    const int cblocks = (kin_ref + SR_COLS - 1) / SR_COLS;
-    const int wblocks = nout_ref * cblocks;          // then ceil(nout_ref / SR_COLS) bias blocks
-    const bool bias_row = (int)blockIdx.x >= wblocks;
-    const int o = bias_row ? nout_ref : blockIdx.x / cblocks;
-    const int c0 = (bias_row ? blockIdx.x - wblocks : blockIdx.x % cblocks) * SR_COLS + 4 * l16;
-    if (bias_row && (bslab == nullptr || gb == nullptr)) return;
+    const int cblocks = (j.kin_ref + SR_COLS - 1) / SR_COLS;
+    const int wblocks = j.nout_ref * cblocks;          // then ceil(nout_ref / SR_COLS) bias blocks
+    const bool bias_row = blk >= wblocks;
+    const int o = bias_row ? j.nout_ref : blk / cblocks;
+    const int c0 = (bias_row ? blk - wblocks : blk % cblocks) * SR_COLS + 4 * l16;
+    if (bias_row && (j.bslab == nullptr || j.gb == nullptr)) return;   // block-uniform
     const float* src;
     size_t st;
     int ncol;
-    if (!bias_row) { src = slab + (size_t)o * ldslab; st = (size_t)nout * ldslab; ncol = kin_ref; }
-    else { src = bslab; st = nout; ncol = nout_ref; }
+    if (!bias_row) { src = j.slab + (size_t)o * j.ldslab; st = (size_t)j.nout * j.ldslab; ncol = j.kin_ref; }
+    else { src = j.bslab; st = j.nout; ncol = j.nout_ref; }
+    const int splits = j.splits;
     const bool vec = (c0 + 4 <= ncol) && ((st & 3) == 0) && ((((uintptr_t)(src + c0)) & 15) == 0);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (c0 < ncol) {
@@ -311,11 +317,16 @@ __global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ s
         const float4 v = part[w][l16];
         r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
     }
-    float* dst = bias_row ? gb + c0 : gw + (size_t)o * kin_ref + c0;
+    float* dst = bias_row ? j.gb + c0 : j.gw + (size_t)o * j.kin_ref + c0;
     const float rv[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
     for (int t = 0; t < 4; ++t)
-        if (c0 + t < ncol) dst[t] = accumulate ? dst[t] + rv[t] : rv[t];
+        if (c0 + t < ncol) dst[t] = j.accumulate ? dst[t] + rv[t] : rv[t];
+}
+
+__global__ __launch_bounds__(256) void k_slab_reduce(SlabJob j) {
+    __shared__ float4 part[SR_GROUPS][16];
+    slab_reduce_block(j, blockIdx.x, part);
 }
 
 }  // namespace nerf
@@ -468,30 +479,37 @@ extern "C" int nerf_linear_bwd_data(const float* dy, int lddy, int k, const floa
     return dispatch_nt<EPI_BWD>(a, as_stream(stream), fl);
 }
 
-extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const float* x, int ldx,
-                                      int kin, int m, int splits, float* slab, int ldslab, int col0,
-                                      float* bslab, const float* dy_cmax, const float* x_cmax, void* stream) {
-    NERF_CHECK_PTR(dy);
-    NERF_CHECK_PTR(x);
-    NERF_CHECK_PTR(slab);
-    NERF_CHECK(nout > 0 && nout % 64 == 0, "%s: nout=%d must be a multiple of 64", __func__, nout);
-    NERF_CHECK(kin > 0 && kin % 64 == 0, "%s: kin=%d must be a multiple of 64", __func__, kin);
+// argument checks + the kernel arguments of one weight-gradient segment
+static int tn_args(const char* fn, const float* dy, int lddy, int nout, const float* x, int ldx, int kin, int m,
+                   int splits, float* slab, int ldslab, int col0, float* bslab, const float* dy_cmax,
+                   const float* x_cmax, TNArgs& a) {
+    NERF_CHECK(dy && x && slab, "%s: null operand", fn);
+    NERF_CHECK(nout > 0 && nout % 64 == 0, "%s: nout=%d must be a multiple of 64", fn, nout);
+    NERF_CHECK(kin > 0 && kin % 64 == 0, "%s: kin=%d must be a multiple of 64", fn, kin);
     NERF_CHECK(splits > 0 && m % splits == 0 && (m / splits) % BK == 0,
-               "%s: m=%d not divisible into %d splits of a multiple of %d rows", __func__, m, splits, BK);
-    NERF_CHECK(lddy % 4 == 0 && ldx % 4 == 0 && ldslab >= col0 + kin, "%s: bad leading dims", __func__);
-    NERF_CHECK_ALIGN16(dy);
-    NERF_CHECK_ALIGN16(x);
+               "%s: m=%d not divisible into %d splits of a multiple of %d rows", fn, m, splits, BK);
+    NERF_CHECK(lddy % 4 == 0 && ldx % 4 == 0 && ldslab >= col0 + kin, "%s: bad leading dims", fn);
+    NERF_CHECK((((uintptr_t)dy | (uintptr_t)x) & 15u) == 0, "%s: dy / x must be 16-byte aligned", fn);
     // the split kernels address a split's rows through 32-bit buffer descriptors (byte offsets)
     NERF_CHECK((int64_t)(m / splits) * (lddy > ldx ? lddy : ldx) * 4 < ((int64_t)1 << 31),
                "%s: %d rows per split x leading dimension %d exceed the 2 GB buffer range; use more splits",
-               __func__, m / splits, lddy > ldx ? lddy : ldx);
-    TNArgs a{};
+               fn, m / splits, lddy > ldx ? lddy : ldx);
+    a = TNArgs{};
     a.dy = dy; a.lddy = lddy; a.x = x; a.ldx = ldx;
     a.rows_per_split = m / splits;
     a.slab = slab; a.ldslab = ldslab; a.col0 = col0; a.slab_stride = (size_t)nout * ldslab;
     a.bslab = bslab; a.nout = nout;
     a.ablate = g_ablate >> 4;
     a.cm_dy = dy_cmax; a.ldcm_dy = nout; a.cm_x = x_cmax; a.ldcm_x = kin;
+    return NERF_OK;
+}
+
+extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const float* x, int ldx,
+                                      int kin, int m, int splits, float* slab, int ldslab, int col0,
+                                      float* bslab, const float* dy_cmax, const float* x_cmax, void* stream) {
+    TNArgs a;
+    int rc = tn_args(__func__, dy, lddy, nout, x, ldx, kin, m, splits, slab, ldslab, col0, bslab, dy_cmax, x_cmax, a);
+    if (rc) return rc;
     // mode 2 runs the fp16 pair kernel when the column maxima are there and every split is
     // whole 128-row groups; otherwise the bf16x3 kernel (it needs no scales)
     const bool h16 = g_precision == 2 && dy_cmax && x_cmax && (m / splits) % 128 == 0;
@@ -524,19 +542,52 @@ extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const
     return check_launch(__func__);
 }
 
+extern "C" int nerf_linear_bwd_weight_seg(const float* dy, int lddy, int nout, const float* x1, int ldx1, int k1,
+                                          const float* x2, int ldx2, int k2, int m, int splits, float* slab,
+                                          int ldslab, float* bslab, const float* dy_cmax, const float* x1_cmax,
+                                          const float* x2_cmax, void* stream) {
+    TNArgs pm, ps;
+    int rc = tn_args(__func__, dy, lddy, nout, x1, ldx1, k1, m, splits, slab, ldslab, 0, bslab, dy_cmax, x1_cmax, pm);
+    if (rc) return rc;
+    rc = tn_args(__func__, dy, lddy, nout, x2, ldx2, k2, m, splits, slab, ldslab, k1, nullptr, dy_cmax, x2_cmax, ps);
+    if (rc) return rc;
+    const int pol = g_tn_policy ? g_tn_policy : kTnDefault;
+    const bool one = g_precision == 2 && pol == 7 && dy_cmax && x1_cmax && x2_cmax && (m / splits) % 128 == 0 &&
+                     tn_seg_supported(nout, k1, k2, splits);
+    if (!one) {   // the same slab from two launches
+        rc = nerf_linear_bwd_weight(dy, lddy, nout, x1, ldx1, k1, m, splits, slab, ldslab, 0, bslab, dy_cmax, x1_cmax,
+                                    stream);
+        if (rc) return rc;
+        return nerf_linear_bwd_weight(dy, lddy, nout, x2, ldx2, k2, m, splits, slab, ldslab, k1, nullptr, dy_cmax,
+                                      x2_cmax, stream);
+    }
+    const double fl = 2.0 * m * nout * (double)(k1 + k2);
+    prof_next(nout % 256 == 0 ? NERF_PROF_DW : NERF_PROF_DW_NARROW,
+              4.0 * m * (double)(nout + k1 + k2) + 4.0 * nout * (double)(k1 + k2) + (bslab ? 4.0 * nout : 0.0));
+    return dispatch_tn_x6_seg(pm, ps, nout, splits, as_stream(stream), fl);
+}
+
+static int slab_job_check(const char* fn, const SlabJob& j) {
+    NERF_CHECK(j.slab && j.gw, "%s: null slab / gradient", fn);
+    NERF_CHECK(j.splits > 0 && j.nout > 0 && j.kin_ref > 0 && j.ldslab >= j.kin_ref && j.nout_ref <= j.nout &&
+                   j.nout_ref > 0,
+               "%s: bad sizes", fn);
+    return NERF_OK;
+}
+// one block per (output row, 64 columns), then the bias row's blocks
+static int slab_job_blocks(const SlabJob& j) {
+    const int cblocks = (j.kin_ref + SR_COLS - 1) / SR_COLS;
+    const int bias_blocks = (j.bslab && j.gb) ? (j.nout_ref + SR_COLS - 1) / SR_COLS : 0;
+    return j.nout_ref * cblocks + bias_blocks;
+}
+
 extern "C" int nerf_slab_reduce(const float* slab, int splits, int nout, int ldslab, int nout_ref,
                                 int kin_ref, const float* bslab, float* gw, float* gb, int accumulate,
                                 void* stream) {
-    NERF_CHECK_PTR(slab);
-    NERF_CHECK_PTR(gw);
-    NERF_CHECK(splits > 0 && nout > 0 && kin_ref > 0 && ldslab >= kin_ref && nout_ref <= nout,
-               "%s: bad sizes", __func__);
-    // one block per (output row, 64 columns), then the bias row's blocks
-    const int cblocks = (kin_ref + SR_COLS - 1) / SR_COLS;
-    const int bias_blocks = (bslab && gb) ? (nout_ref + SR_COLS - 1) / SR_COLS : 0;
-    const int blocks = nout_ref * cblocks + bias_blocks;
-    hipLaunchKernelGGL(k_slab_reduce, dim3(blocks), dim3(256), 0, as_stream(stream), slab, splits,
-                       nout, ldslab, nout_ref, kin_ref, bslab, gw, gb, accumulate);
+    const SlabJob j{slab, splits, nout, ldslab, nout_ref, kin_ref, bslab, gw, gb, accumulate};
+    int rc = slab_job_check(__func__, j);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_slab_reduce, dim3(slab_job_blocks(j)), dim3(256), 0, as_stream(stream), j);
     return check_launch(__func__);
 }
 

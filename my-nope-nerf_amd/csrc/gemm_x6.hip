@@ -777,35 +777,33 @@ __device__ __forceinline__ void tn_mainloop(char* smem, int nkt, int wm0, int wn
 // second read of a dy k-tile hits that XCD's L2.  With BN = kin / 2 this halves the split-K
 // slab bytes of a 256 x 256 layer (twice the rows per split at the same block count)
 // without a second HBM read of dy.  Needs splits % 8 == 0.
-template <int BM, int BN, int WM, int WN, bool H = false, int NS = 1, int CT = 0>
-__global__ __launch_bounds__(64 * WM * WN, WM * WN >= 8 ? 2 : 1) void k_gemm_tn_x6(TNArgs p) {
+// LDS of one TN block: two operand image buffers (the epilogue's per-wave tiles reuse them),
+// + H: the tile's row / column scale exponents
+template <int BM, int BN, int WM, int WN, bool H>
+struct TNSmem {
+    static constexpr int NT = 64 * WM * WN;
+    static constexpr int TN = BN / WN / 32;
+    static constexpr int NP = H ? 2 : 3;
+    static constexpr int BUF = XImg<BM, NP>::BYTES + XImg<BN, NP>::BYTES;
+    static constexpr int LOOP = 2 * BUF;
+    static constexpr int EPI = (NT / 64) * TileLds<TN>::BYTES;
+    static constexpr int MAIN = LOOP > EPI ? LOOP : EPI;
+    static constexpr int BYTES = MAIN + (H ? (BM + BN) * 4 : 0);
+};
+
+// one TN block: output rows o0 .. o0 + BM, column tile jt (x columns jt BN ..), split `split`
+template <int BM, int BN, int WM, int WN, bool H, int NS>
+__device__ __forceinline__ void tn_block(const TNArgs& p, char* smem, int o0, int jt, int split) {
     constexpr int NT = 64 * WM * WN;
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
-    constexpr int NP = H ? 2 : 3;
-    constexpr int BUF = XImg<BM, NP>::BYTES + XImg<BN, NP>::BYTES;
     static_assert(TM >= 1 && TN >= 1, "bad tile");
-    static_assert(2 * BUF >= 2 * BM * 4, "bias scratch");
-
-    constexpr int LOOP_BYTES = 2 * BUF;
-    constexpr int EPI_BYTES = (NT / 64) * TileLds<TN>::BYTES;
-    constexpr int MAIN_BYTES = LOOP_BYTES > EPI_BYTES ? LOOP_BYTES : EPI_BYTES;
-    __shared__ __attribute__((aligned(16))) char smem[MAIN_BYTES + (H ? (BM + BN) * 4 : 0)];
+    static_assert(TNSmem<BM, BN, WM, WN, H>::LOOP >= 2 * BM * 4, "bias scratch");
+    constexpr int MAIN_BYTES = TNSmem<BM, BN, WM, WN, H>::MAIN;
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     const int wm0 = (wave / WN) * WTM;
     const int wn0 = (wave % WN) * WTN;
-    int o0, jt, split;
-    if constexpr (CT > 0) {
-        const int w = blockIdx.x, slot = w >> 3;
-        o0 = 0;
-        jt = slot % CT;
-        split = (slot / CT) * 8 + (w & 7);
-    } else {
-        o0 = blockIdx.x * BM;
-        jt = blockIdx.y;
-        split = blockIdx.z;
-    }
     const int j0 = jt * BN;
     const size_t s0 = (size_t)split * p.rows_per_split;
     const int nkt = p.rows_per_split / XK;
@@ -835,6 +833,41 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN >= 8 ? 2 : 1) void k_gemm_tn_
         __syncthreads();
         for (int c = tid; c < BM; c += NT) p.bslab[(size_t)split * p.nout + o0 + c] = lb[c] + lb[BM + c];
     }
+}
+
+template <int BM, int BN, int WM, int WN, bool H = false, int NS = 1, int CT = 0>
+__global__ __launch_bounds__(64 * WM * WN, WM * WN >= 8 ? 2 : 1) void k_gemm_tn_x6(TNArgs p) {
+    __shared__ __attribute__((aligned(16))) char smem[TNSmem<BM, BN, WM, WN, H>::BYTES];
+    int o0, jt, split;
+    if constexpr (CT > 0) {
+        const int w = blockIdx.x, slot = w >> 3;
+        o0 = 0;
+        jt = slot % CT;
+        split = (slot / CT) * 8 + (w & 7);
+    } else {
+        o0 = blockIdx.x * BM;
+        jt = blockIdx.y;
+        split = blockIdx.z;
+    }
+    tn_block<BM, BN, WM, WN, H, NS>(p, smem, o0, jt, split);
+}
+
+// A layer with a 64-wide second input segment (l4's skip input enc_p, the colour layer's
+// view encoding enc_d) in ONE launch (nerf_linear_bwd_weight_seg): per split, CT column tiles
+// of BN over the first segment (pm) and one BN2 tile over the second (ps: its x, col0 = k1),
+// all CT + 1 on one XCD in consecutive dispatch slots (workgroups go round-robin over the 8
+// XCDs), so the split's dy rows come from HBM once and from that XCD's L2 for the other tiles
+// -- as two launches, the 64-wide one re-read all of dy for a quarter of the columns.
+template <int BM, int BN, int WM, int WN, int BN2, int WM2, int WN2, int CT, int NS>
+__global__ __launch_bounds__(64 * WM * WN, 2) void k_gemm_tn_x6_seg(TNArgs pm, TNArgs ps) {
+    static_assert(WM * WN == WM2 * WN2 && WM * WN == 8, "both tiles at eight waves");
+    constexpr int B1 = TNSmem<BM, BN, WM, WN, true>::BYTES, B2 = TNSmem<BM, BN2, WM2, WN2, true>::BYTES;
+    __shared__ __attribute__((aligned(16))) char smem[B1 > B2 ? B1 : B2];
+    const int w = blockIdx.x, slot = w >> 3;
+    const int jt = slot % (CT + 1);
+    const int split = (slot / (CT + 1)) * 8 + (w & 7);
+    if (jt < CT) tn_block<BM, BN, WM, WN, true, NS>(pm, smem, 0, jt, split);
+    else tn_block<BM, BN2, WM2, WN2, true, NS>(ps, smem, 0, 0, split);
 }
 
 template <int BM, int BN, int WM, int WN, int EPI>
@@ -923,6 +956,22 @@ int dispatch_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, h
     else pick_tn_x6<false>(a, nout, kin, splits, policy, s);
     prof_end(s, flops, h16 ? 3 : 6);
     return check_launch(h16 ? "k_gemm_tn_x6 (fp16 pair)" : "k_gemm_tn_x6");
+}
+
+bool tn_seg_supported(int nout, int k1, int k2, int splits) {
+    return k2 == 64 && k1 == 256 && (nout == 256 || nout == 128) && splits % 8 == 0;
+}
+
+int dispatch_tn_x6_seg(const TNArgs& pm, const TNArgs& ps, int nout, int splits, hipStream_t s, double flops) {
+    prof_begin(s);
+    if (nout == 256)   // l4: two XCD-paired 256 x 128 tiles over h3 + the 256 x 64 tile over enc_p
+        hipLaunchKernelGGL((k_gemm_tn_x6_seg<256, 128, 4, 2, 64, 4, 2, 2, 1>), dim3(3 * splits), dim3(512), 0, s, pm,
+                           ps);
+    else               // colour layer: the 128 x 256 tile over f + the 128 x 64 tile over enc_d
+        hipLaunchKernelGGL((k_gemm_tn_x6_seg<128, 256, 2, 4, 64, 4, 2, 1, 1>), dim3(2 * splits), dim3(512), 0, s, pm,
+                           ps);
+    prof_end(s, flops, 3);
+    return check_launch("k_gemm_tn_x6_seg (fp16 pair)");
 }
 
 }  // namespace nerf

@@ -46,7 +46,7 @@ class ProfKind(ctypes.Structure):
 
 
 PROF_KINDS = ("fwd", "dx", "dw", "dw_narrow")   # NERF_PROF_FWD / _DX / _DW / _DW_NARROW
-ABI_VERSION = 10                   # NERF_HIP_ABI_VERSION
+ABI_VERSION = 11                   # NERF_HIP_ABI_VERSION
 
 
 class ChainLayer(ctypes.Structure):
@@ -68,6 +68,8 @@ _SIGS = {
                               _c_i, _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_linear_bwd_weight": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p,
                                 _c_p], _c_i),
+    "nerf_linear_bwd_weight_seg": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p, _c_i, _c_p,
+                                    _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_linear_bwd_weight_splits": ([_c_i, _c_i, _c_i], _c_i),
     "nerf_slab_reduce": ([_c_p, _c_i, _c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_heads_fwd": ([_c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
@@ -255,6 +257,14 @@ def linear_bwd_weight(dy, nout, x, kin, m, splits, slab, ldslab, col0, bslab, dy
     precision mode 2 runs the fp16 pair kernel."""
     _call("nerf_linear_bwd_weight", _ptr(dy), _ld(dy), nout, _ptr(x), _ld(x), kin, m, splits,
           _ptr(slab), ldslab, col0, _ptr(bslab), _ptr(dy_cmax), _ptr(x_cmax), _stream())
+
+
+def linear_bwd_weight_seg(dy, nout, x1, k1, x2, k2, m, splits, slab, ldslab, bslab, dy_cmax=None, x1_cmax=None,
+                          x2_cmax=None):
+    """Weight gradient of a layer whose input is [x1 | x2] (l4, the colour layer): slab columns
+    [0, k1) from x1 and [k1, k1 + k2) from x2 -- in mode 2 one launch reading dy once."""
+    _call("nerf_linear_bwd_weight_seg", _ptr(dy), _ld(dy), nout, _ptr(x1), _ld(x1), k1, _ptr(x2), _ld(x2), k2, m,
+          splits, _ptr(slab), ldslab, _ptr(bslab), _ptr(dy_cmax), _ptr(x1_cmax), _ptr(x2_cmax), _stream())
 
 
 def bwd_weight_splits(nout, kin, m) -> int:

@@ -418,11 +418,17 @@ class FieldRunner:
             splits = _hip.bwd_weight_splits(l.out_p, k1, Np)
             slab = e(splits * l.out_p * l.kp)
             bslab = e(splits * l.out_p)
-            _hip.linear_bwd_weight(dy, l.out_p, x_in, k1, Np, splits, slab, l.kp, 0, bslab, dy_cmax=dy_cm,
-                                   x_cmax=fcm.get(prev_cm[l.name]))
-            if l.seg2:
-                _hip.linear_bwd_weight(dy, l.out_p, seg_buf[l.seg2], 64, Np, splits, slab, l.kp, k1, None,
-                                       dy_cmax=dy_cm, x_cmax=fcm.get(l.seg2))
+            if l.seg2 and os.environ.get("NERF_DW_SEG", "1") != "0":
+                # both input segments in one launch (dy read once; nerf_linear_bwd_weight_seg).
+                # NERF_DW_SEG=0 (A/B only): the two launches of round 3's first half
+                _hip.linear_bwd_weight_seg(dy, l.out_p, x_in, k1, seg_buf[l.seg2], 64, Np, splits, slab, l.kp, bslab,
+                                           dy_cmax=dy_cm, x1_cmax=fcm.get(prev_cm[l.name]), x2_cmax=fcm.get(l.seg2))
+            else:
+                _hip.linear_bwd_weight(dy, l.out_p, x_in, k1, Np, splits, slab, l.kp, 0, bslab, dy_cmax=dy_cm,
+                                       x_cmax=fcm.get(prev_cm[l.name]))
+                if l.seg2:
+                    _hip.linear_bwd_weight(dy, l.out_p, seg_buf[l.seg2], 64, Np, splits, slab, l.kp, k1, None,
+                                           dy_cmax=dy_cm, x_cmax=fcm.get(l.seg2))
             gb = G(l.linear.bias) if l.out_p == nout_ref else e(l.out_p)
             _hip.slab_reduce(slab, splits, l.out_p, l.kp, nout_ref, kin_ref, bslab, G(W), gb)
             if l.out_p != nout_ref:

@@ -29,8 +29,9 @@ SETTINGS = {
     "heads_joint": (0, 0, {"NERF_HEADS_SIDE": "0"}),
     "chain": (0, 0, {"NERF_CHAIN": "1"}),
     "per_layer": (0, 0, {"NERF_CHAIN": "0"}),
+    "dw_two_launch": (0, 0, {"NERF_DW_SEG": "0"}),
 }
-ENV_KEYS = ("NERF_TAIL_MAIN", "NERF_HEADS_SIDE", "NERF_CHAIN")
+ENV_KEYS = ("NERF_TAIL_MAIN", "NERF_HEADS_SIDE", "NERF_CHAIN", "NERF_DW_SEG")
 
 
 def main():

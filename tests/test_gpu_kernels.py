@@ -195,6 +195,38 @@ def _bwd_weight_case(dev, nout, kin, m, splits):
     assert (gb.cpu().double() - dy.double().sum(0)).abs().max().item() < 1e-4 * max(1, dy.abs().sum(0).max().item())
 
 
+@pytest.mark.parametrize("nout,m,splits", [(256, 131072, 128), (128, 131072, 256), (256, 8192, 16), (128, 4096, 8),
+                                           (256, 4096, 4)])
+def test_linear_bwd_weight_seg(dev, gemm_precision, nout, m, splits):
+    """The two-segment weight gradient (l4's [h3 | enc_p], the colour layer's [f | enc_d]):
+    one launch in mode 2 (TN policy 7, splits % 8 == 0), two otherwise -- bit-identical to
+    the two nerf_linear_bwd_weight calls it replaces (the same tiles, splits and k order),
+    and within 2e-5 of fp64 after the slab reduce; (256, 4096, 4) takes the two-call path."""
+    g = torch.Generator().manual_seed(nout + splits)
+    k1, k2 = 256, 64
+    dy = _rand(m, nout, g=g).to(dev)
+    x1 = _rand(m, k1, g=g).to(dev)
+    x2 = _rand(m, k2, g=g).to(dev)
+    slab_a = torch.full((splits * nout * (k1 + k2),), float("nan"), device=dev)
+    slab_b = torch.full_like(slab_a, float("nan"))
+    bslab_a = torch.full((splits * nout,), float("nan"), device=dev)
+    bslab_b = torch.full_like(bslab_a, float("nan"))
+    _hip.linear_bwd_weight_seg(dy, nout, x1, k1, x2, k2, m, splits, slab_a, k1 + k2, bslab_a, dy_cmax=_cm(dy),
+                               x1_cmax=_cm(x1), x2_cmax=_cm(x2))
+    _hip.linear_bwd_weight(dy, nout, x1, k1, m, splits, slab_b, k1 + k2, 0, bslab_b, dy_cmax=_cm(dy), x_cmax=_cm(x1))
+    _hip.linear_bwd_weight(dy, nout, x2, k2, m, splits, slab_b, k1 + k2, k1, None, dy_cmax=_cm(dy), x_cmax=_cm(x2))
+    torch.cuda.synchronize()
+    assert torch.equal(slab_a, slab_b)
+    assert torch.equal(bslab_a, bslab_b)
+    gw = torch.empty(nout, k1 + k2, device=dev)
+    gb = torch.empty(nout, device=dev)
+    _hip.slab_reduce(slab_a, splits, nout, k1 + k2, nout, k1 + k2, bslab_a, gw, gb)
+    ref = dy.double().t() @ torch.cat([x1, x2], 1).double()
+    torch.cuda.synchronize()
+    assert (gw.double() - ref).abs().max().item() < 2e-5 * ref.abs().max().item()
+    assert (gb.double() - dy.double().sum(0)).abs().max().item() < 1e-4 * max(1, dy.abs().sum(0).max().item())
+
+
 def test_slab_reduce_accumulate(dev):
     """nerf_slab_reduce with accumulate=1 adds onto the existing gradient (train.py's
     gradient accumulation across render calls); split sums in a fixed order."""
@@ -217,7 +249,7 @@ def test_slab_reduce_accumulate(dev):
     assert torch.allclose(gw2, 2 * (gw - gw0), atol=1e-4)
 
 
-@pytest.mark.parametrize("scale_a,scale_b,spread", [(1.0, 0.1, 0), (1e-3, 1e3, 0), (1e-20, 1.0, 0), (1.0, 0.1, 8),
+@pytest.mark.parametrize("scale_a,scale_b,spread",[(1.0, 0.1, 0), (1e-3, 1e3, 0), (1e-20, 1.0, 0), (1.0, 0.1, 8),
                                                     (1e-7, 1.0, 12), (1e4, 1e-6, 0)])
 def test_split_accuracy(dev, scale_a, scale_b, spread):
     """The split-bf16 GEMM (mode 1) and the fp16-pair GEMM (mode 2) against fp64: their
