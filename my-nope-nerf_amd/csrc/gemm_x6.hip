@@ -918,23 +918,28 @@ int dispatch_nt_x6(const NTArgs& a, int epi, int policy, hipStream_t s, double f
     return check_launch(h16 ? "k_gemm_nt_x6 (fp16 pair)" : "k_gemm_nt_x6");
 }
 
+// one register set for the eight-wave TN tiles too: loads issued two and three iterations
+// ahead (register sets 3 / 4) ran the same, 90.3 / 90.8 / 90.6 us per 131072 x 256 x 256
+// weight gradient (profiles/r03/tn_ns_ab.txt) -- the loop is not waiting on load latency
+constexpr int kTnNs8 = 1;
+
 template <bool H>
 static void pick_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, hipStream_t s) {
-    constexpr int NS = 1;   // one register set: tiles loaded 3 ahead ran the same (profiles/r02/tn_pipeline_ab.txt)
+    constexpr int NS = 1;   // the 4-wave tiles: loaded 3 ahead ran the same (profiles/r02/tn_pipeline_ab.txt)
     if (tn_xcd_group(policy, nout, kin, splits) == 2)   // eight waves (two per SIMD), 64 x 64 per wave
-        hipLaunchKernelGGL((k_gemm_tn_x6<256, 128, 4, 2, H, NS, 2>), dim3(2 * splits), dim3(512), 0, s, a);
+        hipLaunchKernelGGL((k_gemm_tn_x6<256, 128, 4, 2, H, kTnNs8, 2>), dim3(2 * splits), dim3(512), 0, s, a);
     else if (policy >= 3 && nout % 256 == 0 && kin % 256 == 0)
         hipLaunchKernelGGL((k_gemm_tn_x6<256, 256, 2, 2, H, NS>), dim3(nout / 256, kin / 256, splits), dim3(256), 0,
                            s, a);
     else if (policy == 7 && nout == 128 && kin % 256 == 0)
         // the colour layer (128 outputs, 256 feature columns): one column tile per 256 inputs, so
         // each split reads its dy rows once (two 128 x 128 column tiles read them twice)
-        hipLaunchKernelGGL((k_gemm_tn_x6<128, 256, 2, 4, H, NS>), dim3(1, kin / 256, splits), dim3(512), 0, s, a);
+        hipLaunchKernelGGL((k_gemm_tn_x6<128, 256, 2, 4, H, kTnNs8>), dim3(1, kin / 256, splits), dim3(512), 0, s, a);
     else if (nout % 128 == 0 && kin % 128 == 0)
         hipLaunchKernelGGL((k_gemm_tn_x6<128, 128, 2, 2, H, NS>), dim3(nout / 128, kin / 128, splits), dim3(256), 0,
                            s, a);
     else if (policy == 7 && nout % 256 == 0 && kin == 64)   // eight waves, 64 x 32 per wave
-        hipLaunchKernelGGL((k_gemm_tn_x6<256, 64, 4, 2, H, NS>), dim3(nout / 256, 1, splits), dim3(512), 0, s, a);
+        hipLaunchKernelGGL((k_gemm_tn_x6<256, 64, 4, 2, H, kTnNs8>), dim3(nout / 256, 1, splits), dim3(512), 0, s, a);
     else if (policy >= 3 && nout % 256 == 0 && kin == 64)
         // a 64-wide input (the encodings: l0, the skip segment of l4) against all 256 outputs in
         // one tile, so each split's dy rows are read once (128 x 64 tiles read them twice)
@@ -965,10 +970,10 @@ bool tn_seg_supported(int nout, int k1, int k2, int splits) {
 int dispatch_tn_x6_seg(const TNArgs& pm, const TNArgs& ps, int nout, int splits, hipStream_t s, double flops) {
     prof_begin(s);
     if (nout == 256)   // l4: two XCD-paired 256 x 128 tiles over h3 + the 256 x 64 tile over enc_p
-        hipLaunchKernelGGL((k_gemm_tn_x6_seg<256, 128, 4, 2, 64, 4, 2, 2, 1>), dim3(3 * splits), dim3(512), 0, s, pm,
+        hipLaunchKernelGGL((k_gemm_tn_x6_seg<256, 128, 4, 2, 64, 4, 2, 2, kTnNs8>), dim3(3 * splits), dim3(512), 0, s, pm,
                            ps);
     else               // colour layer: the 128 x 256 tile over f + the 128 x 64 tile over enc_d
-        hipLaunchKernelGGL((k_gemm_tn_x6_seg<128, 256, 2, 4, 64, 4, 2, 1, 1>), dim3(2 * splits), dim3(512), 0, s, pm,
+        hipLaunchKernelGGL((k_gemm_tn_x6_seg<128, 256, 2, 4, 64, 4, 2, 1, kTnNs8>), dim3(2 * splits), dim3(512), 0, s, pm,
                            ps);
     prof_end(s, flops, 3);
     return check_launch("k_gemm_tn_x6_seg (fp16 pair)");

@@ -32,6 +32,14 @@ KINDS = {
         4 * (M // 128) * D * 9 + 4 * M * 4,
         "reads enc_p + enc_d 67.1 MB + their row maxima 1.0 MB (weights stream from L2); writes the nine 256-wide "
         "outputs 1208 MB + hr 67.1 MB + ReLU words 37.7 MB + column maxima 9.4 MB + raw4 2.1 MB"),
+    "k_gemm_tn_x6_seg<256, 128, 4, 2, 64, 4, 2, 2, 1>": (
+        "dw", 4 * M * (D + D + 64) + 4 * D * (D + 64), "dy 134.2 MB + h3 134.2 MB + enc_p 33.6 MB + dW 0.33 MB "
+        "(l4: two XCD-grouped 256 x 128 tiles over h3 and the 256 x 64 tile over enc_p, dy fetched once per XCD); "
+        "measured writes are the 128 split-K slabs (41.9 MB)"),
+    "k_gemm_tn_x6_seg<128, 256, 2, 4, 64, 4, 2, 1, 1>": (
+        "dw_narrow", 4 * M * (128 + D + 64) + 4 * 128 * (D + 64), "dy 67.1 MB + f 134.2 MB + enc_d 33.6 MB + dW "
+        "0.16 MB (colour layer: the 128 x 256 tile over f and the 128 x 64 tile over enc_d, dy fetched once per XCD); "
+        "measured writes are the 256 split-K slabs (41.9 MB)"),
     "k_gemm_tn_x6<256, 256, 2, 2, true, 1>": (
         "dw", 4 * M * D * 2 + 4 * D * D, "dy 134.2 MB + x 134.2 MB + dW 0.26 MB; measured writes are the 256 "
         "split-K slabs (67 MB)"),
