@@ -21,6 +21,7 @@
 #ifndef NERF_HIP_H
 #define NERF_HIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -37,7 +38,8 @@ extern "C" {
 /* ABI version: 5 added nerf_prof_read_kinds and nerf_render_eval_fused, 6 the 4x4-chain
  * backwards (nerf_pose_c2w_bwd, nerf_mat4_inv_bwd, nerf_mat4_mul(_bwd), nerf_unproject_matrix_bwd)
  * and the depth-prior distortion (nerf_depth_affine(_bwd)), 7 nerf_linear_fwd_heads, 8 nerf_heads_bwd_mode,
- * 9 precision mode 2 as the default, 10 nerf_mlp_chain_train, 11 nerf_linear_bwd_weight_seg. */
+ * 9 precision mode 2 as the default, 10 nerf_mlp_chain_train, 11 nerf_linear_bwd_weight_seg and
+ * nerf_field_backward. */
 #define NERF_HIP_ABI_VERSION 11
 int nerf_hip_abi_version(void);
 const char* nerf_hip_last_error(void);
@@ -139,6 +141,59 @@ int nerf_linear_bwd_weight_seg(const float* dy, int lddy, int nout, const float*
                                const float* x2, int ldx2, int k2, int m, int splits, float* slab, int ldslab,
                                float* bslab, const float* dy_cmax, const float* x1_cmax, const float* x2_cmax,
                                void* stream);
+
+/* ---------------------------------------------------------------------------
+ * The training backward of the field in one host call (ABI 11): FieldRunner.backward's
+ * launch schedule -- composite backward (or a given graw4), heads, then per layer from the
+ * colour layer down the input-gradient GEMM on `stream` and the weight gradient + slab
+ * reduce on `side_stream` behind an event, the last `tail_main` layers' weight gradients on
+ * `stream` after the chain, the encoding backward for ray gradients -- for hidden 256 /
+ * colour 128 in GEMM precision mode 2 (the autograd of official_nerf.py:60-96 and
+ * rendering.py:113-141 that training.py:92 runs).  The same launches in the same order as
+ * the Python schedule, so the gradients are bit-identical to it; the host cost is a few
+ * microseconds per launch instead of a ctypes call + temporaries each.  Layer index l:
+ * 0..7 the trunk l0..l7, 8 the feature layer, 9 the colour layer.  On return `stream` has
+ * waited for `side_stream`.  No allocation: temporaries live in `workspace`
+ * (nerf_field_bwd_workspace_bytes). */
+#define NERF_BWD_LAYERS 10
+typedef struct nerf_field_bwd {
+    int n_pad, n_rays, n_samples, flags, ray_grad, tail_main;
+    /* forward state (nerf_mlp_chain_train / nerf_encode_samples outputs) */
+    const float* z;
+    const float* raw4;
+    const float* enc_p;
+    const float* enc_d;
+    const float* enc_p_cmax;
+    const float* enc_d_cmax;
+    const float* act[NERF_BWD_LAYERS];      /* layer outputs [n_pad][256] (colour layer [n_pad][128]) */
+    const uint32_t* mask[NERF_BWD_LAYERS];  /* ReLU words [n_pad][out/32] (feature layer: NULL) */
+    const float* cmax[NERF_BWD_LAYERS];     /* column maxima [n_pad/128][out] (colour layer: NULL) */
+    const float* pts_o;                     /* ray inputs of nerf_encode_samples (ray_grad only) */
+    const float* pts_d;
+    const float* view;
+    /* packed parameters (nerf_pack_weights, mode 2) */
+    const float* wt[NERF_BWD_LAYERS];       /* f32 W^T [kp][out_p] */
+    const uint16_t* wt_img[NERF_BWD_LAYERS];/* fp16 pair image of W^T */
+    const float* wd;                        /* fc_density weight [256], 16-byte aligned */
+    const float* wc;                        /* fc_rgb weight [3][128] */
+    /* upstream gradient: graw4 [n_pad][4], or g_rgb [R][3] + g_dist [R] through the composite */
+    const float* g_rgb;
+    const float* g_dist;
+    const float* graw4;
+    /* outputs, reference layout */
+    float* gw[NERF_BWD_LAYERS];
+    float* gb[NERF_BWD_LAYERS];
+    float* g_wd;
+    float* g_bd;
+    float* g_wc;
+    float* g_bc;
+    float* g_pts_o;
+    float* g_pts_d;
+    float* g_view;
+    void* workspace;
+} nerf_field_bwd;
+size_t nerf_field_bwd_workspace_bytes(int n_pad, int ray_grad);
+int nerf_field_backward(const nerf_field_bwd* args, void* stream, void* side_stream);
 
 /* Recommended `splits` for nerf_linear_bwd_weight at this shape and tile policy. */
 int nerf_linear_bwd_weight_splits(int nout, int kin, int m);

@@ -1,0 +1,213 @@
+// Native executor of the field backward (nerf_field_backward): the launch schedule of
+// FieldRunner.backward for the D = 256 / colour 128 field in precision mode 2 in one host
+// call -- the autograd of official_nerf.py:60-96 and rendering.py:113-141 as launched by
+// training.py:92.  The Python schedule issues ~60 ctypes launches, ~20 temporaries and ~10
+// cross-stream events per step (0.8 ms of host time at cfg2, profiles/r03/host_split_cfg2.json);
+// here the same launches, in the same order on the same two streams, take a few microseconds
+// each, so the eager step stays GPU-bound on a slow host core.
+//
+// Schedule (per layer, from the colour layer down): the input-gradient GEMM on the caller's
+// stream, the weight gradient + its split-K slab reduce on the side stream once that layer's
+// dy exists (an event), the last `tail_main` layers' weight gradients on the caller's stream
+// after the input-gradient chain.  The head-weight partials run first on the side stream,
+// dyr (the colour layer's dy, gated by its ReLU words) on the caller's.
+#include "common.hpp"
+
+#include <vector>
+
+namespace {
+
+constexpr int L = NERF_BWD_LAYERS;
+constexpr int D = 256, HR = 128;
+// layer table (FieldRunner.layers): output rows, first-segment K, padded K, second segment
+// (0 none, 1 enc_p, 2 enc_d)
+constexpr int OUT_P[L] = {D, D, D, D, D, D, D, D, D, HR};
+constexpr int K1[L] = {64, D, D, D, D, D, D, D, D, D};
+constexpr int KP[L] = {64, D, D, D, D + 64, D, D, D, D, D + 64};
+constexpr int SEG[L] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 2};
+constexpr int NREF[L] = {D, D, D, D, D, D, D, D, D, HR};
+constexpr int KREF[L] = {63, D, D, D, D + 63, D, D, D, D, D + 27};
+constexpr int LF = 8, LR = 9;
+
+struct Carve {
+    char* base;
+    size_t off = 0;
+    float* take(size_t n) {
+        off = (off + 255) & ~size_t(255);
+        float* p = base ? reinterpret_cast<float*>(base + off) : nullptr;
+        off += n * sizeof(float);
+        return p;
+    }
+};
+
+struct Work {
+    float *graw4, *dyr, *dyr_rm, *dyr_cm, *part;
+    float *dx[L], *dx_rm[L], *dx_cm[L];   // dx[l]: gradient w.r.t. layer l's first input (l = 1..9)
+    float *genc_p0, *genc_p4, *genc_d;
+    float *slab[L], *bslab[L];
+    int splits[L];
+};
+
+size_t carve(char* base, int np, int ray_grad, Work& w) {
+    Carve c{base};
+    w.graw4 = c.take((size_t)np * 4);
+    w.dyr = c.take((size_t)np * HR);
+    w.dyr_rm = c.take(np);
+    w.dyr_cm = c.take((size_t)(np / 128) * HR);
+    w.part = c.take((size_t)nerf_heads_part_size(D, np));
+    for (int l = 1; l < L; ++l) {
+        w.dx[l] = c.take((size_t)np * K1[l]);
+        w.dx_rm[l] = c.take(np);
+        w.dx_cm[l] = c.take((size_t)(np / 128) * K1[l]);
+    }
+    w.dx[0] = w.dx_rm[0] = w.dx_cm[0] = nullptr;
+    w.genc_p0 = ray_grad ? c.take((size_t)np * 64) : nullptr;
+    w.genc_p4 = ray_grad ? c.take((size_t)np * 64) : nullptr;
+    w.genc_d = ray_grad ? c.take((size_t)np * 64) : nullptr;
+    for (int l = 0; l < L; ++l) {
+        w.splits[l] = nerf_linear_bwd_weight_splits(OUT_P[l], K1[l], np);
+        w.slab[l] = c.take((size_t)w.splits[l] * OUT_P[l] * KP[l]);
+        w.bslab[l] = c.take((size_t)w.splits[l] * OUT_P[l]);
+    }
+    return c.off + 256;
+}
+
+// events: a per-thread pool (the autograd engine runs backwards on one thread per device)
+struct EventPool {
+    std::vector<hipEvent_t> ev;
+    size_t next = 0;
+    hipEvent_t get() {
+        if (next == ev.size()) {
+            hipEvent_t e;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+            ev.push_back(e);
+        }
+        return ev[next++];
+    }
+};
+thread_local EventPool g_events;
+
+#define RC(x)                \
+    do {                     \
+        const int rc_ = (x); \
+        if (rc_) return rc_; \
+    } while (0)
+
+// side waits for everything issued on main so far
+int fork(hipStream_t main, hipStream_t side) {
+    hipEvent_t e = g_events.get();
+    NERF_CHECK(e != nullptr, "nerf_field_backward: hipEventCreate failed");
+    NERF_CHECK(hipEventRecord(e, main) == hipSuccess && hipStreamWaitEvent(side, e, 0) == hipSuccess,
+               "nerf_field_backward: cross-stream event failed");
+    return NERF_OK;
+}
+
+// weight + bias gradient of layer l (dy: its output gradient) on stream s
+int weight_grad(const nerf_field_bwd& a, const Work& w, int l, const float* dy, const float* dy_cm, void* s) {
+    const int np = a.n_pad;
+    const float* x = l == 0 ? a.enc_p : a.act[l - 1];
+    const float* x_cm = l == 0 ? a.enc_p_cmax : a.cmax[l - 1];
+    if (SEG[l]) {
+        RC(nerf_linear_bwd_weight_seg(dy, OUT_P[l], OUT_P[l], x, K1[l], K1[l], SEG[l] == 1 ? a.enc_p : a.enc_d, 64, 64,
+                                      np, w.splits[l], w.slab[l], KP[l], w.bslab[l], dy_cm, x_cm,
+                                      SEG[l] == 1 ? a.enc_p_cmax : a.enc_d_cmax, s));
+    } else {
+        RC(nerf_linear_bwd_weight(dy, OUT_P[l], OUT_P[l], x, K1[l], K1[l], np, w.splits[l], w.slab[l], KP[l], 0,
+                                  w.bslab[l], dy_cm, x_cm, s));
+    }
+    return nerf_slab_reduce(w.slab[l], w.splits[l], OUT_P[l], KP[l], NREF[l], KREF[l], w.bslab[l], a.gw[l], a.gb[l], 0,
+                            s);
+}
+
+}  // namespace
+
+extern "C" size_t nerf_field_bwd_workspace_bytes(int n_pad, int ray_grad) {
+    if (n_pad <= 0 || n_pad % 128) return 0;
+    Work w;
+    return carve(nullptr, n_pad, ray_grad, w);
+}
+
+extern "C" int nerf_field_backward(const nerf_field_bwd* ap, void* stream, void* side_stream) {
+    NERF_CHECK_PTR(ap);
+    const nerf_field_bwd& a = *ap;
+    const int np = a.n_pad;
+    NERF_CHECK(np > 0 && np % 128 == 0 && a.workspace && side_stream && stream != side_stream,
+               "%s: n_pad=%d (a positive multiple of 128), a workspace and a second stream are required", __func__, np);
+    NERF_CHECK(nerf::gemm_precision() == 2, "%s: the native backward runs GEMM precision mode 2", __func__);
+    NERF_CHECK(a.tail_main >= 0 && a.tail_main <= L, "%s: tail_main=%d", __func__, a.tail_main);
+    NERF_CHECK(a.graw4 || (a.g_rgb && a.g_dist && a.z && a.raw4), "%s: need graw4 or (g_rgb, g_dist, raw4, z)",
+               __func__);
+    for (int l = 0; l < L; ++l) {
+        NERF_CHECK(a.act[l] && a.wt[l] && a.wt_img[l] && a.gw[l] && a.gb[l], "%s: layer %d: missing tensor", __func__,
+                   l);
+        NERF_CHECK((l == LF) == (a.mask[l] == nullptr), "%s: layer %d: ReLU words (none for the feature layer)",
+                   __func__, l);
+        NERF_CHECK((l == LR) == (a.cmax[l] == nullptr), "%s: layer %d: column maxima (none for the colour layer)",
+                   __func__, l);
+    }
+    NERF_CHECK(a.enc_p && a.enc_d && a.enc_p_cmax && a.enc_d_cmax && a.wd && a.wc && a.g_wd && a.g_bd && a.g_wc &&
+                   a.g_bc,
+               "%s: missing encoding / head tensor", __func__);
+    NERF_CHECK(!a.ray_grad || (a.pts_o && a.pts_d && a.view && a.z && a.g_pts_o && a.g_pts_d && a.g_view),
+               "%s: ray gradients need pts_o / pts_d / view / z and their gradient outputs", __func__);
+    Work w;
+    carve(reinterpret_cast<char*>(a.workspace), np, a.ray_grad, w);
+    hipStream_t main = nerf::as_stream(stream), side = nerf::as_stream(side_stream);
+    g_events.next = 0;
+
+    const float* graw4 = a.graw4;
+    if (!graw4) {
+        RC(nerf_composite_bwd(a.raw4, a.z, a.n_rays, a.n_samples, a.flags, a.g_rgb, a.g_dist, w.graw4, np, stream));
+        graw4 = w.graw4;
+    }
+    // heads: the head-weight partials (re-reading h8 and hr) on the side stream, dyr on main
+    RC(fork(main, side));
+    RC(nerf_heads_bwd_mode(2, graw4, a.act[7], D, a.act[LR], HR, nullptr, 0, D, a.wc, nullptr, 0, w.part, np, nullptr,
+                           nullptr, side_stream));
+    RC(nerf_heads_reduce(w.part, D, np, a.g_wd, a.g_bd, a.g_wc, a.g_bc, 0, side_stream));
+    RC(nerf_heads_bwd_mode(1, graw4, nullptr, 0, nullptr, 0, a.mask[LR], HR / 32, D, a.wc, w.dyr, HR, nullptr, np,
+                           w.dyr_rm, w.dyr_cm, stream));
+
+    const float *dy = w.dyr, *dy_rm = w.dyr_rm, *dy_cm = w.dyr_cm;
+    int deferred[L], nd = 0;
+    const float *def_dy[L], *def_cm[L];
+    for (int step = 0; step < L; ++step) {
+        const int l = L - 1 - step;   // lr, lf, l7, ..., l0
+        if (step >= L - a.tail_main) {
+            deferred[nd] = l; def_dy[nd] = dy; def_cm[nd] = dy_cm; ++nd;
+        } else {
+            RC(fork(main, side));
+            RC(weight_grad(a, w, l, dy, dy_cm, side_stream));
+        }
+        // input gradient: dx = (dy W) masked by the ReLU words of the layer's input
+        const int op = OUT_P[l];
+        const uint16_t* img = a.wt_img[l];
+        const int img_rows = KP[l];
+        if (l == 0) {
+            if (a.ray_grad)
+                RC(nerf_linear_bwd_data(dy, op, op, a.wt[l], img, img_rows, nullptr, 0, nullptr, nullptr, 0, w.genc_p0,
+                                        64, np, 64, dy_rm, nullptr, nullptr, stream));
+            break;
+        }
+        if (SEG[l] && a.ray_grad)
+            RC(nerf_linear_bwd_data(dy, op, op, a.wt[l] + (size_t)K1[l] * op, img + (size_t)K1[l] * 8, img_rows,
+                                    nullptr, 0, nullptr, nullptr, 0, SEG[l] == 1 ? w.genc_p4 : w.genc_d, 64, np, 64,
+                                    dy_rm, nullptr, nullptr, stream));
+        const uint32_t* mask = l == LR ? nullptr : a.mask[l - 1];
+        const int ldmask = OUT_P[l - 1 < 0 ? 0 : l - 1] / 32;
+        if (l == LF)   // + the density path: d sigma_raw (graw4[:, 0]) x w_density, rank one
+            RC(nerf_linear_bwd_data(dy, op, op, a.wt[l], img, img_rows, graw4, 4, a.wd, mask, ldmask, w.dx[l], K1[l],
+                                    np, K1[l], dy_rm, w.dx_rm[l], w.dx_cm[l], stream));
+        else
+            RC(nerf_linear_bwd_data(dy, op, op, a.wt[l], img, img_rows, nullptr, 0, nullptr, mask, ldmask, w.dx[l],
+                                    K1[l], np, K1[l], dy_rm, w.dx_rm[l], w.dx_cm[l], stream));
+        dy = w.dx[l]; dy_rm = w.dx_rm[l]; dy_cm = w.dx_cm[l];
+    }
+    for (int i = 0; i < nd; ++i) RC(weight_grad(a, w, deferred[i], def_dy[i], def_cm[i], stream));
+    // join: the side stream's gradients are complete before the caller's stream goes on
+    RC(fork(side, main));
+    if (a.ray_grad)
+        RC(nerf_encode_bwd(a.pts_o, a.pts_d, a.view, a.z, w.genc_p0, w.genc_p4, w.genc_d, a.n_rays, a.n_samples,
+                           a.g_pts_o, a.g_pts_d, a.g_view, stream));
+    return NERF_OK;
+}

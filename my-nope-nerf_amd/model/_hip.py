@@ -49,6 +49,20 @@ PROF_KINDS = ("fwd", "dx", "dw", "dw_narrow")   # NERF_PROF_FWD / _DX / _DW / _D
 ABI_VERSION = 11                   # NERF_HIP_ABI_VERSION
 
 
+_P10 = _c_p * 10
+
+
+class FieldBwd(ctypes.Structure):
+    """nerf_field_bwd (include/nerf_hip.h): the native backward's arguments."""
+    _fields_ = [("n_pad", _c_i), ("n_rays", _c_i), ("n_samples", _c_i), ("flags", _c_i), ("ray_grad", _c_i),
+                ("tail_main", _c_i), ("z", _c_p), ("raw4", _c_p), ("enc_p", _c_p), ("enc_d", _c_p),
+                ("enc_p_cmax", _c_p), ("enc_d_cmax", _c_p), ("act", _P10), ("mask", _P10), ("cmax", _P10),
+                ("pts_o", _c_p), ("pts_d", _c_p), ("view", _c_p), ("wt", _P10), ("wt_img", _P10), ("wd", _c_p),
+                ("wc", _c_p), ("g_rgb", _c_p), ("g_dist", _c_p), ("graw4", _c_p), ("gw", _P10), ("gb", _P10),
+                ("g_wd", _c_p), ("g_bd", _c_p), ("g_wc", _c_p), ("g_bc", _c_p), ("g_pts_o", _c_p), ("g_pts_d", _c_p),
+                ("g_view", _c_p), ("workspace", _c_p)]
+
+
 class ChainLayer(ctypes.Structure):
     """nerf_chain_layer (include/nerf_hip.h)."""
     _fields_ = [("img", _c_p), ("img_rows", _c_i), ("bias", _c_p), ("out", _c_p), ("ldo", _c_i), ("mask", _c_p),
@@ -71,6 +85,8 @@ _SIGS = {
     "nerf_linear_bwd_weight_seg": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p, _c_i, _c_p,
                                     _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_linear_bwd_weight_splits": ([_c_i, _c_i, _c_i], _c_i),
+    "nerf_field_bwd_workspace_bytes": ([_c_i, _c_i], ctypes.c_size_t),
+    "nerf_field_backward": ([_c_p, _c_p, _c_p], _c_i),
     "nerf_slab_reduce": ([_c_p, _c_i, _c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_heads_fwd": ([_c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_heads_part_size": ([_c_i, _c_i], _c_i),
@@ -274,6 +290,16 @@ def bwd_weight_splits(nout, kin, m) -> int:
 def slab_reduce(slab, splits, nout, ldslab, nout_ref, kin_ref, bslab, gw, gb, accumulate=False):
     _call("nerf_slab_reduce", _ptr(slab), splits, nout, ldslab, nout_ref, kin_ref, _ptr(bslab), _ptr(gw),
           _ptr(gb), int(accumulate), _stream())
+
+
+def field_bwd_workspace_bytes(n_pad, ray_grad) -> int:
+    return int(lib().nerf_field_bwd_workspace_bytes(n_pad, int(ray_grad)))
+
+
+def field_backward(args: FieldBwd, side_stream: int):
+    """The training backward of the D = 256 field in one call (nerf_field_backward) on the
+    current stream + `side_stream` (a raw HIP stream handle)."""
+    _call("nerf_field_backward", ctypes.addressof(args), _stream(), side_stream)
 
 
 def heads_fwd(h8, hr, hidden, wd, bd, wc, bc, raw4, n_pad):

@@ -301,6 +301,47 @@ class FieldRunner:
         default = "1" if (self.D == 256 and Np >= 65536) else "0"
         return int(os.environ.get("NERF_HEADS_SIDE", default)) != 0
 
+    def native_backward(self, Np: int) -> bool:
+        """The training backward as one native call (nerf_field_backward, csrc/field_bwd.cpp):
+        the Python schedule below, launch for launch, for the configuration it covers -- GEMM
+        precision mode 2, hidden 256 / colour 128, the split heads backward (Np >= 65536).
+        Bit-identical gradients (tests/test_gpu_native_bwd.py); 0.8 ms of Python host time per
+        cfg2 step become a few microseconds per launch.  NERF_NATIVE_BWD=0 keeps the Python
+        schedule."""
+        return (self.h16 and self.D == 256 and self.HR == 128 and self.heads_side(Np)
+                and os.environ.get("NERF_NATIVE_BWD", "1") != "0")
+
+    def _backward_native(self, st, g_rgb, g_dist, want_ray_grad, graw4, G):
+        Np, R, S = st["Np"], st["R"], st["S"]
+        dev = st["z"].device
+        m = self.m
+        if self._side is None or self._side[0].device != dev:
+            self._side = [torch.cuda.Stream(dev)]
+        acts, masks, cms = st["acts"], st["masks"], st["cmaxes"]
+        names = [l.name for l in self.layers]
+        P = lambda t: None if t is None else t.data_ptr()            # noqa: E731
+        ray = None
+        ray_ptrs = (None, None, None)
+        if want_ray_grad:
+            ray = tuple(torch.empty(R, 3, device=dev) for _ in range(3))
+            ray_ptrs = tuple(t.data_ptr() for t in ray)
+        ws = torch.empty(_hip.field_bwd_workspace_bytes(Np, want_ray_grad), device=dev, dtype=torch.uint8)
+        tail_default = 2 if Np >= 65536 else 0
+        args = _hip.FieldBwd(
+            Np, R, S, st["flags"], int(want_ray_grad), int(os.environ.get("NERF_TAIL_MAIN", str(tail_default))),
+            P(st["z"]), P(st["raw4"]), P(st["enc_p"]), P(st["enc_d"]), P(st["cmaxes"]["enc_p"]),
+            P(st["cmaxes"]["enc_d"]), _hip._P10(*[a.data_ptr() for a in acts]),
+            _hip._P10(*[P(masks.get(n)) for n in names]), _hip._P10(*[P(cms.get(n)) for n in names]),
+            P(st["pts_o"]), P(st["pts_d"]), P(st["view"]),
+            _hip._P10(*[self.wt[n].data_ptr() for n in names]), _hip._P10(*[self.wts[n].data_ptr() for n in names]),
+            self.wd.data_ptr(), self.wc.data_ptr(), P(g_rgb), P(g_dist), P(graw4),
+            _hip._P10(*[G(l.linear.weight).data_ptr() for l in self.layers]),
+            _hip._P10(*[G(l.linear.bias).data_ptr() for l in self.layers]),
+            G(m.fc_density.weight).data_ptr(), G(m.fc_density.bias).data_ptr(), G(m.fc_rgb.weight).data_ptr(),
+            G(m.fc_rgb.bias).data_ptr(), *ray_ptrs, ws.data_ptr())
+        _hip.field_backward(args, self._side[0].cuda_stream)
+        return ray
+
     def param_list(self) -> List[torch.nn.Parameter]:
         """The field's parameters in module order.  Cached: walking the module tree costs ~75 us
         of host time and runs twice per training step; the runner already binds the layers'
@@ -339,6 +380,8 @@ class FieldRunner:
             off += p.numel()
         G = lambda p: grads[id(p)]
 
+        if g_h8 is None and self.native_backward(Np):
+            return [G(p) for p in params], self._backward_native(st, g_rgb, g_dist, want_ray_grad, graw4, G)
         if graw4 is None:
             graw4 = e(Np, 4)
             _hip.composite_bwd(st["raw4"], st["z"], R, S, flags, g_rgb, g_dist, graw4, Np)

@@ -30,8 +30,9 @@ SETTINGS = {
     "chain": (0, 0, {"NERF_CHAIN": "1"}),
     "per_layer": (0, 0, {"NERF_CHAIN": "0"}),
     "dw_two_launch": (0, 0, {"NERF_DW_SEG": "0"}),
+    "python_bwd": (0, 0, {"NERF_NATIVE_BWD": "0"}),
 }
-ENV_KEYS = ("NERF_TAIL_MAIN", "NERF_HEADS_SIDE", "NERF_CHAIN", "NERF_DW_SEG")
+ENV_KEYS = ("NERF_TAIL_MAIN", "NERF_HEADS_SIDE", "NERF_CHAIN", "NERF_DW_SEG", "NERF_NATIVE_BWD")
 
 
 def main():
