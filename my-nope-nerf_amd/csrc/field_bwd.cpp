@@ -64,8 +64,8 @@ size_t carve(char* base, int np, int ray_grad, Work& w) {
     w.genc_p0 = ray_grad ? c.take((size_t)np * 64) : nullptr;
     w.genc_p4 = ray_grad ? c.take((size_t)np * 64) : nullptr;
     w.genc_d = ray_grad ? c.take((size_t)np * 64) : nullptr;
+    for (int l = 0; l < L; ++l) w.splits[l] = nerf_linear_bwd_weight_splits(OUT_P[l], K1[l], np);
     for (int l = 0; l < L; ++l) {
-        w.splits[l] = nerf_linear_bwd_weight_splits(OUT_P[l], K1[l], np);
         w.slab[l] = c.take((size_t)w.splits[l] * OUT_P[l] * KP[l]);
         w.bslab[l] = c.take((size_t)w.splits[l] * OUT_P[l]);
     }

@@ -38,9 +38,10 @@ def _rays(R, S, seed):
 
 
 def _grads(net, fn, native, env=None):
-    old = {k: os.environ.get(k) for k in ("NERF_NATIVE_BWD", *(env or {}))}
+    env = dict(env or {})
+    old = {k: os.environ.get(k) for k in ("NERF_NATIVE_BWD", *env)}
     os.environ["NERF_NATIVE_BWD"] = "1" if native else "0"
-    os.environ.update(env or {})
+    os.environ.update(env)
     try:
         net.zero_grad(set_to_none=True)
         extra = fn()
@@ -97,3 +98,4 @@ def test_native_backward_from_raw_heads(dev, h16):
     g_python = _grads(net, fn, False)
     for a, b in zip(g_native, g_python):
         assert torch.equal(a, b)
+
