@@ -48,3 +48,17 @@ def assert_elementwise(a, b, rtol=RENDER_RTOL, atol=RENDER_ATOL, what=""):
         raise AssertionError(f"{what}: element {i}: |{a_.flatten()[i].item():.9g} - {b_.flatten()[i].item():.9g}| = "
                              f"{err.flatten()[i].item():.3g} > {rtol:g}*|b| + {atol:g} "
                              f"(max-normalised error {(err.max() / b_.abs().max().clamp_min(1e-30)).item():.3g})")
+
+
+def report_err(test: str, name: str, err: float) -> float:
+    """Observed parity error of one checked quantity, appended to $NERF_ERR_REPORT (one JSON
+    line each) when set -- the survey the gradient tolerances are set from; returns err."""
+    import json
+    import os
+    path = os.environ.get("NERF_ERR_REPORT")
+    if path:
+        from model import _hip
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": test, "name": name, "err": float(err),
+                                "mode": _hip.gemm_get_precision()}) + "\n")
+    return err

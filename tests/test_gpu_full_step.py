@@ -15,7 +15,7 @@ import torch
 import model as mdl
 from model.optim import HipAdam
 from oracle import nerf_oracle as orc
-from tests.helpers import camera_K, make_cfg, rigid_c2w
+from tests.helpers import camera_K, make_cfg, report_err, rigid_c2w
 
 pytestmark = pytest.mark.gpu
 
@@ -142,13 +142,14 @@ def test_full_nope_nerf_step_matches_oracle(dev, gemm_precision, case):
         for k in keys:
             a, b = float(lh[k].detach()), float(lo[k].detach())
             assert abs(a - b) <= 1e-4 * abs(b) + 1e-6, f"step {step} {k}: HIP {a} oracle {b}"
-        assert _rel(pose.r.grad, o_pose["r"].grad) < 2e-3, ("r", pose.r.grad, o_pose["r"].grad)
-        assert _rel(pose.t.grad, o_pose["t"].grad) < 2e-3, ("t", pose.t.grad, o_pose["t"].grad)
-        assert _rel(dist.global_scales.grad, o_dist["scales"].grad) < 2e-3
-        assert _rel(dist.global_shifts.grad, o_dist["shifts"].grad) < 2e-3
+        for nm, a, b in (("pose.r", pose.r.grad, o_pose["r"].grad), ("pose.t", pose.t.grad, o_pose["t"].grad),
+                         ("dist.scales", dist.global_scales.grad, o_dist["scales"].grad),
+                         ("dist.shifts", dist.global_shifts.grad, o_dist["shifts"].grad)):
+            # observed <= 5.8e-6 in every GEMM mode (profiles/r03/grad_err_survey.json)
+            assert report_err("full_step", nm, _rel(a, b)) < 1e-4, (nm, a, b)
         for (n1, p1), (n2, p2) in zip(net.named_parameters(), ref.named_parameters()):
             assert n1 == n2
-            assert _nrel(p1.grad, p2.grad) < 2e-3, (step, n1, _nrel(p1.grad, p2.grad))
+            assert report_err("full_step", n1, _nrel(p1.grad, p2.grad)) < 2e-3, (step, n1, _nrel(p1.grad, p2.grad))
         for o in (opt, opt_pose, opt_dist, o_opt, o_opt_pose, o_opt_dist):
             o.step()
     # both optimisers saw the same gradients: the updated parameters agree to ~lr

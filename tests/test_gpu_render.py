@@ -7,7 +7,7 @@ import torch
 from model.official_nerf import OfficialStaticNerf
 from model.rendering import Renderer
 from oracle import nerf_oracle as orc
-from tests.helpers import assert_elementwise, make_cfg, synthetic_rays
+from tests.helpers import assert_elementwise, make_cfg, report_err, synthetic_rays
 
 pytestmark = pytest.mark.gpu
 
@@ -94,8 +94,8 @@ def test_render_backward_matches_oracle(dev, gemm_precision):
     for (n, p), (n2, q) in zip(net.named_parameters(), ref.named_parameters()):
         assert n == n2
         g, gr = p.grad.cpu(), q.grad
-        err = (g - gr).norm() / gr.norm().clamp_min(1e-12)
-        assert err.item() < 2e-3, f"{n}: rel grad err {err.item():.2e}"
+        err = report_err("render_backward", n, ((g - gr).norm() / gr.norm().clamp_min(1e-12)).item())
+        assert err < 2e-3, f"{n}: rel grad err {err:.2e}"
 
 
 def test_render_ray_gradients(dev, gemm_precision):
@@ -117,8 +117,9 @@ def test_render_ray_gradients(dev, gemm_precision):
     w2c = torch.inverse(orc.make_c2w(r, t) @ c2w).unsqueeze(0)
     o = orc.render_nope_nerf(ref, b["pixels"], b["depth"], b["K"], w2c, b["scale"], cfg["rendering"], noise=b["noise"])
     o["rgb"].sum().backward()
-    for a, bb in ((rd.grad.cpu(), r.grad), (td.grad.cpu(), t.grad)):
-        assert ((a - bb).norm() / bb.norm()).item() < 5e-3
+    for nm, a, bb in (("r", rd.grad.cpu(), r.grad), ("t", td.grad.cpu(), t.grad)):
+        # observed <= 1.7e-5 in every GEMM mode (profiles/r03/grad_err_survey.json)
+        assert report_err("render_ray_gradients", nm, ((a - bb).norm() / bb.norm()).item()) < 2e-4
 
 
 def test_points_forward_api(dev, gemm_precision):
