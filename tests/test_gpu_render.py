@@ -98,6 +98,47 @@ def test_render_backward_matches_oracle(dev, gemm_precision):
         assert err < 2e-3, f"{n}: rel grad err {err:.2e}"
 
 
+_REF_GRADS = {}
+
+
+def _reference_grads(cfg, ref, b, gt, dtype):
+    """The oracle's parameter gradients of the render-backward loss in `dtype` (cached)."""
+    key = dtype
+    if key not in _REF_GRADS:
+        r = orc.OracleNerf(hidden_dim=cfg["model"]["hidden_dim"]).to(dtype)
+        r.load_state_dict({k: v.to(dtype) for k, v in ref.state_dict().items()})
+        c = lambda t: t.to(dtype)                                          # noqa: E731
+        o = orc.render_nope_nerf(r, c(b["pixels"]), c(b["depth"]), c(b["K"]), c(b["w2c"]), c(b["scale"]),
+                                 cfg["rendering"], noise=c(b["noise"]))
+        (orc.rgb_full_loss(o["rgb"], c(gt)) + 0.04 * orc.depth_l1_loss(o["depth_pred"], o["depth_gt"])).backward()
+        _REF_GRADS[key] = {n: p.grad.double() for n, p in r.named_parameters()}
+    return _REF_GRADS[key]
+
+
+def test_render_backward_as_accurate_as_reference(dev, gemm_precision):
+    """The HIP parameter gradients against the oracle evaluated in fp64: within 1.5x (+1e-5) of
+    how far the fp32 reference itself lands from fp64.  The early layers' gradients of the
+    fp32 reference are ~2e-3 off its own fp64 value (ReLU / sign decisions near zero), which is
+    why the fp32-vs-fp32 bar of test_render_backward_matches_oracle is 2e-3."""
+    cfg = make_cfg(hidden=256, S=128)
+    net, ref = _pair(cfg, 1)
+    b = synthetic_rays(R=512, S=128, seed=5)
+    gt = torch.rand(1, 512, 3, generator=torch.Generator().manual_seed(6))
+    net = net.to(dev)
+    rnd = Renderer(net, cfg["rendering"], device=dev)
+    out = rnd.nope_nerf(b["pixels"].to(dev), b["depth"].to(dev), b["K"].to(dev), b["w2c"].to(dev),
+                        b["scale"].to(dev), add_noise=True, noise=b["noise"].to(dev))
+    (orc.rgb_full_loss(out["rgb"], gt.to(dev)) + 0.04 * orc.depth_l1_loss(out["depth_pred"], out["depth_gt"])).backward()
+    g32 = _reference_grads(cfg, ref, b, gt, torch.float32)
+    g64 = _reference_grads(cfg, ref, b, gt, torch.float64)
+    for n, p in net.named_parameters():
+        e_hip = ((p.grad.double().cpu() - g64[n]).norm() / g64[n].norm()).item()
+        e_ref = ((g32[n] - g64[n]).norm() / g64[n].norm()).item()
+        report_err("vs_fp64_hip", n, e_hip)
+        report_err("vs_fp64_ref32", n, e_ref)
+        assert e_hip <= 1.5 * e_ref + 1e-5, f"{n}: HIP {e_hip:.2e} vs the fp32 reference's {e_ref:.2e} (both vs fp64)"
+
+
 def test_render_ray_gradients(dev, gemm_precision):
     """pose learning: gradients w.r.t. the camera pose flow through the encodings."""
     cfg = make_cfg(hidden=64, S=64)
