@@ -204,6 +204,46 @@ def cpu_baseline(budget_s=20.0):
                       f"{n} timed steps after 1 warm-up ({el:.1f} s)"}
 
 
+def render_frame_line(dev, frames=3, warmup=1):
+    """The cfg4 workload beside the headline (1 GPU): one 188x621 frame x 128 samples through the
+    reference caller's path (render_dist.render_image -> Renderer -> the fused per-ray eval
+    kernel, samples + encodings + ten linears + heads + composite in one launch), with its MFMA
+    roofline: 2 x 593 408 f32-equivalent FLOP per sample against the fp16-pair
+    peak.  A few frames, ~0.2 s."""
+    from model.common import arange_pixels
+    from model.official_nerf import OfficialStaticNerf
+    from model.render_dist import render_image
+    from model.rendering import Renderer
+    from model.synthetic import camera_K, make_cfg as pkg_cfg, rigid_c2w
+    H, W = 188, 621
+    cfg = pkg_cfg(hidden=HIDDEN, S=SAMPLES)
+    torch.manual_seed(42)
+    net = OfficialStaticNerf(cfg).to(dev)
+    rnd = Renderer(net, cfg["rendering"], device=dev)
+    K = camera_K(H, W, 362.5, 362.5).to(dev)
+    w2c = torch.inverse(rigid_c2w(0)).unsqueeze(0).to(dev)
+    scale = torch.eye(4, device=dev).unsqueeze(0)
+    pix = arange_pixels((H, W), 1, device=dev)[1]
+    for _ in range(warmup):
+        render_image(rnd, pix, K, w2c, scale)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        rgb, _ = render_image(rnd, pix, K, w2c, scale)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / frames
+    if not bool(torch.isfinite(rgb).all()):
+        raise RuntimeError("render: non-finite frame")
+    flops = 2.0 * 593408 * H * W * SAMPLES
+    peak = BF16_MFMA_PEAK_TFLOPS / 3
+    ach = flops / el / 1e12
+    return {"metric": "full-frame eval render rays/s (config 4: 188x621, 128 samples/ray, D=256)",
+            "value": H * W / el, "unit": "rays/s", "ms_per_frame": 1e3 * el, "frames": frames,
+            "kernel": "k_render_fused2 (nerf_render_eval_fused: samples, encodings, ten linears, heads, composite)",
+            "roofline": {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s (f32-equivalent)",
+                         "frac": ach / peak}}
+
+
 def spawn_ranks(n, argv, script=None):
     """--gpus N > 1 without a launcher: run this script under torch.distributed.run as a
     CHILD process (N ranks, one per GPU, rendezvous on 127.0.0.1) and return its exit
@@ -477,6 +517,7 @@ def main():
                 "timing": "per-kind hipEvent pairs around every GEMM launch on its own stream, second timed "
                           "pass of the same K steps (ms_per_step of that pass: %.3f)" % (1e3 * elapsed_hooks /
                                                                                           args.steps)}
+        render = render_frame_line(dev) if world == 1 and args.gemm_precision == "f16x3" else None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             log("timing the CPU baseline (oracle) ...")
@@ -498,7 +539,7 @@ def main():
                           "global_batch": world * RAYS, "seq_len": SAMPLES, "hidden_dim": HIDDEN,
                           "parallelism": f"dp{world}"},
                "final_loss": loss, "train_psnr_last_step": psnr,
-               "roofline": roof, "cpu_baseline": cpu, "alt_gemm": alt}
+               "roofline": roof, "cpu_baseline": cpu, "alt_gemm": alt, "render_cfg4": render}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
