@@ -140,13 +140,21 @@ __device__ __forceinline__ void put_col8(char* img, int c, int g, const float (&
     *reinterpret_cast<uint4*>(d + 2 * I::PLANE) = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
+// Diagnostic builds only (make EXTRA=-DNERF_TN_ABLATE=1; results are wrong): the TN operand
+// strips written as one RNE fp16 word per value (no scale, no residual) -- the split's VALU out
+#ifndef NERF_TN_ABLATE
+#define NERF_TN_ABLATE 0
+#endif
 // fp16 pair form of put_col8 (column scale 2^e)
 template <int ROWS>
 __device__ __forceinline__ void put_col8h(char* img, int c, int g, const float (&v)[8], int e) {
     using I = XImg<ROWS, 2>;
     uint32_t h[4], l[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) split2h(v[2 * t], v[2 * t + 1], e, h[t], l[t]);
+    for (int t = 0; t < 4; ++t) {
+        if constexpr (NERF_TN_ABLATE & 1) { h[t] = pk_f16(v[2 * t], v[2 * t + 1]); l[t] = h[t]; }
+        else split2h(v[2 * t], v[2 * t + 1], e, h[t], l[t]);
+    }
     char* d = img + g * I::HALF + c * 16;
     *reinterpret_cast<uint4*>(d) = make_uint4(h[0], h[1], h[2], h[3]);
     *reinterpret_cast<uint4*>(d + I::PLANE) = make_uint4(l[0], l[1], l[2], l[3]);
