@@ -118,15 +118,17 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 KIND_NAMES = {
     "fwd": "forward NT (nerf_linear_fwd)",
     "dx": "input-gradient NT (nerf_linear_bwd_data)",
-    "dw": "weight-gradient TN on 256x256 tiles (nerf_linear_bwd_weight; algorithmic bytes exclude the split-K "
-          "slabs)",
-    "dw_narrow": "narrow weight-gradient TN (encoding segments, colour layer; nerf_linear_bwd_weight)",
+    "dw": "weight-gradient TN of the 256-output layers (nerf_linear_bwd_weight[_seg]: l1-l3, l5-l7, lf, and l4 "
+          "over [h3 | enc_p] in one launch; algorithmic bytes exclude the split-K slabs)",
+    "dw_narrow": "narrow weight-gradient TN (l0 over enc_p; the colour layer over [f | enc_d] in one launch)",
 }
 KERNEL = {
     "f16x3": {"fwd": "k_gemm_nt_x6<128,256,2,2,0,true,true,2> (fp16 pair, 3 products)",
               "dx": "k_gemm_nt_x6<128,256,2,2,1,true,true,2> (fp16 pair, 3 products)",
-              "dw": "k_gemm_tn_x6<256,128,4,2,true,1,2> (XCD-paired column tiles, 8 waves; fp16 pair, 3 products)",
-              "dw_narrow": "k_gemm_tn_x6<256,64,4,2|128,128,2,2|128,64,2,2,true> (fp16 pair, 3 products)"},
+              "dw": "k_gemm_tn_x6<256,128,4,2,true,1,2> + k_gemm_tn_x6_seg<256,128,4,2,64,4,2,2,1> (XCD-grouped "
+                    "column tiles, 8 waves; fp16 pair, 3 products)",
+              "dw_narrow": "k_gemm_tn_x6<256,64,4,2,true> + k_gemm_tn_x6_seg<128,256,2,4,64,4,2,1,1> (fp16 pair, "
+                           "3 products)"},
     "bf16x6": {"fwd": "k_gemm_nt_x6<256,256,2,2,0,true> (bf16x3 split, 6 products)",
                "dx": "k_gemm_nt_x6<256,256,2,2,1,true> (bf16x3 split, 6 products)",
                "dw": "k_gemm_tn_x6<256,128,4,2,false,1,2> (XCD-paired column tiles; bf16x3 split, 6 products)",
