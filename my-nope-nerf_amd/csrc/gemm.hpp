@@ -76,6 +76,7 @@ struct TNArgs {
     // fp16 pair kernel scales each split's columns by them
     const float* cm_dy; int ldcm_dy;
     const float* cm_x; int ldcm_x;
+    unsigned long long* stamps;   // diagnostic builds (-DNERF_TN_STAMPS=1): per-block phase cycles or NULL
 };
 
 // Backward-data epilogue operands (ReLU bits, rank-1 column), prefetched into registers

@@ -501,6 +501,7 @@ static int tn_args(const char* fn, const float* dy, int lddy, int nout, const fl
     a.bslab = bslab; a.nout = nout;
     a.ablate = g_ablate >> 4;
     a.cm_dy = dy_cmax; a.ldcm_dy = nout; a.cm_x = x_cmax; a.ldcm_x = kin;
+    a.stamps = g_stamps;
     return NERF_OK;
 }
 

@@ -160,6 +160,19 @@ __device__ __forceinline__ void put_col8h(char* img, int c, int g, const float (
     *reinterpret_cast<uint4*>(d + I::PLANE) = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
+// 4 consecutive k of column c (quarter q of the 16-row tile) -> 8-byte pieces of the fp16 pair
+// planes (put_col8h's layout: k-half q >> 1, byte offset 8 (q & 1) inside the column's chunk)
+template <int ROWS>
+__device__ __forceinline__ void put_col4h(char* img, int c, int q, const float (&v)[8], int e) {
+    using I = XImg<ROWS, 2>;
+    uint32_t h[2], l[2];
+    split2h(v[0], v[1], e, h[0], l[0]);
+    split2h(v[2], v[3], e, h[1], l[1]);
+    char* d = img + (q >> 1) * I::HALF + c * 16 + (q & 1) * 8;
+    *reinterpret_cast<uint2*>(d) = make_uint2(h[0], h[1]);
+    *reinterpret_cast<uint2*>(d + I::PLANE) = make_uint2(l[0], l[1]);
+}
+
 // max over the 128-row groups of rows [s0, s0 + rows) of a column-max array cm[group][ld]
 __device__ __forceinline__ float tn_colmax(const float* cm, int ld, size_t s0, int rows, int col) {
     float m = 0.f;
@@ -598,13 +611,21 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void k_gemm_nt_x6(NTArgs p) {
 // ---------------------------------------------------------------------------
 // The strips of a k-tile can be loaded NS tiles ahead of the split that consumes them (NS
 // register sets; dispatch_tn_x6 picks the depth).
+#ifndef NERF_TN_QUARTER
+#define NERF_TN_QUARTER 1
+#endif
+constexpr bool kTnQuarter = NERF_TN_QUARTER != 0;
 template <int BM, int BN, int NT, bool HH = false, int NSET = 1>
 struct TNStager {
     static constexpr bool H = HH;       // fp16 pair images with per-column scales (mode 2)
     static constexpr int NP = H ? 2 : 3;
     static constexpr int NS = NSET;     // register sets (tiles in flight)
     static constexpr int SA = (2 * BM + NT - 1) / NT;
-    static constexpr int SB = (2 * BN + NT - 1) / NT;
+    // BQ: the x tile as 4-row quarter strips, one per thread (4 BN == NT, the 256 x 128 tiles of
+    // eight waves): every wave loads and splits the same share, instead of half the waves a whole
+    // 8-row strip each while the other half wait at the barrier
+    static constexpr bool BQ = HH && kTnQuarter && 4 * BN == NT;
+    static constexpr int SB = BQ ? 1 : (2 * BN + NT - 1) / NT;
     const float* dyb; const float* xb;
     int lddy, ldx;
     int offa[SA], offb[SB];
@@ -613,7 +634,9 @@ struct TNStager {
     float bsum[SA];
     bool do_bias;
     __device__ __forceinline__ bool a_ok(int i) const { return SA * NT == 2 * BM || (int)threadIdx.x + NT * i < 2 * BM; }
-    __device__ __forceinline__ bool b_ok(int i) const { return SB * NT == 2 * BN || (int)threadIdx.x + NT * i < 2 * BN; }
+    __device__ __forceinline__ bool b_ok(int i) const {
+        return BQ || SB * NT == 2 * BN || (int)threadIdx.x + NT * i < 2 * BN;
+    }
 
     // buffer descriptors over this split's dy / x rows: one 32-bit lane offset per strip
     // (VGPR) and the row offset of each of its 8 loads in an SGPR, instead of 16 + 16
@@ -635,7 +658,7 @@ struct TNStager {
 #pragma unroll
         for (int i = 0; i < SB; ++i) {
             const int idx = threadIdx.x + NT * i;
-            offb[i] = 4 * (8 * (idx / BN) * ldx + idx % BN);
+            offb[i] = 4 * ((BQ ? 4 : 8) * (idx / BN) * ldx + idx % BN);
             if (H) eb[i] = row_exp(tn_colmax(p.cm_x, p.ldcm_x, s0, p.rows_per_split, j0 + idx % BN));
         }
         do_bias = bias;
@@ -654,7 +677,7 @@ struct TNStager {
         for (int i = 0; i < SB; ++i)
             if (b_ok(i)) {
 #pragma unroll
-                for (int t = 0; t < 8; ++t)
+                for (int t = 0; t < (BQ ? 4 : 8); ++t)
                     vb[U][i][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, offb[i], sb + t * ldx * 4, 0));
             }
     }
@@ -679,7 +702,8 @@ struct TNStager {
         for (int i = 0; i < SB; ++i)
             if (b_ok(i)) {
                 const int idx = threadIdx.x + NT * i;
-                if constexpr (H) put_col8h<BN>(Bimg, idx % BN, idx / BN, vb[U][i], eb[i]);
+                if constexpr (BQ) put_col4h<BN>(Bimg, idx % BN, idx / BN, vb[U][i], eb[i]);
+                else if constexpr (H) put_col8h<BN>(Bimg, idx % BN, idx / BN, vb[U][i], eb[i]);
                 else put_col8<BN>(Bimg, idx % BN, idx / BN, vb[U][i]);
             }
     }
@@ -707,9 +731,45 @@ struct TNStager {
 // set (kt+1) % NS) into the other buffer, issues the loads of tile kt+NS into the set tile kt
 // used (NS == 1: tile kt+2 into the one set, as before), then the MFMAs (VALU of the split
 // interleaved, 3 per MFMA gap) and one barrier.
+// Diagnostic builds only (make EXTRA=-DNERF_TN_STAMPS=1): per-block cycles of the TN main loop's
+// phases (wave 0; s_memtime between scheduling barriers, which also pins the order the
+// production build may interleave) into TNArgs::stamps[block][8]: fragment reads, the next
+// tile's split (with its load wait), load issue, MFMAs (with the fragment waits), barrier,
+// prologue, epilogue, total
+#ifndef NERF_TN_STAMPS
+#define NERF_TN_STAMPS 0
+#endif
+constexpr bool kTnStamps = NERF_TN_STAMPS != 0;
+struct TnClock {
+    unsigned long long b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long last = 0, start = 0;
+    __device__ __forceinline__ void begin() {
+        if constexpr (kTnStamps) { start = last = __builtin_amdgcn_s_memtime(); }
+    }
+    __device__ __forceinline__ void tick(int k) {
+        if constexpr (kTnStamps) {
+            __builtin_amdgcn_sched_barrier(0);
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            b[k] += t - last;
+            last = t;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    __device__ __forceinline__ void write(unsigned long long* out) {
+        if constexpr (kTnStamps) {
+            b[7] = __builtin_amdgcn_s_memtime() - start;
+            if (out && threadIdx.x == 0) {
+                const size_t blk = (size_t)blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) out[blk * 8 + k] = b[k];
+            }
+        }
+    }
+};
+
 template <int TM, int TN, int BM, int BN, typename Stager>
 __device__ __forceinline__ void tn_mainloop(char* smem, int nkt, int wm0, int wn0, f32x16 (&acc)[TM][TN],
-                                            Stager& st) {
+                                            Stager& st, TnClock& clk) {
     constexpr bool H = Stager::H;
     constexpr int NP = H ? 2 : 3;
     constexpr int NS = Stager::NS;
@@ -745,6 +805,7 @@ __device__ __forceinline__ void tn_mainloop(char* smem, int nkt, int wm0, int wn
     };
     constexpr int NPROD = H ? 3 : 6;
     st.prologue(smem, nkt);
+    clk.tick(5);
     auto iter = [&](int kt, auto uc) {
         constexpr int U = decltype(uc)::value;
         const char* cur = smem + (kt & 1) * BUF;
@@ -754,12 +815,15 @@ __device__ __forceinline__ void tn_mainloop(char* smem, int nkt, int wm0, int wn
         for (int j = 0; j < TN; ++j) rd(cur + boff + 32 * 16 * j, IB::PLANE, b[j]);
 #pragma unroll
         for (int i = 0; i < TM; ++i) rd(cur + aoff + 32 * 16 * i, IA::PLANE, a[i]);
+        clk.tick(0);
         if (kt + 1 < nkt) st.template put<(U + 1) % NS>(wimg, wimg + IA::BYTES, true);
+        clk.tick(1);
         if constexpr (NS == 1) {
             if (kt + 2 < nkt) st.template load<0>(kt + 2);
         } else {
             if (kt + NS < nkt) st.template load<U>(kt + NS);
         }
+        clk.tick(2);
 #pragma unroll
         for (int i = 0; i < TM; ++i) mm(i, a[i], b);
 #pragma unroll
@@ -768,7 +832,9 @@ __device__ __forceinline__ void tn_mainloop(char* smem, int nkt, int wm0, int wn
             __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
+        clk.tick(3);
         __syncthreads();
+        clk.tick(4);
     };
     for (int kt0 = 0; kt0 < nkt; kt0 += NS) {
         iter(kt0, std::integral_constant<int, 0>{});
@@ -823,11 +889,13 @@ __device__ __forceinline__ void tn_block(const TNArgs& p, char* smem, int o0, in
         for (int e = tid; e < BM; e += NT) lea[e] = row_exp(tn_colmax(p.cm_dy, p.ldcm_dy, s0, p.rows_per_split, o0 + e));
         for (int e = tid; e < BN; e += NT) leb[e] = row_exp(tn_colmax(p.cm_x, p.ldcm_x, s0, p.rows_per_split, j0 + e));
     }
+    TnClock clk;
+    clk.begin();
     TNStager<BM, BN, NT, H, NS> st;
     st.init(p, s0, o0, j0, do_bias);
     f32x16 acc[TM][TN];
     zero_acc(acc);
-    tn_mainloop<TM, TN, BM, BN>(smem, nkt, wm0, wn0, acc, st);
+    tn_mainloop<TM, TN, BM, BN>(smem, nkt, wm0, wn0, acc, st, clk);
 
     if constexpr (H) tn_store_lds<TM, TN, true>(p, acc, smem, split, o0, j0, wm0, wn0, lea, leb);
     else tn_store_lds(p, acc, smem, split, o0, j0, wm0, wn0);
@@ -841,6 +909,8 @@ __device__ __forceinline__ void tn_block(const TNArgs& p, char* smem, int o0, in
         __syncthreads();
         for (int c = tid; c < BM; c += NT) p.bslab[(size_t)split * p.nout + o0 + c] = lb[c] + lb[BM + c];
     }
+    clk.tick(6);
+    clk.write(p.stamps);
 }
 
 template <int BM, int BN, int WM, int WN, bool H = false, int NS = 1, int CT = 0>
