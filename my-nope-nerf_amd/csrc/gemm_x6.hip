@@ -160,17 +160,26 @@ __device__ __forceinline__ void put_col8h(char* img, int c, int g, const float (
     *reinterpret_cast<uint4*>(d + I::PLANE) = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
-// 4 consecutive k of column c (quarter q of the 16-row tile) -> 8-byte pieces of the fp16 pair
-// planes (put_col8h's layout: k-half q >> 1, byte offset 8 (q & 1) inside the column's chunk)
-template <int ROWS>
-__device__ __forceinline__ void put_col4h(char* img, int c, int q, const float (&v)[8], int e) {
+// R consecutive k of column c (sub-strip q of the 16-row tile, R = 8 / 4 / 2) -> the pieces of
+// put_col8h's layout: k-half q / (8 / R), byte offset 2 R (q % (8 / R)) inside the column's chunk
+template <int ROWS, int R>
+__device__ __forceinline__ void put_colRh(char* img, int c, int q, const float (&v)[8], int e) {
     using I = XImg<ROWS, 2>;
-    uint32_t h[2], l[2];
-    split2h(v[0], v[1], e, h[0], l[0]);
-    split2h(v[2], v[3], e, h[1], l[1]);
-    char* d = img + (q >> 1) * I::HALF + c * 16 + (q & 1) * 8;
-    *reinterpret_cast<uint2*>(d) = make_uint2(h[0], h[1]);
-    *reinterpret_cast<uint2*>(d + I::PLANE) = make_uint2(l[0], l[1]);
+    constexpr int PER_HALF = 8 / R;
+    char* d = img + (q / PER_HALF) * I::HALF + c * 16 + (q % PER_HALF) * (2 * R);
+    if constexpr (R == 4) {
+        uint32_t h[2], l[2];
+        split2h(v[0], v[1], e, h[0], l[0]);
+        split2h(v[2], v[3], e, h[1], l[1]);
+        *reinterpret_cast<uint2*>(d) = make_uint2(h[0], h[1]);
+        *reinterpret_cast<uint2*>(d + I::PLANE) = make_uint2(l[0], l[1]);
+    } else {
+        static_assert(R == 2, "sub-strips of 4 or 2 rows");
+        uint32_t h, l;
+        split2h(v[0], v[1], e, h, l);
+        *reinterpret_cast<uint32_t*>(d) = h;
+        *reinterpret_cast<uint32_t*>(d + I::PLANE) = l;
+    }
 }
 
 // max over the 128-row groups of rows [s0, s0 + rows) of a column-max array cm[group][ld]
@@ -621,10 +630,12 @@ struct TNStager {
     static constexpr int NP = H ? 2 : 3;
     static constexpr int NS = NSET;     // register sets (tiles in flight)
     static constexpr int SA = (2 * BM + NT - 1) / NT;
-    // BQ: the x tile as 4-row quarter strips, one per thread (4 BN == NT, the 256 x 128 tiles of
-    // eight waves): every wave loads and splits the same share, instead of half the waves a whole
-    // 8-row strip each while the other half wait at the barrier
-    static constexpr bool BQ = HH && kTnQuarter && 4 * BN == NT;
+    // RB: rows per x strip.  With fewer than NT / 2 columns the 8-row strips would go to part of
+    // the threads only; as RB-row sub-strips (RB = 16 BN / NT: 4 for 128 columns, 2 for 64 at
+    // eight waves) every thread takes one and every wave loads and splits the same share instead
+    // of some waves waiting at each barrier for the others
+    static constexpr int RB = (HH && kTnQuarter && NT % BN == 0 && (NT / BN == 4 || NT / BN == 8)) ? 16 * BN / NT : 8;
+    static constexpr bool BQ = RB < 8;
     static constexpr int SB = BQ ? 1 : (2 * BN + NT - 1) / NT;
     const float* dyb; const float* xb;
     int lddy, ldx;
@@ -658,7 +669,7 @@ struct TNStager {
 #pragma unroll
         for (int i = 0; i < SB; ++i) {
             const int idx = threadIdx.x + NT * i;
-            offb[i] = 4 * ((BQ ? 4 : 8) * (idx / BN) * ldx + idx % BN);
+            offb[i] = 4 * (RB * (idx / BN) * ldx + idx % BN);
             if (H) eb[i] = row_exp(tn_colmax(p.cm_x, p.ldcm_x, s0, p.rows_per_split, j0 + idx % BN));
         }
         do_bias = bias;
@@ -677,7 +688,7 @@ struct TNStager {
         for (int i = 0; i < SB; ++i)
             if (b_ok(i)) {
 #pragma unroll
-                for (int t = 0; t < (BQ ? 4 : 8); ++t)
+                for (int t = 0; t < RB; ++t)
                     vb[U][i][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, offb[i], sb + t * ldx * 4, 0));
             }
     }
@@ -702,7 +713,7 @@ struct TNStager {
         for (int i = 0; i < SB; ++i)
             if (b_ok(i)) {
                 const int idx = threadIdx.x + NT * i;
-                if constexpr (BQ) put_col4h<BN>(Bimg, idx % BN, idx / BN, vb[U][i], eb[i]);
+                if constexpr (BQ) put_colRh<BN, RB>(Bimg, idx % BN, idx / BN, vb[U][i], eb[i]);
                 else if constexpr (H) put_col8h<BN>(Bimg, idx % BN, idx / BN, vb[U][i], eb[i]);
                 else put_col8<BN>(Bimg, idx % BN, idx / BN, vb[U][i]);
             }
