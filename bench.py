@@ -246,6 +246,131 @@ def render_frame_line(dev, frames=3, warmup=1):
                          "frac": ach / peak}}
 
 
+def cfg3_setup(dev, capturable=False):
+    """Trainer with pose + distortion learning and the image-pair terms (config 3, reference
+    training.py:214-416) on the two-view synthetic scene -> (trainer, [data view 0, view 1]).
+    capturable: the pose / distortion Adams keep their step counts on the device (graphs)."""
+    import model as mdl
+    from model.optim import HipAdam
+    from model.synthetic import make_cfg as pkg_cfg, vkitti_pair_scene
+    cfg = pkg_cfg(hidden=HIDDEN, S=SAMPLES)
+    t = cfg["training"]
+    t["n_training_points"] = RAYS
+    t["annealing_epochs"], t["scheduling_start"] = 2000, 0      # default.yaml:139: rgb l1 in the early epochs
+    datas, c2w = vkitti_pair_scene(dev, H, W, FOCAL)
+    torch.manual_seed(42)
+    net = mdl.OfficialStaticNerf(cfg)
+    renderer = mdl.Renderer(net, cfg["rendering"], device=dev)
+    nn_model = mdl.get_model(renderer, cfg, device=dev)
+    opt = HipAdam(nn_model.parameters(), lr=1e-3)
+    pose = mdl.LearnPose(2, True, True, cfg, init_c2w=c2w.clone()).to(dev)
+    distn = mdl.Learn_Distortion(2, True, True, cfg).to(dev)
+    # train.py:100, :118; torch's fused Adam (the same update as the default multi-tensor
+    # path, fewer launches), capturable in graphs
+    opt_pose = torch.optim.Adam(pose.parameters(), lr=5e-4, capturable=capturable, fused=True)
+    opt_dist = torch.optim.Adam(distn.parameters(), lr=5e-4, capturable=capturable, fused=True)
+    tr = mdl.Trainer(nn_model, opt, t, device=dev, optimizer_pose=opt_pose, pose_param_net=pose,
+                     optimizer_distortion=opt_dist, distortion_net=distn)
+    return tr, datas
+
+
+def cfg3_measure(dev, graph, steps, warmup):
+    """The cfg3 step, eager or replaying one captured hipGraph per view (the two cameras
+    alternate: both branches of training.py:329-358) -> dict: seconds for `steps` timed steps,
+    median per-step GPU milliseconds (hipEvents at the step boundaries), median host enqueue
+    milliseconds per step, last loss dict."""
+    tr, datas = cfg3_setup(dev, capturable=graph)
+
+    def one(i):
+        return tr.train_step(datas[i % 2], it=i + 1, epoch=0, scheduling_start=0)
+
+    if graph:
+        tr.enable_graph_rng()                 # the ray draw keys on a device counter: new rays every replay
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for i in range(max(warmup, 2)):
+                one(i)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        graphs, outs = [], []
+        for v in range(2):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                outs.append(tr.train_step(datas[v], it=1, epoch=0, scheduling_start=0))
+            graphs.append(g)
+
+        def one(i):  # noqa: F811
+            graphs[i % 2].replay()
+            return outs[i % 2]
+
+    for i in range(warmup):
+        one(i)
+    torch.cuda.synchronize()
+    host = []
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    t0 = time.perf_counter()
+    evs[0].record()
+    for i in range(steps):
+        th = time.perf_counter()
+        ld = one(warmup + i)
+        host.append(time.perf_counter() - th)
+        evs[i + 1].record()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    gpu = statistics.median(evs[i].elapsed_time(evs[i + 1]) for i in range(steps))
+    return {"s": el, "gpu_ms_median": gpu, "host_ms_median": 1e3 * statistics.median(host), "ld": ld}
+
+
+def cfg3_line(dev, steps, warmup, modes=("eager", "graph")):
+    """BASELINE configs[2] beside the headline: the full NoPe-NeRF step -- joint pose +
+    depth-distortion learning, rgb + depth + point-cloud (chamfer, 7 285 points) + reprojection
+    (rgb_s) losses, 188x621, 1024 rays x 128 samples, D = 256 -- eager and as graph replays,
+    with the host enqueue time per step against the GPU time per step."""
+    runs = {}
+    for mode in modes:
+        m = cfg3_measure(dev, mode == "graph", steps, warmup)
+        ld = m["ld"]
+        runs[mode] = {"value": RAYS * steps / m["s"], "ms_per_step": 1e3 * m["s"] / steps,
+                      "gpu_ms_per_step_median": m["gpu_ms_median"],
+                      # host time to enqueue one step: a replay enqueues one graph launch
+                      "host_ms_per_step_median": m["host_ms_median"],
+                      "host_over_gpu": m["host_ms_median"] / m["gpu_ms_median"],
+                      "losses": {k: float(ld[k].detach()) for k in ("loss", "loss_rgb", "loss_depth", "loss_pc",
+                                                                    "loss_rgb_s")}}
+        if not all(math.isfinite(v) for v in runs[mode]["losses"].values()):
+            raise RuntimeError(f"cfg3 {mode}: non-finite loss {runs[mode]['losses']}")
+    best = max(runs, key=lambda k: runs[k]["value"])
+    r = runs[best]
+    return {"metric": "full NoPe-NeRF training rays/sec (config 3: pose + distortion + pc + rgb_s losses)",
+            "value": r["value"], "unit": "rays/s", "ms_per_step": r["ms_per_step"], "steps": steps,
+            "warmup": warmup, "execution": {"eager": "eager", "graph": "graph replay"}[best],
+            "data": "synthetic two-view V_KITTI-shaped scene (model.synthetic.vkitti_pair_scene)",
+            "config": {"workload": "config 3: 188x621, 1024 rays x 128 samples, D=256, pose + distortion learned, "
+                                   "pc chamfer 7285 points, rgb_s reprojection, cameras alternating"},
+            "runs": runs}
+
+
+def rank_attribution(world, steps, el_s, allreduce_ms, dev):
+    """N > 1: what each rank spent of the K timed steps, gathered from every rank -- the
+    all-reduce milliseconds (hipEvents around dist.all_reduce in Trainer.allreduce_grads,
+    training.py; they include the wait for the slowest rank), the rest of the step
+    ("compute"), and each rank's own rays/s -- so a scaling shortfall splits into
+    communication and compute spread."""
+    t = torch.tensor([el_s, allreduce_ms], dtype=torch.float64, device=dev)
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    per = [(float(x[0]), float(x[1])) for x in parts]
+    ar = [a / steps for _, a in per]
+    comp = [(1e3 * s - a) / steps for s, a in per]
+    rps = [RAYS * steps / s for s, _ in per]
+    return {"world_size": world, "allreduce_ms_per_step": max(ar), "allreduce_ms_per_step_min": min(ar),
+            "compute_ms_per_step_max": max(comp), "compute_ms_per_step_min": min(comp),
+            "rays_per_s_per_rank_min": min(rps), "rays_per_s_per_rank_max": max(rps),
+            "per_rank": [{"rank": i, "ms_per_step": 1e3 * s / steps, "allreduce_ms_per_step": a / steps}
+                         for i, (s, a) in enumerate(per)]}
+
+
 def spawn_ranks(n, argv, script=None):
     """--gpus N > 1 without a launcher: run this script under torch.distributed.run as a
     CHILD process (N ranks, one per GPU, rendezvous on 127.0.0.1) and return its exit
@@ -297,24 +422,32 @@ def plumbing(args, world, rank):
     tr = mdl.Trainer(net, None, cfg["training"], device=torch.device("cpu"), pose_param_net=pose,
                      distortion_net=dist_net)
     params = tr.bucket_params()
-    for i, p in enumerate(params):
-        p.grad = None if (rank == 1 and i == 0) else torch.full_like(p, float(rank + 1 + i))
+    steps = max(1, args.steps if args.steps < 30 else 3)
+    tr.time_collectives(True)
     t0 = time.perf_counter()
-    if world > 1:
-        tr.allreduce_grads()
+    for _ in range(steps):
+        for i, p in enumerate(params):
+            p.grad = None if (rank == 1 and i == 0) else torch.full_like(p, float(rank + 1 + i))
+        if world > 1:
+            tr.allreduce_grads()
     el = time.perf_counter() - t0
     for i, p in enumerate(params):
         ranks_with = [r for r in range(world) if not (r == 1 and i == 0)]
         want = sum(r + 1 + i for r in ranks_with) / world
         if p.grad is None or not torch.allclose(p.grad, torch.full_like(p, want)):
             raise RuntimeError(f"plumbing: parameter {i} not averaged over the ranks")
+    att = rank_attribution(world, steps, el, tr.collective_ms(), torch.device("cpu")) if world > 1 else None
     if world > 1:
         dist.barrier()
     if rank == 0:
-        print(json.dumps({"plumbing": True, "n_gpus": world, "world_size": dist.get_world_size() if world > 1 else 1,
-                          "bucket_params": len(params), "bucket_elems": sum(p.numel() for p in params),
-                          "allreduce_s": el, "data": "CPU gloo plumbing check of the launcher and gradient "
-                                                    "all-reduce; not a measurement"}), flush=True)
+        out = {"plumbing": True, "n_gpus": world, "world_size": dist.get_world_size() if world > 1 else 1,
+               "steps": steps, "bucket_params": len(params), "bucket_elems": sum(p.numel() for p in params),
+               "allreduce_s": el, "data": "CPU gloo plumbing check of the launcher and gradient all-reduce; "
+                                          "not a measurement"}
+        if att is not None:
+            out["allreduce_ms_per_step"] = att["allreduce_ms_per_step"]
+            out["multi_gpu"] = att
+        print(json.dumps(out), flush=True)
 
 
 def main():
@@ -332,6 +465,9 @@ def main():
                          "N > 1 runs eager (RCCL capture is not exercised on this pool)")
     ap.add_argument("--no-alt", dest="alt", action="store_false",
                     help="skip timing the other GEMM arithmetics (reported as alt_gemm)")
+    ap.add_argument("--no-cfg3", dest="cfg3", action="store_false",
+                    help="skip the config-3 line (full NoPe-NeRF step, eager and graph; 1 GPU)")
+    ap.add_argument("--cfg3-steps", type=int, default=20)
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU gloo check of the rank launcher + gradient all-reduce (tests), no GPU")
     args = ap.parse_args()
@@ -351,6 +487,7 @@ def main():
     cfg = make_cfg()
     data, c2w = synthetic_scene(dev)
     medians = {}      # median per-step milliseconds (hipEvents at the step boundaries) per timed pass
+    attributions = {}  # N > 1: per-rank all-reduce / compute split of the timed pass (rank_attribution)
 
     def measure(precision, with_hooks=True):
         """W warm-up + K timed train steps with the GEMMs in `precision` (0 exact-f32 MFMA,
@@ -371,6 +508,7 @@ def main():
             if world > 1:
                 dist.barrier()
             _hip.prof_enable(hooks)
+            trainer.time_collectives(world > 1 and not hooks)   # hipEvents around the all-reduce
             evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
             t0 = time.perf_counter()
             evs[0].record()
@@ -378,6 +516,7 @@ def main():
                 ld = one(it0 + i)
                 evs[i + 1].record()           # step boundaries on the launch stream (no host sync)
             torch.cuda.synchronize()
+            t_local = time.perf_counter() - t0       # this rank's own time, before the barrier
             if world > 1:
                 dist.barrier()
             t1 = time.perf_counter()
@@ -386,6 +525,9 @@ def main():
             _hip.prof_enable(False)
             el = t1 - t0
             med = statistics.median(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+            if world > 1 and not hooks:
+                timed.attribution = rank_attribution(world, args.steps, t_local, trainer.collective_ms(), dev)
+            trainer.time_collectives(False)
             if world > 1:
                 t = torch.tensor([el, med], device=dev, dtype=torch.float64)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -395,8 +537,10 @@ def main():
 
         for i in range(args.warmup):
             one(i)
+        timed.attribution = None
         el, ld, _, _ = timed(args.warmup, False)
         medians[precision] = timed.median_ms
+        attributions[precision] = timed.attribution
         if with_hooks:
             el_h, _, stats, kinds = timed(args.warmup + args.steps, True)
         else:
@@ -520,6 +664,11 @@ def main():
                           "pass of the same K steps (ms_per_step of that pass: %.3f)" % (1e3 * elapsed_hooks /
                                                                                           args.steps)}
         render = render_frame_line(dev) if world == 1 and args.gemm_precision == "f16x3" else None
+        full = None
+        if world == 1 and args.cfg3:
+            log("timing config 3 (the full NoPe-NeRF step) ...")
+            full = cfg3_line(dev, args.cfg3_steps, 3)
+            _hip.gemm_set_precision(main_prec)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             log("timing the CPU baseline (oracle) ...")
@@ -541,7 +690,12 @@ def main():
                           "global_batch": world * RAYS, "seq_len": SAMPLES, "hidden_dim": HIDDEN,
                           "parallelism": f"dp{world}"},
                "final_loss": loss, "train_psnr_last_step": psnr,
-               "roofline": roof, "cpu_baseline": cpu, "alt_gemm": alt, "render_cfg4": render}
+               "roofline": roof, "cpu_baseline": cpu, "alt_gemm": alt, "render_cfg4": render, "full_cfg3": full}
+        att = attributions.get(main_prec)
+        if att is not None:
+            out["world_size"] = world
+            out["allreduce_ms_per_step"] = att["allreduce_ms_per_step"]
+            out["multi_gpu"] = att
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -127,9 +127,26 @@ extern "C" size_t nerf_field_bwd_workspace_bytes(int n_pad, int ray_grad) {
     return carve(nullptr, n_pad, ray_grad, w);
 }
 
+namespace {
+int schedule(const nerf_field_bwd& a, void* stream, void* side_stream);
+}  // namespace
+
 extern "C" int nerf_field_backward(const nerf_field_bwd* ap, void* stream, void* side_stream) {
     NERF_CHECK_PTR(ap);
-    const nerf_field_bwd& a = *ap;
+    const int rc = schedule(*ap, stream, side_stream);
+    if (rc == NERF_OK || !side_stream || stream == side_stream) return rc;
+    // a launch failed part-way: the side stream may still run weight-gradient kernels on the
+    // workspace; join it into the caller's stream on this exit too, so the caller's allocator
+    // cannot hand the workspace out again while they write it (the error code is kept)
+    hipEvent_t e = g_events.get();
+    if (e && hipEventRecord(e, nerf::as_stream(side_stream)) == hipSuccess)
+        (void)hipStreamWaitEvent(nerf::as_stream(stream), e, 0);
+    return rc;
+}
+
+namespace {
+
+int schedule(const nerf_field_bwd& a, void* stream, void* side_stream) {
     const int np = a.n_pad;
     NERF_CHECK(np > 0 && np % 128 == 0 && a.workspace && side_stream && stream != side_stream,
                "%s: n_pad=%d (a positive multiple of 128), a workspace and a second stream are required", __func__, np);
@@ -211,3 +228,4 @@ extern "C" int nerf_field_backward(const nerf_field_bwd* ap, void* stream, void*
                            a.g_pts_o, a.g_pts_d, a.g_view, stream));
     return NERF_OK;
 }
+}  // namespace

@@ -85,8 +85,14 @@ class FieldRunner:
         self._plist = None
         # optional persistent gradient buffer (Trainer.allreduce_grads): when set, the backward
         # writes the parameter gradients as views of grad_buffer[:n] in param_list() order, so
-        # the data-parallel all-reduce runs in place on it
+        # the data-parallel all-reduce runs in place on it.  It is handed out once per step: the
+        # first backward that finds every field gradient None takes it (grad_buffer_taken), a
+        # second field backward in the same autograd pass (e.g. a render and an infer_occ summed
+        # into one loss: autograd accumulates into param.grad only after both ran) writes a
+        # fresh flat instead of overwriting the first one's views; the Trainer releases it after
+        # the all-reduce and at the start of every step (release_grad_buffer)
         self.grad_buffer = None
+        self.grad_buffer_taken = False
 
     # ------------------------------------------------------------------ packing
     def _alloc(self, device):
@@ -342,6 +348,11 @@ class FieldRunner:
         _hip.field_backward(args, self._side[0].cuda_stream)
         return ray
 
+    def release_grad_buffer(self):
+        """The persistent gradient buffer may be handed out again (Trainer: after the
+        all-reduce and when a step starts)."""
+        self.grad_buffer_taken = False
+
     def param_list(self) -> List[torch.nn.Parameter]:
         """The field's parameters in module order.  Cached: walking the module tree costs ~75 us
         of host time and runs twice per training step; the runner already binds the layers'
@@ -368,10 +379,11 @@ class FieldRunner:
         params = self.param_list()
         n_par = sum(p.numel() for p in params)
         buf = self.grad_buffer
-        if (buf is not None and buf.device == dev and buf.numel() >= n_par
+        if (buf is not None and not self.grad_buffer_taken and buf.device == dev and buf.numel() >= n_par
                 and all(p.grad is None for p in params)):
             # autograd hands these views on as param.grad (no other gradient to accumulate into)
             flat = buf[:n_par]
+            self.grad_buffer_taken = True
         else:
             flat = torch.empty(n_par, device=dev, dtype=torch.float32)
         grads, off = {}, 0
@@ -650,6 +662,8 @@ class FieldTrunkFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, runner: FieldRunner, p, *params):
+        # an unused output gets None, not a zero tensor: g_h8 None keeps the native backward
+        ctx.set_materialize_grads(False)
         n = p.shape[0]
         zeros = torch.zeros_like(p)
         raw4, _, _, _, st = runner.forward(p, zeros, zeros, None, 0.0, 0.0, 1, 0, keep=True, composite=False)

@@ -16,6 +16,23 @@ import torch.nn.functional as F
 from .field import FieldRunner, eval_points, trunk_points
 
 
+class _FirstOrderOnly(torch.autograd.Function):
+    """Marks the normals of OfficialStaticNerf.gradient: the HIP backward is first order, so
+    the normals carry no gradient of their own.  Anchored to a field parameter, a loss that
+    reaches them (a second derivative through the field, e.g. rgb + w * normal) fails loudly
+    in its backward instead of silently dropping the normal term."""
+
+    @staticmethod
+    def forward(ctx, g, anchor):
+        return g.clone()
+
+    @staticmethod
+    def backward(ctx, gg):
+        raise RuntimeError("nerf_hip: a loss reached OfficialStaticNerf.gradient()'s normals; second derivatives "
+                           "through the HIP field are not supported (the reference's create_graph=True path, "
+                           "official_nerf.py:46-58)")
+
+
 class OfficialStaticNerf(nn.Module):
     def __init__(self, cfg):
         super().__init__()
@@ -87,13 +104,17 @@ class OfficialStaticNerf(nn.Module):
         return rgb
 
     def gradient(self, p, it):
-        """official_nerf.py:46-58: -d(density_raw)/dp, through the HIP backward.  As in the
-        reference the result is built with create_graph=True; the HIP backward is first order
-        only, so backpropagating a loss through these normals (a second derivative) raises
-        instead of returning a silently wrong gradient."""
+        """official_nerf.py:46-58: -d(density_raw)/dp, through the HIP backward.  The reference
+        builds the result with create_graph=True; the HIP backward is first order, so the
+        values are the same but they carry no second-order graph: when the field's parameters
+        require grad the result is anchored to them by _FirstOrderOnly, and any loss that
+        reaches it raises in its backward (no reference loss does, losses.py:164-228)."""
         with torch.enable_grad():
             p = p.detach().requires_grad_(True)
             raw = eval_points(self, p.reshape(-1, 3), torch.zeros_like(p).reshape(-1, 3))
             y = raw[:, 0:1]
-            g = torch.autograd.grad(y, p, torch.ones_like(y), create_graph=True, retain_graph=True)[0]
+            g = torch.autograd.grad(y, p, torch.ones_like(y), retain_graph=False)[0]
+            anchor = self.fc_density.bias
+            if anchor.requires_grad:
+                g = _FirstOrderOnly.apply(g, anchor)
             return -g.unsqueeze(1)

@@ -185,7 +185,7 @@ class Renderer(nn.Module):
         -d sigma_raw/dp / (|.| + 1e-5) from the HIP field backward; returns |n - n_jitter| per
         surface point.  ``noise`` injects the U[0,1) jitter (N,3).  The reference builds the
         normals with create_graph=True; here they are first order (OfficialStaticNerf.gradient):
-        a loss backpropagated through the result raises."""
+        a loss backpropagated through the result raises in its backward (_FirstOrderOnly)."""
         surface = (cam + ray * d_src.unsqueeze(-1))[mask]
         n = surface.shape[0]
         if noise is None:

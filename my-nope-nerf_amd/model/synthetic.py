@@ -80,3 +80,32 @@ def vkitti_scene(dev, seed=0, H=VKITTI_H, W=VKITTI_W, focal=VKITTI_FOCAL):
         if k not in ("img.idx", "img.depth_mask"):
             data[k] = v.to(dev)
     return data, c2w
+
+
+def vkitti_pair_scene(dev, H=VKITTI_H, W=VKITTI_W, focal=VKITTI_FOCAL):
+    """Config 3's two-view V_KITTI-shaped scene: two textured images with depth priors
+    (U[1, 8], ~5 % holes) and camera 1 offset from camera 0, as two data dicts whose
+    reference keys (dataset.py:330-364: img.ref_imgs / ref_depths / ref_idxs / ref_pose_gt)
+    point at the other view.  Returns ([data view 0, data view 1], c2w [2, 4, 4])."""
+    g = torch.Generator().manual_seed(0)
+    yy, xx = torch.meshgrid(torch.linspace(0, 1, H), torch.linspace(0, 1, W), indexing="ij")
+    imgs, depths = [], []
+    for s in (0, 1):
+        img = torch.stack([0.5 + 0.4 * torch.sin(6 * xx + 2 * yy + 0.3 * s), 0.5 + 0.4 * torch.cos(5 * yy),
+                           0.3 + 0.3 * xx * yy], 0).unsqueeze(0)
+        imgs.append((img + 0.02 * torch.rand(img.shape, generator=g)).clamp(0, 1).to(dev))
+        d = 1.0 + 7.0 * torch.rand(1, H, W, generator=g)
+        d[torch.rand(1, H, W, generator=g) < 0.05] = 0.0
+        depths.append(d.to(dev))
+    c2w = torch.stack([rigid_c2w(0), rigid_c2w(0)])
+    c2w[1, :3, 3] += torch.tensor([0.1, 0.0, -0.2])
+    K = camera_K(H, W, focal, focal).to(dev)
+    datas = []
+    for cam in (0, 1):
+        ref = 1 - cam
+        datas.append({"img": imgs[cam], "img.depth": depths[cam], "img.depth_mask": (depths[cam] > 0).cpu(),
+                      "img.camera_mat": K, "img.scale_mat": torch.eye(4, device=dev).unsqueeze(0),
+                      "img.pose_gt": c2w[cam].unsqueeze(0).to(dev), "img.idx": torch.tensor([cam]),
+                      "img.ref_imgs": imgs[ref], "img.ref_depths": depths[ref], "img.ref_idxs": torch.tensor([ref]),
+                      "img.ref_pose_gt": c2w[ref].unsqueeze(0).to(dev)})
+    return datas, c2w

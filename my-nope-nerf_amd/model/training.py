@@ -15,6 +15,7 @@ runs and what it waits for:
 from __future__ import annotations
 
 import os
+import time
 
 import numpy as np
 import torch
@@ -73,6 +74,27 @@ class Trainer(object):
         self._n_inplace = 0
         self._flag_cache = {}
         self._submodules = {}      # module -> its submodule list, for the per-step train-mode check
+        self._comm_timer = None    # time_collectives: the all-reduces' (start, end) hipEvents / CPU seconds
+
+    def time_collectives(self, on=True):
+        """Time every gradient all-reduce from now on (hipEvents on the launch stream around
+        dist.all_reduce; perf_counter on CPU tensors) until switched off; collective_ms() sums
+        them.  The event time includes the wait for the slowest rank.  Off: no events."""
+        self._comm_timer = [] if on else None
+
+    def collective_ms(self):
+        """Milliseconds of the all-reduces timed since time_collectives(True) (synchronises on
+        the last event)."""
+        if not self._comm_timer:
+            return 0.0
+        total = 0.0
+        for rec in self._comm_timer:
+            if isinstance(rec, tuple):
+                rec[1].synchronize()
+                total += rec[0].elapsed_time(rec[1])
+            else:
+                total += 1e3 * rec
+        return total
 
     def enable_graph_rng(self):
         """Make a step replayable from a captured hipGraph with fresh randomness: the ray
@@ -98,6 +120,9 @@ class Trainer(object):
                 o.zero_grad()
         if self.world_size > 1 and self._flat is None:
             self._bucket_buffer(self.device)   # before the first backward: the field writes its gradients into it
+        runner = self._field_runner() if self._n_inplace else None
+        if runner is not None:
+            runner.release_grad_buffer()       # the step's first field backward may take the bucket
         loss_dict = self.compute_loss(data, it=it, epoch=epoch, scheduling_start=scheduling_start,
                                       out_render_path=render_path)
         loss_dict["loss"].backward()
@@ -182,9 +207,26 @@ class Trainer(object):
         if zero:
             torch._foreach_zero_(zero)
         flat[-n:].copy_(flags)
+        timer = self._comm_timer
+        if timer is not None:
+            if flat.is_cuda:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            else:
+                t0 = time.perf_counter()
         dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+        if timer is not None:
+            if flat.is_cuda:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                timer.append((e0, e1))
+            else:
+                timer.append(time.perf_counter() - t0)
         flat[:-n].mul_(1.0 / self.world_size)
         present = flat[-n:].tolist() if any(missing) else None
+        runner = self._field_runner() if self._n_inplace else None
+        if runner is not None:
+            runner.release_grad_buffer()
         for i, (p, v) in enumerate(zip(params, views)):
             if p.grad is None:
                 if present[i] > 0:

@@ -1,16 +1,8 @@
 """Benchmark of the full NoPe-NeRF training step (BASELINE.json configs[2], config 3 of
-SURVEY.md section 8(d)): joint pose + depth-distortion learning with the rgb, depth,
-point-cloud (chamfer) and reprojection (rgb_s) losses on a V_KITTI-shaped two-view scene
-(188x621, 1024 rays x 128 samples, D = 256, point clouds at 47x155 = 7285 points).
-Steps alternate the two cameras (both branches of training.py:329-358).  Inputs resident
-in HBM; synthetic data (no dataset offline).  Prints one JSON line.
+SURVEY.md section 8(d)) on its own: the same measurement bench.py reports as "full_cfg3"
+(bench.cfg3_line), with more steps.  Prints one JSON line.
 
     python scripts/bench_full.py [--steps K --warmup W] [--mode both|eager|graph]
-
-Times the step enqueued eagerly and as replays of one captured hipGraph per view (the ray
-sampler keys on a device step counter, the pose / distortion Adams are capturable fused
-ones, so each replay trains on fresh rays with correct bias corrections) and reports the
-faster as `value`, both under `runs` with their host enqueue times.
 """
 from __future__ import annotations
 
@@ -18,7 +10,6 @@ import argparse
 import json
 import os
 import sys
-import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "my-nope-nerf_amd"))
@@ -26,109 +17,9 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-H, W, FOCAL = 188, 621, 362.5
-RAYS, SAMPLES, HIDDEN = 1024, 128, 256
-
-
-def scene(dev):
-    from tests.helpers import camera_K, rigid_c2w
-    g = torch.Generator().manual_seed(0)
-    yy, xx = torch.meshgrid(torch.linspace(0, 1, H), torch.linspace(0, 1, W), indexing="ij")
-    imgs, depths = [], []
-    for s in (0, 1):
-        img = torch.stack([0.5 + 0.4 * torch.sin(6 * xx + 2 * yy + 0.3 * s), 0.5 + 0.4 * torch.cos(5 * yy),
-                           0.3 + 0.3 * xx * yy], 0).unsqueeze(0)
-        imgs.append((img + 0.02 * torch.rand(img.shape, generator=g)).clamp(0, 1).to(dev))
-        d = 1.0 + 7.0 * torch.rand(1, H, W, generator=g)
-        d[torch.rand(1, H, W, generator=g) < 0.05] = 0.0
-        depths.append(d.to(dev))
-    c2w = torch.stack([rigid_c2w(0), rigid_c2w(0)])
-    c2w[1, :3, 3] += torch.tensor([0.1, 0.0, -0.2])
-    K = camera_K(H, W, FOCAL, FOCAL).to(dev)
-    datas = []
-    for cam in (0, 1):
-        ref = 1 - cam
-        datas.append({"img": imgs[cam], "img.depth": depths[cam], "img.depth_mask": (depths[cam] > 0).cpu(),
-                      "img.camera_mat": K, "img.scale_mat": torch.eye(4, device=dev).unsqueeze(0),
-                      "img.pose_gt": c2w[cam].unsqueeze(0).to(dev), "img.idx": torch.tensor([cam]),
-                      "img.ref_imgs": imgs[ref], "img.ref_depths": depths[ref], "img.ref_idxs": torch.tensor([ref]),
-                      "img.ref_pose_gt": c2w[ref].unsqueeze(0).to(dev)})
-    return datas, c2w
-
-
-def setup(dev, capturable=False):
-    """Trainer with pose + distortion learning and the image-pair terms (config 3) on the
-    two-view synthetic scene -> (trainer, [data view 0, data view 1]).  capturable: the
-    pose / distortion Adams keep their step counts on the device (hipGraph capture)."""
-    import model as mdl
-    from model.optim import HipAdam
-    from tests.helpers import make_cfg
-    cfg = make_cfg(hidden=HIDDEN, S=SAMPLES)
-    t = cfg["training"]
-    t["n_training_points"] = RAYS
-    t["annealing_epochs"], t["scheduling_start"] = 2000, 0      # default.yaml:139: rgb l1 in the early epochs
-    datas, c2w = scene(dev)
-    torch.manual_seed(42)
-    net = mdl.OfficialStaticNerf(cfg)
-    renderer = mdl.Renderer(net, cfg["rendering"], device=dev)
-    nn_model = mdl.get_model(renderer, cfg, device=dev)
-    opt = HipAdam(nn_model.parameters(), lr=1e-3)
-    pose = mdl.LearnPose(2, True, True, cfg, init_c2w=c2w.clone()).to(dev)
-    distn = mdl.Learn_Distortion(2, True, True, cfg).to(dev)
-    # train.py:100, :118; one fused kernel per optimiser (torch's fused Adam: the same update as
-    # the default multi-tensor path, ~8 launches fewer per optimiser and step), capturable in graphs
-    opt_pose = torch.optim.Adam(pose.parameters(), lr=5e-4, capturable=capturable, fused=True)
-    opt_dist = torch.optim.Adam(distn.parameters(), lr=5e-4, capturable=capturable, fused=True)
-    tr = mdl.Trainer(nn_model, opt, t, device=dev, optimizer_pose=opt_pose, pose_param_net=pose,
-                     optimizer_distortion=opt_dist, distortion_net=distn)
-    return tr, datas
-
-
-def measure(dev, graph, steps, warmup):
-    """(seconds for `steps` timed steps, last loss dict, median host enqueue seconds per step)
-    of the cfg3 step, eager or replaying one captured hipGraph per view."""
-    tr, datas = setup(dev, capturable=graph)
-
-    def one(i):
-        return tr.train_step(datas[i % 2], it=i + 1, epoch=0, scheduling_start=0)
-
-    if graph:
-        # one graph per view replays the same launches without the host; the ray sampler keys
-        # on a device counter and the pose / distortion Adams are capturable, so every replay
-        # trains on new rays with correct bias corrections
-        tr.enable_graph_rng()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for i in range(warmup):
-                one(i)
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        graphs, outs = [], []
-        for v in range(2):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                outs.append(tr.train_step(datas[v], it=1, epoch=0, scheduling_start=0))
-            graphs.append(g)
-
-        def one(i):  # noqa: F811
-            graphs[i % 2].replay()
-            return outs[i % 2]
-
-    for i in range(warmup):
-        one(i)
-    torch.cuda.synchronize()
-    host = []
-    t0 = time.perf_counter()
-    for i in range(steps):
-        th = time.perf_counter()
-        ld = one(warmup + i)
-        host.append(time.perf_counter() - th)
-    torch.cuda.synchronize()
-    return time.perf_counter() - t0, ld, sorted(host)[len(host) // 2]
-
 
 def main():
+    import bench
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
@@ -136,31 +27,14 @@ def main():
     ap.add_argument("--mode", choices=["both", "eager", "graph"], default="both",
                     help="eager enqueue, hipGraph replay of the two views' captured train_steps, or both "
                          "(default; value = the faster, both reported)")
-    ap.add_argument("--eager", dest="mode", action="store_const", const="eager", help="same as --mode eager")
     args = ap.parse_args()
     from model import _hip
     dev = torch.device("cuda", 0)
     _hip.load_library()
-    _hip.gemm_set_precision({"f32": 0, "bf16x6": 1, "f16x3": 2}[args.gemm_precision])
-    runs = {}
-    for mode in (["eager", "graph"] if args.mode == "both" else [args.mode]):
-        el, ld, host = measure(dev, mode == "graph", args.steps, args.warmup)
-        runs[mode] = {"value": RAYS * args.steps / el, "ms_per_step": 1e3 * el / args.steps,
-                      # host time to enqueue one step (median): below ms_per_step = GPU-bound
-                      "host_ms_per_step_median": 1e3 * host,
-                      "losses": {k: float(ld[k].detach()) for k in ("loss", "loss_rgb", "loss_depth", "loss_pc",
-                                                                    "loss_rgb_s")}}
-    best = max(runs, key=lambda k: runs[k]["value"])
-    r = runs[best]
-    out = {"metric": "full NoPe-NeRF training rays/sec (config 3: pose + distortion + pc + rgb_s losses)",
-           "value": r["value"], "unit": "rays/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-           "ms_per_step": r["ms_per_step"], "dtype": "f32", "gemm_arithmetic": args.gemm_precision,
-           "data": "synthetic two-view V_KITTI-shaped scene",
-           "execution": {"eager": "eager enqueue", "graph": "hipGraph replay of the captured train_step per view "
-                         "(device ray-draw counter: new rays every replay)"}[best],
-           "config": {"workload": "config 3: 188x621, 1024 rays x 128 samples, D=256, pose+distortion learned, "
-                                  "pc chamfer 7285 points, rgb_s reprojection"},
-           "losses": r["losses"], "host_ms_per_step_median": r["host_ms_per_step_median"], "runs": runs}
+    _hip.gemm_set_precision(bench.PRECISION[args.gemm_precision])
+    modes = ["eager", "graph"] if args.mode == "both" else [args.mode]
+    out = bench.cfg3_line(dev, args.steps, args.warmup, modes)
+    out["gemm_arithmetic"] = args.gemm_precision
     print(json.dumps(out))
 
 

@@ -184,6 +184,12 @@ def test_bench_launcher_spawns_ranks():
     line = json.loads(out.stdout.strip().splitlines()[-1])
     assert line["plumbing"] and line["n_gpus"] == 2 and line["world_size"] == 2
     assert line["bucket_elems"] > 595_000            # NeRF (595 844) + pose + distortion parameters
+    # the N > 1 attribution fields bench.py prints under RCCL (rank_attribution), from the same code
+    assert line["allreduce_ms_per_step"] > 0 and line["multi_gpu"]["world_size"] == 2
+    mg = line["multi_gpu"]
+    assert len(mg["per_rank"]) == 2 and mg["allreduce_ms_per_step_min"] <= mg["allreduce_ms_per_step"]
+    assert mg["rays_per_s_per_rank_min"] <= mg["rays_per_s_per_rank_max"]
+    assert mg["compute_ms_per_step_min"] <= mg["compute_ms_per_step_max"]
     bad = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--plumbing", "--gpus", "3"],
                          capture_output=True, text=True, timeout=120, env=dict(env, WORLD_SIZE="2"), cwd=root)
     assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr

@@ -71,9 +71,11 @@ def test_normal_loss_branch_matches_oracle_and_refuses_second_order(dev):
     want = orc.normal_diff(ref, cam, ray, d_src, mask, jitter)
     assert out["normal"].shape == want.shape
     assert (out["normal"].detach().cpu() - want).abs().max().item() < 2e-3
+    assert out["normal"].requires_grad          # anchored: a loss on it reaches _FirstOrderOnly
     (out["rgb"].square().sum()).backward(retain_graph=True)       # the first-order path still trains
-    with pytest.raises(RuntimeError):
-        out["normal"].sum().backward()
+    # a combined loss (rgb + w * normal) must fail loudly, not drop the normal term
+    with pytest.raises(RuntimeError, match="second derivatives"):
+        (out["rgb"].square().sum() + 0.1 * out["normal"].sum()).backward()
     # eval renders carry no normal term (rendering.py:127: `not eval_`)
     with torch.no_grad():
         ev = rnd.nope_nerf(b["pixels"].to(dev), b["depth"].to(dev), b["K"].to(dev), b["w2c"].to(dev),
