@@ -121,14 +121,17 @@ KIND_NAMES = {
     "dw": "weight-gradient TN of the 256-output layers (nerf_linear_bwd_weight[_seg]: l1-l3, l5-l7, lf, and l4 "
           "over [h3 | enc_p] in one launch; algorithmic bytes exclude the split-K slabs)",
     "dw_narrow": "narrow weight-gradient TN (l0 over enc_p; the colour layer over [f | enc_d] in one launch)",
+    "chain_fwd": "training forward chain (nerf_mlp_chain_train: ten linears + heads, every output saved, one launch)",
+    "chain_bwd": "input-gradient chain (nerf_mlp_chain_bwd: dyr + nine input gradients, every dy saved, one launch)",
 }
 KERNEL = {
     "f16x3": {"fwd": "k_gemm_nt_x6<128,256,2,2,0,true,true,2> (fp16 pair, 3 products)",
               "dx": "k_gemm_nt_x6<128,256,2,2,1,true,true,2> (fp16 pair, 3 products)",
-              "dw": "k_gemm_tn_x6<256,128,4,2,true,1,2> + k_gemm_tn_x6_seg<256,128,4,2,64,4,2,2,1> (XCD-grouped "
-                    "column tiles, 8 waves; fp16 pair, 3 products)",
-              "dw_narrow": "k_gemm_tn_x6<256,64,4,2,true> + k_gemm_tn_x6_seg<128,256,2,4,64,4,2,1,1> (fp16 pair, "
-                           "3 products)"},
+              "dw": "k_wgrad_pair + k_wgrad_seg<256,128,2,64> (XCD-paired 256x128 column tiles, 4 waves; fp16 "
+                    "pair, 3 products)",
+              "dw_narrow": "k_wgrad_one<256,64> + k_wgrad_seg<128,256,1,64> (4 waves; fp16 pair, 3 products)",
+              "chain_fwd": "k_mlp_chain_train2 (8 waves x 16 rows, 16x16x32 f16 MFMA; fp16 pair, 3 products)",
+              "chain_bwd": "k_mlp_chain_bwd (8 waves x 16 rows, 16x16x32 f16 MFMA; fp16 pair, 3 products)"},
     "bf16x6": {"fwd": "k_gemm_nt_x6<256,256,2,2,0,true> (bf16x3 split, 6 products)",
                "dx": "k_gemm_nt_x6<256,256,2,2,1,true> (bf16x3 split, 6 products)",
                "dw": "k_gemm_tn_x6<256,128,4,2,false,1,2> (XCD-paired column tiles; bf16x3 split, 6 products)",

@@ -39,8 +39,9 @@ extern "C" {
  * backwards (nerf_pose_c2w_bwd, nerf_mat4_inv_bwd, nerf_mat4_mul(_bwd), nerf_unproject_matrix_bwd)
  * and the depth-prior distortion (nerf_depth_affine(_bwd)), 7 nerf_linear_fwd_heads, 8 nerf_heads_bwd_mode,
  * 9 precision mode 2 as the default, 10 nerf_mlp_chain_train, 11 nerf_linear_bwd_weight_seg and
- * nerf_field_backward. */
-#define NERF_HIP_ABI_VERSION 11
+ * nerf_field_backward, 12 nerf_mlp_chain_bwd, nerf_field_bwd.bwd_chain, TN policy 8 and the
+ * Adam hyper slot 6 (1 - beta2). */
+#define NERF_HIP_ABI_VERSION 12
 int nerf_hip_abi_version(void);
 const char* nerf_hip_last_error(void);
 
@@ -158,6 +159,7 @@ int nerf_linear_bwd_weight_seg(const float* dy, int lddy, int nout, const float*
 #define NERF_BWD_LAYERS 10
 typedef struct nerf_field_bwd {
     int n_pad, n_rays, n_samples, flags, ray_grad, tail_main;
+    int bwd_chain;   /* 1: the input gradients by nerf_mlp_chain_bwd (ABI 12), 0: the per-layer schedule */
     /* forward state (nerf_mlp_chain_train / nerf_encode_samples outputs) */
     const float* z;
     const float* raw4;
@@ -208,10 +210,11 @@ int nerf_slab_reduce(const float* slab, int splits, int nout, int ldslab, int no
 /* GEMM tile policy (tuning knob; 0 = built-in default).  nt: 1 = 128x128 / 4 waves,
  * 2 = 128x256 / 8 waves, 3 = 256x256 / 8 waves (exact-f32 kernels; the fp16 pair kernels
  * run 128x256 tiles at 3, and the fused-heads launches always one column block);
- * tn (weight gradient): 3 = 256x256 tiles, 7 (default) = in the split modes a 256 x 256
- * layer as XCD-paired 256x128 column tiles of 8 waves, the 64-wide inputs' 256x64 tile
- * and the colour layer's 128x256 tile at 8 waves.  The policy changes
- * nerf_linear_bwd_weight_splits. */
+ * tn (weight gradient): 3 = 256x256 tiles, 7 = in the split modes a 256 x 256 layer as
+ * XCD-paired 256x128 column tiles of 8 waves, the 64-wide inputs' 256x64 tile and the
+ * colour layer's 128x256 tile at 8 waves; 8 (default) = the splits and tiles of 7 with the
+ * 4-wave kernels of wgrad.hip in precision mode 2 (bit-identical slabs; shapes they do not
+ * cover run as 7).  The policy changes nerf_linear_bwd_weight_splits (7 and 8 alike). */
 int nerf_gemm_set_policy(int nt_policy, int tn_policy);
 
 /* f32 arithmetic of the GEMM family (process-wide; default 2 since ABI 9):
@@ -289,6 +292,38 @@ int nerf_render_eval_fused(const float* pts_o, const float* pts_d, const float* 
                            float near_z, float far_z, int flags, const nerf_chain_layer* layers, const float* wd,
                            const float* bd, const float* wc, const float* bc, float* rgb, float* dist, float* alpha,
                            float* z, void* stream);
+
+/* The input-gradient chain (ABI 12; official_nerf.py:60-96 backward as training.py:92 runs
+ * it, for hidden 256 / colour 128 in GEMM precision mode 2): ONE launch computes, per
+ * 128-row block, dyr (the colour layer's output gradient: graw4's rgb-logit gradients . fc_rgb,
+ * gated by the colour layer's ReLU words -- replaces nerf_heads_bwd_mode 1) and the nine input
+ * gradients dx = dy W [+ d sigma_raw x w_density at the feature layer], masked by the ReLU
+ * words of each layer's input, with dy resident in registers as row-scaled fp16 pairs and
+ * W^T streamed by LDS-DMA -- the nine nerf_linear_bwd_data launches of the per-layer path.
+ * Layer order i = 0..8: colour layer, feature layer, l7 .. l1.  D_0 = dyr [n_pad][128],
+ * D_i (i >= 1) the gradient at the output of forward layer 9 - i ([n_pad][256]; D_9 is the
+ * gradient at l0's output).  Every D_i is saved (f32 rebuilt from the fp16 pair consumed,
+ * within 2^-22 relative of the f32 value), with its per-128-row-group column maxima
+ * ([n_pad/128][128 or 256]) and row maxima ([n_pad]) -- the weight-gradient and ray-gradient
+ * GEMMs' operands. */
+typedef struct nerf_chain_bwd {
+    const float* graw4;             /* [n_pad][4]: d(sigma_raw, rgb logits), 16-byte aligned */
+    const uint32_t* hr_mask;        /* the colour layer's ReLU words [n_pad][ld_hr_mask >= 4] */
+    int ld_hr_mask;
+    const float* wd;                /* fc_density weight [256], 16-byte aligned */
+    const float* wc;                /* fc_rgb weight [3][128] (padded) */
+    const uint16_t* wt_img[9];      /* fp16 pair images of W^T (rows = input features), layer order */
+    int wt_img_rows[9];
+    const uint32_t* in_mask[9];     /* ReLU words of layer i's input [n_pad][ld >= 8] (i = 0 unused) */
+    int ld_in_mask[9];
+    float* dy[10];                  /* D_0 .. D_9 */
+    int lddy[10];
+    float* dy_cmax[10];
+    float* dy_rmax[10];
+    float* scratch;                 /* >= 512 floats of device scratch */
+    int n_pad;
+} nerf_chain_bwd;
+int nerf_mlp_chain_bwd(const nerf_chain_bwd* a, void* stream);
 
 /* Diagnostics only: per-block phase cycles of nerf_mlp_chain_fwd into buf[(n_pad/128)*6]
  * uint64 (DMA wait, barrier, MFMA section, epilogue, total, end time); NULL switches off. */
@@ -374,7 +409,9 @@ int nerf_pack_weights(const nerf_pack_desc* descs, int n, void* stream);
 /* ---------------------------------------------------------------------------
  * Adam (torch.optim.Adam semantics, amsgrad False) over one flat fp32 buffer.
  * Replaces optimizer.step() (training.py:93-99).  hyper (device, 8 floats) =
- * {step, lr, beta1, beta2, eps, weight_decay, 0, ticket}; the update uses step + 1 and
+ * {step, lr, beta1, beta2, eps, weight_decay, 1 - beta2, ticket} (1 - beta2 rounded once
+ * from the caller's double, as torch passes it; 0 = derive it from the f32 beta2); the
+ * bias corrections are taken in double; the update uses step + 1 and
  * the last workgroup to finish stores it back (one launch; a captured graph replays the
  * correct bias corrections).  hyper[7] is a completion counter: zero it once. */
 int nerf_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
@@ -527,7 +564,9 @@ int nerf_prof_read(double* gemm_ms, int64_t* gemm_launches, double* gemm_flops, 
 #define NERF_PROF_DX 1
 #define NERF_PROF_DW 2
 #define NERF_PROF_DW_NARROW 3
-#define NERF_PROF_KINDS 4
+#define NERF_PROF_CHAIN_FWD 4   /* nerf_mlp_chain_train: the ten forward linears + heads in one launch */
+#define NERF_PROF_CHAIN_BWD 5   /* nerf_mlp_chain_bwd: dyr + the nine input gradients in one launch */
+#define NERF_PROF_KINDS 6
 typedef struct nerf_prof_kind {
     double ms;
     int64_t launches;

@@ -1406,6 +1406,361 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_train2(ChainFwdArgs p) {
             __uint_as_float(reinterpret_cast<const uint32_t*>(smem + Y::O_CMX)[(8 & 1) * 256 + tid - CROWS]);
 }
 
+// ---------------------------------------------------------------------------
+// The input-gradient chain (nerf_mlp_chain_bwd): the backward mirror of k_mlp_chain_train2.
+// The autograd of official_nerf.py:60-96 under training.py:92 walks the layers from the
+// colour layer down; each layer's input gradient dx = dy W (+ the density head's rank-one
+// term d sigma_raw x w_density at the feature layer, official_nerf.py:66), masked by the
+// ReLU bits of the layer's input, is the next layer's dy.  A block keeps its 128 rows' dy
+// resident in registers as row-scaled fp16 pairs through all nine input gradients -- the
+// layer loop of k_mlp_chain_train2 with the weight-transpose images (rows = input features)
+// streaming through the LDS ring -- and saves every dy beside the next layer's MFMAs for the
+// weight gradients: f32 (rebuilt from the pair it consumed), per-128-row-group column maxima
+// and row maxima.  Against nine input-gradient launches this removes the read of every dy
+// (134 MB per 256-wide layer at 1024 x 128 samples), the in-kernel split of every A operand,
+// eight launch gaps and k_heads_dyr: the first dy (the colour layer's, dyr) is computed in
+// the prologue from graw4, fc_rgb and the colour layer's ReLU words (k_heads_dyr's
+// arithmetic, render.hip).
+// Layer order i = 0..8: the colour layer (K = 128), lf, l7, ..., l1.  D_i is layer i's A
+// operand: D_0 = dyr, D_{i+1} = layer i's output; D_9 (the gradient at l0's output) is
+// stored by the last epilogue.
+// ---------------------------------------------------------------------------
+struct ChainBwdArgs {
+    nerf_chain_bwd a;
+};
+
+namespace b2 {
+using f2::NTH;
+using f2::SBYTES;
+using f2::SHALF;
+using f2::SPLANE;
+constexpr int NL = 9;
+constexpr int KS_[NL] = {8, 16, 16, 16, 16, 16, 16, 16, 16};   // 16-k steps: the layer's output width / 16
+constexpr int kb(int i) { return i == 0 ? 0 : kb(i - 1) + KS_[i - 1]; }
+constexpr int CTB = kb(NL);
+constexpr int layer_of(int tt) { int i = 0; while (i + 1 < NL && kb(i + 1) <= tt) ++i; return i; }
+constexpr bool first_step(int tt) { return tt < CTB && kb(layer_of(tt)) == tt; }
+// LDS-DMA instructions per wave at 16-k step tt: 2 ring pieces, +1 at a layer's first step
+// (waves 0-3 the weight-row exponents, waves 4-7 the block's ReLU words of the layer input)
+constexpr int dma_count(int tt) { return tt >= CTB ? 0 : 2 + (first_step(tt) ? 1 : 0); }
+constexpr int NSLOT = 8, D = NSLOT / 2 - 1;   // ring slots, 32-k steps in flight
+constexpr int nks(int i) { return KS_[i] / 2; }
+constexpr int kfirst(int i) { return i == 0 ? 0 : kfirst(i - 1) + nks(i - 1); }
+constexpr int layer_of_k(int k) { int i = 0; while (i + 1 < NL && kfirst(i + 1) <= k) ++i; return i; }
+constexpr int tt_of_k(int k) { return kb(layer_of_k(k)) + 2 * (k - kfirst(layer_of_k(k))); }
+constexpr int dma_ops_k(int k) { return dma_count(tt_of_k(k) + 2 * D) + dma_count(tt_of_k(k) + 2 * D + 1); }
+// stores of 32-k step k, all issued after its DMAs: the two dy pieces, at a layer's first
+// step the previous dy's column maxima, at a layer's last step the epilogue's row-max store
+constexpr int st_ops_k(int k) {
+    const int i = layer_of_k(k), u = k - kfirst(i);
+    return 2 + (u == 0 && i >= 1 ? 1 : 0) + (u == nks(i) - 1 && i < NL - 1 ? 1 : 0);
+}
+// the counted wait of 32-k step k: for the DMAs issued D steps earlier (vmcnt counts loads,
+// stores and LDS-DMA together in issue order; ops left out only make a wait stricter)
+constexpr int wait_n(int k) {
+    int n = k >= D ? st_ops_k(k - D) : 0;
+    for (int i = (k - D + 1 > 0 ? k - D + 1 : 0); i < k; ++i) n += dma_ops_k(i) + st_ops_k(i);
+    if (k < D)
+        for (int t = 2 * k + 2; t < 2 * D; ++t) n += dma_count(t);
+    return n;
+}
+static_assert(wait_n(0) == dma_count(2) + dma_count(3) + dma_count(4) + dma_count(5), "prologue waits");
+
+constexpr int O_RING = 0;
+constexpr int O_LEB = NSLOT * SBYTES;            // [2][256 rows][16 B] weight-row exponent chunks
+constexpr int O_EXP = O_LEB + 2 * 256 * 16;      // [2][256] float 2^-e of the weight rows
+constexpr int O_MASK = O_EXP + 2 * 256 * 4;      // [2][128 rows][8 words] ReLU words of the layer input
+constexpr int O_CMX = O_MASK + 2 * 128 * 32;     // [2][256] uint column maxima (LDS atomics)
+constexpr int O_FX = O_CMX + 2 * 256 * 4;        // fc_density [256], fc_rgb [3][128]
+constexpr int BYTES = O_FX + (256 + 384) * 4;
+static_assert(BYTES <= 160 * 1024, "LDS");
+
+struct State : f2::State {
+    float gr0;   // d sigma_raw of the lane's row (the feature layer's rank-one term)
+};
+
+template <int TT>
+__device__ __forceinline__ void dma(const nerf_chain_bwd& p, State& st) {
+    if constexpr (TT < CTB) {
+        constexpr int i = layer_of(TT);
+        constexpr int s = TT - kb(i);
+        constexpr int ks = KS_[i];
+        const uint16_t* img = p.wt_img[i];
+        const int rows = p.wt_img_rows[i];
+        char* slot = st.lds + O_RING + (TT % NSLOT) * SBYTES;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int c = st.tid + NTH * q;             // 16-byte chunk of the step's 256 image rows
+            const int ph = c >> 8, n = c & 255;         // plane * 2 + k-half (wave-uniform), image row
+            const uint32_t off = (uint32_t)((((ph >> 1) * (2 * ks) + 2 * s + (ph & 1)) * rows + n) * 16);
+            cdma16(img, off, slot + ph * SHALF + (n - st.lane) * 16);
+        }
+        if constexpr (s == 0) {
+            if (st.wave < 4 || i == 0) {
+                // the weight-row exponents (plane 2, chunk 0 of each image row); the colour
+                // layer (its input f has no ReLU) repeats them on waves 4-7: same bytes, same place
+                const int w = st.wave & 3;
+                cdma16(img, (uint32_t)((2 * (2 * ks) * rows + 64 * w + st.lane) * 16),
+                       st.lds + O_LEB + (i & 1) * 4096 + 64 * w * 16);
+            } else {
+                // the block's ReLU words of the layer input: wave 4 + w rows 32 w .. 32 w + 31
+                const int w = st.wave - 4;
+                const int r = 32 * w + (st.lane >> 1);
+                cdma16(p.in_mask[i] + st.m0 * p.ld_in_mask[i], (uint32_t)((r * p.ld_in_mask[i] + 4 * (st.lane & 1)) * 4),
+                       st.lds + O_MASK + (i & 1) * 4096 + 32 * w * 32);
+            }
+        }
+    }
+}
+template <int T0, int N>
+__device__ __forceinline__ void dma_n(const nerf_chain_bwd& p, State& st) {
+    if constexpr (N > 0) {
+        dma<T0>(p, st);
+        dma_n<T0 + 1, N - 1>(p, st);
+    }
+}
+
+// D_i's features 32 u + 8 g + k0 .. + 3 of the lane's row, rebuilt from the pair this k-step
+// consumes: stored, and their column maxima over the wave's 16 rows (DPP quad max, then LDS
+// atomics from the quads' first lanes) into the parity-(i & 1) array
+template <int i, int u, int j>
+__device__ __forceinline__ void save_piece(const nerf_chain_bwd& p, State& st, const uint4& ah, const uint4& al) {
+    if constexpr (j == 1 || j == 2) {
+        constexpr int k0 = 4 * (j - 1);
+        int rl = st.rl;
+        asm volatile("" : "+v"(rl));
+        const size_t row = st.m0 + rl;
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = f2::rebuilt(ah, al, k0 + k, st.er);
+        *reinterpret_cast<float4*>(p.dy[i] + row * p.lddy[i] + 32 * u + 8 * st.g + k0) = make_float4(v[0], v[1], v[2], v[3]);
+        uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + O_CMX) + (i & 1) * 256 + 32 * u + 8 * st.g + k0;
+        float c[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            c[k] = fabsf(v[k]);
+            c[k] = fmaxf(c[k], dpp_f<0xB1>(0.f, c[k]));
+            c[k] = fmaxf(c[k], dpp_f<0x4E>(0.f, c[k]));
+        }
+        if ((st.n & 3) == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) atomicMax(cm + k, __float_as_uint(c[k]));
+        }
+    }
+}
+
+template <int i, int u, int j>
+__device__ __forceinline__ void tiles(const nerf_chain_bwd& p, State& st, const uint4& ah, const uint4& al,
+                                      const char* base, uint4 (&wh)[2], uint4 (&wl)[2], f2::SplitTmp& q) {
+    if constexpr (j < 16) {
+        if constexpr (j + 1 < 16) {
+            wh[(j + 1) & 1] = *reinterpret_cast<const uint4*>(base + 256 * (j + 1));
+            wl[(j + 1) & 1] = *reinterpret_cast<const uint4*>(base + 256 * (j + 1) + SPLANE);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        st.acc[j] = f2::mfma16(wh[j & 1], al, st.acc[j]);   // hi . lo
+        st.acc[j] = f2::mfma16(wl[j & 1], ah, st.acc[j]);   // lo . hi
+        st.acc[j] = f2::mfma16(wh[j & 1], ah, st.acc[j]);   // hi . hi
+        save_piece<i, u, j>(p, st, ah, al);
+        // the next k-step's A fragment from the previous epilogue's f32 tiles (layer 0's are
+        // all split in the prologue)
+        if constexpr (i >= 1 && u + 1 < nks(i)) {
+            if constexpr (j == f2::split_tile<16, false>(0)) f2::split_a<u + 1>(st, q);
+            if constexpr (j == f2::split_tile<16, false>(1)) f2::split_b<u + 1>(st, q);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        tiles<i, u, j + 1>(p, st, ah, al, base, wh, wl, q);
+    }
+}
+
+template <int i, int u>
+__device__ __forceinline__ void kstep(const nerf_chain_bwd& p, State& st) {
+    constexpr int TT = kb(i) + 2 * u;
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_n(kfirst(i) + u)) : "memory");
+    __syncthreads();
+    dma<TT + 2 * D>(p, st);
+    dma<TT + 2 * D + 1>(p, st);
+    if constexpr (u == 0) {
+        // this layer's weight-row exponents (landed with step TT) as the scales 2^-e, read by
+        // its epilogue behind later barriers
+        if (st.tid < 256)
+            reinterpret_cast<float*>(st.lds + O_EXP)[(i & 1) * 256 + st.tid] = __builtin_amdgcn_ldexpf(
+                1.f, -*reinterpret_cast<const int*>(st.lds + O_LEB + (i & 1) * 4096 + st.tid * 16));
+        if constexpr (i >= 1) {
+            // D_{i-1}'s column maxima (complete since layer i-1's last step) out and cleared;
+            // D_0 is 128 wide: waves 4-7 store theirs to the scratch row (one store op per wave)
+            constexpr int W = i - 1 == 0 ? 128 : 256;
+            if (st.lane < 32) {
+                uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + O_CMX) + ((i - 1) & 1) * 256 + 32 * st.wave + st.lane;
+                float* dst = 32 * st.wave < W ? p.dy_cmax[i - 1] + (st.m0 / CROWS) * W + 32 * st.wave + st.lane
+                                              : p.scratch + 64 * st.wave + st.lane;
+                *dst = __uint_as_float(*cm);
+                *cm = 0u;
+            }
+        }
+    }
+    const uint4& ah = st.act_hi[u];
+    const uint4& al = st.act_lo[u];
+    // lane (g, n) reads k-chunk g: slot of step TT + (g >> 1), k-half g & 1, image row 16 j + n
+    const char* s0 = st.lds + O_RING + (TT % NSLOT) * SBYTES;
+    const char* s1 = st.lds + O_RING + ((TT + 1) % NSLOT) * SBYTES;
+    const char* base = ((st.g >> 1) ? s1 : s0) + (st.g & 1) * SHALF + st.n * 16;
+    uint4 wh[2], wl[2];
+    wh[0] = *reinterpret_cast<const uint4*>(base);
+    wl[0] = *reinterpret_cast<const uint4*>(base + SPLANE);
+    f2::SplitTmp q;
+    tiles<i, u, 0>(p, st, ah, al, base, wh, wl, q);
+}
+
+template <int i, int u>
+__device__ __forceinline__ void ksteps(const nerf_chain_bwd& p, State& st) {
+    if constexpr (u < nks(i)) {
+        kstep<i, u>(p, st);
+        ksteps<i, u + 1>(p, st);
+    }
+}
+
+// layer i: k-loop, then the epilogue -- unscale, the feature layer's rank-one term, the
+// input's ReLU mask -> D_{i+1} (features 16 j + 4 g + c of the lane's row), its row max and
+// the next A operand (k-step 0 now, the rest during the next layer's k-steps); the last
+// layer stores D_9 and its column maxima here
+template <int i>
+__device__ __forceinline__ void layer(const nerf_chain_bwd& p, State& st) {
+    constexpr bool last = i == NL - 1;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) st.acc[j] = f2::f32x4{0.f, 0.f, 0.f, 0.f};
+    ksteps<i, 0>(p, st);
+    int g4 = 4 * st.g;
+    asm volatile("" : "+v"(g4));
+    const float* le = reinterpret_cast<const float*>(st.lds + O_EXP) + (i & 1) * 256 + g4;
+    const float sr = __builtin_amdgcn_ldexpf(1.f, -st.er);
+    const f2::pf2 sr2 = {sr, sr};
+    uint32_t mw[8];
+    if constexpr (i >= 1) {
+        const uint4* mrow = reinterpret_cast<const uint4*>(st.lds + O_MASK + (i & 1) * 4096 + st.rl * 32);
+        const uint4 a = mrow[0], b = mrow[1];
+        mw[0] = a.x; mw[1] = a.y; mw[2] = a.z; mw[3] = a.w;
+        mw[4] = b.x; mw[5] = b.y; mw[6] = b.z; mw[7] = b.w;
+    }
+    float rmx = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int f0 = 16 * j + g4;
+        const float4 s4 = *reinterpret_cast<const float4*>(le + 16 * j);
+        const f2::pf2 x01 = (f2::pf2{st.acc[j][0], st.acc[j][1]} * sr2) * f2::pf2{s4.x, s4.y};
+        const f2::pf2 x23 = (f2::pf2{st.acc[j][2], st.acc[j][3]} * sr2) * f2::pf2{s4.z, s4.w};
+        f2::f32x4 x;
+        x[0] = x01[0]; x[1] = x01[1]; x[2] = x23[0]; x[3] = x23[1];
+        if constexpr (i == 1) {   // + d sigma_raw x w_density (the density head reads h7)
+            const float4 w4 = *reinterpret_cast<const float4*>(st.fx + f0);
+            x[0] += st.gr0 * w4.x; x[1] += st.gr0 * w4.y; x[2] += st.gr0 * w4.z; x[3] += st.gr0 * w4.w;
+        }
+        if constexpr (i >= 1) {
+            const uint32_t bits = mw[j >> 1] >> ((j & 1) * 16 + g4);
+            x[0] = (bits & 1u) ? x[0] : 0.f;
+            x[1] = (bits & 2u) ? x[1] : 0.f;
+            x[2] = (bits & 4u) ? x[2] : 0.f;
+            x[3] = (bits & 8u) ? x[3] : 0.f;
+        }
+        st.xs[j] = x;
+        rmx = fmaxf(rmx, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+        if constexpr (last) {
+            *reinterpret_cast<float4*>(p.dy[NL] + (st.m0 + st.rl) * p.lddy[NL] + f0) = make_float4(x[0], x[1], x[2], x[3]);
+            uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + O_CMX) + (NL & 1) * 256 + f0;
+            float c[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                c[k] = fabsf(x[k]);
+                c[k] = fmaxf(c[k], dpp_f<0xB1>(0.f, c[k]));
+                c[k] = fmaxf(c[k], dpp_f<0x4E>(0.f, c[k]));
+            }
+            if ((st.n & 3) == 0) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) atomicMax(cm + k, __float_as_uint(c[k]));
+            }
+        }
+    }
+    // the row's max over its four 16-lane rows (lanes n, n + 16, n + 32, n + 48)
+    float m = fmaxf(rmx, __shfl_xor(rmx, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    if (st.g == 0) p.dy_rmax[i + 1][st.m0 + st.rl] = m;
+    if constexpr (!last) {
+        st.er = row_exp(m);
+        f2::SplitTmp q;
+        f2::split_a<0>(st, q);
+        f2::split_b<0>(st, q);
+    }
+}
+
+}  // namespace b2
+
+__global__ __launch_bounds__(512, 2) void k_mlp_chain_bwd(ChainBwdArgs args) {
+    using namespace b2;
+    const nerf_chain_bwd& p = args.a;
+    __shared__ __attribute__((aligned(16))) char smem[BYTES];
+    State st;
+    st.lds = smem;
+    st.fx = reinterpret_cast<float*>(smem + O_FX);
+    st.tid = threadIdx.x;
+    st.wave = __builtin_amdgcn_readfirstlane(st.tid >> 6);
+    st.lane = st.tid & 63; st.n = st.lane & 15; st.g = st.lane >> 4;
+    st.m0 = (size_t)blockIdx.x * CROWS;
+    st.rl = 16 * st.wave + st.n;
+    // head weights into LDS, both column-max parities cleared
+    if (st.tid < 256) st.fx[st.tid] = p.wd[st.tid];
+    for (int e = st.tid; e < 384; e += NTH) st.fx[256 + e] = p.wc[e];
+    reinterpret_cast<uint32_t*>(smem + O_CMX)[st.tid] = 0u;
+    const size_t row = st.m0 + st.rl;
+    const float4 gr = *reinterpret_cast<const float4*>(p.graw4 + row * 4);
+    const uint4 mr = *reinterpret_cast<const uint4*>(p.hr_mask + row * p.ld_hr_mask);
+    st.gr0 = gr.x;
+    __syncthreads();
+    // D_0 = dyr: (d rgb logits) . fc_rgb, gated by the colour layer's ReLU bits (render.hip
+    // k_heads_dyr), the lane's features 32 t + 8 g + e -- already the fragment layout
+    float d[4][8];
+    float m = 0.f;
+    const uint32_t mwr[4] = {mr.x, mr.y, mr.z, mr.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int f = 32 * t + 8 * st.g + e;
+            float v = fmaf(gr.w, st.fx[256 + 256 + f], fmaf(gr.z, st.fx[256 + 128 + f], gr.y * st.fx[256 + f]));
+            v = ((mwr[t] >> (8 * st.g + e)) & 1u) ? v : 0.f;
+            d[t][e] = v;
+            m = fmaxf(m, fabsf(v));
+        }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    if (st.g == 0) p.dy_rmax[0][row] = m;
+    st.er = row_exp(m);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        frag_from8(make_float4(d[t][0], d[t][1], d[t][2], d[t][3]), make_float4(d[t][4], d[t][5], d[t][6], d[t][7]),
+                   st.er, st.act_hi[t], st.act_lo[t]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    dma_n<0, 2 * D>(p, st);
+    layer<0>(p, st);
+    layer<1>(p, st);
+    layer<2>(p, st);
+    layer<3>(p, st);
+    layer<4>(p, st);
+    layer<5>(p, st);
+    layer<6>(p, st);
+    layer<7>(p, st);
+    layer<8>(p, st);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // D_8's (parity 0, saved by layer 8's k-steps) and D_9's (parity 1, the last epilogue)
+    // column maxima
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const size_t grp = (size_t)blockIdx.x;
+    const int par = tid >> 8, f = tid & 255;
+    p.dy_cmax[NL - 1 + par][grp * 256 + f] = __uint_as_float(reinterpret_cast<const uint32_t*>(smem + O_CMX)[tid]);
+}
+
 }  // namespace nerf
 
 using namespace nerf;
@@ -1471,7 +1826,13 @@ extern "C" int nerf_mlp_chain_train(const float* enc_p, const float* enc_d, cons
     }
     a.wd = wd; a.bd = bd; a.wc = wc; a.bc = bc; a.raw4 = raw4;
     a.stamps = g_chain_stamps;
+    // algorithmic work per row: the ten linears (padded K: 64, 256 x 3, 320, 256 x 4, colour 320)
+    // + both heads; HBM: the two encodings read, every output (f32), ReLU word and raw4 written
+    const double rows = (double)n_pad;
+    prof_next(NERF_PROF_CHAIN_FWD, rows * (2 * 64 * 4 + 9 * 256 * 4 + 128 * 4 + 9 * 32 + 4 * 4));
+    prof_begin(as_stream(stream));
     hipLaunchKernelGGL(k_mlp_chain_train2, dim3(n_pad / CROWS), dim3(f2::NTH), 0, as_stream(stream), a);
+    prof_end(as_stream(stream), 2.0 * rows * (256.0 * 64 + 7 * 256 * 256 + 256 * 320 + 128 * 320 + 4 * 256), 3);
     return check_launch(__func__);
 }
 
@@ -1521,4 +1882,39 @@ extern "C" int nerf_render_eval_fused(const float* pts_o, const float* pts_d, co
 extern "C" int nerf_chain_debug_stamps(void* buf) {
     g_chain_stamps = reinterpret_cast<unsigned long long*>(buf);
     return NERF_OK;
+}
+
+extern "C" int nerf_mlp_chain_bwd(const nerf_chain_bwd* a, void* stream) {
+    NERF_CHECK_PTR(a);
+    const nerf_chain_bwd& p = *a;
+    NERF_CHECK(p.n_pad > 0 && p.n_pad % CROWS == 0, "%s: n_pad=%d must be a positive multiple of %d", __func__,
+               p.n_pad, CROWS);
+    NERF_CHECK(gemm_precision() == 2, "%s: the chain runs in GEMM precision mode 2 (fp16 pair images)", __func__);
+    NERF_CHECK(p.graw4 && p.hr_mask && p.ld_hr_mask >= 4 && p.wd && p.wc && p.scratch,
+               "%s: graw4, the colour layer's ReLU words (ld >= 4), wd, wc and a scratch row are required", __func__);
+    NERF_CHECK_ALIGN16(p.graw4); NERF_CHECK_ALIGN16(p.wd);
+    NERF_CHECK((((uintptr_t)p.hr_mask) & 15u) == 0 && p.ld_hr_mask % 4 == 0, "%s: hr_mask 16-byte rows", __func__);
+    for (int i = 0; i < 9; ++i) {
+        NERF_CHECK(p.wt_img[i] && (((uintptr_t)p.wt_img[i]) & 15u) == 0 && p.wt_img_rows[i] >= 256,
+                   "%s: layer %d: weight-transpose image missing, unaligned or < 256 rows", __func__, i);
+        NERF_CHECK(i == 0 || (p.in_mask[i] && p.ld_in_mask[i] >= 8 && (((uintptr_t)p.in_mask[i]) & 15u) == 0 &&
+                              p.ld_in_mask[i] % 4 == 0),
+                   "%s: layer %d: the input's ReLU words (ld >= 8, 16-byte rows) are required", __func__, i);
+    }
+    for (int i = 0; i < 10; ++i) {
+        const int w = i == 0 ? 128 : 256;
+        NERF_CHECK(p.dy[i] && p.lddy[i] >= w && p.lddy[i] % 4 == 0 && (((uintptr_t)p.dy[i]) & 15u) == 0 &&
+                       p.dy_cmax[i] && p.dy_rmax[i],
+                   "%s: D_%d: output, column maxima and row maxima are mandatory (ld >= %d, 16-byte aligned)", __func__,
+                   i, w);
+    }
+    ChainBwdArgs args{p};
+    // algorithmic work per row: dyr (3 x 128) and nine 256-output GEMMs (K = 128, then 256);
+    // HBM: graw4 and the ReLU words read, D_0 .. D_9 (f32) and their row maxima written
+    const double rows = (double)p.n_pad;
+    prof_next(NERF_PROF_CHAIN_BWD, rows * (16 + 16 + 8 * 32 + 128 * 4 + 9 * 256 * 4 + 10 * 4));
+    prof_begin(as_stream(stream));
+    hipLaunchKernelGGL(k_mlp_chain_bwd, dim3(p.n_pad / CROWS), dim3(f2::NTH), 0, as_stream(stream), args);
+    prof_end(as_stream(stream), 2.0 * rows * (3.0 * 128 + 128 * 256 + 8 * 256 * 256), 3);
+    return check_launch(__func__);
 }

@@ -41,7 +41,7 @@ struct Carve {
 };
 
 struct Work {
-    float *graw4, *dyr, *dyr_rm, *dyr_cm, *part;
+    float *graw4, *dyr, *dyr_rm, *dyr_cm, *part, *scratch;
     float *dx[L], *dx_rm[L], *dx_cm[L];   // dx[l]: gradient w.r.t. layer l's first input (l = 1..9)
     float *genc_p0, *genc_p4, *genc_d;
     float *slab[L], *bslab[L];
@@ -55,6 +55,7 @@ size_t carve(char* base, int np, int ray_grad, Work& w) {
     w.dyr_rm = c.take(np);
     w.dyr_cm = c.take((size_t)(np / 128) * HR);
     w.part = c.take((size_t)nerf_heads_part_size(D, np));
+    w.scratch = c.take(512);
     for (int l = 1; l < L; ++l) {
         w.dx[l] = c.take((size_t)np * K1[l]);
         w.dx_rm[l] = c.take(np);
@@ -117,6 +118,72 @@ int weight_grad(const nerf_field_bwd& a, const Work& w, int l, const float* dy, 
     }
     return nerf_slab_reduce(w.slab[l], w.splits[l], OUT_P[l], KP[l], NREF[l], KREF[l], w.bslab[l], a.gw[l], a.gb[l], 0,
                             s);
+}
+
+// The schedule with the input-gradient chain (bwd_chain): dyr and the nine input gradients in
+// one launch (nerf_mlp_chain_bwd) on the caller's stream; then every layer's weight gradient on
+// the caller's stream (each 4-wave TN launch fills the chip on its own) with its split-K
+// reduce on the side stream behind an event, so a reduce runs beside the next layer's TN; the
+// ray gradients (pose learning) as three input-gradient GEMMs over the saved dy of the colour
+// layer, l4 and l0.  The head-weight partials were forked to the side stream before the chain.
+int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, void* stream, void* side_stream) {
+    const int np = a.n_pad;
+    hipStream_t main = nerf::as_stream(stream), side = nerf::as_stream(side_stream);
+    // D_0 = dyr, D_i = dx[10 - i]: the gradient at the output of layer 9 - i
+    nerf_chain_bwd c{};
+    c.graw4 = graw4;
+    c.hr_mask = a.mask[LR];
+    c.ld_hr_mask = HR / 32;
+    c.wd = a.wd;
+    c.wc = a.wc;
+    for (int i = 0; i < 9; ++i) {
+        const int l = LR - i;
+        c.wt_img[i] = a.wt_img[l];
+        c.wt_img_rows[i] = KP[l];
+        c.in_mask[i] = l == LR ? nullptr : a.mask[l - 1];
+        c.ld_in_mask[i] = OUT_P[l - 1 < 0 ? 0 : l - 1] / 32;
+    }
+    c.dy[0] = w.dyr; c.lddy[0] = HR; c.dy_cmax[0] = w.dyr_cm; c.dy_rmax[0] = w.dyr_rm;
+    for (int i = 1; i < 10; ++i) {
+        const int l = 10 - i;
+        c.dy[i] = w.dx[l]; c.lddy[i] = K1[l]; c.dy_cmax[i] = w.dx_cm[l]; c.dy_rmax[i] = w.dx_rm[l];
+    }
+    c.scratch = w.scratch;
+    c.n_pad = np;
+    RC(nerf_mlp_chain_bwd(&c, stream));
+    auto dy_of = [&](int l, const float*& dy, const float*& cm, const float*& rm) {
+        if (l == LR) { dy = w.dyr; cm = w.dyr_cm; rm = w.dyr_rm; }
+        else { dy = w.dx[l + 1]; cm = w.dx_cm[l + 1]; rm = w.dx_rm[l + 1]; }
+    };
+    for (int l = LR; l >= 0; --l) {
+        const float *dy, *cm, *rm;
+        dy_of(l, dy, cm, rm);
+        const int op = OUT_P[l];
+        const float* x = l == 0 ? a.enc_p : a.act[l - 1];
+        const float* x_cm = l == 0 ? a.enc_p_cmax : a.cmax[l - 1];
+        if (SEG[l])
+            RC(nerf_linear_bwd_weight_seg(dy, op, op, x, K1[l], K1[l], SEG[l] == 1 ? a.enc_p : a.enc_d, 64, 64, np,
+                                          w.splits[l], w.slab[l], KP[l], w.bslab[l], cm, x_cm,
+                                          SEG[l] == 1 ? a.enc_p_cmax : a.enc_d_cmax, stream));
+        else
+            RC(nerf_linear_bwd_weight(dy, op, op, x, K1[l], K1[l], np, w.splits[l], w.slab[l], KP[l], 0, w.bslab[l], cm,
+                                      x_cm, stream));
+        RC(fork(main, side));
+        RC(nerf_slab_reduce(w.slab[l], w.splits[l], OUT_P[l], KP[l], NREF[l], KREF[l], w.bslab[l], a.gw[l], a.gb[l], 0,
+                            side_stream));
+        if (a.ray_grad && (l == LR || l == 4 || l == 0)) {
+            // d enc: the encoding segment's rows of W^T (l0: all of them) against this dy
+            const int k0 = l == 0 ? 0 : K1[l];
+            float* out = l == LR ? w.genc_d : l == 4 ? w.genc_p4 : w.genc_p0;
+            RC(nerf_linear_bwd_data(dy, op, op, a.wt[l] + (size_t)k0 * op, a.wt_img[l] + (size_t)k0 * 8, KP[l], nullptr, 0,
+                                    nullptr, nullptr, 0, out, 64, np, 64, rm, nullptr, nullptr, stream));
+        }
+    }
+    RC(fork(side, main));
+    if (a.ray_grad)
+        RC(nerf_encode_bwd(a.pts_o, a.pts_d, a.view, a.z, w.genc_p0, w.genc_p4, w.genc_d, a.n_rays, a.n_samples,
+                           a.g_pts_o, a.g_pts_d, a.g_view, stream));
+    return NERF_OK;
 }
 
 }  // namespace
@@ -182,8 +249,11 @@ int schedule(const nerf_field_bwd& a, void* stream, void* side_stream) {
     RC(nerf_heads_bwd_mode(2, graw4, a.act[7], D, a.act[LR], HR, nullptr, 0, D, a.wc, nullptr, 0, w.part, np, nullptr,
                            nullptr, side_stream));
     RC(nerf_heads_reduce(w.part, D, np, a.g_wd, a.g_bd, a.g_wc, a.g_bc, 0, side_stream));
-    RC(nerf_heads_bwd_mode(1, graw4, nullptr, 0, nullptr, 0, a.mask[LR], HR / 32, D, a.wc, w.dyr, HR, nullptr, np,
-                           w.dyr_rm, w.dyr_cm, stream));
+    if (!a.bwd_chain)
+        RC(nerf_heads_bwd_mode(1, graw4, nullptr, 0, nullptr, 0, a.mask[LR], HR / 32, D, a.wc, w.dyr, HR, nullptr, np,
+                               w.dyr_rm, w.dyr_cm, stream));
+
+    if (a.bwd_chain) return chain_schedule(a, w, graw4, stream, side_stream);
 
     const float *dy = w.dyr, *dy_rm = w.dyr_rm, *dy_cm = w.dyr_cm;
     int deferred[L], nd = 0;

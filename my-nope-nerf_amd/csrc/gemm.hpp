@@ -641,11 +641,11 @@ __device__ __forceinline__ void tn_store_lds(const TNArgs& p, f32x16 (&acc)[TM][
     });
 }
 
-// TN policy 7 (the default, nerf_gemm_set_policy): a 256 x 256 weight gradient in the split modes
-// runs as XCD-paired 256 x 128 column tiles of eight waves (k_gemm_tn_x6 CT = 2), twice the rows
+// TN policies 7 and 8 (8 the default, nerf_gemm_set_policy): a 256 x 256 weight gradient in the split
+// modes runs as XCD-paired 256 x 128 column tiles of eight waves (k_gemm_tn_x6 CT = 2), twice the rows
 // per split at the same block count; needs a split count that is a multiple of 8
 inline int tn_xcd_group(int policy, int nout, int kin, int splits) {
-    return (policy == 7 && nout == 256 && kin == 256 && splits % 8 == 0) ? 2 : 0;
+    return (policy >= 7 && nout == 256 && kin == 256 && splits % 8 == 0) ? 2 : 0;
 }
 
 // split-bf16 launchers (gemm_x6.hip); policy as nerf_gemm_set_policy
@@ -654,6 +654,12 @@ int dispatch_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, h
                    bool h16 = false);
 // the two-segment weight gradient in one launch (fp16 pair, TN policy 7 shapes only)
 bool tn_seg_supported(int nout, int k1, int k2, int splits);
-int dispatch_tn_x6_seg(const TNArgs& pm, const TNArgs& ps, int nout, int splits, hipStream_t s, double flops);
+int dispatch_tn_x6_seg(const TNArgs& pm, const TNArgs& ps, int nout, int splits, int policy, hipStream_t s,
+                       double flops);
+// the 4-wave weight-gradient kernels (wgrad.hip): which shapes they cover, and their launchers
+bool wgrad_supported(int nout, int kin, int splits, int rows_per_split);
+bool wgrad_seg_supported(int nout, int k1, int k2, int splits, int rows_per_split);
+void launch_wgrad(const TNArgs& a, int nout, int kin, int splits, hipStream_t s);
+void launch_wgrad_seg(const TNArgs& pm, const TNArgs& ps, int nout, int splits, hipStream_t s);
 
 }  // namespace nerf

@@ -351,14 +351,15 @@ static int launch_nt(const NTArgs& a, hipStream_t s, double flops) {
 // 3 = 256x256/8 waves (exact-f32 kernels; the split kernels: 128x256 fp16 pair, 256x256 bf16x3)
 static int g_nt_policy = 0;
 static int g_tn_policy = 0;
-// default TN policy (g_tn_policy 0): 7 -- a 256 x 256 weight gradient in the split modes as
+// TN policy 7 -- a 256 x 256 weight gradient in the split modes as
 // XCD-paired 256 x 128 column tiles of eight waves (128 splits, half the slab bytes), the
 // 64-wide inputs' 256 x 64 tile and the colour layer's 128 x 256 tile with eight waves (one
 // column tile: each split reads its dy rows once); 87 vs 104 us per 131072 x 256 x 256 layer
 // with its slab reduce, 37 vs 44 us per 256 x 64 one (profiles/r02/dw_xcd_group_ab.txt).
 // Policy 3 is the round-2 256 x 256 tile at one wave per SIMD (also the fallback when a split
-// count is not a multiple of 8).
-static const int kTnDefault = 7;
+// count is not a multiple of 8).  Policy 8 (the default since round 4): the splits and tiles
+// of 7 on the 4-wave kernels of wgrad.hip in precision mode 2, bit-identical slabs.
+static const int kTnDefault = 8;
 
 // f32 arithmetic (nerf_gemm_set_precision): 0 = exact-f32 MFMA, 1 = split-bf16 emulation
 // (6 products), 2 = row-scaled fp16 pair (3 products; the library default since ABI 9 -- the
@@ -553,7 +554,7 @@ extern "C" int nerf_linear_bwd_weight_seg(const float* dy, int lddy, int nout, c
     rc = tn_args(__func__, dy, lddy, nout, x2, ldx2, k2, m, splits, slab, ldslab, k1, nullptr, dy_cmax, x2_cmax, ps);
     if (rc) return rc;
     const int pol = g_tn_policy ? g_tn_policy : kTnDefault;
-    const bool one = g_precision == 2 && pol == 7 && dy_cmax && x1_cmax && x2_cmax && (m / splits) % 128 == 0 &&
+    const bool one = g_precision == 2 && pol >= 7 && dy_cmax && x1_cmax && x2_cmax && (m / splits) % 128 == 0 &&
                      tn_seg_supported(nout, k1, k2, splits);
     if (!one) {   // the same slab from two launches
         rc = nerf_linear_bwd_weight(dy, lddy, nout, x1, ldx1, k1, m, splits, slab, ldslab, 0, bslab, dy_cmax, x1_cmax,
@@ -565,7 +566,7 @@ extern "C" int nerf_linear_bwd_weight_seg(const float* dy, int lddy, int nout, c
     const double fl = 2.0 * m * nout * (double)(k1 + k2);
     prof_next(nout % 256 == 0 ? NERF_PROF_DW : NERF_PROF_DW_NARROW,
               4.0 * m * (double)(nout + k1 + k2) + 4.0 * nout * (double)(k1 + k2) + (bslab ? 4.0 * nout : 0.0));
-    return dispatch_tn_x6_seg(pm, ps, nout, splits, as_stream(stream), fl);
+    return dispatch_tn_x6_seg(pm, ps, nout, splits, pol, as_stream(stream), fl);
 }
 
 static int slab_job_check(const char* fn, const SlabJob& j) {
@@ -593,8 +594,8 @@ extern "C" int nerf_slab_reduce(const float* slab, int splits, int nout, int lds
 }
 
 extern "C" int nerf_gemm_set_policy(int nt_policy, int tn_policy) {
-    NERF_CHECK(nt_policy >= 0 && nt_policy <= 3 && (tn_policy == 0 || tn_policy == 3 || tn_policy == 7),
-               "%s: policies are 0..3 (NT) and 0, 3, 7 (TN)", __func__);
+    NERF_CHECK(nt_policy >= 0 && nt_policy <= 3 && (tn_policy == 0 || tn_policy == 3 || tn_policy == 7 || tn_policy == 8),
+               "%s: policies are 0..3 (NT) and 0, 3, 7, 8 (TN)", __func__);
     g_nt_policy = nt_policy;
     g_tn_policy = tn_policy;
     return NERF_OK;
@@ -606,8 +607,8 @@ extern "C" int nerf_gemm_set_policy(int nt_policy, int tn_policy) {
 extern "C" int nerf_linear_bwd_weight_splits(int nout, int kin, int m) {
     const int pol = g_tn_policy ? g_tn_policy : kTnDefault;
     int tiles, target;
-    if (pol == 7 && g_precision >= 1 && nout == 256 && kin == 256) { tiles = 2; target = 256; }   // XCD pairs
-    else if (pol == 7 && g_precision >= 1 && nout == 128 && kin % 256 == 0) { tiles = kin / 256; target = 256; }
+    if (pol >= 7 && g_precision >= 1 && nout == 256 && kin == 256) { tiles = 2; target = 256; }   // XCD pairs
+    else if (pol >= 7 && g_precision >= 1 && nout == 128 && kin % 256 == 0) { tiles = kin / 256; target = 256; }
     else if (pol >= 3 && nout % 256 == 0 && kin % 256 == 0) { tiles = (nout / 256) * (kin / 256); target = 256; }
     else if (pol >= 3 && nout % 256 == 0 && kin == 64 && g_precision >= 1) { tiles = nout / 256; target = 256; }
     else { tiles = ((nout + 127) / 128) * ((kin + 127) / 128); target = 512; }

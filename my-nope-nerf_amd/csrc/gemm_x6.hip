@@ -30,6 +30,7 @@
 // its row max (max |x| over the row), read here as NTArgs::ar1 / ar2; the weight image's
 // per-row exponents sit in plane 2 of the image (nerf_pack_weights).
 #include "gemm.hpp"
+#include "x16.hpp"
 
 #include <cstdlib>
 
@@ -37,9 +38,6 @@ namespace nerf {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int XK = 16;   // K per LDS tile
 
@@ -70,19 +68,6 @@ __device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& 
     l = pk_bf16(ra - __uint_as_float(m << 16), rb - __uint_as_float(m & 0xffff0000u));
 }
 
-__device__ __forceinline__ uint32_t pk_f16(float a, float b) {
-    f32x2 v = {a, b};
-    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2v));   // RNE
-}
-
-// (a, b) scaled by 2^e -> packed fp16 pairs hi, lo with a 2^e = hi.x + lo.x (+ <= 2^-22 |a| 2^e)
-__device__ __forceinline__ void split2h(float a, float b, int e, uint32_t& h, uint32_t& l) {
-    a = __builtin_amdgcn_ldexpf(a, e);
-    b = __builtin_amdgcn_ldexpf(b, e);
-    h = pk_f16(a, b);
-    const f16x2v hv = __builtin_bit_cast(f16x2v, h);
-    l = pk_f16(a - (float)hv[0], b - (float)hv[1]);
-}
 
 // bytes of one k-half image of ROWS rows (+128 B bank offset between the halves);
 // NP planes (3: bf16 hi/mid/lo, 2: fp16 hi/lo)
@@ -96,10 +81,6 @@ struct XImg {
 __device__ __forceinline__ f32x16 mfma_bf16(const uint4& a, const uint4& b, const f32x16& c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
                                                    0, 0, 0);
-}
-__device__ __forceinline__ f32x16 mfma_f16(const uint4& a, const uint4& b, const f32x16& c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
-                                                  0, 0, 0);
 }
 
 // float4 along k at (row, k = 4q) -> the three planes' 8-byte pieces of that row's chunk
@@ -182,12 +163,6 @@ __device__ __forceinline__ void put_colRh(char* img, int c, int q, const float (
     }
 }
 
-// max over the 128-row groups of rows [s0, s0 + rows) of a column-max array cm[group][ld]
-__device__ __forceinline__ float tn_colmax(const float* cm, int ld, size_t s0, int rows, int col) {
-    float m = 0.f;
-    for (int g = (int)(s0 / 128); g < (int)((s0 + rows) / 128); ++g) m = fmaxf(m, cm[(size_t)g * ld + col]);
-    return m;
-}
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
@@ -1020,14 +995,14 @@ static void pick_tn_x6(const TNArgs& a, int nout, int kin, int splits, int polic
     else if (policy >= 3 && nout % 256 == 0 && kin % 256 == 0)
         hipLaunchKernelGGL((k_gemm_tn_x6<256, 256, 2, 2, H, NS>), dim3(nout / 256, kin / 256, splits), dim3(256), 0,
                            s, a);
-    else if (policy == 7 && nout == 128 && kin % 256 == 0)
+    else if (policy >= 7 && nout == 128 && kin % 256 == 0)
         // the colour layer (128 outputs, 256 feature columns): one column tile per 256 inputs, so
         // each split reads its dy rows once (two 128 x 128 column tiles read them twice)
         hipLaunchKernelGGL((k_gemm_tn_x6<128, 256, 2, 4, H, kTnNs8>), dim3(1, kin / 256, splits), dim3(512), 0, s, a);
     else if (nout % 128 == 0 && kin % 128 == 0)
         hipLaunchKernelGGL((k_gemm_tn_x6<128, 128, 2, 2, H, NS>), dim3(nout / 128, kin / 128, splits), dim3(256), 0,
                            s, a);
-    else if (policy == 7 && nout % 256 == 0 && kin == 64)   // eight waves, 64 x 32 per wave
+    else if (policy >= 7 && nout % 256 == 0 && kin == 64)   // eight waves, 64 x 32 per wave
         hipLaunchKernelGGL((k_gemm_tn_x6<256, 64, 4, 2, H, kTnNs8>), dim3(nout / 256, 1, splits), dim3(512), 0, s, a);
     else if (policy >= 3 && nout % 256 == 0 && kin == 64)
         // a 64-wide input (the encodings: l0, the skip segment of l4) against all 256 outputs in
@@ -1046,7 +1021,9 @@ static void pick_tn_x6(const TNArgs& a, int nout, int kin, int splits, int polic
 int dispatch_tn_x6(const TNArgs& a, int nout, int kin, int splits, int policy, hipStream_t s, double flops,
                    bool h16) {
     prof_begin(s);
-    if (h16) pick_tn_x6<true>(a, nout, kin, splits, policy, s);
+    if (h16 && policy == 8 && wgrad_supported(nout, kin, splits, a.rows_per_split))
+        launch_wgrad(a, nout, kin, splits, s);
+    else if (h16) pick_tn_x6<true>(a, nout, kin, splits, policy, s);
     else pick_tn_x6<false>(a, nout, kin, splits, policy, s);
     prof_end(s, flops, h16 ? 3 : 6);
     return check_launch(h16 ? "k_gemm_tn_x6 (fp16 pair)" : "k_gemm_tn_x6");
@@ -1056,9 +1033,12 @@ bool tn_seg_supported(int nout, int k1, int k2, int splits) {
     return k2 == 64 && k1 == 256 && (nout == 256 || nout == 128) && splits % 8 == 0;
 }
 
-int dispatch_tn_x6_seg(const TNArgs& pm, const TNArgs& ps, int nout, int splits, hipStream_t s, double flops) {
+int dispatch_tn_x6_seg(const TNArgs& pm, const TNArgs& ps, int nout, int splits, int policy, hipStream_t s,
+                       double flops) {
     prof_begin(s);
-    if (nout == 256)   // l4: two XCD-paired 256 x 128 tiles over h3 + the 256 x 64 tile over enc_p
+    if (policy == 8 && wgrad_seg_supported(nout, 256, 64, splits, pm.rows_per_split))
+        launch_wgrad_seg(pm, ps, nout, splits, s);
+    else if (nout == 256)   // l4: two XCD-paired 256 x 128 tiles over h3 + the 256 x 64 tile over enc_p
         hipLaunchKernelGGL((k_gemm_tn_x6_seg<256, 128, 4, 2, 64, 4, 2, 2, kTnNs8>), dim3(3 * splits), dim3(512), 0, s, pm,
                            ps);
     else               // colour layer: the 128 x 256 tile over f + the 128 x 64 tile over enc_d

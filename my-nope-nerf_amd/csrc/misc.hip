@@ -138,15 +138,18 @@ __global__ __launch_bounds__(256) void k_pack(PackBatch pb) {
 // eps, wd, -, ticket}) so a captured hipGraph replays correct bias corrections; an lr change
 // reaches a replay once the host pushes it into the device block (HipAdam.sync_hyper()
 // between replays).  Every workgroup uses step + 1; the last one to finish (ticket) stores it.
-__device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v, float b1, float b2, float eps,
-                                          float wd, float sbc2, float step_size) {
+// one element of torch's Adam (the foreach path, torch/optim/adam.py): om1 = 1 - beta1,
+// om2 = 1 - beta2 as torch passes them (Python doubles rounded once to f32; 1.f - 0.999f is
+// 1.3e-5 off 0.001)
+__device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v, float om1, float b2, float om2,
+                                          float eps, float wd, float sbc2, float step_size) {
     if (wd != 0.f) g = g + wd * p;
-    const float mi = m + (1.f - b1) * (g - m);   // lerp_ as torch does
-    const float vi = v * b2 + (1.f - b2) * g * g;
+    const float mi = m + om1 * (g - m);          // exp_avg.lerp_(grad, 1 - beta1)
+    const float vi = v * b2 + om2 * g * g;       // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
     m = mi;
     v = vi;
     const float denom = sqrtf(vi) / sbc2 + eps;
-    p = p + (-step_size * mi) / denom;           // addcdiv_(m, denom, value=-step_size)
+    p = p + (-step_size) * (mi / denom);         // addcdiv_(m, denom, value=-step_size)
     return p;
 }
 
@@ -157,9 +160,14 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float
                                               float* __restrict__ m, float* __restrict__ v, int64_t n,
                                               float* __restrict__ hyper) {
     const float step = hyper[0] + 1.f, lr = hyper[1], b1 = hyper[2], b2 = hyper[3], eps = hyper[4], wd = hyper[5];
-    const float bc1 = 1.f - powf(b1, step);
-    const float sbc2 = sqrtf(1.f - powf(b2, step));
-    const float step_size = lr / bc1;
+    // hyper[6]: 1 - beta2 from the host's doubles (0: derive it here, as before ABI 12); the
+    // bias corrections in double like torch's Python scalars (1 - beta2^t cancels: in f32
+    // it is ~1e-5 off at small t)
+    const float om2 = hyper[6] != 0.f ? hyper[6] : 1.f - b2;
+    const float om1 = (float)(1.0 - (double)b1);
+    const double bc1 = 1.0 - pow((double)b1, (double)step);
+    const float sbc2 = (float)sqrt(1.0 - pow(1.0 - (double)om2, (double)step));
+    const float step_size = (float)((double)lr / bc1);
     const int64_t n4 = n >> 2;
     float4* p4 = reinterpret_cast<float4*>(p);
     float4* m4 = reinterpret_cast<float4*>(m);
@@ -168,14 +176,14 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         float4 pp = p4[i], mm = m4[i], vv = v4[i];
         const float4 gg = g4[i];
-        adam_one(pp.x, gg.x, mm.x, vv.x, b1, b2, eps, wd, sbc2, step_size);
-        adam_one(pp.y, gg.y, mm.y, vv.y, b1, b2, eps, wd, sbc2, step_size);
-        adam_one(pp.z, gg.z, mm.z, vv.z, b1, b2, eps, wd, sbc2, step_size);
-        adam_one(pp.w, gg.w, mm.w, vv.w, b1, b2, eps, wd, sbc2, step_size);
+        adam_one(pp.x, gg.x, mm.x, vv.x, om1, b2, om2, eps, wd, sbc2, step_size);
+        adam_one(pp.y, gg.y, mm.y, vv.y, om1, b2, om2, eps, wd, sbc2, step_size);
+        adam_one(pp.z, gg.z, mm.z, vv.z, om1, b2, om2, eps, wd, sbc2, step_size);
+        adam_one(pp.w, gg.w, mm.w, vv.w, om1, b2, om2, eps, wd, sbc2, step_size);
         p4[i] = pp; m4[i] = mm; v4[i] = vv;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0)
-        for (int64_t i = n4 * 4; i < n; ++i) adam_one(p[i], g[i], m[i], v[i], b1, b2, eps, wd, sbc2, step_size);
+        for (int64_t i = n4 * 4; i < n; ++i) adam_one(p[i], g[i], m[i], v[i], om1, b2, om2, eps, wd, sbc2, step_size);
     __syncthreads();                              // this workgroup has read hyper[0]
     if (threadIdx.x == 0) {
         unsigned* ticket = reinterpret_cast<unsigned*>(hyper + 7);

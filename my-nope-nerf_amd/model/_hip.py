@@ -45,8 +45,8 @@ class ProfKind(ctypes.Structure):
                 ("bytes", ctypes.c_double), ("mfma_flops", ctypes.c_double), ("exact_f32", _c_i)]
 
 
-PROF_KINDS = ("fwd", "dx", "dw", "dw_narrow")   # NERF_PROF_FWD / _DX / _DW / _DW_NARROW
-ABI_VERSION = 11                   # NERF_HIP_ABI_VERSION
+PROF_KINDS = ("fwd", "dx", "dw", "dw_narrow", "chain_fwd", "chain_bwd")   # NERF_PROF_FWD .. _CHAIN_BWD
+ABI_VERSION = 12                   # NERF_HIP_ABI_VERSION
 
 
 _P10 = _c_p * 10
@@ -55,12 +55,20 @@ _P10 = _c_p * 10
 class FieldBwd(ctypes.Structure):
     """nerf_field_bwd (include/nerf_hip.h): the native backward's arguments."""
     _fields_ = [("n_pad", _c_i), ("n_rays", _c_i), ("n_samples", _c_i), ("flags", _c_i), ("ray_grad", _c_i),
-                ("tail_main", _c_i), ("z", _c_p), ("raw4", _c_p), ("enc_p", _c_p), ("enc_d", _c_p),
+                ("tail_main", _c_i), ("bwd_chain", _c_i), ("z", _c_p), ("raw4", _c_p), ("enc_p", _c_p), ("enc_d", _c_p),
                 ("enc_p_cmax", _c_p), ("enc_d_cmax", _c_p), ("act", _P10), ("mask", _P10), ("cmax", _P10),
                 ("pts_o", _c_p), ("pts_d", _c_p), ("view", _c_p), ("wt", _P10), ("wt_img", _P10), ("wd", _c_p),
                 ("wc", _c_p), ("g_rgb", _c_p), ("g_dist", _c_p), ("graw4", _c_p), ("gw", _P10), ("gb", _P10),
                 ("g_wd", _c_p), ("g_bd", _c_p), ("g_wc", _c_p), ("g_bc", _c_p), ("g_pts_o", _c_p), ("g_pts_d", _c_p),
                 ("g_view", _c_p), ("workspace", _c_p)]
+
+
+class ChainBwd(ctypes.Structure):
+    """nerf_chain_bwd (include/nerf_hip.h): the input-gradient chain's arguments."""
+    _fields_ = [("graw4", _c_p), ("hr_mask", _c_p), ("ld_hr_mask", _c_i), ("wd", _c_p), ("wc", _c_p),
+                ("wt_img", _c_p * 9), ("wt_img_rows", _c_i * 9), ("in_mask", _c_p * 9), ("ld_in_mask", _c_i * 9),
+                ("dy", _c_p * 10), ("lddy", _c_i * 10), ("dy_cmax", _c_p * 10), ("dy_rmax", _c_p * 10),
+                ("scratch", _c_p), ("n_pad", _c_i)]
 
 
 class ChainLayer(ctypes.Structure):
@@ -87,6 +95,7 @@ _SIGS = {
     "nerf_linear_bwd_weight_splits": ([_c_i, _c_i, _c_i], _c_i),
     "nerf_field_bwd_workspace_bytes": ([_c_i, _c_i], ctypes.c_size_t),
     "nerf_field_backward": ([_c_p, _c_p, _c_p], _c_i),
+    "nerf_mlp_chain_bwd": ([_c_p, _c_p], _c_i),
     "nerf_slab_reduce": ([_c_p, _c_i, _c_i, _c_i, _c_i, _c_i, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_heads_fwd": ([_c_p, _c_i, _c_p, _c_i, _c_i, _c_p, _c_p, _c_p, _c_p, _c_p, _c_i, _c_p], _c_i),
     "nerf_heads_part_size": ([_c_i, _c_i], _c_i),
@@ -302,6 +311,11 @@ def field_backward(args: FieldBwd, side_stream: int):
     _call("nerf_field_backward", ctypes.addressof(args), _stream(), side_stream)
 
 
+def mlp_chain_bwd(args: ChainBwd):
+    """dyr and the nine input gradients of the D = 256 field in one launch (nerf_mlp_chain_bwd)."""
+    _call("nerf_mlp_chain_bwd", ctypes.addressof(args), _stream())
+
+
 def heads_fwd(h8, hr, hidden, wd, bd, wc, bc, raw4, n_pad):
     _call("nerf_heads_fwd", _ptr(h8), _ld(h8), _ptr(hr), _ld(hr), hidden, _ptr(wd), _ptr(bd), _ptr(wc),
           _ptr(bc), _ptr(raw4), n_pad, _stream())
@@ -512,7 +526,8 @@ def prof_enable(on: bool):
 
 def prof_read_kinds():
     """Per-kind GEMM records since prof_enable (call before prof_read, which resets them):
-    {"fwd"|"dx"|"dw"|"dw_narrow": {ms, launches, flops, bytes, mfma_flops, exact_f32}}."""
+    {"fwd"|"dx"|"dw"|"dw_narrow"|"chain_fwd"|"chain_bwd": {ms, launches, flops, bytes, mfma_flops,
+    exact_f32}}."""
     arr = (ProfKind * len(PROF_KINDS))()
     _call("nerf_prof_read_kinds", arr, len(PROF_KINDS))
     return {name: {f: getattr(arr[i], f) for f, _ in ProfKind._fields_} for i, name in enumerate(PROF_KINDS)}

@@ -317,6 +317,12 @@ class FieldRunner:
         return (self.h16 and self.D == 256 and self.HR == 128 and self.heads_side(Np)
                 and os.environ.get("NERF_NATIVE_BWD", "1") != "0")
 
+    def bwd_chain(self) -> bool:
+        """The native backward's input gradients as one launch (nerf_mlp_chain_bwd: dyr and the
+        nine input-gradient GEMMs with dy resident in registers) -- the default; NERF_BWD_CHAIN=0
+        runs them as nine nerf_linear_bwd_data launches beside the weight gradients."""
+        return os.environ.get("NERF_BWD_CHAIN", "1") != "0"
+
     def _backward_native(self, st, g_rgb, g_dist, want_ray_grad, graw4, G):
         Np, R, S = st["Np"], st["R"], st["S"]
         dev = st["z"].device
@@ -335,7 +341,7 @@ class FieldRunner:
         tail_default = 2 if Np >= 65536 else 0
         args = _hip.FieldBwd(
             Np, R, S, st["flags"], int(want_ray_grad), int(os.environ.get("NERF_TAIL_MAIN", str(tail_default))),
-            P(st["z"]), P(st["raw4"]), P(st["enc_p"]), P(st["enc_d"]), P(st["cmaxes"]["enc_p"]),
+            int(self.bwd_chain()), P(st["z"]), P(st["raw4"]), P(st["enc_p"]), P(st["enc_d"]), P(st["cmaxes"]["enc_p"]),
             P(st["cmaxes"]["enc_d"]), _hip._P10(*[a.data_ptr() for a in acts]),
             _hip._P10(*[P(masks.get(n)) for n in names]), _hip._P10(*[P(cms.get(n)) for n in names]),
             P(st["pts_o"]), P(st["pts_d"]), P(st["view"]),

@@ -53,7 +53,8 @@ class HipAdam(torch.optim.Optimizer):
         g = self.param_groups[0]
         h = (float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]), float(g["weight_decay"]))
         if h != self._hyper_host:      # lr schedulers edit param_groups; push the change
-            self._hyper[1:6].copy_(torch.tensor(h, dtype=torch.float32), non_blocking=False)
+            # slot 6: 1 - beta2 from the Python doubles (torch's addcmul_ value), not 1.f - beta2_f32
+            self._hyper[1:7].copy_(torch.tensor(h + (1.0 - h[2],), dtype=torch.float32), non_blocking=False)
             self._hyper_host = h
 
     def _flat_grad(self):

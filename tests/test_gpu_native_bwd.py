@@ -1,9 +1,13 @@
 """The native field backward (nerf_field_backward, csrc/field_bwd.cpp) against the Python
-schedule it replaces (FieldRunner.backward with NERF_NATIVE_BWD=0): the same kernels in
-the same order, so every parameter gradient and every ray gradient must be bit-identical.
-Training-size batches (Np >= 65536, where the native path runs), with and without ray
-gradients (pose learning), from the composite backward and from a given graw4
-(eval_points); also under a tail of 0 and 3 deferred weight gradients."""
+schedule it replaces (FieldRunner.backward with NERF_NATIVE_BWD=0).  With the per-layer
+input gradients (NERF_BWD_CHAIN=0) it runs the same kernels in the same order, so every
+parameter gradient and every ray gradient must be bit-identical; with the input-gradient
+chain (nerf_mlp_chain_bwd, the default) the input gradients accumulate in another MFMA order
+and the saved dy are the fp16 pairs the chain consumed (within 2^-22 relative), so the
+gradients agree to 1e-5 relative L2 per tensor.  Training-size batches (Np >= 65536, where
+the native path runs), with and without ray gradients (pose learning), from the composite
+backward and from a given graw4 (eval_points); also under a tail of 0 and 3 deferred weight
+gradients."""
 import os
 
 import pytest
@@ -55,9 +59,20 @@ def _grads(net, fn, native, env=None):
                 os.environ[k] = v
 
 
+def _agree(a, b, chain):
+    assert torch.isfinite(a).all()
+    if chain == "0":
+        assert torch.equal(a, b)
+    else:
+        scale = b.norm().item()
+        assert (a - b).norm().item() <= 1e-5 * scale + 1e-30, (a - b).norm().item() / max(scale, 1e-30)
+        assert (a - b).abs().max().item() <= 1e-4 * b.abs().max().item() + 1e-30
+
+
+@pytest.mark.parametrize("chain", ["0", "1"])
 @pytest.mark.parametrize("ray_grad,R,S,tail", [(False, 1024, 128, None), (True, 1024, 128, None),
                                                (False, 600, 128, "0"), (True, 520, 128, "3")])
-def test_native_backward_bit_identical(dev, h16, ray_grad, R, S, tail):
+def test_native_backward_bit_identical(dev, h16, ray_grad, R, S, tail, chain):
     net = _net(dev, seed=R)
     o, d, noise = _rays(R, S, seed=R + 1)
     runner = net.hip_runner()
@@ -69,17 +84,18 @@ def test_native_backward_bit_identical(dev, h16, ray_grad, R, S, tail):
         (rgb.square().sum() + 0.1 * dist.sum()).backward()
         return [oo, dd] if ray_grad else []
 
-    env = {"NERF_TAIL_MAIN": tail} if tail is not None else None
+    env = {"NERF_TAIL_MAIN": tail} if tail is not None else {}
+    env["NERF_BWD_CHAIN"] = chain
     g_native = _grads(net, fn, True, env)
     g_python = _grads(net, fn, False, env)
     n_pad = (R * S + 127) // 128 * 128
     assert n_pad >= 65536 and runner.native_backward(n_pad)
     for a, b in zip(g_native, g_python):
-        assert torch.equal(a, b)
-        assert torch.isfinite(a).all()
+        _agree(a, b, chain)
 
 
-def test_native_backward_from_raw_heads(dev, h16):
+@pytest.mark.parametrize("chain", ["0", "1"])
+def test_native_backward_from_raw_heads(dev, h16, chain):
     """eval_points (FieldRawFn): the backward starts from a given graw4, no composite."""
     net = _net(dev, seed=3)
     n = 70000
@@ -94,8 +110,8 @@ def test_native_backward_from_raw_heads(dev, h16):
         (raw[:, 0].square().sum() + raw[:, 1:].sum()).backward()
         return [pp, vv]
 
-    g_native = _grads(net, fn, True)
-    g_python = _grads(net, fn, False)
+    g_native = _grads(net, fn, True, {"NERF_BWD_CHAIN": chain})
+    g_python = _grads(net, fn, False, {"NERF_BWD_CHAIN": chain})
     for a, b in zip(g_native, g_python):
-        assert torch.equal(a, b)
+        _agree(a, b, chain)
 

@@ -119,15 +119,18 @@ def test_dw_split_policy():
     try:
         assert _hip.bwd_weight_splits(256, 256, 131072) == 256     # exact f32: 256 x 256 tiles
         assert _hip.bwd_weight_splits(128, 256, 131072) == 256
-        # split modes, default TN policy 7: XCD-paired 256 x 128 column tiles, 2 blocks per split;
-        # the colour layer's 128 x 256 tile, one block per split
+        # split modes, default TN policy 8 (7's tiles on the 4-wave kernels): XCD-paired
+        # 256 x 128 column tiles, 2 blocks per split; the colour layer's 128 x 256 tile, one per split
         _hip.gemm_set_precision(2)
         assert _hip.bwd_weight_splits(256, 256, 131072) == 128
         assert _hip.bwd_weight_splits(256, 64, 131072) == 256
         assert _hip.bwd_weight_splits(128, 256, 131072) == 256
+        for pol in (7, 8):
+            _hip.gemm_set_policy(0, pol)
+            assert _hip.bwd_weight_splits(256, 256, 131072) == 128
         _hip.gemm_set_policy(0, 3)
         assert _hip.bwd_weight_splits(256, 256, 131072) == 256
-        for bad in (1, 4, 5, 6, 8, 9, -1):
+        for bad in (1, 4, 5, 6, 9, -1):
             with pytest.raises(RuntimeError):
                 _hip.gemm_set_policy(0, bad)
     finally:
