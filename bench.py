@@ -636,7 +636,7 @@ def main():
                            (d["mfma"]["achieved_tflops_f32eq"], d["mfma"]["peak_tflops_f32eq"],
                             "TFLOP/s (f32-equivalent)"))
         traffic, traffic_note = None, None
-        tpath = next((q for q in (os.path.join(ROOT, "profiles", r, "gemm_traffic.json") for r in ("r03", "r02"))
+        tpath = next((q for q in (os.path.join(ROOT, "profiles", r, "gemm_traffic.json") for r in ("r04", "r03", "r02"))
                       if os.path.exists(q)), "")
         if tpath and args.gemm_precision == "f16x3":
             # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC

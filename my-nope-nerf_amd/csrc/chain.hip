@@ -934,10 +934,29 @@ __device__ __forceinline__ void enc_frag(const float* row, int t, int g, int er,
 // atomics from the quads' first lanes).  The work is spread over the step's MFMA tiles (piece
 // j after tile j's MFMAs): the two waves of a SIMD reach their k-steps together, so short VALU
 // pieces between MFMA groups keep the matrix pipe fed where one block of VALU would not
+// (hi + lo) 2^-e from fp16 half K & 1 of the pair words: two v_fma_mix_f32 reading the fp16
+// halves in place, lo 2^-e then hi 2^-e + that -- both exact (power-of-two scale, the sum is
+// an f32), so the value is ldexp((float)hi + (float)lo, -e) bit for bit at half the VALU
 __device__ __forceinline__ float rebuilt(const uint4& ah, const uint4& al, int k, int er) {
-    const ch16x2 h = __builtin_bit_cast(ch16x2, (&ah.x)[k >> 1]);
-    const ch16x2 o = __builtin_bit_cast(ch16x2, (&al.x)[k >> 1]);
-    return __builtin_amdgcn_ldexpf((float)h[k & 1] + (float)o[k & 1], -er);
+    const uint32_t h = (&ah.x)[k >> 1], l = (&al.x)[k >> 1];
+    const float s = __builtin_amdgcn_ldexpf(1.f, -er);
+    float t, v;
+    if (k & 1) {
+        asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(t) : "v"(l), "v"(s));
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(v) : "v"(h), "v"(s), "v"(t));
+    } else {
+        asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel_hi:[1,0,0]" : "=v"(t) : "v"(l), "v"(s));
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(v) : "v"(h), "v"(s), "v"(t));
+    }
+    return v;
+}
+// max of |v| over the lane's quad as float bits (non-negative floats order like their bits):
+// v_and + two v_max_u32_dpp, no old-value moves or NaN canonicalisation
+__device__ __forceinline__ uint32_t quad_absmax_bits(float v) {
+    uint32_t b = __float_as_uint(v) & 0x7fffffffu;
+    b = max(b, (uint32_t)__builtin_amdgcn_mov_dpp((int)b, 0xB1, 0xF, 0xF, true));   // quad_perm [1,0,3,2]
+    b = max(b, (uint32_t)__builtin_amdgcn_mov_dpp((int)b, 0x4E, 0xF, 0xF, true));   // quad_perm [2,3,0,1]
+    return b;
 }
 template <int l, int u, int j, int ntj>
 __device__ __forceinline__ void save_piece(const ChainFwdArgs& p, State& st, const uint4& ah, const uint4& al,
@@ -957,16 +976,12 @@ __device__ __forceinline__ void save_piece(const ChainFwdArgs& p, State& st, con
                 make_float4(v[0], v[1], v[2], v[3]);
         if constexpr (kSaveFused && !(kTrAblate & 2)) {   // column maxima of these 4 features, from v
             uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + Y::O_CMX) + ((l - 1) & 1) * 256 + 32 * u + 8 * st.g + k0;
-            float c[4];
+            uint32_t c[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                c[k] = fabsf(v[k]);
-                c[k] = fmaxf(c[k], dpp_f<0xB1>(0.f, c[k]));
-                c[k] = fmaxf(c[k], dpp_f<0x4E>(0.f, c[k]));
-            }
+            for (int k = 0; k < 4; ++k) c[k] = quad_absmax_bits(v[k]);
             if ((st.n & 3) == 0) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) atomicMax(cm + k, __float_as_uint(c[k]));
+                for (int k = 0; k < 4; ++k) atomicMax(cm + k, c[k]);
             }
         }
         if constexpr (!(kTrAblate & 2) && l - 1 != 8) {   // lf has no ReLU
@@ -1535,16 +1550,12 @@ __device__ __forceinline__ void save_piece(const nerf_chain_bwd& p, State& st, c
         for (int k = 0; k < 4; ++k) v[k] = f2::rebuilt(ah, al, k0 + k, st.er);
         *reinterpret_cast<float4*>(p.dy[i] + row * p.lddy[i] + 32 * u + 8 * st.g + k0) = make_float4(v[0], v[1], v[2], v[3]);
         uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + O_CMX) + (i & 1) * 256 + 32 * u + 8 * st.g + k0;
-        float c[4];
+        uint32_t c[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            c[k] = fabsf(v[k]);
-            c[k] = fmaxf(c[k], dpp_f<0xB1>(0.f, c[k]));
-            c[k] = fmaxf(c[k], dpp_f<0x4E>(0.f, c[k]));
-        }
+        for (int k = 0; k < 4; ++k) c[k] = f2::quad_absmax_bits(v[k]);
         if ((st.n & 3) == 0) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) atomicMax(cm + k, __float_as_uint(c[k]));
+            for (int k = 0; k < 4; ++k) atomicMax(cm + k, c[k]);
         }
     }
 }
@@ -1668,16 +1679,12 @@ __device__ __forceinline__ void layer(const nerf_chain_bwd& p, State& st) {
         if constexpr (last) {
             *reinterpret_cast<float4*>(p.dy[NL] + (st.m0 + st.rl) * p.lddy[NL] + f0) = make_float4(x[0], x[1], x[2], x[3]);
             uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + O_CMX) + (NL & 1) * 256 + f0;
-            float c[4];
+            uint32_t c[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                c[k] = fabsf(x[k]);
-                c[k] = fmaxf(c[k], dpp_f<0xB1>(0.f, c[k]));
-                c[k] = fmaxf(c[k], dpp_f<0x4E>(0.f, c[k]));
-            }
+            for (int k = 0; k < 4; ++k) c[k] = f2::quad_absmax_bits(x[k]);
             if ((st.n & 3) == 0) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) atomicMax(cm + k, __float_as_uint(c[k]));
+                for (int k = 0; k < 4; ++k) atomicMax(cm + k, c[k]);
             }
         }
     }

@@ -6,16 +6,17 @@
 // Same arithmetic as gemm_x6.hip's TN kernels, bit for bit: each split's columns scaled by
 // the power of two of their maximum over the split (from the producers' per-128-row-group
 // column maxima), split into RNE fp16 (hi, lo) pairs, and hi.lo + lo.hi + hi.hi accumulated
-// on v_mfma_f32_32x32x16_f16 over 16-row k-steps in row order.  What differs is the data
-// movement, built for one wave per SIMD:
-//   * 4 waves per block, 2 x 2 wave tiles of 128 x 64 (or 64 x 128) outputs: 24 MFMAs per
-//     16-row k-step and wave between LDS fragment reads, against 12 in the 8-wave kernel;
-//   * 32-row stages (two k-steps) per block barrier, against one k-step;
-//   * operands loaded straight to registers as dwordx4 / dwordx2 row pieces (a wave moves
-//     one 1 KB / 512 B row of the tile per instruction, 16 loads per thread and stage,
-//     against 24 scalar dword loads per thread per 32 rows), NS stages in flight;
-//   * each thread owns an 8-row strip of CA + CB columns, splits it and writes one 16-byte
-//     fragment chunk per column and plane (the image layout of gemm_x6.hip's XImg).
+// on v_mfma_f32_32x32x16_f16 over 16-row k-steps in row order.  What differs is the work
+// split inside a block: 8 waves, two per SIMD, in two roles (MI355X_MICROARCH.md "Two waves
+// per SIMD": a matrix wave beside a load wave on each SIMD):
+//   * waves 0-3 (MFMA): 2 x 2 wave tiles of 128 x 64 (or 64 x 128) outputs, accumulators in
+//     AGPRs, 24 MFMAs per 16-row k-step between LDS fragment reads, 48 per 32-row stage;
+//   * waves 4-7 (load + split): each thread owns an 8-row strip of CA + CB columns per
+//     stage, loaded straight to registers as dwordx4 / dwordx2 row pieces (one 1 KB / 512 B
+//     row of the tile per wave instruction) two stages ahead, split into fp16 pairs and
+//     written as one 16-byte fragment chunk per column and plane (gemm_x6.hip's XImg layout);
+// one block barrier per 32-row stage, so a SIMD's split VALU runs beside its MFMAs instead
+// of between them.
 // The 256-output layers run as two XCD-paired 256 x 128 column tiles per split (workgroups
 // w and w + 8 share an XCD, so the second read of each dy stage is an L2 hit); the layers with
 // a 64-wide second input segment (l4 over [h3 | enc_p], the colour layer over [f | enc_d],
@@ -26,9 +27,9 @@
 namespace nerf {
 namespace wg {
 
-constexpr int NTH = 256;   // 4 waves, one per SIMD
+constexpr int NTH = 512;   // 8 waves, two per SIMD: 4 MFMA waves + 4 load / split waves
 constexpr int KS = 32;     // rows per pipeline stage: two 16-row MFMA k-steps
-constexpr int NS = 3;      // register stages: loads issued two stages ahead of their split
+constexpr int NS = 2;      // register stages of a load wave: loads issued two stages ahead of their split
 
 template <int BO, int BK>
 struct Cfg {
@@ -43,7 +44,7 @@ struct Cfg {
     static constexpr int LOOP = 2 * BUF;               // double-buffered
     static constexpr int EPI = 4 * TileLds<TN>::BYTES;
     static constexpr int MAIN = LOOP > EPI ? LOOP : EPI;
-    static constexpr int BYTES = MAIN + (BO + BK) * 4;  // + the tile's column exponents
+    static constexpr int BYTES = MAIN + (BO + BK) * 4 + 4 * BO * 4;  // + column exponents, bias partials
     static_assert(TM >= 1 && TN >= 1 && CA >= 1 && CB >= 1 && CA <= 4 && CB <= 4, "tile");
 };
 
@@ -74,183 +75,198 @@ __device__ __forceinline__ void put_strip(char* d, int plane_bytes, const float 
     *reinterpret_cast<uint4*>(d + plane_bytes) = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
-// one block: output rows o0 .. o0 + BO (dy columns), column tile jt (x columns jt BK ..), split
-template <int BO, int BK>
+// one block: output rows o0 .. o0 + BO (dy columns), column tile jt (x columns jt BK ..), split;
+// BIAS: the load waves also sum the dy columns (the bias gradient; one column tile per split)
+template <int BO, int BK, bool BIAS>
 __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int jt, int split) {
     using C = Cfg<BO, BK>;
     constexpr int CA = C::CA, CB = C::CB, TM = C::TM, TN = C::TN;
     const int tid = threadIdx.x;
-    const int lane = tid & 63, l32 = lane & 31, hi = lane >> 5;
+    const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm0 = (wave >> 1) * C::WO, wn0 = (wave & 1) * C::WK;
     const int j0 = jt * BK;
     const size_t s0 = (size_t)split * p.rows_per_split;
     const int nst = p.rows_per_split / KS;
-    const bool do_bias = p.bslab != nullptr && jt == 0;
-
-    // column exponents: the tile's in LDS for the epilogue, this thread's own in registers
-    int* lea = reinterpret_cast<int*>(smem + C::MAIN);
+    int* lea = reinterpret_cast<int*>(smem + C::MAIN);   // the tile's column exponents (epilogue)
     int* leb = lea + BO;
+    float* lbias = reinterpret_cast<float*>(leb + BK);   // [4 load waves][BO] bias partials
     for (int e = tid; e < BO; e += NTH) lea[e] = row_exp(tn_colmax(p.cm_dy, p.ldcm_dy, s0, p.rows_per_split, o0 + e));
     for (int e = tid; e < BK; e += NTH) leb[e] = row_exp(tn_colmax(p.cm_x, p.ldcm_x, s0, p.rows_per_split, j0 + e));
-    int ea[CA], eb[CB];
-#pragma unroll
-    for (int c = 0; c < CA; ++c) ea[c] = row_exp(tn_colmax(p.cm_dy, p.ldcm_dy, s0, p.rows_per_split, o0 + CA * lane + c));
-#pragma unroll
-    for (int c = 0; c < CB; ++c) eb[c] = row_exp(tn_colmax(p.cm_x, p.ldcm_x, s0, p.rows_per_split, j0 + CB * lane + c));
 
-    // the split's rows as buffer resources: a lane's column offset in a VGPR, the row offset
-    // (stage, this wave's 8-row strip, row) wave-uniform in an SGPR
-    const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(p.dy + s0 * p.lddy + o0), (short)0, (p.rows_per_split * p.lddy - o0) * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(p.x + s0 * p.ldx + j0), (short)0, (p.rows_per_split * p.ldx - j0) * 4, 0x00020000);
-    const int va_off = 4 * CA * lane, vb_off = 4 * CB * lane;
-
-    float va[NS][8][CA], vb[NS][8][CB];
-    float bsum[CA];
+    if (wave >= 4) {
+        // ---- load / split waves: rows 8 lw .. 8 lw + 7 of every stage, CA + CB columns ----
+        const int lw = wave - 4;
+        int ea[CA], eb[CB];
 #pragma unroll
-    for (int c = 0; c < CA; ++c) bsum[c] = 0.f;
-
-    auto load = [&](auto uc, int t) {
-        constexpr int U = decltype(uc)::value;
-        t = t < nst ? t : nst - 1;   // the tail re-loads the last stage: uniform wait counts
-        const int r0 = KS * t + 8 * wave;
+        for (int c = 0; c < CA; ++c) ea[c] = row_exp(tn_colmax(p.cm_dy, p.ldcm_dy, s0, p.rows_per_split, o0 + CA * lane + c));
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            load_row<CA>(va[U][i], rdy, va_off, (r0 + i) * p.lddy * 4);
-            load_row<CB>(vb[U][i], rx, vb_off, (r0 + i) * p.ldx * 4);
-        }
-    };
-    // split stage U's strips into image buffer `buf` (this wave: k-step wave >> 1, k-half wave & 1)
-    auto put = [&](auto uc, char* buf) {
-        constexpr int U = decltype(uc)::value;
-        char* ks = buf + (wave >> 1) * C::KSTEP;
+        for (int c = 0; c < CB; ++c) eb[c] = row_exp(tn_colmax(p.cm_x, p.ldcm_x, s0, p.rows_per_split, j0 + CB * lane + c));
+        // the split's rows as buffer resources: the lane's column offset in a VGPR, the row
+        // offset (stage, strip, row) wave-uniform in an SGPR
+        const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(p.dy + s0 * p.lddy + o0), (short)0, (p.rows_per_split * p.lddy - o0) * 4, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(p.x + s0 * p.ldx + j0), (short)0, (p.rows_per_split * p.ldx - j0) * 4, 0x00020000);
+        const int va_off = 4 * CA * lane, vb_off = 4 * CB * lane;
+        float va[NS][8][CA], vb[NS][8][CB];
+        float bsum[CA];
 #pragma unroll
-        for (int c = 0; c < CA; ++c) {
-            float v[8];
+        for (int c = 0; c < CA; ++c) bsum[c] = 0.f;
+        auto load = [&](auto uc, int t) {
+            constexpr int U = decltype(uc)::value;
+            t = t < nst ? t : nst - 1;   // the tail re-loads the last stage: every iteration is alike
+            const int r0 = KS * t + 8 * lw;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = va[U][i][c];
-            put_strip(ks + (wave & 1) * C::AH + (CA * lane + c) * 16, C::AP, v, ea[c]);
-            if (do_bias) {
-                float s = 0.f;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) s += v[i];
-                bsum[c] += s;
+            for (int i = 0; i < 8; ++i) {
+                load_row<CA>(va[U][i], rdy, va_off, (r0 + i) * p.lddy * 4);
+                load_row<CB>(vb[U][i], rx, vb_off, (r0 + i) * p.ldx * 4);
             }
-        }
+        };
+        // stage in register set U -> image buffer `buf` (k-step lw >> 1, k-half lw & 1);
+        // `real` false: the tail's clamped re-split, left out of the bias sums
+        auto put = [&](auto uc, char* buf, bool real) {
+            constexpr int U = decltype(uc)::value;
+            char* ks = buf + (lw >> 1) * C::KSTEP;
+            // one column at a time (scheduling barriers): hoisting every column's scaling ahead
+            // of the conversions runs out of registers and reuses in-flight load destinations
 #pragma unroll
-        for (int c = 0; c < CB; ++c) {
-            float v[8];
+            for (int c = 0; c < CA; ++c) {
+                __builtin_amdgcn_sched_barrier(0);
+                float v[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = vb[U][i][c];
-            put_strip(ks + 2 * C::AP + (wave & 1) * C::BH + (CB * lane + c) * 16, C::BP, v, eb[c]);
-        }
-    };
-
-    f32x16 acc[TM][TN];
-    zero_acc(acc);
-    // one 16-row k-step from an image buffer: fragments, then 3 products per 32 x 32 tile
-    auto kstep = [&](const char* ks) {
-        uint4 a[TM][2], b[TN][2];
+                for (int i = 0; i < 8; ++i) v[i] = va[U][i][c];
+                put_strip(ks + (lw & 1) * C::AH + (CA * lane + c) * 16, C::AP, v, ea[c]);
+                if constexpr (BIAS) {
+                    float sm = 0.f;
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-                b[j][q] = *reinterpret_cast<const uint4*>(ks + 2 * C::AP + q * C::BP + hi * C::BH + (wn0 + 32 * j + l32) * 16);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-                a[i][q] = *reinterpret_cast<const uint4*>(ks + q * C::AP + hi * C::AH + (wm0 + 32 * i + l32) * 16);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                f32x16 c = acc[i][j];
-                c = mfma_f16(a[i][0], b[j][1], c);   // hi.lo
-                c = mfma_f16(a[i][1], b[j][0], c);   // lo.hi
-                c = mfma_f16(a[i][0], b[j][0], c);   // hi.hi
-                acc[i][j] = c;
+                    for (int i = 0; i < 8; ++i) sm += v[i];
+                    bsum[c] += real ? sm : 0.f;
+                }
             }
-    };
-
-    // prologue: stages 0 .. NS-1 in flight, stage 0 split into buffer 0
-    load(std::integral_constant<int, 0>{}, 0);
-    load(std::integral_constant<int, 1>{}, 1);
-    load(std::integral_constant<int, 2>{}, 2);
-    static_assert(NS == 3, "prologue issues NS stages");
-    put(std::integral_constant<int, 0>{}, smem);
-    __syncthreads();
-
-    // iteration s: MFMAs of stage s (buffer s & 1) beside the split of stage s + 1 into the
-    // other buffer and the loads of stage s + NS into the registers stage s used
-    auto iter = [&](int s, auto uc) {
-        constexpr int U = decltype(uc)::value;          // s % NS
-        const char* cur = smem + (s & 1) * C::BUF;
-        char* nxt = smem + ((s + 1) & 1) * C::BUF;
-        if (s + 1 < nst) put(std::integral_constant<int, (U + 1) % NS>{}, nxt);
-        load(std::integral_constant<int, U>{}, s + NS);
-        kstep(cur);
-        kstep(cur + C::KSTEP);
+#pragma unroll
+            for (int c = 0; c < CB; ++c) {
+                __builtin_amdgcn_sched_barrier(0);
+                float v[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] = vb[U][i][c];
+                put_strip(ks + 2 * C::AP + (lw & 1) * C::BH + (CB * lane + c) * 16, C::BP, v, eb[c]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        load(std::integral_constant<int, 0>{}, 0);
+        load(std::integral_constant<int, 1>{}, 1);
+        put(std::integral_constant<int, 0>{}, smem, true);
+        load(std::integral_constant<int, 0>{}, 2);
         __syncthreads();
-    };
-    for (int s0i = 0; s0i < nst; s0i += NS) {
-        iter(s0i, std::integral_constant<int, 0>{});
-        if (s0i + 1 < nst) iter(s0i + 1, std::integral_constant<int, 1>{});
-        if (s0i + 2 < nst) iter(s0i + 2, std::integral_constant<int, 2>{});
+        // iteration s: stage s + 1 (set (s + 1) & 1, loaded two iterations ago) into buffer
+        // (s + 1) & 1, then the loads of stage s + 3 into the set it freed
+        auto iter = [&](int s, auto uc) {
+            constexpr int U = decltype(uc)::value;   // (s + 1) & 1
+            put(uc, smem + ((s + 1) & 1) * C::BUF, s + 1 < nst);
+            load(uc, s + 3);
+            __syncthreads();
+        };
+        int s = 0;
+        for (; s + 2 <= nst; s += 2) {
+            iter(s, std::integral_constant<int, 1>{});
+            iter(s + 1, std::integral_constant<int, 0>{});
+        }
+        if (s < nst) iter(s, std::integral_constant<int, 1>{});
+        if constexpr (BIAS) {
+#pragma unroll
+            for (int c = 0; c < CA; ++c) lbias[lw * BO + CA * lane + c] = bsum[c];
+        }
+    } else {
+        // ---- MFMA waves: a 2 x 2 grid of WO x WK wave tiles ----
+        const int l32 = lane & 31, hi = lane >> 5;
+        const int wm0 = (wave >> 1) * C::WO, wn0 = (wave & 1) * C::WK;
+        f32x16 acc[TM][TN];
+        zero_acc(acc);
+        auto kstep = [&](const char* ks) {
+            uint4 a[TM][2], b[TN][2];
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    b[j][q] = *reinterpret_cast<const uint4*>(ks + 2 * C::AP + q * C::BP + hi * C::BH + (wn0 + 32 * j + l32) * 16);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    a[i][q] = *reinterpret_cast<const uint4*>(ks + q * C::AP + hi * C::AH + (wm0 + 32 * i + l32) * 16);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    f32x16 c = acc[i][j];
+                    c = mfma_f16(a[i][0], b[j][1], c);   // hi.lo
+                    c = mfma_f16(a[i][1], b[j][0], c);   // lo.hi
+                    c = mfma_f16(a[i][0], b[j][0], c);   // hi.hi
+                    acc[i][j] = c;
+                }
+        };
+        __syncthreads();
+        for (int s = 0; s < nst; ++s) {
+            const char* cur = smem + (s & 1) * C::BUF;
+            kstep(cur);
+            kstep(cur + C::KSTEP);
+            __syncthreads();
+        }
+        tn_store_lds<TM, TN, true>(p, acc, smem, split, o0, j0, wm0, wn0, lea, leb);
     }
-
-    tn_store_lds<TM, TN, true>(p, acc, smem, split, o0, j0, wm0, wn0, lea, leb);
-    if (do_bias) {
-        // per-wave strip sums -> column sums, added in wave (row-strip) order: deterministic
-        __syncthreads();
-        float* lb = reinterpret_cast<float*>(smem);
-#pragma unroll
-        for (int c = 0; c < CA; ++c) lb[wave * BO + CA * lane + c] = bsum[c];
+    if constexpr (BIAS) {
+        // the load waves' strip sums -> column sums, added in strip order: deterministic
         __syncthreads();
         for (int c = tid; c < BO; c += NTH)
-            p.bslab[(size_t)split * p.nout + o0 + c] = ((lb[c] + lb[BO + c]) + lb[2 * BO + c]) + lb[3 * BO + c];
+            p.bslab[(size_t)split * p.nout + o0 + c] =
+                ((lbias[c] + lbias[BO + c]) + lbias[2 * BO + c]) + lbias[3 * BO + c];
     }
+}
+
+// the block of column tile jt, with the bias sums where the layer wants them (column tile 0)
+template <int BO, int BK>
+__device__ __forceinline__ void block_any(const TNArgs& p, char* smem, int o0, int jt, int split) {
+    if (jt == 0 && p.bslab != nullptr) block<BO, BK, true>(p, smem, o0, jt, split);
+    else block<BO, BK, false>(p, smem, o0, jt, split);
 }
 
 }  // namespace wg
 
 // a 256 x 256 layer: two XCD-paired 256 x 128 column tiles per split (splits % 8 == 0)
-__global__ __launch_bounds__(wg::NTH, 1) void k_wgrad_pair(TNArgs p) {
+__global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_pair(TNArgs p) {
     __shared__ __attribute__((aligned(16))) char smem[wg::Cfg<256, 128>::BYTES];
     const int w = blockIdx.x, slot = w >> 3;
-    wg::block<256, 128>(p, smem, 0, slot & 1, (slot >> 1) * 8 + (w & 7));
+    wg::block_any<256, 128>(p, smem, 0, slot & 1, (slot >> 1) * 8 + (w & 7));
 }
 
 // one BO x BK tile per split (l0: 256 outputs over the 64 encoding columns)
 template <int BO, int BK>
-__global__ __launch_bounds__(wg::NTH, 1) void k_wgrad_one(TNArgs p) {
+__global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_one(TNArgs p) {
     __shared__ __attribute__((aligned(16))) char smem[wg::Cfg<BO, BK>::BYTES];
-    wg::block<BO, BK>(p, smem, 0, 0, blockIdx.x);
+    wg::block_any<BO, BK>(p, smem, 0, 0, blockIdx.x);
 }
 
 // two input segments, all tiles of a split on one XCD in consecutive dispatch slots: l4 (256
 // outputs: two 256 x 128 tiles over h3 + a 256 x 64 tile over enc_p) and the colour layer (128
 // outputs: a 128 x 256 tile over f + a 128 x 64 tile over enc_d)
 template <int BO, int BK, int CT, int BK2>
-__global__ __launch_bounds__(wg::NTH, 1) void k_wgrad_seg(TNArgs pm, TNArgs ps) {
+__global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_seg(TNArgs pm, TNArgs ps) {
     constexpr int B1 = wg::Cfg<BO, BK>::BYTES, B2 = wg::Cfg<BO, BK2>::BYTES;
     __shared__ __attribute__((aligned(16))) char smem[B1 > B2 ? B1 : B2];
     const int w = blockIdx.x, slot = w >> 3;
     const int jt = slot % (CT + 1), split = (slot / (CT + 1)) * 8 + (w & 7);
-    if (jt < CT) wg::block<BO, BK>(pm, smem, 0, jt, split);
-    else wg::block<BO, BK2>(ps, smem, 0, 0, split);
+    if (jt < CT) wg::block_any<BO, BK>(pm, smem, 0, jt, split);
+    else wg::block_any<BO, BK2>(ps, smem, 0, 0, split);
 }
 
 // which shapes the 4-wave kernels cover (the rest stay on gemm_x6.hip's TN kernels)
 bool wgrad_supported(int nout, int kin, int splits, int rows_per_split) {
-    if (rows_per_split % wg::KS != 0 || rows_per_split < wg::NS * wg::KS) return false;
+    if (rows_per_split % wg::KS != 0 || rows_per_split < 3 * wg::KS) return false;
     return (nout == 256 && kin == 256 && splits % 8 == 0) || (nout == 256 && kin == 64) ||
            (nout == 128 && (kin == 256 || kin == 64));
 }
 bool wgrad_seg_supported(int nout, int k1, int k2, int splits, int rows_per_split) {
-    return rows_per_split % wg::KS == 0 && rows_per_split >= wg::NS * wg::KS && k1 == 256 && k2 == 64 &&
+    return rows_per_split % wg::KS == 0 && rows_per_split >= 3 * wg::KS && k1 == 256 && k2 == 64 &&
            (nout == 256 || nout == 128) && splits % 8 == 0;
 }
 

@@ -40,6 +40,22 @@ KINDS = {
         "dw_narrow", 4 * M * (128 + D + 64) + 4 * 128 * (D + 64), "dy 67.1 MB + f 134.2 MB + enc_d 33.6 MB + dW "
         "0.16 MB (colour layer: the 128 x 256 tile over f and the 128 x 64 tile over enc_d, dy fetched once per XCD); "
         "measured writes are the 256 split-K slabs (41.9 MB)"),
+    "nerf::k_wgrad_pair": (
+        "dw", 4 * M * D * 2 + 4 * D * D, "dy 134.2 MB + x 134.2 MB + dW 0.26 MB; the two XCD-paired 256 x 128 "
+        "column tiles of a split read dy from HBM once; measured writes are the 128 split-K slabs (33.6 MB)"),
+    "k_wgrad_seg<256, 128, 2, 64>": (
+        "dw", 4 * M * (D + D + 64) + 4 * D * (D + 64), "dy 134.2 MB + h3 134.2 MB + enc_p 33.6 MB + dW 0.33 MB "
+        "(l4); measured writes are the 128 split-K slabs (41.9 MB)"),
+    "k_wgrad_seg<128, 256, 1, 64>": (
+        "dw_narrow", 4 * M * (128 + D + 64) + 4 * 128 * (D + 64), "dyr 67.1 MB + f 134.2 MB + enc_d 33.6 MB + dW "
+        "0.16 MB (colour layer); measured writes are the 256 split-K slabs (41.9 MB)"),
+    "k_wgrad_one<256, 64>": (
+        "dw_narrow", 4 * M * (D + 64) + 4 * D * 64, "dy 134.2 MB + enc_p 33.6 MB + dW 0.07 MB (l0); measured writes "
+        "are the 256 split-K slabs (16.8 MB)"),
+    "nerf::k_mlp_chain_bwd": (
+        "chain_bwd", M * (16 + 16 + 8 * 32) + 4 * M * 128 + 4 * M * D * 9 + 4 * M * 10 + 4 * (M // 128) * (128 + 9 * D),
+        "reads graw4 2.1 MB + the ReLU words of ten layers 37.7 MB (weights stream from L2); writes dyr 67.1 MB + "
+        "the nine 256-wide input gradients 1208 MB + row maxima 5.2 MB + column maxima 9.4 MB"),
     "k_gemm_tn_x6<256, 256, 2, 2, true, 1>": (
         "dw", 4 * M * D * 2 + 4 * D * D, "dy 134.2 MB + x 134.2 MB + dW 0.26 MB; measured writes are the 256 "
         "split-K slabs (67 MB)"),
@@ -78,7 +94,7 @@ def main():
         out.append(e)
     print(json.dumps({"source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / --pmc WRITE_SIZE / SQ counters "
                                 "(separate passes) of `bench.py --steps 3 --warmup 2 --no-alt --no-cpu-baseline`, "
-                                "--kernel-include-regex 'k_gemm_(nt|tn)_x6|k_mlp_chain_train2'; FETCH_SIZE x2 (gfx950 correction)",
+                                "--kernel-include-regex 'k_gemm_(nt|tn)_x6|k_wgrad|k_mlp_chain'; FETCH_SIZE x2 (gfx950 correction)",
                       "launches": out}, indent=1))
 
 
