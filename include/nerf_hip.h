@@ -316,7 +316,7 @@ typedef struct nerf_chain_bwd {
     int wt_img_rows[9];
     const uint32_t* in_mask[9];     /* ReLU words of layer i's input [n_pad][ld >= 8] (i = 0 unused) */
     int ld_in_mask[9];
-    float* dy[10];                  /* D_0 .. D_9 */
+    float* dy[10];                  /* D_0 .. D_9 (lddy 128 for D_0, 256 for the others) */
     int lddy[10];
     float* dy_cmax[10];
     float* dy_rmax[10];

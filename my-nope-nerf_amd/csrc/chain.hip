@@ -950,6 +950,18 @@ __device__ __forceinline__ float rebuilt(const uint4& ah, const uint4& al, int k
     }
     return v;
 }
+typedef unsigned cu32x4 __attribute__((ext_vector_type(4)));
+// a float4 into a row-major [128 rows][W] f32 tile of one block through a buffer resource: the
+// lane's row / column byte offset in one VGPR, the block base in SGPRs, the k-step's column
+// offset an immediate -- no 64-bit per-lane address arithmetic per store
+template <int W>
+__device__ __forceinline__ void tile_store4(float* block_base, int voff, int imm_bytes, float a, float b, float c,
+                                            float d) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc((void*)block_base, (short)0, 128 * W * 4, 0x00020000);
+    const cu32x4 v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), __float_as_uint(d)};
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, imm_bytes, 0);
+}
 // max of |v| over the lane's quad as float bits (non-negative floats order like their bits):
 // v_and + two v_max_u32_dpp, no old-value moves or NaN canonicalisation
 __device__ __forceinline__ uint32_t quad_absmax_bits(float v) {
@@ -972,8 +984,7 @@ __device__ __forceinline__ void save_piece(const ChainFwdArgs& p, State& st, con
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = rebuilt(ah, al, k0 + k, st.er);
         if constexpr (!(kTrAblate & 1))
-            *reinterpret_cast<float4*>(P.out + row * P.ldo + 32 * u + 8 * st.g + k0) =
-                make_float4(v[0], v[1], v[2], v[3]);
+            tile_store4<256>(P.out + st.m0 * 256, (rl * 256 + 8 * st.g) * 4, (32 * u + k0) * 4, v[0], v[1], v[2], v[3]);
         if constexpr (kSaveFused && !(kTrAblate & 2)) {   // column maxima of these 4 features, from v
             uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + Y::O_CMX) + ((l - 1) & 1) * 256 + 32 * u + 8 * st.g + k0;
             uint32_t c[4];
@@ -1544,11 +1555,11 @@ __device__ __forceinline__ void save_piece(const nerf_chain_bwd& p, State& st, c
         constexpr int k0 = 4 * (j - 1);
         int rl = st.rl;
         asm volatile("" : "+v"(rl));
-        const size_t row = st.m0 + rl;
         float v[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = f2::rebuilt(ah, al, k0 + k, st.er);
-        *reinterpret_cast<float4*>(p.dy[i] + row * p.lddy[i] + 32 * u + 8 * st.g + k0) = make_float4(v[0], v[1], v[2], v[3]);
+        constexpr int W = i == 0 ? 128 : 256;   // D_0 = dyr is 128 wide
+        f2::tile_store4<W>(p.dy[i] + st.m0 * W, (rl * W + 8 * st.g) * 4, (32 * u + k0) * 4, v[0], v[1], v[2], v[3]);
         uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + O_CMX) + (i & 1) * 256 + 32 * u + 8 * st.g + k0;
         uint32_t c[4];
 #pragma unroll
@@ -1821,8 +1832,10 @@ extern "C" int nerf_mlp_chain_train(const float* enc_p, const float* enc_d, cons
                    "%s: layer %d: image / bias not 16-byte aligned or image rows %d < %d", __func__, l, L.img_rows,
                    L_OUT[l]);
         // every output is mandatory: the k-steps' vmcnt waits count these stores at compile time
-        NERF_CHECK(L.out && L.ldo >= L_OUT[l] && L.ldo % 4 == 0 && (((uintptr_t)L.out) & 15u) == 0,
-                   "%s: layer %d: the training chain saves every layer output (ldo %d)", __func__, l, L.ldo);
+        NERF_CHECK(L.out && L.ldo >= L_OUT[l] && L.ldo % 4 == 0 && (((uintptr_t)L.out) & 15u) == 0 &&
+                       (l == CNL - 1 || L.ldo == 256),
+                   "%s: layer %d: the training chain saves every layer output (ldo %d; 256 for l0..lf)", __func__, l,
+                   L.ldo);
         NERF_CHECK(l == 8 || (L.mask && L.ldmask >= L_OUT[l] / 32 && L.ldmask % 2 == 0 &&
                               (((uintptr_t)L.mask) & 7u) == 0),
                    "%s: layer %d: the ReLU words are mandatory (ldmask %d, even, 8-byte aligned)", __func__, l, L.ldmask);
@@ -1910,9 +1923,8 @@ extern "C" int nerf_mlp_chain_bwd(const nerf_chain_bwd* a, void* stream) {
     }
     for (int i = 0; i < 10; ++i) {
         const int w = i == 0 ? 128 : 256;
-        NERF_CHECK(p.dy[i] && p.lddy[i] >= w && p.lddy[i] % 4 == 0 && (((uintptr_t)p.dy[i]) & 15u) == 0 &&
-                       p.dy_cmax[i] && p.dy_rmax[i],
-                   "%s: D_%d: output, column maxima and row maxima are mandatory (ld >= %d, 16-byte aligned)", __func__,
+        NERF_CHECK(p.dy[i] && p.lddy[i] == w && (((uintptr_t)p.dy[i]) & 15u) == 0 && p.dy_cmax[i] && p.dy_rmax[i],
+                   "%s: D_%d: output, column maxima and row maxima are mandatory (ld == %d, 16-byte aligned)", __func__,
                    i, w);
     }
     ChainBwdArgs args{p};

@@ -160,8 +160,7 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
         __syncthreads();
         // iteration s: stage s + 1 (set (s + 1) & 1, loaded two iterations ago) into buffer
         // (s + 1) & 1, then the loads of stage s + 3 into the set it freed
-        auto iter = [&](int s, auto uc) {
-            constexpr int U = decltype(uc)::value;   // (s + 1) & 1
+        auto iter = [&](int s, auto uc) {   // uc: the register set of stage s + 1, (s + 1) & 1
             put(uc, smem + ((s + 1) & 1) * C::BUF, s + 1 < nst);
             load(uc, s + 3);
             __syncthreads();

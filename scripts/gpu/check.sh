@@ -32,6 +32,23 @@ for step in "$@"; do
     full)
       timeout -k 10 300 python -u scripts/bench_full.py --steps 40 --warmup 5 > $OUT/bench_full.json 2> $OUT/bench_full.err || exit $?
       tail -1 $OUT/bench_full.json ;;
+    pmc:*)
+      # one PMC pass (its own run, --kernel-trace only): pmc:<set> with the sets below
+      C1="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS"
+      C2="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT"
+      BENCH="$R/bench.py --steps 3 --warmup 2 --no-alt --no-cpu-baseline --no-cfg3 --exec eager"
+      STEPRX='k_gemm_(nt|tn)_x6|k_wgrad|k_mlp_chain'
+      case "${step#pmc:}" in
+        wg1) RX=k_wgrad_pair; CT="$C1"; CMD="$R/scripts/wgrad_bench.py --loop 20" ;;
+        wg2) RX=k_wgrad_pair; CT="$C2"; CMD="$R/scripts/wgrad_bench.py --loop 20" ;;
+        ch1) RX=k_mlp_chain; CT="$C1"; CMD="$BENCH" ;;
+        ch2) RX=k_mlp_chain; CT="$C2"; CMD="$BENCH" ;;
+        fetch) RX="$STEPRX"; CT="FETCH_SIZE"; CMD="$BENCH" ;;
+        write) RX="$STEPRX"; CT="WRITE_SIZE"; CMD="$BENCH" ;;
+        *) echo "unknown pmc set $step"; exit 2 ;;
+      esac
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv --kernel-include-regex "$RX" --pmc $CT -d $OUT/pmc_${step#pmc:} -o run -- python3 $CMD > $OUT/pmc_${step#pmc:}.log 2>&1) || exit $?
+      echo "pmc ok: ${step#pmc:}" ;;
     py:*)
       args=${step#py:}
       (cd $R/scripts && timeout -k 10 300 python -u $args > $OUT/py_$(echo $args | tr ' /' '__' | cut -c1-60).txt 2>&1) || exit $?
