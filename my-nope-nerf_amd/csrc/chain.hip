@@ -755,34 +755,7 @@ constexpr int dma_count(int tt) {
     return tt >= CT ? 0 : (L_OUT[layer_of(tt)] == 256 ? 2 : 1) + (kbase(layer_of(tt)) == tt ? 1 : 0);
 }
 
-#ifndef NERF_TRAIN_ABLATE
-#define NERF_TRAIN_ABLATE 0   // diagnostic builds only: 1 no activation stores, 2 no ReLU words / column maxima
-#endif
-constexpr int kTrAblate = NERF_TRAIN_ABLATE;
-#ifndef NERF_COLMAX_ROW
-#define NERF_COLMAX_ROW 0     // A/B: column maxima reduced over the whole 16-lane row before the LDS atomic
-#endif
-constexpr bool kColmaxRow = NERF_COLMAX_ROW != 0;
-#ifndef NERF_SAVE_FUSED
-#define NERF_SAVE_FUSED 1     // A/B: 0 = the column maxima rebuilt per feature at MFMA tiles 3-10 (slower, r03l)
-#endif
-constexpr bool kSaveFused = NERF_SAVE_FUSED != 0;
-#ifndef NERF_SAVE_DEPHASE
-#define NERF_SAVE_DEPHASE 0   // A/B: 1 = waves 4-7 run their save pieces half a k-step later (slower: the per-tile
-                              // wave-dependent branches break the MFMA issue, chain_phase_stamps.txt)
-#endif
-constexpr bool kSaveDephase = NERF_SAVE_DEPHASE != 0;
-#ifndef NERF_SPLIT_JIT
-#define NERF_SPLIT_JIT 1      // A/B: 0 = the whole next-layer A operand split in the epilogue
-#endif
-constexpr bool kSplitJit = NERF_SPLIT_JIT != 0;
-#ifndef NERF_SPLIT_DEPHASE
-#define NERF_SPLIT_DEPHASE 0  // 1 spills at two waves per SIMD (the wave-dependent placement merges live ranges)
-#endif
-constexpr bool kSplitDephase = NERF_SPLIT_DEPHASE != 0;
-#ifndef NERF_SPLIT_TILE
-#define NERF_SPLIT_TILE 8     // the MFMA tile (of 16) after which a k-step splits the next k-step's fragment
-#endif
+constexpr int kSplitTile = 8;   // the MFMA tile (of 16) after which a k-step splits the next k-step's fragment
 
 // the counted waits.  Every 32-k step k (global over the chain) waits for the DMAs issued D
 // steps earlier; vmcnt counts loads, stores and LDS-DMA together in issue order, so the count
@@ -802,8 +775,7 @@ template <bool TR>
 constexpr int st_ops_k(int k) {
     const int l = layer_of_k(k), u = k - kfirst(l);
     if (!TR || l == 0) return 0;
-    return (u < 8 && !(kTrAblate & 1) ? 2 : 0) + (u == 7 && l - 1 != 8 && !(kTrAblate & 2) ? 1 : 0) +
-           (u == 0 && l >= 2 && !(kTrAblate & 2) ? 1 : 0);
+    return (u < 8 ? 2 : 0) + (u == 7 && l - 1 != 8 ? 1 : 0) + (u == 0 && l >= 2 ? 1 : 0);
 }
 template <bool TR>
 constexpr int wait_n(int k) {
@@ -983,9 +955,8 @@ __device__ __forceinline__ void save_piece(const ChainFwdArgs& p, State& st, con
         float v[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = rebuilt(ah, al, k0 + k, st.er);
-        if constexpr (!(kTrAblate & 1))
-            tile_store4<256>(P.out + st.m0 * 256, (rl * 256 + 8 * st.g) * 4, (32 * u + k0) * 4, v[0], v[1], v[2], v[3]);
-        if constexpr (kSaveFused && !(kTrAblate & 2)) {   // column maxima of these 4 features, from v
+        tile_store4<256>(P.out + st.m0 * 256, (rl * 256 + 8 * st.g) * 4, (32 * u + k0) * 4, v[0], v[1], v[2], v[3]);
+        {   // column maxima of these 4 features, from v
             uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + Y::O_CMX) + ((l - 1) & 1) * 256 + 32 * u + 8 * st.g + k0;
             uint32_t c[4];
 #pragma unroll
@@ -995,7 +966,7 @@ __device__ __forceinline__ void save_piece(const ChainFwdArgs& p, State& st, con
                 for (int k = 0; k < 4; ++k) atomicMax(cm + k, c[k]);
             }
         }
-        if constexpr (!(kTrAblate & 2) && l - 1 != 8) {   // lf has no ReLU
+        if constexpr (l - 1 != 8) {   // lf has no ReLU
 #pragma unroll
             for (int k = 0; k < 4; ++k) bits |= (v[k] > 0.f ? 1u : 0u) << (k0 + k);
             if constexpr (j == 2) {
@@ -1004,24 +975,6 @@ __device__ __forceinline__ void save_piece(const ChainFwdArgs& p, State& st, con
                 else st.mk0 = st.g == (u >> 1) ? w : st.mk0;
                 if constexpr (u == 7)
                     *reinterpret_cast<uint2*>(P.mask + row * P.ldmask + 2 * st.g) = make_uint2(st.mk0, st.mk1);
-            }
-        }
-    }
-    if constexpr (!kSaveFused && !(kTrAblate & 2) && j >= 3) {   // column maxima: one feature per tile (two for 8 tiles)
-        constexpr int per = ntj >= 11 ? 1 : 2;
-        constexpr int k0 = (j - 3) * per;
-        uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + Y::O_CMX) + ((l - 1) & 1) * 256 + 32 * u + 8 * st.g;
-#pragma unroll
-        for (int k = k0; k < k0 + per && k < 8; ++k) {
-            float c = fabsf(rebuilt(ah, al, k, st.er));
-            c = fmaxf(c, dpp_f<0xB1>(0.f, c));
-            c = fmaxf(c, dpp_f<0x4E>(0.f, c));
-            if constexpr (kColmaxRow) {       // the whole 16-lane row, one atomic per row
-                c = fmaxf(c, dpp_f<0x141>(0.f, c));
-                c = fmaxf(c, dpp_f<0x140>(0.f, c));
-                if (st.n == 0) atomicMax(cm + k, __float_as_uint(c));
-            } else {
-                if ((st.n & 3) == 0) atomicMax(cm + k, __float_as_uint(c));
             }
         }
     }
@@ -1059,38 +1012,39 @@ __device__ __forceinline__ void split_b(State& st, const SplitTmp& q) {
 // sharing a SIMD (w, w + 4) take them half a step apart
 template <int ntj, bool second>
 constexpr int split_tile(int half) {
-    return ((second ? ntj / 2 : 0) + (ntj >= 16 ? NERF_SPLIT_TILE : NERF_SPLIT_TILE / 2) + half) % ntj;
+    return ((second ? ntj / 2 : 0) + (ntj >= 16 ? kSplitTile : kSplitTile / 2) + half) % ntj;
 }
 template <int l, int u, int j, int ntj, bool second>
 __device__ __forceinline__ void split_piece(State& st, SplitTmp& q) {
-    if constexpr (kSplitJit && l > 0 && u + 1 < 8) {
+    if constexpr (l > 0 && u + 1 < 8) {
         if constexpr (j == split_tile<ntj, second>(0)) split_a<u + 1>(st, q);
         if constexpr (j == split_tile<ntj, second>(1)) split_b<u + 1>(st, q);
     }
 }
 
+// weight fragments are read PF tiles ahead of their MFMAs (a ring of PF + 1 fragment pairs):
+// one tile gives a read the three MFMAs of the tile before it (~48 cycles x 2 waves) to land,
+// less than the LDS latency under eight waves' traffic
+template <bool TR>
+constexpr int pf_tiles() { return TR ? 1 : 3; }
+
 // tile j of a k-step (compile-time j, so the save pieces are placed between MFMA groups)
 template <int l, int u, bool TR, int j, int ntj, int nact>
 __device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, const uint4& ah, const uint4& al,
-                                            const char* base, uint4 (&wh)[2], uint4 (&wl)[2], uint32_t& bits,
-                                            SplitTmp& q) {
+                                            const char* base, uint4 (&wh)[pf_tiles<TR>() + 1],
+                                            uint4 (&wl)[pf_tiles<TR>() + 1], uint32_t& bits, SplitTmp& q) {
+    constexpr int PF = pf_tiles<TR>(), R = PF + 1;
     if constexpr (j < ntj) {
-        if constexpr (j + 1 < ntj) {
-            wh[(j + 1) & 1] = *reinterpret_cast<const uint4*>(base + 256 * (j + 1));
-            wl[(j + 1) & 1] = *reinterpret_cast<const uint4*>(base + 256 * (j + 1) + SPLANE);
+        if constexpr (j + PF < ntj) {
+            wh[(j + PF) % R] = *reinterpret_cast<const uint4*>(base + 256 * (j + PF));
+            wl[(j + PF) % R] = *reinterpret_cast<const uint4*>(base + 256 * (j + PF) + SPLANE);
         }
         __builtin_amdgcn_sched_barrier(0);
-        st.acc[j] = mfma16(wh[j & 1], al, st.acc[j]);   // hi . lo
-        st.acc[j] = mfma16(wl[j & 1], ah, st.acc[j]);   // lo . hi
-        st.acc[j] = mfma16(wh[j & 1], ah, st.acc[j]);   // hi . hi
-        if constexpr (TR && u < nact) {
-            // waves w and w + 4 share a SIMD: the second half runs its pieces half a step later,
-            // so one wave's VALU piece meets the other wave's MFMAs, not its VALU piece
-            if (!kSaveDephase || st.wave < 4) save_piece<l, u, j, ntj>(p, st, ah, al, bits);
-            else save_piece<l, u, (j + ntj / 2) % ntj, ntj>(p, st, ah, al, bits);
-        }
-        if (!kSplitDephase || st.wave < 4) split_piece<l, u, j, ntj, false>(st, q);
-        else split_piece<l, u, j, ntj, true>(st, q);
+        st.acc[j] = mfma16(wh[j % R], al, st.acc[j]);   // hi . lo
+        st.acc[j] = mfma16(wl[j % R], ah, st.acc[j]);   // lo . hi
+        st.acc[j] = mfma16(wh[j % R], ah, st.acc[j]);   // hi . hi
+        if constexpr (TR && u < nact) save_piece<l, u, j, ntj>(p, st, ah, al, bits);
+        split_piece<l, u, j, ntj, false>(st, q);
         __builtin_amdgcn_sched_barrier(0);
         mstep_tiles<l, u, TR, j + 1, ntj, nact>(p, st, ah, al, base, wh, wl, bits, q);
     }
@@ -1119,7 +1073,7 @@ __device__ __forceinline__ void kstep(const ChainFwdArgs& p, State& st) {
         if (st.tid < L_OUT[l])   // as the scale 2^-e of the weight row (exact)
             reinterpret_cast<float*>(st.lds + Y::O_EXP)[(l & 1) * 256 + st.tid] = __builtin_amdgcn_ldexpf(
                 1.f, -*reinterpret_cast<const int*>(st.lds + Y::O_LEB + (l & 1) * 4096 + st.tid * 16));
-        if constexpr (TR && l >= 2 && !(kTrAblate & 2)) {
+        if constexpr (TR && l >= 2) {
             // layer l - 2's column maxima over the block's 128 rows (its 128-row group), complete
             // since layer l - 1's last step: wave w stores features 32 w .. + 31 and clears them
             if (st.lane < 32) {
@@ -1135,11 +1089,13 @@ __device__ __forceinline__ void kstep(const ChainFwdArgs& p, State& st) {
     const char* s0 = st.lds + Y::O_RING + (TT % Y::NSLOT) * SBYTES;
     const char* s1 = st.lds + Y::O_RING + ((TT + 1) % Y::NSLOT) * SBYTES;
     const char* base = ((st.g >> 1) ? s1 : s0) + (st.g & 1) * SHALF + st.n * 16;
-    // weight fragments one tile ahead of their MFMAs (the next tile's reads have the three
-    // MFMAs of this one, ~48 cycles x 2 waves, to land)
-    uint4 wh[2], wl[2];
-    wh[0] = *reinterpret_cast<const uint4*>(base);
-    wl[0] = *reinterpret_cast<const uint4*>(base + SPLANE);
+    constexpr int PF = pf_tiles<TR>();
+    uint4 wh[PF + 1], wl[PF + 1];
+#pragma unroll
+    for (int t = 0; t < PF; ++t) {
+        wh[t] = *reinterpret_cast<const uint4*>(base + 256 * t);
+        wl[t] = *reinterpret_cast<const uint4*>(base + 256 * t + SPLANE);
+    }
     uint32_t bits = 0;
     SplitTmp q;
     mstep_tiles<l, u, TR, 0, ntj, nact>(p, st, ah, al, base, wh, wl, bits, q);
@@ -1223,7 +1179,7 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
             hs2 += x[0] * w2.x + x[1] * w2.y + x[2] * w2.z + x[3] * w2.w;
         }
     }
-    if constexpr (last_tr && !(kTrAblate & 2)) {
+    if constexpr (last_tr) {
         const nerf_chain_layer& L = p.L[l];
         if (2 * st.g < L_OUT[l] / 32)
             *reinterpret_cast<uint2*>(L.mask + (st.m0 + st.rl) * L.ldmask + 2 * st.g) = make_uint2(st.mk0, st.mk1);
@@ -1269,15 +1225,6 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
         SplitTmp q;
         split_a<0>(st, q);
         split_b<0>(st, q);
-        if constexpr (!kSplitJit) {
-            split_a<1>(st, q); split_b<1>(st, q);
-            split_a<2>(st, q); split_b<2>(st, q);
-            split_a<3>(st, q); split_b<3>(st, q);
-            split_a<4>(st, q); split_b<4>(st, q);
-            split_a<5>(st, q); split_b<5>(st, q);
-            split_a<6>(st, q); split_b<6>(st, q);
-            split_a<7>(st, q); split_b<7>(st, q);
-        }
         if constexpr (l == 3) {   // training: the encodings in HBM
             const float* er_row = TR ? p.enc_p + (st.m0 + st.rl) * 64
                                      : reinterpret_cast<const float*>(st.lds + Y::O_ENC) + st.rl * 64;
@@ -1427,7 +1374,7 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_train2(ChainFwdArgs p) {
     const size_t m0 = (size_t)blockIdx.x * CROWS;
     if (tid < CROWS)
         *reinterpret_cast<float4*>(p.raw4 + (m0 + tid) * 4) = *reinterpret_cast<const float4*>(st.fx + FX_RAW + 4 * tid);
-    else if (tid < CROWS + 256 && !(kTrAblate & 2))
+    else if (tid < CROWS + 256)
         p.L[8].cmax[(m0 / CROWS) * L_OUT[8] + tid - CROWS] =
             __uint_as_float(reinterpret_cast<const uint32_t*>(smem + Y::O_CMX)[(8 & 1) * 256 + tid - CROWS]);
 }
@@ -1571,18 +1518,21 @@ __device__ __forceinline__ void save_piece(const nerf_chain_bwd& p, State& st, c
     }
 }
 
+constexpr int PF = 3;   // weight fragments read PF tiles ahead of their MFMAs (f2::pf_tiles)
+
 template <int i, int u, int j>
 __device__ __forceinline__ void tiles(const nerf_chain_bwd& p, State& st, const uint4& ah, const uint4& al,
-                                      const char* base, uint4 (&wh)[2], uint4 (&wl)[2], f2::SplitTmp& q) {
+                                      const char* base, uint4 (&wh)[PF + 1], uint4 (&wl)[PF + 1], f2::SplitTmp& q) {
+    constexpr int R = PF + 1;
     if constexpr (j < 16) {
-        if constexpr (j + 1 < 16) {
-            wh[(j + 1) & 1] = *reinterpret_cast<const uint4*>(base + 256 * (j + 1));
-            wl[(j + 1) & 1] = *reinterpret_cast<const uint4*>(base + 256 * (j + 1) + SPLANE);
+        if constexpr (j + PF < 16) {
+            wh[(j + PF) % R] = *reinterpret_cast<const uint4*>(base + 256 * (j + PF));
+            wl[(j + PF) % R] = *reinterpret_cast<const uint4*>(base + 256 * (j + PF) + SPLANE);
         }
         __builtin_amdgcn_sched_barrier(0);
-        st.acc[j] = f2::mfma16(wh[j & 1], al, st.acc[j]);   // hi . lo
-        st.acc[j] = f2::mfma16(wl[j & 1], ah, st.acc[j]);   // lo . hi
-        st.acc[j] = f2::mfma16(wh[j & 1], ah, st.acc[j]);   // hi . hi
+        st.acc[j] = f2::mfma16(wh[j % R], al, st.acc[j]);   // hi . lo
+        st.acc[j] = f2::mfma16(wl[j % R], ah, st.acc[j]);   // lo . hi
+        st.acc[j] = f2::mfma16(wh[j % R], ah, st.acc[j]);   // hi . hi
         save_piece<i, u, j>(p, st, ah, al);
         // the next k-step's A fragment from the previous epilogue's f32 tiles (layer 0's are
         // all split in the prologue)
@@ -1627,9 +1577,12 @@ __device__ __forceinline__ void kstep(const nerf_chain_bwd& p, State& st) {
     const char* s0 = st.lds + O_RING + (TT % NSLOT) * SBYTES;
     const char* s1 = st.lds + O_RING + ((TT + 1) % NSLOT) * SBYTES;
     const char* base = ((st.g >> 1) ? s1 : s0) + (st.g & 1) * SHALF + st.n * 16;
-    uint4 wh[2], wl[2];
-    wh[0] = *reinterpret_cast<const uint4*>(base);
-    wl[0] = *reinterpret_cast<const uint4*>(base + SPLANE);
+    uint4 wh[PF + 1], wl[PF + 1];
+#pragma unroll
+    for (int t = 0; t < PF; ++t) {
+        wh[t] = *reinterpret_cast<const uint4*>(base + 256 * t);
+        wl[t] = *reinterpret_cast<const uint4*>(base + 256 * t + SPLANE);
+    }
     f2::SplitTmp q;
     tiles<i, u, 0>(p, st, ah, al, base, wh, wl, q);
 }
@@ -1888,12 +1841,7 @@ extern "C" int nerf_render_eval_fused(const float* pts_o, const float* pts_d, co
     a.wd = wd; a.bd = bd; a.wc = wc; a.bc = bc;
     a.rgb = rgb; a.dist = dist; a.alpha = alpha; a.z = z;
     a.stamps = g_chain_stamps;
-    // NERF_FUSED_V1=1 (A/B only): the round-2 kernel, 4 waves x 32 rows at one wave per SIMD
-    static const bool v1 = [] { const char* e = getenv("NERF_FUSED_V1"); return e && atoi(e) != 0; }();
-    if (v1)
-        hipLaunchKernelGGL(k_mlp_chain_fwd<true>, dim3(a.n_pad / CROWS), dim3(256), 0, as_stream(stream), a);
-    else
-        hipLaunchKernelGGL(k_render_fused2, dim3(a.n_pad / CROWS), dim3(f2::NTH), 0, as_stream(stream), a);
+    hipLaunchKernelGGL(k_render_fused2, dim3(a.n_pad / CROWS), dim3(f2::NTH), 0, as_stream(stream), a);
     return check_launch(__func__);
 }
 

@@ -41,6 +41,9 @@ for step in "$@"; do
       case "${step#pmc:}" in
         wg1) RX=k_wgrad_pair; CT="$C1"; CMD="$R/scripts/wgrad_bench.py --loop 20" ;;
         wg2) RX=k_wgrad_pair; CT="$C2"; CMD="$R/scripts/wgrad_bench.py --loop 20" ;;
+        wgf) RX=k_wgrad_pair; CT="FETCH_SIZE"; CMD="$R/scripts/wgrad_bench.py --loop 20" ;;
+        wgw) RX=k_wgrad_pair; CT="WRITE_SIZE"; CMD="$R/scripts/wgrad_bench.py --loop 20" ;;
+        wgh) RX=k_wgrad_pair; CT="TCC_HIT_sum TCC_MISS_sum"; CMD="$R/scripts/wgrad_bench.py --loop 20" ;;
         ch1) RX=k_mlp_chain; CT="$C1"; CMD="$BENCH" ;;
         ch2) RX=k_mlp_chain; CT="$C2"; CMD="$BENCH" ;;
         fetch) RX="$STEPRX"; CT="FETCH_SIZE"; CMD="$BENCH" ;;
