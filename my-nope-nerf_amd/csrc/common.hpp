@@ -56,6 +56,16 @@ __device__ __forceinline__ int row_exp(float rmax) {
 
 // GEMM arithmetic mode (nerf_gemm_set_precision), host side
 int gemm_precision();
+// several split-K slab reduces (nerf_slab_reduce without accumulate) in one launch
+constexpr int kSlabJobsMax = 10;
+struct SlabJobDesc {
+    const float* slab;
+    int splits, nout, ldslab, nout_ref, kin_ref;
+    const float* bslab;
+    float* gw;
+    float* gb;
+};
+int slab_reduce_jobs(const SlabJobDesc* d, int n, hipStream_t s);
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -155,6 +155,20 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
         if (l == LR) { dy = w.dyr; cm = w.dyr_cm; rm = w.dyr_rm; }
         else { dy = w.dx[l + 1]; cm = w.dx_cm[l + 1]; rm = w.dx_rm[l + 1]; }
     };
+    // the weight gradients back to back on the caller's stream (each needs only the chain's
+    // saved dy), their slab reduces batched into two launches on the side stream: after the
+    // first kReduceGroup layers' TNs (beside the rest) and after the last (beside encode_bwd).
+    // A cross-stream event costs ~7 us of idle on the stream that records it; one per layer
+    // was ~80 us per step.
+    constexpr int kReduceGroup = 5;
+    nerf::SlabJobDesc jobs[L];
+    int nj = 0;
+    auto flush = [&]() -> int {
+        RC(fork(main, side));
+        RC(nerf::slab_reduce_jobs(jobs, nj, side));
+        nj = 0;
+        return NERF_OK;
+    };
     for (int l = LR; l >= 0; --l) {
         const float *dy, *cm, *rm;
         dy_of(l, dy, cm, rm);
@@ -168,9 +182,8 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
         else
             RC(nerf_linear_bwd_weight(dy, op, op, x, K1[l], K1[l], np, w.splits[l], w.slab[l], KP[l], 0, w.bslab[l], cm,
                                       x_cm, stream));
-        RC(fork(main, side));
-        RC(nerf_slab_reduce(w.slab[l], w.splits[l], OUT_P[l], KP[l], NREF[l], KREF[l], w.bslab[l], a.gw[l], a.gb[l], 0,
-                            side_stream));
+        jobs[nj++] = nerf::SlabJobDesc{w.slab[l], w.splits[l], OUT_P[l], KP[l], NREF[l], KREF[l], w.bslab[l], a.gw[l],
+                                       a.gb[l]};
         if (a.ray_grad && (l == LR || l == 4 || l == 0)) {
             // d enc: the encoding segment's rows of W^T (l0: all of them) against this dy
             const int k0 = l == 0 ? 0 : K1[l];
@@ -178,11 +191,12 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
             RC(nerf_linear_bwd_data(dy, op, op, a.wt[l] + (size_t)k0 * op, a.wt_img[l] + (size_t)k0 * 8, KP[l], nullptr, 0,
                                     nullptr, nullptr, 0, out, 64, np, 64, rm, nullptr, nullptr, stream));
         }
+        if (l == LR - kReduceGroup + 1 || l == 0) RC(flush());
     }
-    RC(fork(side, main));
     if (a.ray_grad)
         RC(nerf_encode_bwd(a.pts_o, a.pts_d, a.view, a.z, w.genc_p0, w.genc_p4, w.genc_d, a.n_rays, a.n_samples,
                            a.g_pts_o, a.g_pts_d, a.g_view, stream));
+    RC(fork(side, main));
     return NERF_OK;
 }
 

@@ -329,6 +329,22 @@ __global__ __launch_bounds__(256) void k_slab_reduce(SlabJob j) {
     slab_reduce_block(j, blockIdx.x, part);
 }
 
+// several layers' reduces in one launch (the field backward's weight gradients, one launch per
+// group of layers instead of one per layer): job k owns blocks first[k] .. first[k + 1]; each
+// block runs k_slab_reduce's arithmetic, so the gradients are the same bits
+struct SlabJobs {
+    SlabJob j[kSlabJobsMax];
+    int first[kSlabJobsMax + 1];
+    int n;
+};
+__global__ __launch_bounds__(256) void k_slab_reduce_jobs(SlabJobs js) {
+    __shared__ float4 part[SR_GROUPS][16];
+    const int b = blockIdx.x;
+    int k = 0;
+    while (k + 1 < js.n && b >= js.first[k + 1]) ++k;
+    slab_reduce_block(js.j[k], b - js.first[k], part);
+}
+
 }  // namespace nerf
 
 using namespace nerf;
@@ -592,6 +608,24 @@ extern "C" int nerf_slab_reduce(const float* slab, int splits, int nout, int lds
     hipLaunchKernelGGL(k_slab_reduce, dim3(slab_job_blocks(j)), dim3(256), 0, as_stream(stream), j);
     return check_launch(__func__);
 }
+
+namespace nerf {
+int slab_reduce_jobs(const SlabJobDesc* d, int n, hipStream_t s) {
+    NERF_CHECK(n >= 1 && n <= kSlabJobsMax, "%s: %d jobs (1..%d)", __func__, n, kSlabJobsMax);
+    SlabJobs js{};
+    js.n = n;
+    js.first[0] = 0;
+    for (int k = 0; k < n; ++k) {
+        js.j[k] = SlabJob{d[k].slab, d[k].splits, d[k].nout, d[k].ldslab, d[k].nout_ref, d[k].kin_ref,
+                          d[k].bslab, d[k].gw, d[k].gb, 0};
+        int rc = slab_job_check(__func__, js.j[k]);
+        if (rc) return rc;
+        js.first[k + 1] = js.first[k] + slab_job_blocks(js.j[k]);
+    }
+    hipLaunchKernelGGL(k_slab_reduce_jobs, dim3(js.first[n]), dim3(256), 0, s, js);
+    return check_launch(__func__);
+}
+}  // namespace nerf
 
 extern "C" int nerf_gemm_set_policy(int nt_policy, int tn_policy) {
     NERF_CHECK(nt_policy >= 0 && nt_policy <= 3 && (tn_policy == 0 || tn_policy == 3 || tn_policy == 7 || tn_policy == 8),

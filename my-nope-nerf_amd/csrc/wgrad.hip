@@ -24,12 +24,14 @@
 #include "gemm.hpp"
 #include "x16.hpp"
 
+#include <utility>
+
 namespace nerf {
 namespace wg {
 
 constexpr int NTH = 512;   // 8 waves, two per SIMD: 4 MFMA waves + 4 load / split waves
 constexpr int KS = 32;     // rows per pipeline stage: two 16-row MFMA k-steps
-constexpr int NS = 2;      // register stages of a load wave: loads issued two stages ahead of their split
+constexpr int NS = 3;      // register stages of a load wave: loads issued three stages ahead of their split
 
 template <int BO, int BK>
 struct Cfg {
@@ -47,6 +49,16 @@ struct Cfg {
     static constexpr int BYTES = MAIN + (BO + BK) * 4 + 4 * BO * 4;  // + column exponents, bias partials
     static_assert(TM >= 1 && TN >= 1 && CA >= 1 && CB >= 1 && CA <= 4 && CB <= 4, "tile");
 };
+
+// f(integral_constant<0>), ..., f(integral_constant<N - 1>), in order
+template <class F, int... I>
+__device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void unroll(F&& f) {
+    unroll_seq(f, std::make_integer_sequence<int, N>{});
+}
 
 typedef unsigned wg_u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned wg_u32x2 __attribute__((ext_vector_type(2)));
@@ -153,24 +165,31 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
             }
             __builtin_amdgcn_sched_barrier(0);
         };
-        load(std::integral_constant<int, 0>{}, 0);
-        load(std::integral_constant<int, 1>{}, 1);
+        // prologue: stages 0 .. NS - 1 in flight, stage 0 split into buffer 0, stage NS's loads
+        // into the set it freed
+        unroll<NS>([&](auto u) { load(u, decltype(u)::value); });
         put(std::integral_constant<int, 0>{}, smem, true);
-        load(std::integral_constant<int, 0>{}, 2);
+        load(std::integral_constant<int, 0>{}, NS);
         __syncthreads();
-        // iteration s: stage s + 1 (set (s + 1) & 1, loaded two iterations ago) into buffer
-        // (s + 1) & 1, then the loads of stage s + 3 into the set it freed
-        auto iter = [&](int s, auto uc) {   // uc: the register set of stage s + 1, (s + 1) & 1
+        // iteration s: stage s + 1 (register set (s + 1) % NS, loaded NS iterations ago) into
+        // buffer (s + 1) & 1, then the loads of stage s + 1 + NS into the set it freed
+        auto iter = [&](int s, auto uc) {
             put(uc, smem + ((s + 1) & 1) * C::BUF, s + 1 < nst);
-            load(uc, s + 3);
+            load(uc, s + 1 + NS);
             __syncthreads();
         };
+        // trips of NS straight-line iterations, so that every set index is a constant and the
+        // vmcnt waits count the loads issued since (a loop-carried set would wait for all)
         int s = 0;
-        for (; s + 2 <= nst; s += 2) {
-            iter(s, std::integral_constant<int, 1>{});
-            iter(s + 1, std::integral_constant<int, 0>{});
-        }
-        if (s < nst) iter(s, std::integral_constant<int, 1>{});
+        for (; s + NS <= nst; s += NS)
+            unroll<NS>([&](auto r) {
+                constexpr int R = decltype(r)::value;
+                iter(s + R, std::integral_constant<int, (R + 1) % NS>{});
+            });
+        unroll<NS - 1>([&](auto r) {
+            constexpr int R = decltype(r)::value;
+            if (s + R < nst) iter(s + R, std::integral_constant<int, (R + 1) % NS>{});
+        });
         if constexpr (BIAS) {
 #pragma unroll
             for (int c = 0; c < CA; ++c) lbias[lw * BO + CA * lane + c] = bsum[c];
@@ -181,35 +200,51 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
         const int wm0 = (wave >> 1) * C::WO, wn0 = (wave & 1) * C::WK;
         f32x16 acc[TM][TN];
         zero_acc(acc);
-        auto kstep = [&](const char* ks) {
-            uint4 a[TM][2], b[TN][2];
+        // the fragments of a stage's two k-steps in two register sets: each set is read one
+        // k-step (24 MFMAs) before its MFMAs, so no LDS latency sits between MFMAs; the block
+        // barrier sits between the two k-steps (stage s + 1's images are complete there, and
+        // stage s's second k-step is already in registers)
+        uint4 fa[2][TM][2], fb[2][TN][2];
+        auto frag = [&](auto kc, const char* ks) {
+            constexpr int K = decltype(kc)::value;
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
                 for (int q = 0; q < 2; ++q)
-                    b[j][q] = *reinterpret_cast<const uint4*>(ks + 2 * C::AP + q * C::BP + hi * C::BH + (wn0 + 32 * j + l32) * 16);
+                    fb[K][j][q] = *reinterpret_cast<const uint4*>(ks + 2 * C::AP + q * C::BP + hi * C::BH + (wn0 + 32 * j + l32) * 16);
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int q = 0; q < 2; ++q)
-                    a[i][q] = *reinterpret_cast<const uint4*>(ks + q * C::AP + hi * C::AH + (wm0 + 32 * i + l32) * 16);
+                    fa[K][i][q] = *reinterpret_cast<const uint4*>(ks + q * C::AP + hi * C::AH + (wm0 + 32 * i + l32) * 16);
+        };
+        auto mma = [&](auto kc) {
+            constexpr int K = decltype(kc)::value;
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
                     f32x16 c = acc[i][j];
-                    c = mfma_f16(a[i][0], b[j][1], c);   // hi.lo
-                    c = mfma_f16(a[i][1], b[j][0], c);   // lo.hi
-                    c = mfma_f16(a[i][0], b[j][0], c);   // hi.hi
+                    c = mfma_f16(fa[K][i][0], fb[K][j][1], c);   // hi.lo
+                    c = mfma_f16(fa[K][i][1], fb[K][j][0], c);   // lo.hi
+                    c = mfma_f16(fa[K][i][0], fb[K][j][0], c);   // hi.hi
                     acc[i][j] = c;
                 }
         };
+        constexpr std::integral_constant<int, 0> k0{};
+        constexpr std::integral_constant<int, 1> k1{};
         __syncthreads();
+        frag(k0, smem);
         for (int s = 0; s < nst; ++s) {
             const char* cur = smem + (s & 1) * C::BUF;
-            kstep(cur);
-            kstep(cur + C::KSTEP);
+            frag(k1, cur + C::KSTEP);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(k0);
             __syncthreads();
+            // (the last iteration reads buffer nst & 1 to no use: straight-line waits)
+            frag(k0, smem + ((s + 1) & 1) * C::BUF);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(k1);
         }
         tn_store_lds<TM, TN, true>(p, acc, smem, split, o0, j0, wm0, wn0, lea, leb);
     }
