@@ -57,10 +57,22 @@ __device__ __forceinline__ uint32_t cpk(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, ch16x2));   // RNE
 }
 // already scaled (a, b) -> fp16 pair words (hi, lo)
+// MIX: the residual a - hi (exact in f32) by one v_fma_mix_f32 per value, -hi x 1 + a reading
+// the fp16 half in place, instead of a conversion back to f32 and a subtraction -- the same
+// bits at two thirds of the VALU (the training chain keeps the conversions: the mix form
+// costs it a register it does not have)
+template <bool MIX = true>
 __device__ __forceinline__ void csplit(float a, float b, uint32_t& h, uint32_t& l) {
     h = cpk(a, b);
-    const ch16x2 hv = __builtin_bit_cast(ch16x2, h);
-    l = cpk(a - (float)hv[0], b - (float)hv[1]);
+    if constexpr (MIX) {
+        float ra, rb;
+        asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(ra) : "v"(h), "v"(a));
+        asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(rb) : "v"(h), "v"(b));
+        l = cpk(ra, rb);
+    } else {
+        const ch16x2 hv = __builtin_bit_cast(ch16x2, h);
+        l = cpk(a - (float)hv[0], b - (float)hv[1]);
+    }
 }
 
 typedef __attribute__((address_space(3))) void clds_t;
@@ -77,10 +89,10 @@ __device__ __forceinline__ void frag_from8(const float4& u, const float4& v, int
     const float s2 = __builtin_amdgcn_ldexpf(u.z, e), s3 = __builtin_amdgcn_ldexpf(u.w, e);
     const float s4 = __builtin_amdgcn_ldexpf(v.x, e), s5 = __builtin_amdgcn_ldexpf(v.y, e);
     const float s6 = __builtin_amdgcn_ldexpf(v.z, e), s7 = __builtin_amdgcn_ldexpf(v.w, e);
-    csplit(s0, s1, hi.x, lo.x);
-    csplit(s2, s3, hi.y, lo.y);
-    csplit(s4, s5, hi.z, lo.z);
-    csplit(s6, s7, hi.w, lo.w);
+    csplit<false>(s0, s1, hi.x, lo.x);
+    csplit<false>(s2, s3, hi.y, lo.y);
+    csplit<false>(s4, s5, hi.z, lo.z);
+    csplit<false>(s6, s7, hi.w, lo.w);
 }
 
 }  // namespace
@@ -986,14 +998,14 @@ __device__ __forceinline__ void save_piece(const ChainFwdArgs& p, State& st, con
 // B1 B3): row r then holds its 8 consecutive features).  Two halves (split; exchange) so the
 // k-step can place them at two MFMA tiles
 struct SplitTmp { uint32_t ha0, la0, ha1, la1, hb0, lb0, hb1, lb1; };
-template <int t>
+template <int t, bool MIX = true>
 __device__ __forceinline__ void split_a(State& st, SplitTmp& q) {
     const int e = st.er;
     const f32x4 A = st.xs[2 * t], B = st.xs[2 * t + 1];
-    csplit(__builtin_amdgcn_ldexpf(A[0], e), __builtin_amdgcn_ldexpf(A[1], e), q.ha0, q.la0);
-    csplit(__builtin_amdgcn_ldexpf(A[2], e), __builtin_amdgcn_ldexpf(A[3], e), q.ha1, q.la1);
-    csplit(__builtin_amdgcn_ldexpf(B[0], e), __builtin_amdgcn_ldexpf(B[1], e), q.hb0, q.lb0);
-    csplit(__builtin_amdgcn_ldexpf(B[2], e), __builtin_amdgcn_ldexpf(B[3], e), q.hb1, q.lb1);
+    csplit<MIX>(__builtin_amdgcn_ldexpf(A[0], e), __builtin_amdgcn_ldexpf(A[1], e), q.ha0, q.la0);
+    csplit<MIX>(__builtin_amdgcn_ldexpf(A[2], e), __builtin_amdgcn_ldexpf(A[3], e), q.ha1, q.la1);
+    csplit<MIX>(__builtin_amdgcn_ldexpf(B[0], e), __builtin_amdgcn_ldexpf(B[1], e), q.hb0, q.lb0);
+    csplit<MIX>(__builtin_amdgcn_ldexpf(B[2], e), __builtin_amdgcn_ldexpf(B[3], e), q.hb1, q.lb1);
 }
 template <int t>
 __device__ __forceinline__ void split_b(State& st, const SplitTmp& q) {
@@ -1014,10 +1026,10 @@ template <int ntj, bool second>
 constexpr int split_tile(int half) {
     return ((second ? ntj / 2 : 0) + (ntj >= 16 ? kSplitTile : kSplitTile / 2) + half) % ntj;
 }
-template <int l, int u, int j, int ntj, bool second>
+template <int l, int u, int j, int ntj, bool second, bool MIX>
 __device__ __forceinline__ void split_piece(State& st, SplitTmp& q) {
     if constexpr (l > 0 && u + 1 < 8) {
-        if constexpr (j == split_tile<ntj, second>(0)) split_a<u + 1>(st, q);
+        if constexpr (j == split_tile<ntj, second>(0)) split_a<u + 1, MIX>(st, q);
         if constexpr (j == split_tile<ntj, second>(1)) split_b<u + 1>(st, q);
     }
 }
@@ -1044,7 +1056,7 @@ __device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, co
         st.acc[j] = mfma16(wl[j % R], ah, st.acc[j]);   // lo . hi
         st.acc[j] = mfma16(wh[j % R], ah, st.acc[j]);   // hi . hi
         if constexpr (TR && u < nact) save_piece<l, u, j, ntj>(p, st, ah, al, bits);
-        split_piece<l, u, j, ntj, false>(st, q);
+        split_piece<l, u, j, ntj, false, !TR>(st, q);
         __builtin_amdgcn_sched_barrier(0);
         mstep_tiles<l, u, TR, j + 1, ntj, nact>(p, st, ah, al, base, wh, wl, bits, q);
     }
@@ -1223,7 +1235,7 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
         const int e = st.er;
         // k-step 0's fragment now; the others during the next layer's k-steps (split_piece)
         SplitTmp q;
-        split_a<0>(st, q);
+        split_a<0, !TR>(st, q);
         split_b<0>(st, q);
         if constexpr (l == 3) {   // training: the encodings in HBM
             const float* er_row = TR ? p.enc_p + (st.m0 + st.rl) * 64

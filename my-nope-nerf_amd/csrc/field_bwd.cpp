@@ -156,16 +156,15 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
         else { dy = w.dx[l + 1]; cm = w.dx_cm[l + 1]; rm = w.dx_rm[l + 1]; }
     };
     // the weight gradients back to back on the caller's stream (each needs only the chain's
-    // saved dy), their slab reduces batched into two launches on the side stream: after the
-    // first kReduceGroup layers' TNs (beside the rest) and after the last (beside encode_bwd).
-    // A cross-stream event costs ~7 us of idle on the stream that records it; one per layer
-    // was ~80 us per step.
-    constexpr int kReduceGroup = 5;
+    // saved dy), their slab reduces batched: layers lr .. l5 on the side stream after l5's TN
+    // (beside l4 .. l2's), l4 .. l2 on the side stream after l2's (beside l1's and l0's), l1's
+    // and l0's on the caller's stream at the end (a cross-stream event costs ~7 us of idle on the stream that
+    // records it, and the join another; one fork per layer was ~80 us per step)
     nerf::SlabJobDesc jobs[L];
     int nj = 0;
-    auto flush = [&]() -> int {
-        RC(fork(main, side));
-        RC(nerf::slab_reduce_jobs(jobs, nj, side));
+    auto flush = [&](hipStream_t s) -> int {
+        if (s != main) RC(fork(main, s));
+        RC(nerf::slab_reduce_jobs(jobs, nj, s));
         nj = 0;
         return NERF_OK;
     };
@@ -191,7 +190,8 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
             RC(nerf_linear_bwd_data(dy, op, op, a.wt[l] + (size_t)k0 * op, a.wt_img[l] + (size_t)k0 * 8, KP[l], nullptr, 0,
                                     nullptr, nullptr, 0, out, 64, np, 64, rm, nullptr, nullptr, stream));
         }
-        if (l == LR - kReduceGroup + 1 || l == 0) RC(flush());
+        if (l == 5 || l == 2) RC(flush(side));
+        if (l == 0) RC(flush(main));
     }
     if (a.ray_grad)
         RC(nerf_encode_bwd(a.pts_o, a.pts_d, a.view, a.z, w.genc_p0, w.genc_p4, w.genc_d, a.n_rays, a.n_samples,

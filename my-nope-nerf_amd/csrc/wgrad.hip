@@ -102,17 +102,17 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
     int* lea = reinterpret_cast<int*>(smem + C::MAIN);   // the tile's column exponents (epilogue)
     int* leb = lea + BO;
     float* lbias = reinterpret_cast<float*>(leb + BK);   // [4 load waves][BO] bias partials
-    for (int e = tid; e < BO; e += NTH) lea[e] = row_exp(tn_colmax(p.cm_dy, p.ldcm_dy, s0, p.rows_per_split, o0 + e));
-    for (int e = tid; e < BK; e += NTH) leb[e] = row_exp(tn_colmax(p.cm_x, p.ldcm_x, s0, p.rows_per_split, j0 + e));
+    // the column exponents: every thread its share (one round trip to the producers' group
+    // maxima), in both roles -- the load waves issue their first NS stages before theirs
+    auto exponents = [&]() {
+        for (int e = tid; e < BO; e += NTH) lea[e] = row_exp(tn_colmax(p.cm_dy, p.ldcm_dy, s0, p.rows_per_split, o0 + e));
+        for (int e = tid; e < BK; e += NTH) leb[e] = row_exp(tn_colmax(p.cm_x, p.ldcm_x, s0, p.rows_per_split, j0 + e));
+        __syncthreads();
+    };
 
     if (wave >= 4) {
         // ---- load / split waves: rows 8 lw .. 8 lw + 7 of every stage, CA + CB columns ----
         const int lw = wave - 4;
-        int ea[CA], eb[CB];
-#pragma unroll
-        for (int c = 0; c < CA; ++c) ea[c] = row_exp(tn_colmax(p.cm_dy, p.ldcm_dy, s0, p.rows_per_split, o0 + CA * lane + c));
-#pragma unroll
-        for (int c = 0; c < CB; ++c) eb[c] = row_exp(tn_colmax(p.cm_x, p.ldcm_x, s0, p.rows_per_split, j0 + CB * lane + c));
         // the split's rows as buffer resources: the lane's column offset in a VGPR, the row
         // offset (stage, strip, row) wave-uniform in an SGPR
         const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc(
@@ -121,9 +121,6 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
             (void*)(p.x + s0 * p.ldx + j0), (short)0, (p.rows_per_split * p.ldx - j0) * 4, 0x00020000);
         const int va_off = 4 * CA * lane, vb_off = 4 * CB * lane;
         float va[NS][8][CA], vb[NS][8][CB];
-        float bsum[CA];
-#pragma unroll
-        for (int c = 0; c < CA; ++c) bsum[c] = 0.f;
         auto load = [&](auto uc, int t) {
             constexpr int U = decltype(uc)::value;
             t = t < nst ? t : nst - 1;   // the tail re-loads the last stage: every iteration is alike
@@ -134,6 +131,16 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
                 load_row<CB>(vb[U][i], rx, vb_off, (r0 + i) * p.ldx * 4);
             }
         };
+        unroll<NS>([&](auto u) { load(u, decltype(u)::value); });
+        exponents();
+        int ea[CA], eb[CB];
+#pragma unroll
+        for (int c = 0; c < CA; ++c) ea[c] = lea[CA * lane + c];
+#pragma unroll
+        for (int c = 0; c < CB; ++c) eb[c] = leb[CB * lane + c];
+        float bsum[CA];
+#pragma unroll
+        for (int c = 0; c < CA; ++c) bsum[c] = 0.f;
         // stage in register set U -> image buffer `buf` (k-step lw >> 1, k-half lw & 1);
         // `real` false: the tail's clamped re-split, left out of the bias sums
         auto put = [&](auto uc, char* buf, bool real) {
@@ -165,9 +172,8 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
             }
             __builtin_amdgcn_sched_barrier(0);
         };
-        // prologue: stages 0 .. NS - 1 in flight, stage 0 split into buffer 0, stage NS's loads
-        // into the set it freed
-        unroll<NS>([&](auto u) { load(u, decltype(u)::value); });
+        // prologue (stages 0 .. NS - 1 in flight): stage 0 split into buffer 0, stage NS's
+        // loads into the set it freed
         put(std::integral_constant<int, 0>{}, smem, true);
         load(std::integral_constant<int, 0>{}, NS);
         __syncthreads();
@@ -196,6 +202,7 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
         }
     } else {
         // ---- MFMA waves: a 2 x 2 grid of WO x WK wave tiles ----
+        exponents();
         const int l32 = lane & 31, hi = lane >> 5;
         const int wm0 = (wave >> 1) * C::WO, wn0 = (wave & 1) * C::WK;
         f32x16 acc[TM][TN];

@@ -6,6 +6,7 @@ checked bit-identical to policy 7's.
     python scripts/wgrad_bench.py            # timings (us per launch, median of 3 x 20)
     python scripts/wgrad_bench.py --loop N   # N back-to-back policy-8 launches of the 256 x 256
                                              # layer only (for rocprofv3 --pmc passes)
+    python scripts/wgrad_bench.py --lib my-nope-nerf_amd/lib/ab/x.so ...   # a diagnostic build
 """
 import argparse
 import os
@@ -13,6 +14,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "my-nope-nerf_amd"))
+if "--lib" in sys.argv:   # a diagnostic build in place of the tree's library (read at import)
+    os.environ["NERF_HIP_LIB"] = os.path.join(ROOT, sys.argv[sys.argv.index("--lib") + 1])
 import torch  # noqa: E402
 
 from model import _hip  # noqa: E402
@@ -65,6 +68,7 @@ def shape(dev, nout, kin, check=True):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--loop", type=int, default=0)
+    ap.add_argument("--lib", default=None, help="library path relative to the repo root (diagnostic builds)")
     ap.add_argument("--shapes", default="256x256,256x64,128x256,128x64")
     ap.add_argument("--no-check", dest="check", action="store_false",
                     help="skip the policy 7 / 8 bit-identity check (diagnostic builds via NERF_HIP_LIB)")
