@@ -66,6 +66,7 @@ struct SlabJobDesc {
     float* gb;
 };
 int slab_reduce_jobs(const SlabJobDesc* d, int n, hipStream_t s);
+constexpr int kWgradPairsMax = 4;
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

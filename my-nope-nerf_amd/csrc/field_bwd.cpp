@@ -156,10 +156,11 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
         else { dy = w.dx[l + 1]; cm = w.dx_cm[l + 1]; rm = w.dx_rm[l + 1]; }
     };
     // the weight gradients back to back on the caller's stream (each needs only the chain's
-    // saved dy), their slab reduces batched: layers lr .. l5 on the side stream after l5's TN
-    // (beside l4 .. l2's), l4 .. l2 on the side stream after l2's (beside l1's and l0's), l1's
-    // and l0's on the caller's stream at the end (a cross-stream event costs ~7 us of idle on the stream that
-    // records it, and the join another; one fork per layer was ~80 us per step)
+    // saved dy): the colour layer (two segments), l_f .. l5 in one launch, l4 (two segments),
+    // l3 .. l1 in one launch, l0. Their slab reduces are batched: lr .. l5 on the side stream
+    // after l5's (beside l4 .. l1's), l4 .. l1 on the side stream after l1's (beside l0's),
+    // l0's on the caller's stream at the end (a cross-stream event costs ~7 us of idle on the
+    // stream that records it, and the join another; one fork per layer was ~80 us per step)
     nerf::SlabJobDesc jobs[L];
     int nj = 0;
     auto flush = [&](hipStream_t s) -> int {
@@ -168,12 +169,20 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
         nj = 0;
         return NERF_OK;
     };
-    for (int l = LR; l >= 0; --l) {
-        const float *dy, *cm, *rm;
+    auto job = [&](int l) {
+        jobs[nj++] = nerf::SlabJobDesc{w.slab[l], w.splits[l], OUT_P[l], KP[l], NREF[l], KREF[l], w.bslab[l], a.gw[l],
+                                       a.gb[l]};
+    };
+    auto x_of = [&](int l, const float*& x, const float*& x_cm) {
+        x = l == 0 ? a.enc_p : a.act[l - 1];
+        x_cm = l == 0 ? a.enc_p_cmax : a.cmax[l - 1];
+    };
+    // one layer's weight gradient (+ its encoding-row input gradient for ray gradients)
+    auto single = [&](int l) -> int {
+        const float *dy, *cm, *rm, *x, *x_cm;
         dy_of(l, dy, cm, rm);
+        x_of(l, x, x_cm);
         const int op = OUT_P[l];
-        const float* x = l == 0 ? a.enc_p : a.act[l - 1];
-        const float* x_cm = l == 0 ? a.enc_p_cmax : a.cmax[l - 1];
         if (SEG[l])
             RC(nerf_linear_bwd_weight_seg(dy, op, op, x, K1[l], K1[l], SEG[l] == 1 ? a.enc_p : a.enc_d, 64, 64, np,
                                           w.splits[l], w.slab[l], KP[l], w.bslab[l], cm, x_cm,
@@ -181,8 +190,7 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
         else
             RC(nerf_linear_bwd_weight(dy, op, op, x, K1[l], K1[l], np, w.splits[l], w.slab[l], KP[l], 0, w.bslab[l], cm,
                                       x_cm, stream));
-        jobs[nj++] = nerf::SlabJobDesc{w.slab[l], w.splits[l], OUT_P[l], KP[l], NREF[l], KREF[l], w.bslab[l], a.gw[l],
-                                       a.gb[l]};
+        job(l);
         if (a.ray_grad && (l == LR || l == 4 || l == 0)) {
             // d enc: the encoding segment's rows of W^T (l0: all of them) against this dy
             const int k0 = l == 0 ? 0 : K1[l];
@@ -190,9 +198,30 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
             RC(nerf_linear_bwd_data(dy, op, op, a.wt[l] + (size_t)k0 * op, a.wt_img[l] + (size_t)k0 * 8, KP[l], nullptr, 0,
                                     nullptr, nullptr, 0, out, 64, np, 64, rm, nullptr, nullptr, stream));
         }
-        if (l == 5 || l == 2) RC(flush(side));
-        if (l == 0) RC(flush(main));
-    }
+        return NERF_OK;
+    };
+    // the 256 x 256 layers hi .. lo (descending) in one launch
+    auto pairs = [&](int hi, int lo) -> int {
+        nerf_wgrad_job wj[nerf::kWgradPairsMax];
+        int n = 0;
+        for (int l = hi; l >= lo; --l) {
+            const float *dy, *cm, *rm, *x, *x_cm;
+            dy_of(l, dy, cm, rm);
+            x_of(l, x, x_cm);
+            NERF_CHECK(!SEG[l] && OUT_P[l] == D && K1[l] == D && w.splits[l] == w.splits[hi], "layer %d", l);
+            wj[n++] = nerf_wgrad_job{dy, OUT_P[l], x, K1[l], w.slab[l], KP[l], w.bslab[l], cm, x_cm};
+            job(l);
+        }
+        return nerf_linear_bwd_weight_multi(wj, n, np, w.splits[hi], stream);
+    };
+    RC(single(LR));
+    RC(pairs(LF, 5));
+    RC(flush(side));
+    RC(single(4));
+    RC(pairs(3, 1));
+    RC(flush(side));
+    RC(single(0));
+    RC(flush(main));
     if (a.ray_grad)
         RC(nerf_encode_bwd(a.pts_o, a.pts_d, a.view, a.z, w.genc_p0, w.genc_p4, w.genc_d, a.n_rays, a.n_samples,
                            a.g_pts_o, a.g_pts_d, a.g_view, stream));

@@ -661,5 +661,11 @@ bool wgrad_supported(int nout, int kin, int splits, int rows_per_split);
 bool wgrad_seg_supported(int nout, int k1, int k2, int splits, int rows_per_split);
 void launch_wgrad(const TNArgs& a, int nout, int kin, int splits, hipStream_t s);
 void launch_wgrad_seg(const TNArgs& pm, const TNArgs& ps, int nout, int splits, hipStream_t s);
+// several 256 x 256 layers of the same split count in one launch (k_wgrad_pairs)
+struct TNPairs {
+    TNArgs a[kWgradPairsMax];
+    int n;
+};
+void launch_wgrad_pairs(const TNPairs& m, int splits, hipStream_t s);
 
 }  // namespace nerf

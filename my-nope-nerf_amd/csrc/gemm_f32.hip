@@ -560,6 +560,39 @@ extern "C" int nerf_linear_bwd_weight(const float* dy, int lddy, int nout, const
     return check_launch(__func__);
 }
 
+// several 256 x 256 weight gradients of one split count (the field backward's consecutive
+// 256-wide layers) in one launch of k_wgrad_pairs when the fp16-pair 4-wave kernels cover them;
+// otherwise one nerf_linear_bwd_weight per layer (the same slabs either way)
+extern "C" int nerf_linear_bwd_weight_multi(const nerf_wgrad_job* j, int n, int m, int splits, void* stream) {
+    NERF_CHECK_PTR(j);
+    hipStream_t s = as_stream(stream);
+    NERF_CHECK(n >= 1 && n <= kWgradPairsMax, "%s: %d layers (1..%d)", __func__, n, kWgradPairsMax);
+    const int pol = g_tn_policy ? g_tn_policy : kTnDefault;
+    bool fused = n > 1 && g_precision == 2 && pol == 8 && splits > 0 && m % splits == 0 && (m / splits) % 128 == 0 &&
+                 wgrad_supported(256, 256, splits, m / splits);
+    TNPairs tp{};
+    for (int i = 0; i < n && fused; ++i) {
+        fused = j[i].dy_cmax && j[i].x_cmax;
+        int rc = tn_args(__func__, j[i].dy, j[i].lddy, 256, j[i].x, j[i].ldx, 256, m, splits, j[i].slab, j[i].ldslab, 0,
+                         j[i].bslab, j[i].dy_cmax, j[i].x_cmax, tp.a[i]);
+        if (rc) return rc;
+    }
+    if (!fused) {
+        for (int i = 0; i < n; ++i) {
+            int rc = nerf_linear_bwd_weight(j[i].dy, j[i].lddy, 256, j[i].x, j[i].ldx, 256, m, splits, j[i].slab,
+                                            j[i].ldslab, 0, j[i].bslab, j[i].dy_cmax, j[i].x_cmax, s);
+            if (rc) return rc;
+        }
+        return NERF_OK;
+    }
+    tp.n = n;
+    prof_next(NERF_PROF_DW, n * (4.0 * m * 512.0 + 4.0 * 256 * 256 + 4.0 * 256));
+    prof_begin(s);
+    launch_wgrad_pairs(tp, splits, s);
+    prof_end(s, n * 2.0 * m * 256.0 * 256.0, 3);
+    return check_launch("k_wgrad_pairs");
+}
+
 extern "C" int nerf_linear_bwd_weight_seg(const float* dy, int lddy, int nout, const float* x1, int ldx1, int k1,
                                           const float* x2, int ldx2, int k2, int m, int splits, float* slab,
                                           int ldslab, float* bslab, const float* dy_cmax, const float* x1_cmax,

@@ -46,7 +46,8 @@ struct Cfg {
     static constexpr int LOOP = 2 * BUF;               // double-buffered
     static constexpr int EPI = 4 * TileLds<TN>::BYTES;
     static constexpr int MAIN = LOOP > EPI ? LOOP : EPI;
-    static constexpr int BYTES = MAIN + (BO + BK) * 4 + 4 * BO * 4;  // + column exponents, bias partials
+    // + column exponents (two sets: consecutive layers of one launch alternate), bias partials
+    static constexpr int BYTES = MAIN + 2 * (BO + BK) * 4 + 4 * BO * 4;
     static_assert(TM >= 1 && TN >= 1 && CA >= 1 && CB >= 1 && CA <= 4 && CB <= 4, "tile");
 };
 
@@ -89,8 +90,10 @@ __device__ __forceinline__ void put_strip(char* d, int plane_bytes, const float 
 
 // one block: output rows o0 .. o0 + BO (dy columns), column tile jt (x columns jt BK ..), split;
 // BIAS: the load waves also sum the dy columns (the bias gradient; one column tile per split)
+// par: which exponent set (consecutive layers of one launch alternate, so a layer's exponents
+// can be written while the previous layer's epilogue still reads its own)
 template <int BO, int BK, bool BIAS>
-__device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int jt, int split) {
+__device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int jt, int split, int par) {
     using C = Cfg<BO, BK>;
     constexpr int CA = C::CA, CB = C::CB, TM = C::TM, TN = C::TN;
     const int tid = threadIdx.x;
@@ -99,9 +102,9 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
     const int j0 = jt * BK;
     const size_t s0 = (size_t)split * p.rows_per_split;
     const int nst = p.rows_per_split / KS;
-    int* lea = reinterpret_cast<int*>(smem + C::MAIN);   // the tile's column exponents (epilogue)
+    int* lea = reinterpret_cast<int*>(smem + C::MAIN) + par * (BO + BK);   // the tile's column exponents
     int* leb = lea + BO;
-    float* lbias = reinterpret_cast<float*>(leb + BK);   // [4 load waves][BO] bias partials
+    float* lbias = reinterpret_cast<float*>(smem + C::MAIN) + 2 * (BO + BK);   // [4 load waves][BO] bias partials
     // the column exponents: every thread its share (one round trip to the producers' group
     // maxima), in both roles -- the load waves issue their first NS stages before theirs
     auto exponents = [&]() {
@@ -179,9 +182,18 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
         __syncthreads();
         // iteration s: stage s + 1 (register set (s + 1) % NS, loaded NS iterations ago) into
         // buffer (s + 1) & 1, then the loads of stage s + 1 + NS into the set it freed
+        // The bias partials are final after iteration nst - 2 (stage nst - 1); they go to LDS in
+        // the last iteration, before its barrier, so the MFMA waves (past that barrier) sum them
+        // and no barrier follows the loop: the load waves go straight on to a next layer
         auto iter = [&](int s, auto uc) {
             put(uc, smem + ((s + 1) & 1) * C::BUF, s + 1 < nst);
             load(uc, s + 1 + NS);
+            if constexpr (BIAS) {
+                if (s == nst - 1) {
+#pragma unroll
+                    for (int c = 0; c < CA; ++c) lbias[lw * BO + CA * lane + c] = bsum[c];
+                }
+            }
             __syncthreads();
         };
         // trips of NS straight-line iterations, so that every set index is a constant and the
@@ -196,10 +208,6 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
             constexpr int R = decltype(r)::value;
             if (s + R < nst) iter(s + R, std::integral_constant<int, (R + 1) % NS>{});
         });
-        if constexpr (BIAS) {
-#pragma unroll
-            for (int c = 0; c < CA; ++c) lbias[lw * BO + CA * lane + c] = bsum[c];
-        }
     } else {
         // ---- MFMA waves: a 2 x 2 grid of WO x WK wave tiles ----
         exponents();
@@ -253,22 +261,21 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
             __builtin_amdgcn_sched_barrier(0);
             mma(k1);
         }
+        if constexpr (BIAS) {
+            // the load waves' strip sums -> column sums, added in strip order: deterministic
+            for (int c = tid; c < BO; c += NTH / 2)
+                p.bslab[(size_t)split * p.nout + o0 + c] =
+                    ((lbias[c] + lbias[BO + c]) + lbias[2 * BO + c]) + lbias[3 * BO + c];
+        }
         tn_store_lds<TM, TN, true>(p, acc, smem, split, o0, j0, wm0, wn0, lea, leb);
-    }
-    if constexpr (BIAS) {
-        // the load waves' strip sums -> column sums, added in strip order: deterministic
-        __syncthreads();
-        for (int c = tid; c < BO; c += NTH)
-            p.bslab[(size_t)split * p.nout + o0 + c] =
-                ((lbias[c] + lbias[BO + c]) + lbias[2 * BO + c]) + lbias[3 * BO + c];
     }
 }
 
 // the block of column tile jt, with the bias sums where the layer wants them (column tile 0)
 template <int BO, int BK>
-__device__ __forceinline__ void block_any(const TNArgs& p, char* smem, int o0, int jt, int split) {
-    if (jt == 0 && p.bslab != nullptr) block<BO, BK, true>(p, smem, o0, jt, split);
-    else block<BO, BK, false>(p, smem, o0, jt, split);
+__device__ __forceinline__ void block_any(const TNArgs& p, char* smem, int o0, int jt, int split, int par = 0) {
+    if (jt == 0 && p.bslab != nullptr) block<BO, BK, true>(p, smem, o0, jt, split, par);
+    else block<BO, BK, false>(p, smem, o0, jt, split, par);
 }
 
 }  // namespace wg
@@ -278,6 +285,17 @@ __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_pair(TNArgs p) {
     __shared__ __attribute__((aligned(16))) char smem[wg::Cfg<256, 128>::BYTES];
     const int w = blockIdx.x, slot = w >> 3;
     wg::block_any<256, 128>(p, smem, 0, slot & 1, (slot >> 1) * 8 + (w & 7));
+}
+
+// several consecutive 256 x 256 layers in one launch (l_f .. l5, l3 .. l1 of the field backward):
+// a block walks the layers in order, its load waves issuing a layer's first stages while its
+// MFMA waves still store the previous layer's slab -- one prologue ramp and one launch per
+// group instead of per layer; each layer's slabs are those of its own k_wgrad_pair launch
+__global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_pairs(TNPairs m) {
+    __shared__ __attribute__((aligned(16))) char smem[wg::Cfg<256, 128>::BYTES];
+    const int w = blockIdx.x, slot = w >> 3;
+    for (int i = 0; i < m.n; ++i)
+        wg::block_any<256, 128>(m.a[i], smem, 0, slot & 1, (slot >> 1) * 8 + (w & 7), i & 1);
 }
 
 // one BO x BK tile per split (l0: 256 outputs over the 64 encoding columns)
@@ -320,6 +338,10 @@ void launch_wgrad(const TNArgs& a, int nout, int kin, int splits, hipStream_t s)
         hipLaunchKernelGGL((k_wgrad_one<128, 256>), dim3(splits), dim3(wg::NTH), 0, s, a);
     else
         hipLaunchKernelGGL((k_wgrad_one<128, 64>), dim3(splits), dim3(wg::NTH), 0, s, a);
+}
+
+void launch_wgrad_pairs(const TNPairs& m, int splits, hipStream_t s) {
+    hipLaunchKernelGGL(k_wgrad_pairs, dim3(2 * splits), dim3(wg::NTH), 0, s, m);
 }
 
 void launch_wgrad_seg(const TNArgs& pm, const TNArgs& ps, int nout, int splits, hipStream_t s) {

@@ -63,6 +63,12 @@ class FieldBwd(ctypes.Structure):
                 ("g_view", _c_p), ("workspace", _c_p)]
 
 
+class WgradJob(ctypes.Structure):
+    """nerf_wgrad_job (include/nerf_hip.h): one 256 x 256 layer of nerf_linear_bwd_weight_multi."""
+    _fields_ = [("dy", _c_p), ("lddy", _c_i), ("x", _c_p), ("ldx", _c_i), ("slab", _c_p), ("ldslab", _c_i),
+                ("bslab", _c_p), ("dy_cmax", _c_p), ("x_cmax", _c_p)]
+
+
 class ChainBwd(ctypes.Structure):
     """nerf_chain_bwd (include/nerf_hip.h): the input-gradient chain's arguments."""
     _fields_ = [("graw4", _c_p), ("hr_mask", _c_p), ("ld_hr_mask", _c_i), ("wd", _c_p), ("wc", _c_p),
@@ -92,6 +98,7 @@ _SIGS = {
                                 _c_p], _c_i),
     "nerf_linear_bwd_weight_seg": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p, _c_i, _c_p,
                                     _c_p, _c_p, _c_p, _c_p], _c_i),
+    "nerf_linear_bwd_weight_multi": ([_c_p, _c_i, _c_i, _c_i, _c_p], _c_i),
     "nerf_linear_bwd_weight_splits": ([_c_i, _c_i, _c_i], _c_i),
     "nerf_field_bwd_workspace_bytes": ([_c_i, _c_i], ctypes.c_size_t),
     "nerf_field_backward": ([_c_p, _c_p, _c_p], _c_i),
@@ -290,6 +297,17 @@ def linear_bwd_weight_seg(dy, nout, x1, k1, x2, k2, m, splits, slab, ldslab, bsl
     [0, k1) from x1 and [k1, k1 + k2) from x2 -- in mode 2 one launch reading dy once."""
     _call("nerf_linear_bwd_weight_seg", _ptr(dy), _ld(dy), nout, _ptr(x1), _ld(x1), k1, _ptr(x2), _ld(x2), k2, m,
           splits, _ptr(slab), ldslab, _ptr(bslab), _ptr(dy_cmax), _ptr(x1_cmax), _ptr(x2_cmax), _stream())
+
+
+def linear_bwd_weight_multi(layers, m, splits):
+    """Several 256 x 256 weight gradients in one launch (mode 2, TN policy 8): layers is a list of
+    (dy, x, slab, bslab, dy_cmax, x_cmax), each as linear_bwd_weight(dy, 256, x, 256, m, splits,
+    slab, 256, 0, bslab, dy_cmax, x_cmax) would write it."""
+    jobs = (WgradJob * len(layers))()
+    for j, (dy, x, slab, bslab, dcm, xcm) in zip(jobs, layers):
+        j.dy, j.lddy, j.x, j.ldx = _ptr(dy), _ld(dy), _ptr(x), _ld(x)
+        j.slab, j.ldslab, j.bslab, j.dy_cmax, j.x_cmax = _ptr(slab), 256, _ptr(bslab), _ptr(dcm), _ptr(xcm)
+    _call("nerf_linear_bwd_weight_multi", ctypes.addressof(jobs), len(layers), m, splits, _stream())
 
 
 def bwd_weight_splits(nout, kin, m) -> int:

@@ -28,7 +28,7 @@ KINDS = {
         "256 x 128 column tiles, so dy is fetched by two blocks of one XCD; measured writes are the 128 split-K "
         "slabs (33.6 MB)"),
     "nerf::k_mlp_chain_train2": (
-        "chain_train", 4 * M * 64 * 2 + 4 * M * 2 + 4 * M * D * 9 + 4 * M * 128 + 4 * M * 9 * 8 + 4 * M * 4 +
+        "chain_fwd", 4 * M * 64 * 2 + 4 * M * 2 + 4 * M * D * 9 + 4 * M * 128 + 4 * M * 9 * 8 + 4 * M * 4 +
         4 * (M // 128) * D * 9 + 4 * M * 4,
         "reads enc_p + enc_d 67.1 MB + their row maxima 1.0 MB (weights stream from L2); writes the nine 256-wide "
         "outputs 1208 MB + hr 67.1 MB + ReLU words 37.7 MB + column maxima 9.4 MB + raw4 2.1 MB"),

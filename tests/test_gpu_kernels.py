@@ -262,6 +262,35 @@ def test_wgrad_4wave_matches_8wave(dev, nout, kin, m, splits):
     assert (b8 - ref).abs().max().item() <= 2 * (b7 - ref).abs().max().item() + 1e-6 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("n,m,splits", [(4, 131072, 128), (3, 131072, 128), (2, 4096, 8), (1, 131072, 128)])
+def test_wgrad_multi_matches_single(dev, n, m, splits):
+    """nerf_linear_bwd_weight_multi (k_wgrad_pairs: a block walks n layers, the exponent sets
+    alternating, a layer's first loads beside the previous layer's slab stores) against one
+    nerf_linear_bwd_weight per layer: every slab and bias partial bit-identical."""
+    prev = _hip.gemm_get_precision()
+    _hip.gemm_set_precision(2)
+    try:
+        g = torch.Generator().manual_seed(n * 31 + m)
+        layers, want = [], []
+        for i in range(n):
+            dy = _rand(m, 256, g=g).to(dev)
+            x = _rand(m, 256, g=g).clamp_min(0).to(dev)
+            dy[:, i] *= 1e-5
+            slab = torch.full((splits * 256 * 256,), float("nan"), device=dev)
+            bslab = torch.full((splits * 256,), float("nan"), device=dev)
+            layers.append((dy, x, slab, bslab, _cm(dy), _cm(x)))
+            s1, b1 = torch.full_like(slab, float("nan")), torch.full_like(bslab, float("nan"))
+            _hip.linear_bwd_weight(dy, 256, x, 256, m, splits, s1, 256, 0, b1, dy_cmax=_cm(dy), x_cmax=_cm(x))
+            want.append((s1, b1))
+        _hip.linear_bwd_weight_multi(layers, m, splits)
+        torch.cuda.synchronize()
+        for (dy, x, slab, bslab, _, _), (s1, b1) in zip(layers, want):
+            assert torch.equal(slab, s1)
+            assert torch.equal(bslab, b1)
+    finally:
+        _hip.gemm_set_precision(prev)
+
+
 def test_slab_reduce_accumulate(dev):
     """nerf_slab_reduce with accumulate=1 adds onto the existing gradient (train.py's
     gradient accumulation across render calls); split sums in a fixed order."""
