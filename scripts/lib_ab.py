@@ -1,0 +1,44 @@
+"""A/B of whole libraries on the cfg2 training step: bench.py (eager, no alt / cpu / cfg3 /
+render lines) in one child process per library and round, libraries interleaved over rounds;
+prints each run's ms/step and the per-library median.  Diagnostic builds are made outside the
+tree's sources and are not committed.
+
+    python scripts/lib_ab.py [--rounds 2] my-nope-nerf_amd/lib/ab/x.so ...
+"""
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("libs", nargs="*")
+    args = ap.parse_args()
+    libs = ["my-nope-nerf_amd/lib/libnerf_hip.so"] + args.libs
+    res = {lib: [] for lib in libs}
+    for r in range(args.rounds):
+        for lib in libs:
+            env = dict(os.environ, NERF_HIP_LIB=os.path.join(ROOT, lib))
+            out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(args.steps),
+                                  "--warmup", "5", "--no-alt", "--no-cpu-baseline", "--no-cfg3",
+                                  "--exec", "eager"], env=env, capture_output=True, text=True, timeout=600)
+            line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+            if not line:
+                print(lib, "FAILED", out.stderr[-600:], flush=True)
+                sys.exit(1)
+            d = json.loads(line[-1])
+            res[lib].append(d["ms_per_step"])
+            print(f"round {r} {lib}: {d['ms_per_step']:.4f} ms/step", flush=True)
+    for lib, v in res.items():
+        print(f"median {lib}: {statistics.median(v):.4f} ms/step over {len(v)}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
