@@ -143,13 +143,13 @@ int nerf_linear_bwd_weight_seg(const float* dy, int lddy, int nout, const float*
                                float* bslab, const float* dy_cmax, const float* x1_cmax, const float* x2_cmax,
                                void* stream);
 
-/* The weight gradients of n (1..4) layers of 256 outputs over 256 inputs with one split count
+/* The weight gradients of n (1..8) layers of 256 outputs over 256 inputs with one split count
  * (the field's consecutive hidden layers, official_nerf.py:65-86 under training.py:92): the same
  * slabs as n nerf_linear_bwd_weight(dy_i, lddy_i, 256, x_i, ldx_i, 256, m, splits, slab_i,
  * ldslab_i, 0, bslab_i, dy_cmax_i, x_cmax_i) calls, bit for bit.  In precision mode 2 under TN
  * policy 8 with every job's column maxima it is ONE launch whose blocks walk the layers in
  * order (a layer's first loads overlap the previous layer's slab stores); otherwise the n calls. */
-typedef struct nerf_wgrad_job {
+typedef struct nerf_wgrad_job {   /* (slab columns from 0, ldslab >= 256) */
     const float* dy; int lddy;
     const float* x; int ldx;
     float* slab; int ldslab;

@@ -66,7 +66,14 @@ struct SlabJobDesc {
     float* gb;
 };
 int slab_reduce_jobs(const SlabJobDesc* d, int n, hipStream_t s);
-constexpr int kWgradPairsMax = 4;
+constexpr int kWgradPairsMax = 8;
+// two 256 x 64 weight gradients over the position encoding in one launch (l4's enc_p segment and
+// l0, nerf_linear_bwd_weight's arguments each): a's splits first, then b's, on the 4-wave kernel
+int wgrad_narrow_pair(const float* dy_a, int lddy_a, const float* x_a, int ldx_a, int splits_a, float* slab_a,
+                      int ldslab_a, int col0_a, float* bslab_a, const float* dcm_a, const float* xcm_a,
+                      const float* dy_b, int lddy_b, const float* x_b, int ldx_b, int splits_b, float* slab_b,
+                      int ldslab_b, int col0_b, float* bslab_b, const float* dcm_b, const float* xcm_b, int m,
+                      hipStream_t s);
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -13,6 +13,7 @@
 // dyr (the colour layer's dy, gated by its ReLU words) on the caller's.
 #include "common.hpp"
 
+#include <cstdlib>
 #include <vector>
 
 namespace {
@@ -155,73 +156,145 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
         if (l == LR) { dy = w.dyr; cm = w.dyr_cm; rm = w.dyr_rm; }
         else { dy = w.dx[l + 1]; cm = w.dx_cm[l + 1]; rm = w.dx_rm[l + 1]; }
     };
-    // the weight gradients back to back on the caller's stream (each needs only the chain's
-    // saved dy): the colour layer (two segments), l_f .. l5 in one launch, l4 (two segments),
-    // l3 .. l1 in one launch, l0. Their slab reduces are batched: lr .. l5 on the side stream
-    // after l5's (beside l4 .. l1's), l4 .. l1 on the side stream after l1's (beside l0's),
-    // l0's on the caller's stream at the end (a cross-stream event costs ~7 us of idle on the
-    // stream that records it, and the join another; one fork per layer was ~80 us per step)
-    nerf::SlabJobDesc jobs[L];
-    int nj = 0;
-    auto flush = [&](hipStream_t s) -> int {
-        if (s != main) RC(fork(main, s));
-        RC(nerf::slab_reduce_jobs(jobs, nj, s));
-        nj = 0;
-        return NERF_OK;
-    };
-    auto job = [&](int l) {
-        jobs[nj++] = nerf::SlabJobDesc{w.slab[l], w.splits[l], OUT_P[l], KP[l], NREF[l], KREF[l], w.bslab[l], a.gw[l],
-                                       a.gb[l]};
-    };
-    auto x_of = [&](int l, const float*& x, const float*& x_cm) {
-        x = l == 0 ? a.enc_p : a.act[l - 1];
-        x_cm = l == 0 ? a.enc_p_cmax : a.cmax[l - 1];
-    };
-    // one layer's weight gradient (+ its encoding-row input gradient for ray gradients)
-    auto single = [&](int l) -> int {
-        const float *dy, *cm, *rm, *x, *x_cm;
-        dy_of(l, dy, cm, rm);
-        x_of(l, x, x_cm);
-        const int op = OUT_P[l];
-        if (SEG[l])
-            RC(nerf_linear_bwd_weight_seg(dy, op, op, x, K1[l], K1[l], SEG[l] == 1 ? a.enc_p : a.enc_d, 64, 64, np,
-                                          w.splits[l], w.slab[l], KP[l], w.bslab[l], cm, x_cm,
-                                          SEG[l] == 1 ? a.enc_p_cmax : a.enc_d_cmax, stream));
-        else
-            RC(nerf_linear_bwd_weight(dy, op, op, x, K1[l], K1[l], np, w.splits[l], w.slab[l], KP[l], 0, w.bslab[l], cm,
-                                      x_cm, stream));
-        job(l);
-        if (a.ray_grad && (l == LR || l == 4 || l == 0)) {
-            // d enc: the encoding segment's rows of W^T (l0: all of them) against this dy
+    // the weight-gradient schedule: 1 (the default) as measured in r04n; 2 the balanced one
+    // (NERF_WGRAD_SCHED=2: one eight-layer launch, the encoding segments of l4 and l0 together)
+    const char* ws = std::getenv("NERF_WGRAD_SCHED");
+    if (ws && std::atoi(ws) == 2) {
+        // the weight gradients back to back on the caller's stream (each needs only the chain's
+        // saved dy): the colour layer's two segments (f, enc_d) as two launches; l_f .. l1 -- with
+        // l4's h3 segment -- as ONE launch (k_wgrad_pairs: a block walks the eight 256 x 256
+        // layers); l4's enc_p segment and l0 as one launch (both 256 x 64 over enc_p). The slab
+        // reduces: every layer but l4 and l0 on the side stream after the eight-layer launch (beside
+        // the last one), l4's and l0's on the caller's stream at the end (a cross-stream event costs
+        // ~7 us of idle on the stream that records it; one fork per layer was ~80 us per step)
+        nerf::SlabJobDesc jobs[L];
+        int nj = 0;
+        auto flush = [&](hipStream_t s) -> int {
+            if (s != main) RC(fork(main, s));
+            RC(nerf::slab_reduce_jobs(jobs, nj, s));
+            nj = 0;
+            return NERF_OK;
+        };
+        auto job = [&](int l) {
+            jobs[nj++] = nerf::SlabJobDesc{w.slab[l], w.splits[l], OUT_P[l], KP[l], NREF[l], KREF[l], w.bslab[l], a.gw[l],
+                                           a.gb[l]};
+        };
+        // the encoding rows of W^T against a layer's dy (ray gradients: lr, l4, l0)
+        auto enc_rows = [&](int l) -> int {
+            if (!a.ray_grad) return NERF_OK;
+            const float *dy, *cm, *rm;
+            dy_of(l, dy, cm, rm);
+            const int op = OUT_P[l];
             const int k0 = l == 0 ? 0 : K1[l];
             float* out = l == LR ? w.genc_d : l == 4 ? w.genc_p4 : w.genc_p0;
-            RC(nerf_linear_bwd_data(dy, op, op, a.wt[l] + (size_t)k0 * op, a.wt_img[l] + (size_t)k0 * 8, KP[l], nullptr, 0,
-                                    nullptr, nullptr, 0, out, 64, np, 64, rm, nullptr, nullptr, stream));
+            return nerf_linear_bwd_data(dy, op, op, a.wt[l] + (size_t)k0 * op, a.wt_img[l] + (size_t)k0 * 8, KP[l], nullptr,
+                                        0, nullptr, nullptr, 0, out, 64, np, 64, rm, nullptr, nullptr, stream);
+        };
+        {   // the colour layer: [f | enc_d]
+            const float *dy, *cm, *rm;
+            dy_of(LR, dy, cm, rm);
+            RC(nerf_linear_bwd_weight(dy, HR, HR, a.act[LF], K1[LR], K1[LR], np, w.splits[LR], w.slab[LR], KP[LR], 0,
+                                      w.bslab[LR], cm, a.cmax[LF], stream));
+            RC(nerf_linear_bwd_weight(dy, HR, HR, a.enc_d, 64, 64, np, w.splits[LR], w.slab[LR], KP[LR], K1[LR], nullptr,
+                                      cm, a.enc_d_cmax, stream));
+            job(LR);
+            RC(enc_rows(LR));
         }
-        return NERF_OK;
-    };
-    // the 256 x 256 layers hi .. lo (descending) in one launch
-    auto pairs = [&](int hi, int lo) -> int {
-        nerf_wgrad_job wj[nerf::kWgradPairsMax];
-        int n = 0;
-        for (int l = hi; l >= lo; --l) {
+        {   // l_f .. l1 (l4: its h3 segment) in one launch
+            nerf_wgrad_job wj[nerf::kWgradPairsMax];
+            int n = 0;
+            for (int l = LF; l >= 1; --l) {
+                const float *dy, *cm, *rm;
+                dy_of(l, dy, cm, rm);
+                NERF_CHECK(OUT_P[l] == D && K1[l] == D && w.splits[l] == w.splits[LF], "layer %d", l);
+                wj[n++] = nerf_wgrad_job{dy, D, a.act[l - 1], D, w.slab[l], KP[l], w.bslab[l], cm, a.cmax[l - 1]};
+                if (l != 4) job(l);
+            }
+            RC(nerf_linear_bwd_weight_multi(wj, n, np, w.splits[LF], stream));
+        }
+        RC(flush(side));
+        {   // l4's enc_p segment and l0 in one launch
+            const float *dy4, *cm4, *rm4, *dy0, *cm0, *rm0;
+            dy_of(4, dy4, cm4, rm4);
+            dy_of(0, dy0, cm0, rm0);
+            RC(nerf::wgrad_narrow_pair(dy4, D, a.enc_p, 64, w.splits[4], w.slab[4], KP[4], K1[4], nullptr, cm4, a.enc_p_cmax,
+                                       dy0, D, a.enc_p, 64, w.splits[0], w.slab[0], KP[0], 0, w.bslab[0], cm0, a.enc_p_cmax,
+                                       np, main));
+            job(4);
+            job(0);
+            RC(enc_rows(4));
+            RC(enc_rows(0));
+        }
+        RC(flush(main));
+    } else {
+        // the weight gradients back to back on the caller's stream (each needs only the chain's
+        // saved dy): the colour layer (two segments), l_f .. l5 in one launch, l4 (two segments),
+        // l3 .. l1 in one launch, l0. Their slab reduces are batched: lr .. l5 on the side stream
+        // after l5's (beside l4 .. l1's), l4 .. l1 on the side stream after l1's (beside l0's),
+        // l0's on the caller's stream at the end (a cross-stream event costs ~7 us of idle on the
+        // stream that records it, and the join another; one fork per layer was ~80 us per step)
+        nerf::SlabJobDesc jobs[L];
+        int nj = 0;
+        auto flush = [&](hipStream_t s) -> int {
+            if (s != main) RC(fork(main, s));
+            RC(nerf::slab_reduce_jobs(jobs, nj, s));
+            nj = 0;
+            return NERF_OK;
+        };
+        auto job = [&](int l) {
+            jobs[nj++] = nerf::SlabJobDesc{w.slab[l], w.splits[l], OUT_P[l], KP[l], NREF[l], KREF[l], w.bslab[l], a.gw[l],
+                                           a.gb[l]};
+        };
+        auto x_of = [&](int l, const float*& x, const float*& x_cm) {
+            x = l == 0 ? a.enc_p : a.act[l - 1];
+            x_cm = l == 0 ? a.enc_p_cmax : a.cmax[l - 1];
+        };
+        // one layer's weight gradient (+ its encoding-row input gradient for ray gradients)
+        auto single = [&](int l) -> int {
             const float *dy, *cm, *rm, *x, *x_cm;
             dy_of(l, dy, cm, rm);
             x_of(l, x, x_cm);
-            NERF_CHECK(!SEG[l] && OUT_P[l] == D && K1[l] == D && w.splits[l] == w.splits[hi], "layer %d", l);
-            wj[n++] = nerf_wgrad_job{dy, OUT_P[l], x, K1[l], w.slab[l], KP[l], w.bslab[l], cm, x_cm};
+            const int op = OUT_P[l];
+            if (SEG[l])
+                RC(nerf_linear_bwd_weight_seg(dy, op, op, x, K1[l], K1[l], SEG[l] == 1 ? a.enc_p : a.enc_d, 64, 64, np,
+                                              w.splits[l], w.slab[l], KP[l], w.bslab[l], cm, x_cm,
+                                              SEG[l] == 1 ? a.enc_p_cmax : a.enc_d_cmax, stream));
+            else
+                RC(nerf_linear_bwd_weight(dy, op, op, x, K1[l], K1[l], np, w.splits[l], w.slab[l], KP[l], 0, w.bslab[l], cm,
+                                          x_cm, stream));
             job(l);
-        }
-        return nerf_linear_bwd_weight_multi(wj, n, np, w.splits[hi], stream);
-    };
-    RC(single(LR));
-    RC(pairs(LF, 5));
-    RC(flush(side));
-    RC(single(4));
-    RC(pairs(3, 1));
-    RC(flush(side));
-    RC(single(0));
-    RC(flush(main));
+            if (a.ray_grad && (l == LR || l == 4 || l == 0)) {
+                // d enc: the encoding segment's rows of W^T (l0: all of them) against this dy
+                const int k0 = l == 0 ? 0 : K1[l];
+                float* out = l == LR ? w.genc_d : l == 4 ? w.genc_p4 : w.genc_p0;
+                RC(nerf_linear_bwd_data(dy, op, op, a.wt[l] + (size_t)k0 * op, a.wt_img[l] + (size_t)k0 * 8, KP[l], nullptr, 0,
+                                        nullptr, nullptr, 0, out, 64, np, 64, rm, nullptr, nullptr, stream));
+            }
+            return NERF_OK;
+        };
+        // the 256 x 256 layers hi .. lo (descending) in one launch
+        auto pairs = [&](int hi, int lo) -> int {
+            nerf_wgrad_job wj[nerf::kWgradPairsMax];
+            int n = 0;
+            for (int l = hi; l >= lo; --l) {
+                const float *dy, *cm, *rm, *x, *x_cm;
+                dy_of(l, dy, cm, rm);
+                x_of(l, x, x_cm);
+                NERF_CHECK(!SEG[l] && OUT_P[l] == D && K1[l] == D && w.splits[l] == w.splits[hi], "layer %d", l);
+                wj[n++] = nerf_wgrad_job{dy, OUT_P[l], x, K1[l], w.slab[l], KP[l], w.bslab[l], cm, x_cm};
+                job(l);
+            }
+            return nerf_linear_bwd_weight_multi(wj, n, np, w.splits[hi], stream);
+        };
+        RC(single(LR));
+        RC(pairs(LF, 5));
+        RC(flush(side));
+        RC(single(4));
+        RC(pairs(3, 1));
+        RC(flush(side));
+        RC(single(0));
+        RC(flush(main));
+    }
     if (a.ray_grad)
         RC(nerf_encode_bwd(a.pts_o, a.pts_d, a.view, a.z, w.genc_p0, w.genc_p4, w.genc_d, a.n_rays, a.n_samples,
                            a.g_pts_o, a.g_pts_d, a.g_view, stream));

@@ -667,5 +667,6 @@ struct TNPairs {
     int n;
 };
 void launch_wgrad_pairs(const TNPairs& m, int splits, hipStream_t s);
+void launch_wgrad_two(const TNArgs& a, int na, const TNArgs& b, int nb, hipStream_t s);
 
 }  // namespace nerf

@@ -593,6 +593,38 @@ extern "C" int nerf_linear_bwd_weight_multi(const nerf_wgrad_job* j, int n, int 
     return check_launch("k_wgrad_pairs");
 }
 
+namespace nerf {
+int wgrad_narrow_pair(const float* dy_a, int lddy_a, const float* x_a, int ldx_a, int splits_a, float* slab_a,
+                      int ldslab_a, int col0_a, float* bslab_a, const float* dcm_a, const float* xcm_a,
+                      const float* dy_b, int lddy_b, const float* x_b, int ldx_b, int splits_b, float* slab_b,
+                      int ldslab_b, int col0_b, float* bslab_b, const float* dcm_b, const float* xcm_b, int m,
+                      hipStream_t s) {
+    const int pol = g_tn_policy ? g_tn_policy : kTnDefault;
+    const bool fused = g_precision == 2 && pol == 8 && dcm_a && xcm_a && dcm_b && xcm_b && m % splits_a == 0 &&
+                       m % splits_b == 0 && (m / splits_a) % 128 == 0 && (m / splits_b) % 128 == 0 &&
+                       wgrad_supported(256, 64, splits_a, m / splits_a) && wgrad_supported(256, 64, splits_b, m / splits_b);
+    if (!fused) {
+        int rc = nerf_linear_bwd_weight(dy_a, lddy_a, 256, x_a, ldx_a, 64, m, splits_a, slab_a, ldslab_a, col0_a, bslab_a,
+                                        dcm_a, xcm_a, s);
+        if (rc) return rc;
+        return nerf_linear_bwd_weight(dy_b, lddy_b, 256, x_b, ldx_b, 64, m, splits_b, slab_b, ldslab_b, col0_b, bslab_b,
+                                      dcm_b, xcm_b, s);
+    }
+    TNArgs a, b;
+    int rc = tn_args(__func__, dy_a, lddy_a, 256, x_a, ldx_a, 64, m, splits_a, slab_a, ldslab_a, col0_a, bslab_a, dcm_a,
+                     xcm_a, a);
+    if (rc) return rc;
+    rc = tn_args(__func__, dy_b, lddy_b, 256, x_b, ldx_b, 64, m, splits_b, slab_b, ldslab_b, col0_b, bslab_b, dcm_b, xcm_b,
+                 b);
+    if (rc) return rc;
+    prof_next(NERF_PROF_DW_NARROW, 2 * (4.0 * m * 320.0 + 4.0 * 256 * 64) + (bslab_a ? 1024.0 : 0.0) + (bslab_b ? 1024.0 : 0.0));
+    prof_begin(s);
+    launch_wgrad_two(a, splits_a, b, splits_b, s);
+    prof_end(s, 2 * 2.0 * m * 256.0 * 64.0, 3);
+    return check_launch("k_wgrad_two");
+}
+}  // namespace nerf
+
 extern "C" int nerf_linear_bwd_weight_seg(const float* dy, int lddy, int nout, const float* x1, int ldx1, int k1,
                                           const float* x2, int ldx2, int k2, int m, int splits, float* slab,
                                           int ldslab, float* bslab, const float* dy_cmax, const float* x1_cmax,

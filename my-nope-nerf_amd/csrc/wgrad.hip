@@ -298,6 +298,16 @@ __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_pairs(TNPairs m) {
         wg::block_any<256, 128>(m.a[i], smem, 0, slot & 1, (slot >> 1) * 8 + (w & 7), i & 1);
 }
 
+// two layers' 256 x 64 tiles in one launch: a's splits (blocks 0 .. na - 1), then b's (l4's
+// enc_p segment at 1024 rows per split, then l0 at 512: the long blocks are dispatched first,
+// the short ones fill in behind them -- one full-chip wave instead of two half-empty launches)
+__global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_two(TNArgs a, int na, TNArgs b) {
+    __shared__ __attribute__((aligned(16))) char smem[wg::Cfg<256, 64>::BYTES];
+    const int w = blockIdx.x;
+    if (w < na) wg::block_any<256, 64>(a, smem, 0, 0, w);
+    else wg::block_any<256, 64>(b, smem, 0, 0, w - na);
+}
+
 // one BO x BK tile per split (l0: 256 outputs over the 64 encoding columns)
 template <int BO, int BK>
 __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_one(TNArgs p) {
@@ -338,6 +348,10 @@ void launch_wgrad(const TNArgs& a, int nout, int kin, int splits, hipStream_t s)
         hipLaunchKernelGGL((k_wgrad_one<128, 256>), dim3(splits), dim3(wg::NTH), 0, s, a);
     else
         hipLaunchKernelGGL((k_wgrad_one<128, 64>), dim3(splits), dim3(wg::NTH), 0, s, a);
+}
+
+void launch_wgrad_two(const TNArgs& a, int na, const TNArgs& b, int nb, hipStream_t s) {
+    hipLaunchKernelGGL(k_wgrad_two, dim3(na + nb), dim3(wg::NTH), 0, s, a, na, b);
 }
 
 void launch_wgrad_pairs(const TNPairs& m, int splits, hipStream_t s) {

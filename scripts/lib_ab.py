@@ -35,7 +35,10 @@ def main():
                 sys.exit(1)
             d = json.loads(line[-1])
             res[lib].append(d["ms_per_step"])
-            print(f"round {r} {lib}: {d['ms_per_step']:.4f} ms/step", flush=True)
+            rk = d.get("roofline", {}).get("per_kind", {})
+            kinds = " ".join(f"{k} {v['avg_launch_us']:.1f}us" for k, v in rk.items())
+            frame = (d.get("render_cfg4") or {}).get("ms_per_frame", float("nan"))
+            print(f"round {r} {lib}: {d['ms_per_step']:.4f} ms/step  frame {frame:.2f} ms  {kinds}", flush=True)
     for lib, v in res.items():
         print(f"median {lib}: {statistics.median(v):.4f} ms/step over {len(v)}", flush=True)
 

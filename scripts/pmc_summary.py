@@ -43,6 +43,19 @@ KINDS = {
     "nerf::k_wgrad_pair": (
         "dw", 4 * M * D * 2 + 4 * D * D, "dy 134.2 MB + x 134.2 MB + dW 0.26 MB; the two XCD-paired 256 x 128 "
         "column tiles of a split read dy from HBM once; measured writes are the 128 split-K slabs (33.6 MB)"),
+    "nerf::k_wgrad_pairs": (
+        "dw", 8 * (4 * M * D * 2 + 4 * D * D), "eight 256 x 256 layers (l_f .. l1, l4 over its h3 segment) in one "
+        "launch: per layer dy 134.2 MB + x 134.2 MB + dW 0.26 MB; measured writes are the 8 x 128 split-K slabs "
+        "(268 MB)"),
+    "nerf::k_wgrad_two": (
+        "dw_narrow", 4 * M * (D + 64) * 2 + 2 * 4 * D * 64, "l4's enc_p segment and l0 in one launch: per layer dy "
+        "134.2 MB + enc_p 33.6 MB + dW 0.07 MB; measured writes are the split-K slabs (8.4 + 16.8 MB)"),
+    "k_wgrad_one<128, 256>": (
+        "dw_narrow", 4 * M * (128 + D) + 4 * 128 * D, "dyr 67.1 MB + f 134.2 MB + dW 0.13 MB (colour layer, f "
+        "segment); measured writes are the 256 split-K slabs (33.6 MB)"),
+    "k_wgrad_one<128, 64>": (
+        "dw_narrow", 4 * M * (128 + 64) + 4 * 128 * 64, "dyr 67.1 MB + enc_d 33.6 MB + dW 0.03 MB (colour layer, "
+        "enc_d segment); measured writes are the 256 split-K slabs (8.4 MB)"),
     "k_wgrad_seg<256, 128, 2, 64>": (
         "dw", 4 * M * (D + D + 64) + 4 * D * (D + 64), "dy 134.2 MB + h3 134.2 MB + enc_p 33.6 MB + dW 0.33 MB "
         "(l4); measured writes are the 128 split-K slabs (41.9 MB)"),

@@ -7,7 +7,7 @@ and the saved dy are the fp16 pairs the chain consumed (within 2^-22 relative), 
 gradients agree to 1e-5 relative L2 per tensor.  Training-size batches (Np >= 65536, where
 the native path runs), with and without ray gradients (pose learning), from the composite
 backward and from a given graw4 (eval_points); also under a tail of 0 and 3 deferred weight
-gradients."""
+gradients, and with the chain under both weight-gradient schedules (NERF_WGRAD_SCHED 1 / 2)."""
 import os
 
 import pytest
@@ -69,10 +69,10 @@ def _agree(a, b, chain):
         assert (a - b).abs().max().item() <= 1e-4 * b.abs().max().item() + 1e-30
 
 
-@pytest.mark.parametrize("chain", ["0", "1"])
+@pytest.mark.parametrize("chain,sched", [("0", "1"), ("1", "1"), ("1", "2")])
 @pytest.mark.parametrize("ray_grad,R,S,tail", [(False, 1024, 128, None), (True, 1024, 128, None),
                                                (False, 600, 128, "0"), (True, 520, 128, "3")])
-def test_native_backward_bit_identical(dev, h16, ray_grad, R, S, tail, chain):
+def test_native_backward_bit_identical(dev, h16, ray_grad, R, S, tail, chain, sched):
     net = _net(dev, seed=R)
     o, d, noise = _rays(R, S, seed=R + 1)
     runner = net.hip_runner()
@@ -86,6 +86,7 @@ def test_native_backward_bit_identical(dev, h16, ray_grad, R, S, tail, chain):
 
     env = {"NERF_TAIL_MAIN": tail} if tail is not None else {}
     env["NERF_BWD_CHAIN"] = chain
+    env["NERF_WGRAD_SCHED"] = sched      # the chain's weight-gradient schedules (field_bwd.cpp)
     g_native = _grads(net, fn, True, env)
     g_python = _grads(net, fn, False, env)
     n_pad = (R * S + 127) // 128 * 128
