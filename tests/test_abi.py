@@ -52,6 +52,16 @@ def test_abi_version_and_error_path(lib):
     assert rc == -1 and b"n_rays" in lib.nerf_hip_last_error()
     rc = lib.nerf_camera_rays(1, 1, None, 4, 1, None, 1, None, 1, 1, None, None)
     assert rc == -1 and b"cam" in lib.nerf_hip_last_error()
+    # several weight gradients in one launch: 1..8 layers, each job checked before any launch
+    import ctypes
+    from model import _hip
+    jobs = (_hip.WgradJob * 9)()
+    rc = lib.nerf_linear_bwd_weight_multi(ctypes.addressof(jobs), 9, 131072, 128, None)
+    assert rc == -1 and b"layers" in lib.nerf_hip_last_error()
+    rc = lib.nerf_linear_bwd_weight_multi(ctypes.addressof(jobs), 0, 131072, 128, None)
+    assert rc == -1
+    rc = lib.nerf_linear_bwd_weight_multi(None, 2, 131072, 128, None)
+    assert rc == -1
 
 
 def test_ops_refuse_cpu_tensors(lib):
