@@ -76,7 +76,7 @@ struct TNArgs {
     // fp16 pair kernel scales each split's columns by them
     const float* cm_dy; int ldcm_dy;
     const float* cm_x; int ldcm_x;
-    unsigned long long* stamps;   // diagnostic builds (-DNERF_TN_STAMPS=1): per-block phase cycles or NULL
+    unsigned long long* stamps;   // unused (the round-3 TN phase stamps were a diagnostic build)
 };
 
 // Backward-data epilogue operands (ReLU bits, rank-1 column), prefetched into registers
@@ -404,17 +404,6 @@ __device__ __forceinline__ void bfly_max_dpp(float (&v)[NV], int sl, int& base) 
 //        stored values is max-accumulated into lrm (LDS, float bits) for NTArgs::c_rmax.
 //   lvb (optional): the column block's bias (FWD) / v (BWD) staged in LDS by the kernel; a global load
 //        issued between the stores would make its wait retire every earlier store first.
-// Diagnostic builds only (make EXTRA=-DNERF_EPI_ABLATE=...; results are wrong): 8 = no
-// output stores (a checksum per lane instead), 16 = no row / column maxima.
-#ifndef NERF_EPI_ABLATE
-#define NERF_EPI_ABLATE 0
-#endif
-constexpr int kEpiAblate = NERF_EPI_ABLATE;
-// Diagnostic builds only (EXTRA=-DNERF_EPI_STAMPS=1): phase stamps inside the NT epilogue
-#ifndef NERF_EPI_STAMPS
-#define NERF_EPI_STAMPS 0
-#endif
-constexpr bool kEpiStamps = NERF_EPI_STAMPS != 0;
 
 template <int TM, int TN, int EPI, bool H = false, bool HD = false>
 __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc)[TM][TN], int m0, int n0, int wm0,
@@ -446,13 +435,9 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
             acc[i][j][4 * q + 3] = __builtin_amdgcn_ldexpf(acc[i][j][4 * q + 3], -(er[i] + eb.w));
         }
     };
-    float chk = 0.f;
-    auto out4 = [&](float* dst, const float4& x) {
-        if constexpr (kEpiAblate & 8) chk += x.x + x.y + x.z + x.w;
-        else store_out4(dst, x);
-    };
+    auto out4 = [&](float* dst, const float4& x) { store_out4(dst, x); };
     auto track = [&](int i, int j, int q, const float4& x) {
-        if constexpr (H && !(kEpiAblate & 16)) {
+        if constexpr (H) {
             rmx[i] = fmaxf(rmx[i], fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
             if (lcm) {
 #pragma unroll
@@ -582,9 +567,7 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
                     if (hf == 0) lhs[(wm0 + 32 * i + sl) * 3 + c] = v;
                 }
     }
-    if constexpr (kEpiStamps) stamp(p.stamps, 4);
-    if constexpr (kEpiAblate & 8) p.c[(size_t)(m0 + wm0 + sl) * p.ldc + n0 + wn0 + hf] = chk;
-    if constexpr (H && !(kEpiAblate & 16)) {
+    if constexpr (H) {
         // the lane pair (lane, lane ^ 32) holds one row's features of this wave; the other
         // waves along N meet in LDS (non-negative floats order like their bits)
 #pragma unroll
@@ -612,7 +595,6 @@ __device__ __forceinline__ void nt_epilogue_direct(const NTArgs& p, f32x16 (&acc
             }
         }
     }
-    if constexpr (kEpiStamps) stamp(p.stamps, 5);
 }
 
 // TN epilogue through the LDS writer: float4 slab stores.  H: undo the scales 2^(ea[row] +

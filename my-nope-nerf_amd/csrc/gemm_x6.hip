@@ -41,18 +41,6 @@ typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 
 constexpr int XK = 16;   // K per LDS tile
 
-// Diagnostic builds only (make EXTRA=-DNERF_NT_ABLATE=...; results are wrong): the NT main
-// loop without its B-image DMAs (2), its raw-A DMAs (4) or the split VALU of A (8)
-#ifndef NERF_NT_ABLATE
-#define NERF_NT_ABLATE 0
-#endif
-constexpr int kNtAblate = NERF_NT_ABLATE;
-// Experiment (make EXTRA=-DNERF_NT_SPREAD=1): the DMA / split schedule of the NT main loop
-// spread between the MFMAs (x6_mainloop_pf)
-#ifndef NERF_NT_SPREAD
-#define NERF_NT_SPREAD 0
-#endif
-constexpr bool kNtSpread = NERF_NT_SPREAD != 0;
 
 __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
     f32x2 v = {a, b};
@@ -121,21 +109,13 @@ __device__ __forceinline__ void put_col8(char* img, int c, int g, const float (&
     *reinterpret_cast<uint4*>(d + 2 * I::PLANE) = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
-// Diagnostic builds only (make EXTRA=-DNERF_TN_ABLATE=1; results are wrong): the TN operand
-// strips written as one RNE fp16 word per value (no scale, no residual) -- the split's VALU out
-#ifndef NERF_TN_ABLATE
-#define NERF_TN_ABLATE 0
-#endif
 // fp16 pair form of put_col8 (column scale 2^e)
 template <int ROWS>
 __device__ __forceinline__ void put_col8h(char* img, int c, int g, const float (&v)[8], int e) {
     using I = XImg<ROWS, 2>;
     uint32_t h[4], l[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        if constexpr (NERF_TN_ABLATE & 1) { h[t] = pk_f16(v[2 * t], v[2 * t + 1]); l[t] = h[t]; }
-        else split2h(v[2 * t], v[2 * t + 1], e, h[t], l[t]);
-    }
+    for (int t = 0; t < 4; ++t) split2h(v[2 * t], v[2 * t + 1], e, h[t], l[t]);
     char* d = img + g * I::HALF + c * 16;
     *reinterpret_cast<uint4*>(d) = make_uint4(h[0], h[1], h[2], h[3]);
     *reinterpret_cast<uint4*>(d + I::PLANE) = make_uint4(l[0], l[1], l[2], l[3]);
@@ -249,39 +229,6 @@ __device__ __forceinline__ void x6_mainloop_pf(char* smem, int nkt, int wm0, int
     stamp(stamps, 1);
 
     auto iter = [&](int kt, uint4 (&ac)[TM][NP], uint4 (&bc)[TN][NP], uint4 (&an)[TM][NP], uint4 (&bn)[TN][NP]) {
-        if constexpr (kNtSpread && H && TM == 2 && TN == 4 && Stager::B_C == 4 && Stager::A_F4 == 2) {
-            // NERF_NT_SPREAD: the split first, then one LDS-DMA piece before each of the first six
-            // 32x32 output tiles' three MFMAs, so a piece's issue cost overlaps the MFMAs in flight
-            // instead of stalling the wave at the top of the k-step
-            char* wimg = smem + (kt & 1) * BUF;
-            const char* nbuf = smem + ((kt + 1) & 1) * BUF;
-            {
-                float4 raw[Stager::A_F4];
-                st.read_raw3(kt, raw);
-                st.split_raw(raw, wimg);
-            }
-            rdB(nbuf, bn);
-            rdA(nbuf, an, 0, 1);
-            const int ktb = st.clamp(kt + 2, nkt), kta = st.clamp(kt + 4, nkt);
-            auto tile = [&](int i, int j) {
-                f32x16 c = acc[i][j];
-                c = mf(ac[i][0], bc[j][1], c);
-                c = mf(ac[i][1], bc[j][0], c);
-                c = mf(ac[i][0], bc[j][0], c);
-                acc[i][j] = c;
-            };
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                if (t < 4) { if constexpr (!(kNtAblate & 2)) st.dma_b_piece(ktb, wimg + IA::BYTES, t); }
-                else if (t < 6) { if constexpr (!(kNtAblate & 4)) st.dma_a_piece(kta, (kt + 1) % Stager::NSLOT, t - 4); }
-                tile(t / TN, t % TN);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            rdA(nbuf, an, 1, 2);
-            st.wait3();
-            __syncthreads();
-            return;
-        }
         char* wimg = smem + (kt & 1) * BUF;
         const char* nbuf = smem + ((kt + 1) & 1) * BUF;
         constexpr int HT = (TM + 1) / 2;
@@ -420,12 +367,12 @@ struct NTStager {
     // iteration kt: B image of tile kt+2 into buffer kt&1 (lands this iteration), then raw A
     // of tile kt+4 into slot (kt+4)%3 = (kt+1)%3 (lands next iteration)
     __device__ __forceinline__ void dma3(int kt, int nkt, char* Bimg) {
-        if constexpr (!(kNtAblate & 2)) dma_b(clamp(kt + 2, nkt), Bimg);
-        if constexpr (!(kNtAblate & 4)) dma_a(clamp(kt + 4, nkt), (kt + 1) % NSLOT);
+        dma_b(clamp(kt + 2, nkt), Bimg);
+        dma_a(clamp(kt + 4, nkt), (kt + 1) % NSLOT);
     }
     __device__ __forceinline__ void read_raw3(int kt, float4 (&v)[A_F4]) { read_slot((kt + 2) % NSLOT, v); }
     __device__ __forceinline__ void split_raw(const float4 (&v)[A_F4], char* Aimg) {
-        if constexpr (!(kNtAblate & 8)) put(v, Aimg);
+        put(v, Aimg);
     }
     // one float4 of the split (NERF_NT_SPREAD schedule)
     __device__ __forceinline__ void split_piece(const float4 (&v)[A_F4], char* Aimg, int i) {
@@ -571,7 +518,6 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void k_gemm_nt_x6(NTArgs p) {
                 for (int e = threadIdx.x; e < NG * BN; e += NT)
                     p.c_cmax[(size_t)(m0 / 128 + e / BN) * p.ldcm + n0 + e % BN] = __uint_as_float(lcm[e]);
         }
-        if constexpr (kEpiStamps) stamp(p.stamps, 9);
         dma_wait();      // the last (clamped) raw-A DMA lands before the workgroup's LDS is released
     } else {
         NTEpiPrefetch<BM, BN, NT, EPI> pf;
@@ -595,10 +541,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void k_gemm_nt_x6(NTArgs p) {
 // ---------------------------------------------------------------------------
 // The strips of a k-tile can be loaded NS tiles ahead of the split that consumes them (NS
 // register sets; dispatch_tn_x6 picks the depth).
-#ifndef NERF_TN_QUARTER
-#define NERF_TN_QUARTER 1
-#endif
-constexpr bool kTnQuarter = NERF_TN_QUARTER != 0;
+
 template <int BM, int BN, int NT, bool HH = false, int NSET = 1>
 struct TNStager {
     static constexpr bool H = HH;       // fp16 pair images with per-column scales (mode 2)
@@ -609,7 +552,7 @@ struct TNStager {
     // the threads only; as RB-row sub-strips (RB = 16 BN / NT: 4 for 128 columns, 2 for 64 at
     // eight waves) every thread takes one and every wave loads and splits the same share instead
     // of some waves waiting at each barrier for the others
-    static constexpr int RB = (HH && kTnQuarter && NT % BN == 0 && (NT / BN == 4 || NT / BN == 8)) ? 16 * BN / NT : 8;
+    static constexpr int RB = (HH && NT % BN == 0 && (NT / BN == 4 || NT / BN == 8)) ? 16 * BN / NT : 8;
     static constexpr bool BQ = RB < 8;
     static constexpr int SB = BQ ? 1 : (2 * BN + NT - 1) / NT;
     const float* dyb; const float* xb;
@@ -717,40 +660,11 @@ struct TNStager {
 // set (kt+1) % NS) into the other buffer, issues the loads of tile kt+NS into the set tile kt
 // used (NS == 1: tile kt+2 into the one set, as before), then the MFMAs (VALU of the split
 // interleaved, 3 per MFMA gap) and one barrier.
-// Diagnostic builds only (make EXTRA=-DNERF_TN_STAMPS=1): per-block cycles of the TN main loop's
-// phases (wave 0; s_memtime between scheduling barriers, which also pins the order the
-// production build may interleave) into TNArgs::stamps[block][8]: fragment reads, the next
-// tile's split (with its load wait), load issue, MFMAs (with the fragment waits), barrier,
-// prologue, epilogue, total
-#ifndef NERF_TN_STAMPS
-#define NERF_TN_STAMPS 0
-#endif
-constexpr bool kTnStamps = NERF_TN_STAMPS != 0;
+// phase-clock hooks of the TN main loop (the round-3 stamp build is retired: no-ops)
 struct TnClock {
-    unsigned long long b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long last = 0, start = 0;
-    __device__ __forceinline__ void begin() {
-        if constexpr (kTnStamps) { start = last = __builtin_amdgcn_s_memtime(); }
-    }
-    __device__ __forceinline__ void tick(int k) {
-        if constexpr (kTnStamps) {
-            __builtin_amdgcn_sched_barrier(0);
-            const unsigned long long t = __builtin_amdgcn_s_memtime();
-            b[k] += t - last;
-            last = t;
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-    __device__ __forceinline__ void write(unsigned long long* out) {
-        if constexpr (kTnStamps) {
-            b[7] = __builtin_amdgcn_s_memtime() - start;
-            if (out && threadIdx.x == 0) {
-                const size_t blk = (size_t)blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) out[blk * 8 + k] = b[k];
-            }
-        }
-    }
+    __device__ __forceinline__ void begin() {}
+    __device__ __forceinline__ void tick(int) {}
+    __device__ __forceinline__ void write(unsigned long long*) {}
 };
 
 template <int TM, int TN, int BM, int BN, typename Stager>
