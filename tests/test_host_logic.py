@@ -170,3 +170,21 @@ def test_ray_resampling_guarantee():
     mask2 = torch.ones(1, 100, 100, dtype=torch.bool)
     mask2[0, :5] = False
     assert tr2.sample_rays(10000, mask2, True, img=torch.rand(1, 3, 100, 100), hw=(100, 100))[0].shape == (64,)
+
+
+def test_hip_adam_hyper_block():
+    """HipAdam's device hyper-parameter block (k_adam reads it): slot 6 is 1 - beta2 formed in
+    double on the host and rounded once, as torch's Adam forms it -- not 1 - f32(beta2) -- and an
+    edited param_group (an LR scheduler) is pushed on the next sync (checked on the GPU against
+    torch's Adam in tests/test_gpu_checkpoint.py)."""
+    from model.optim import HipAdam
+    p = torch.nn.Parameter(torch.zeros(10))
+    opt = HipAdam([p], lr=1e-3, betas=(0.9, 0.999), eps=1e-8)
+    h = opt._hyper
+    assert h[1].item() == torch.tensor(1e-3).item() and h[2].item() == torch.tensor(0.9).item()
+    assert h[6].item() == torch.tensor(1.0 - 0.999, dtype=torch.float32).item()
+    assert h[6].item() != (1.0 - torch.tensor(0.999, dtype=torch.float32)).item()
+    opt.param_groups[0]["lr"] = 5e-4
+    opt.sync_hyper()
+    assert opt._hyper[1].item() == torch.tensor(5e-4).item()
+    assert p.data.data_ptr() == opt._flat.data_ptr()     # parameters are views of the flat buffer
