@@ -41,7 +41,7 @@ extern "C" {
  * 9 precision mode 2 as the default, 10 nerf_mlp_chain_train, 11 nerf_linear_bwd_weight_seg and
  * nerf_field_backward, 12 nerf_mlp_chain_bwd, nerf_field_bwd.bwd_chain, TN policy 8 and the
  * Adam hyper slot 6 (1 - beta2). */
-#define NERF_HIP_ABI_VERSION 12
+#define NERF_HIP_ABI_VERSION 13
 int nerf_hip_abi_version(void);
 const char* nerf_hip_last_error(void);
 
@@ -173,7 +173,8 @@ int nerf_linear_bwd_weight_multi(const nerf_wgrad_job* jobs, int n, int m, int s
  * (nerf_field_bwd_workspace_bytes). */
 #define NERF_BWD_LAYERS 10
 typedef struct nerf_field_bwd {
-    int n_pad, n_rays, n_samples, flags, ray_grad, tail_main;
+    int n_pad, n_rays, n_samples, flags, ray_grad, tail_main;   /* tail_main: the per-layer schedule only
+                                                                   (bwd_chain = 0); ignored by the chain's */
     int bwd_chain;   /* 1: the input gradients by nerf_mlp_chain_bwd (ABI 12), 0: the per-layer schedule */
     /* forward state (nerf_mlp_chain_train / nerf_encode_samples outputs) */
     const float* z;
@@ -191,6 +192,8 @@ typedef struct nerf_field_bwd {
     /* packed parameters (nerf_pack_weights, mode 2) */
     const float* wt[NERF_BWD_LAYERS];       /* f32 W^T [kp][out_p] */
     const uint16_t* wt_img[NERF_BWD_LAYERS];/* fp16 pair image of W^T */
+    const uint16_t* wt_cimg[NERF_BWD_LAYERS];/* its chain image (nerf_pack_desc dst_cts; ABI 13): the
+                                               input-gradient chain's operand (bwd_chain = 1) */
     const float* wd;                        /* fc_density weight [256], 16-byte aligned */
     const float* wc;                        /* fc_rgb weight [3][128] */
     /* upstream gradient: graw4 [n_pad][4], or g_rgb [R][3] + g_dist [R] through the composite */
@@ -262,7 +265,9 @@ int nerf_gemm_debug_ablate(int mask);
  * registers from layer to layer (row-scaled fp16 pairs, three MFMA products, as mode 2).
  * layers[10] = l0..l7, fc_feature, rgb_layers[0]; per layer the fp16 pair weight image
  * written by nerf_pack_weights in mode 2 ([out_p][K]: K = 64, 256, 256, 256, 320, 256,
- * 256, 256, 256, 320; out_p = 256 except 128 for the colour layer) and the bias; optional
+ * 256, 256, 256, 320; out_p = 256 except 128 for the colour layer; for THIS entry the plain
+ * image dst_s, for nerf_mlp_chain_train and nerf_render_eval_fused the chain image dst_cs
+ * with perm_k = 256 for l1..lr, 0 for l0 -- ABI 13) and the bias; optional
  * outputs: the f32 activation (the backward's saved tensor; NULL in eval renders), the ReLU
  * bits and the column maxima per 128-row group (mode 2's weight-gradient scales; not for
  * the colour layer).  enc_p / enc_d and their row maxima as written by nerf_encode_samples.
@@ -280,7 +285,8 @@ int nerf_mlp_chain_fwd(const float* enc_p, const float* enc_d, const float* enc_
 /* The training forward chain (official_nerf.py:60-96 under training.py:70-92): the ten
  * linears of nerf_mlp_chain_fwd in ONE launch at two waves per SIMD, saving what the per-layer
  * kernels (nerf_linear_fwd) save for the backward -- every layer output (out, mandatory; the
- * trunk layers' rebuilt from the fp16 pair the next layer consumed, within 2^-22 relative),
+ * f32 epilogue values -- ABI 12 saved the trunk layers' rebuilt from the fp16 pair the next
+ * layer consumed), the weight images being the chain images (dst_cs, ABI 13),
  * the ReLU words (mask, mandatory except for lf, ldmask even) and the per-128-row-group column
  * maxima (cmax, mandatory except for the colour layer) -- plus raw4 [n_pad][4] = (sigma_raw,
  * rgb logits) from the density / colour heads in the l7 / colour-layer epilogues (wd [256],
@@ -317,8 +323,8 @@ int nerf_render_eval_fused(const float* pts_o, const float* pts_d, const float* 
  * W^T streamed by LDS-DMA -- the nine nerf_linear_bwd_data launches of the per-layer path.
  * Layer order i = 0..8: colour layer, feature layer, l7 .. l1.  D_0 = dyr [n_pad][128],
  * D_i (i >= 1) the gradient at the output of forward layer 9 - i ([n_pad][256]; D_9 is the
- * gradient at l0's output).  Every D_i is saved (f32 rebuilt from the fp16 pair consumed,
- * within 2^-22 relative of the f32 value), with its per-128-row-group column maxima
+ * gradient at l0's output).  Every D_i is saved (the f32 value; ABI 12 saved it rebuilt from
+ * the fp16 pair consumed), with its per-128-row-group column maxima
  * ([n_pad/128][128 or 256]) and row maxima ([n_pad]) -- the weight-gradient and ray-gradient
  * GEMMs' operands. */
 typedef struct nerf_chain_bwd {
@@ -327,7 +333,8 @@ typedef struct nerf_chain_bwd {
     int ld_hr_mask;
     const float* wd;                /* fc_density weight [256], 16-byte aligned */
     const float* wc;                /* fc_rgb weight [3][128] (padded) */
-    const uint16_t* wt_img[9];      /* fp16 pair images of W^T (rows = input features), layer order */
+    const uint16_t* wt_img[9];      /* chain images of W^T (nerf_pack_desc dst_cts: rows = input
+                                       features, K in chain order; ABI 13), layer order */
     int wt_img_rows[9];
     const uint32_t* in_mask[9];     /* ReLU words of layer i's input [n_pad][ld >= 8] (i = 0 unused) */
     int ld_in_mask[9];
@@ -343,6 +350,9 @@ int nerf_mlp_chain_bwd(const nerf_chain_bwd* a, void* stream);
 /* Diagnostics only: per-block phase cycles of nerf_mlp_chain_fwd into buf[(n_pad/128)*6]
  * uint64 (DMA wait, barrier, MFMA section, epilogue, total, end time); NULL switches off. */
 int nerf_chain_debug_stamps(void* buf);
+/* 1 when the library was built with NERF_CHAIN_STAMPS (the two-wave chains then stamp too;
+ * production builds carry no stamp instructions in them), else 0. */
+int nerf_chain_stamps_built(void);
 
 /* ---------------------------------------------------------------------------
  * Output heads (density + colour logits), forward and backward.
@@ -408,7 +418,13 @@ int nerf_encode_bwd(const float* pts_o, const float* pts_d, const float* view, c
  * In GEMM precision mode 2 the same buffers receive the fp16 pair form instead: each image
  * row r scaled by 2^e_r (row max -> [2^14, 2^15)), planes 0 / 1 = fp16 hi / lo, and e_r as
  * an int32 in the first word of plane 2's chunk 0 of that row (u16 index
- * ((2*K/8)*rows + r)*8). */
+ * ((2*K/8)*rows + r)*8).
+ * dst_cs / dst_cts (optional, mode 2 only; ABI 13): the CHAIN images of dst / dst_t -- the
+ * same fp16 pair form, with the first perm_k columns of dst_cs (every column of dst_cts) in
+ * chain order: within each 32 columns, image column 8 g + i holds column 4 g + i (i < 4) or
+ * 16 + 4 g + i - 4 (i >= 4) of the 32 (common.hpp chain_perm), the order in which the
+ * 16x16x32 MFMA accumulators of the two-wave chains hold a layer's outputs.  perm_k % 32 == 0,
+ * ld_t % 32 == 0 when dst_cts is given. */
 #define NERF_MAX_PACK 24
 typedef struct {
     const float* src;
@@ -418,17 +434,23 @@ typedef struct {
     uint16_t* dst_s;   /* optional bf16x3 split image of dst:   [3][ld_dst/8][rows_s][8] */
     uint16_t* dst_ts;  /* optional bf16x3 split image of dst_t: [3][ld_t/8][rows_t][8]  */
     int rows_s;        /* image rows of dst_s (>= rows, rows past `rows` zero; 0 = rows) */
+    uint16_t* dst_cs;  /* optional chain image of dst (mode 2): dst_s's form, K in chain order */
+    uint16_t* dst_cts; /* optional chain image of dst_t (mode 2) */
+    int perm_k;        /* leading columns of dst_cs in chain order (multiple of 32) */
 } nerf_pack_desc;
 int nerf_pack_weights(const nerf_pack_desc* descs, int n, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Adam (torch.optim.Adam semantics, amsgrad False) over one flat fp32 buffer.
- * Replaces optimizer.step() (training.py:93-99).  hyper (device, 8 floats) =
- * {step, lr, beta1, beta2, eps, weight_decay, 1 - beta2, ticket} (1 - beta2 rounded once
- * from the caller's double, as torch passes it; 0 = derive it from the f32 beta2); the
- * bias corrections are taken in double; the update uses step + 1 and
- * the last workgroup to finish stores it back (one launch; a captured graph replays the
- * correct bias corrections).  hyper[7] is a completion counter: zero it once. */
+ * Replaces optimizer.step() (training.py:93-99): torch's foreach Adam op for op (lerp_, mul_,
+ * addcmul_, sqrt, div_, add_, addcdiv_).  hyper (device, 16 floats, 8-byte aligned; ABI 13) =
+ * {step, lr, beta1, beta2, eps, weight_decay, 1 - beta2, ticket, lr, beta1, beta2 as doubles in
+ * slots 8-13, 1 - beta1, 1.0}: 1 - beta1 / 1 - beta2 rounded once from the caller's doubles and
+ * the bias corrections lr / (1 - beta1^t), sqrt(1 - beta2^t) taken in double, as torch forms
+ * them (slot 15 != 1: the doubles are ignored and derived from the f32 slots; slot 6 == 0:
+ * 1 - beta2 from the f32 beta2).  The update uses step + 1 and the last workgroup to finish
+ * stores it back (one launch; a captured graph replays the correct bias corrections).
+ * hyper[7] is a completion counter: zero it once. */
 int nerf_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                    int64_t n, float* hyper, void* stream);
 

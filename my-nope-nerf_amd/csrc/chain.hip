@@ -712,25 +712,33 @@ __global__ __launch_bounds__(256) void k_mlp_chain_fwd(ChainFwdArgs p) {
 }
 
 // ---------------------------------------------------------------------------
-// The fused per-ray eval kernel at two waves per SIMD (k_render_fused2, the default of
-// nerf_render_eval_fused).  Same per-ray path as k_mlp_chain_fwd<true> -- samples and
-// encodings in the prologue, the ten linears with the activations resident in registers,
-// the heads in the l7 / colour-layer epilogues, the composite at the end -- but a block's 128
-// rows are 8 waves x 16 rows on v_mfma_f32_16x16x32_f16 instead of 4 waves x 32 rows on
-// 32x32x16: a wave's accumulators (16 rows x 256 outputs) and its A operand (16 rows x 256
-// as fp16 pairs) are 64 + 64 registers, so the kernel fits 256 registers and two waves share
-// each SIMD -- one wave's epilogue (unscale, bias, ReLU, re-split: VALU) runs beside the
-// other wave's MFMAs instead of leaving the matrix pipe idle (the 32-row kernel spends a
-// third of its cycles in epilogues at one wave per SIMD, profiles/r03/fused_eval_phases.txt).
+// The chains at two waves per SIMD: the fused per-ray eval kernel (k_render_fused2, the
+// default of nerf_render_eval_fused), the training forward (k_mlp_chain_train2) and the
+// input-gradient chain (k_mlp_chain_bwd).  Same per-ray path as k_mlp_chain_fwd -- the ten
+// linears with the activations resident in registers, the weights streaming through an LDS
+// ring -- but a block's 128 rows are 8 waves x 16 rows on v_mfma_f32_16x16x32_f16: a wave's
+// accumulators (16 rows x 256 outputs) and its A operand (16 rows x 256 as fp16 pairs) are 64
+// + 64 registers, so the kernels fit 256 registers and two waves share each SIMD.
 //
-// Operand-swapped 16x16x32 MFMAs: A = a weight fragment (lane l: feature l & 15, k = 8 (l >> 4)
-// .. + 7), B = an activation fragment (sample l & 15, the same k), so D[feature][sample] puts
-// sample l & 15 in lane l with features 4 (l >> 4) .. + 3 of the 16-feature tile.  The next
-// layer's fragment for k-step t needs features 32 t + 8 (l >> 4) .. + 7 of the lane's sample:
-// tiles 2 t and 2 t + 1 are re-split to fp16 pairs and moved between the 16-lane rows by one
-// v_permlane32_swap and one v_permlane16_swap per word (rows (A0 A1 A2 A3 | B0 B1 B2 B3) ->
-// (A0 A1 | A2 A3 | B0 B1 | B2 B3) pairs).
+// Operand-swapped 16x16x32 MFMAs: A = a weight fragment (lane l: image row l & 15, k = 8 (l >>
+// 4) .. + 7), B = an activation fragment (sample l & 15, the same k), so D[feature][sample]
+// puts sample l & 15 in lane l with features 16 j + 4 (l >> 4) .. + 3 of tile j (the "tile
+// layout").  The next layer's k-step t takes tiles 2t and 2t + 1 AS THEY LIE: lane (g, n)'s
+// eight k are features 32 t + 4 g + 0..3 and 32 t + 16 + 4 g + 0..3, and the weight images of
+// these kernels (nerf_pack_weights' chain images, dst_cs / dst_cts) hold their K columns in
+// that order (chain_perm).  No data moves between lanes to form an A fragment.
+//
+// Per value of an A operand: two v_fma_mix{lo,hi}_f16 (the fp16 pair hi = RNE(x 2^e), lo =
+// RNE(x 2^e - hi), read from the f32 epilogue value and the scale 2^e in place, msplit).  The
+// training kernels save what the next GEMMs need beside their MFMAs, from the same registers:
+// the f32 epilogue value (two float4 stores per tile pair), its column maxima over the
+// wave's 16 rows (two DPP steps per value with |.| modifiers, one LDS atomic max per lane
+// quad) and, in the forward, the ReLU words (from the fp16 hi words: two bits per
+// v_pk_min_u16 + v_dot2_u32_u16, one LDS atomic or per lane and k-step).
 // ---------------------------------------------------------------------------
+#ifndef NERF_CHAIN_STAMPS
+#define NERF_CHAIN_STAMPS 0   // diagnostic builds only (make EXTRA=-DNERF_CHAIN_STAMPS=1): phase stamps
+#endif
 namespace f2 {
 constexpr int NW = 8;                   // waves per block, two per SIMD
 constexpr int NTH = 64 * NW;            // threads
@@ -743,8 +751,9 @@ constexpr int FX_WD = 0, FX_WC = 256;   // fc_density weight [256], fc_rgb weigh
 // LDS map.  Eval: a 6-slot weight ring (two 32-k steps in flight) and the position-encoding
 // tile the prologue computes.  Training (TR): the encodings come from HBM, so their 32 KB go
 // to two more ring slots (three 32-k steps in flight: a store issued beside a k-step's
-// MFMAs has three k-steps to complete before a wait counts it, see wait_n) and the column
-// maxima of the block's 128-row group ([2 parities][256] uint, LDS atomics)
+// MFMAs has three k-steps to complete before a wait counts it, see wait_n), the column
+// maxima of the block's 128-row group ([2 parities][256] uint, LDS atomic max) and its ReLU
+// words ([2 parities][128 rows][8] uint, LDS atomic or)
 template <bool TR>
 struct LY {
     static constexpr int NSLOT = TR ? 8 : 6;
@@ -755,8 +764,9 @@ struct LY {
     static constexpr int O_BIAS = O_EXP + 2 * 256 * 4;        // [2][256] float
     static constexpr int O_ENC = O_BIAS + 2 * 256 * 4;        // eval: [128][64] float position encodings
     static constexpr int O_CMX = O_ENC;                       // training: [2][256] uint column maxima
-    static constexpr int O_RMX = O_ENC + (TR ? 2 * 256 * 4 : 128 * 64 * 4);   // eval: [4][128] row maxima
-    static constexpr int O_FX = O_RMX + 4 * 128 * 4;          // head weights, raw4 / z rows, view records
+    static constexpr int O_MSK = O_CMX + 2 * 256 * 4;         // training: [2][128][8] uint ReLU words
+    static constexpr int O_RMX = O_ENC + 128 * 64 * 4;        // eval: [4][128] row maxima
+    static constexpr int O_FX = TR ? O_MSK + 2 * 128 * 32 : O_RMX + 4 * 128 * 4;   // head weights, raw4, ...
     static constexpr int FX_FLOATS = TR ? FX_ENCD : FX_ENCD + (CROWS / 2) * ENCD_REC;
     static constexpr int BYTES = O_FX + FX_FLOATS * 4;
     static_assert(BYTES <= 160 * 1024, "LDS");
@@ -767,14 +777,11 @@ constexpr int dma_count(int tt) {
     return tt >= CT ? 0 : (L_OUT[layer_of(tt)] == 256 ? 2 : 1) + (kbase(layer_of(tt)) == tt ? 1 : 0);
 }
 
-constexpr int kSplitTile = 8;   // the MFMA tile (of 16) after which a k-step splits the next k-step's fragment
-
 // the counted waits.  Every 32-k step k (global over the chain) waits for the DMAs issued D
 // steps earlier; vmcnt counts loads, stores and LDS-DMA together in issue order, so the count
 // is every vector-memory op the wave issued after them: the later steps' DMAs and, in the
-// training kernel, the stores each step issues after its DMAs (the previous layer's
-// activation pieces, its ReLU words at step 7, at a layer's first step the column maxima of
-// the layer before).  Ops left out of the count only make a wait stricter.
+// training kernel, the stores each step issues after its DMAs (st_ops_k).  Ops left out of
+// the count only make a wait stricter.
 constexpr int nks(int l) { return L_KS[l] / 2; }
 constexpr int kfirst(int l) { return l == 0 ? 0 : kfirst(l - 1) + nks(l - 1); }
 constexpr int layer_of_k(int k) { int l = 0; while (l + 1 < CNL && kfirst(l + 1) <= k) ++l; return l; }
@@ -783,11 +790,14 @@ template <bool TR>
 constexpr int dma_ops_k(int k) {
     return dma_count(tt_of_k(k) + 2 * LY<TR>::D) + dma_count(tt_of_k(k) + 2 * LY<TR>::D + 1);
 }
+// training, layer l >= 1, k-step u: the previous layer's output is saved two float4 stores per
+// tile pair (pairs 0 and 1 at u = 0, pair u + 1 at u = 1..6); at u = 0 of l >= 2 layer l - 2's
+// column maxima and ReLU words leave LDS (one store each)
 template <bool TR>
 constexpr int st_ops_k(int k) {
     const int l = layer_of_k(k), u = k - kfirst(l);
     if (!TR || l == 0) return 0;
-    return (u < 8 ? 2 : 0) + (u == 7 && l - 1 != 8 ? 1 : 0) + (u == 0 && l >= 2 ? 1 : 0);
+    return u == 0 ? 4 + (l >= 2 ? 2 : 0) : (u <= 6 ? 2 : 0);
 }
 template <bool TR>
 constexpr int wait_n(int k) {
@@ -803,6 +813,7 @@ static_assert(wait_n<false>(0) == dma_count(2) + dma_count(3), "eval waits");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float pf2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f32x4 mfma16(const uint4& w, const uint4& a, const f32x4& c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(ch16x8, w), __builtin_bit_cast(ch16x8, a), c,
@@ -817,42 +828,81 @@ __device__ __forceinline__ uint32_t rows_or(uint32_t v) {
     const auto b = __builtin_amdgcn_permlane32_swap(r, r, false, false);
     return b[0] | b[1];
 }
+// the chains' row exponent: row_exp capped at 127 so that 2^e is an f32 (rows below 2^-113
+// keep a smaller scale; nothing overflows)
+__device__ __forceinline__ int chain_exp(float m) {
+    const int e = row_exp(m);
+    return e > 127 ? 127 : e;
+}
+
+// fp16 pair words of (x0, x1) at scale s = 2^e (exact): hi = RNE(x s) per half (two
+// v_fma_mix{lo,hi}_f16 x s + 0), lo = RNE(x s - hi) (x s - hi is exact in f32; the fp16 half
+// of hi is read in place) -- the bits of ldexp + v_cvt_pk_f16_f32 + residual + convert at half
+// the VALU
+__device__ __forceinline__ uint32_t mhi(float x0, float x1, float s) {
+    uint32_t h;
+    asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
+        "v_fma_mixhi_f16 %0, %3, %2, 0"
+        : "=&v"(h) : "v"(x0), "v"(s), "v"(x1));
+    return h;
+}
+__device__ __forceinline__ uint32_t mlo(float x0, float x1, float s, uint32_t h) {
+    uint32_t l;
+    asm("v_fma_mixlo_f16 %0, %1, %2, -%4 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %0, %3, %2, -%4 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "=&v"(l) : "v"(x0), "v"(s), "v"(x1), "v"(h));
+    return l;
+}
+// 16 bytes per lane from (g + voff) into LDS at lds + 16 lane; g and lds wave-uniform (SGPRs:
+// the address arithmetic is scalar), voff the lane's 16-byte offset
+__device__ __forceinline__ void dma16(const void* g, uint32_t voff, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(g), "s"(lds) : "memory", "m0");
+}
 
 struct State {
     char* lds;
+    uint32_t lds0;                      // LDS address of the block's buffer (wave-uniform)
     float* fx;
     int tid, wave, lane, n, g;          // n = lane & 15 (the lane's sample in the wave), g = lane >> 4
     size_t m0;
     int rl;                             // the lane's row in the block (16 wave + n)
+    uint32_t voff16;                    // 16 lane: the lane's offset in a 16-byte-per-lane LDS-DMA
+    int vrow;                           // (rl 256 + 4 g) 4: the lane's byte offset in a [128][256] f32 tile
     int er;                             // row exponent of the current A operand
-    uint32_t mk0, mk1;                  // training: the lane's two ReLU words of the previous layer
+    float ser;                          // 2^er
+    uint32_t mk0, mk1;                  // training: the colour layer's ReLU words
+    u16x2 rk0, rk1;                     // ReLU-bit weights {1, 2} << 4 g, {4, 8} << 4 g (relu_word)
     unsigned long long t_wait, t_bar, t_epi, t_pro, t_last, t_start;   // diagnostics (stamps): cycles in the
                                                        // k-step waits, barriers, layer epilogues, prologue
     uint4 act_hi[8], act_lo[8];         // A operand: 8 k-steps of 32 (the 256 activations)
     uint4 enc_hi[2], enc_lo[2];         // encoding segment (64 columns) of the current layer
     f32x4 acc[16];                      // 16 rows x 256 outputs
-    f32x4 xs[16];                       // the previous layer's outputs not yet split into act (k-step
-                                        // t + 1's tiles are split during k-step t: split_pieces)
+    f32x4 xs[16];                       // the previous epilogue's outputs (tile layout), split into act
+                                        // and saved during the next layer's k-steps
 };
 
-// diagnostics (nerf_chain_debug_stamps): cycles since the last tick into *bucket
+// diagnostics (nerf_chain_debug_stamps, NERF_CHAIN_STAMPS builds): cycles since the last tick
 __device__ __forceinline__ void tick(const ChainFwdArgs& p, State& st, unsigned long long* bucket) {
-    if (p.stamps == nullptr) return;
-    __builtin_amdgcn_sched_barrier(0);
-    const unsigned long long t = __builtin_amdgcn_s_memtime();
-    if (bucket) *bucket += t - st.t_last;
-    st.t_last = t;
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (NERF_CHAIN_STAMPS) {
+        if (p.stamps == nullptr) return;
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        if (bucket) *bucket += t - st.t_last;
+        st.t_last = t;
+        __builtin_amdgcn_sched_barrier(0);
+    }
 }
 
 // per block (wave 0): k-step waits, barriers, prologue, layer epilogues, total, and the tail
 // (from the last epilogue to here)
 __device__ __forceinline__ void write_stamps(const ChainFwdArgs& p, State& st) {
-    if (p.stamps && threadIdx.x == 0) {
-        const unsigned long long t = __builtin_amdgcn_s_memtime();
-        unsigned long long* o = p.stamps + (size_t)blockIdx.x * 6;
-        o[0] = st.t_wait; o[1] = st.t_bar; o[2] = st.t_pro; o[3] = st.t_epi;
-        o[4] = t - st.t_start; o[5] = t - st.t_last;
+    if constexpr (NERF_CHAIN_STAMPS) {
+        if (p.stamps && threadIdx.x == 0) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            unsigned long long* o = p.stamps + (size_t)blockIdx.x * 6;
+            o[0] = st.t_wait; o[1] = st.t_bar; o[2] = st.t_pro; o[3] = st.t_epi;
+            o[4] = t - st.t_start; o[5] = t - st.t_last;
+        }
     }
 }
 
@@ -860,7 +910,8 @@ __device__ __forceinline__ void write_stamps(const ChainFwdArgs& p, State& st) {
 // layer) + at a layer's first step one piece per wave: waves 0-3 the weight-row exponents
 // (64 image rows each), waves 4-7 the biases (16 lanes x 4 floats each); the 128-wide layer's
 // extra waves repeat the first ones (same bytes to the same place), so every wave issues the
-// same count (its vmcnt waits are compile-time)
+// same count (its vmcnt waits are compile-time).  A wave's piece is 64 consecutive image rows
+// of one plane and k-half: everything but the lane's 16-byte offset is wave-uniform
 template <int TT, bool TR>
 __device__ __forceinline__ void dma(const ChainFwdArgs& p, State& st) {
     using Y = LY<TR>;
@@ -870,24 +921,24 @@ __device__ __forceinline__ void dma(const ChainFwdArgs& p, State& st) {
         constexpr int ks = L_KS[l];
         constexpr int NO = L_OUT[l];
         const nerf_chain_layer& L = p.L[l];
-        char* slot = st.lds + Y::O_RING + (TT % Y::NSLOT) * SBYTES;
+        const char* img = reinterpret_cast<const char*>(L.img);
+        const uint32_t slot = st.lds0 + Y::O_RING + (TT % Y::NSLOT) * SBYTES;
 #pragma unroll
         for (int i = 0; i < (NO == 256 ? 2 : 1); ++i) {
-            const int c = st.tid + NTH * i;              // 16-byte chunk of the step's image rows
-            const int ph = c / NO, n = c % NO;           // plane * 2 + k-half (wave-uniform), image row
-            const uint32_t off = (uint32_t)(((ph >> 1) * (2 * ks) + 2 * s + (ph & 1)) * L.img_rows + n) * 16;
-            cdma16(L.img, off, slot + ph * SHALF + (n - st.lane) * 16);
+            const int ph = NO == 256 ? (st.wave >> 2) + 2 * i : (st.wave >> 1);   // plane * 2 + k-half
+            const int n0 = NO == 256 ? 64 * (st.wave & 3) : 64 * (st.wave & 1);   // first image row
+            const int chunk = (ph >> 1) * (2 * ks) + 2 * s + (ph & 1);
+            dma16(img + (chunk * NO + n0) * 16, st.voff16, slot + ph * SHALF + n0 * 16);
         }
         if constexpr (s == 0) {
             if (st.wave < 4) {
                 const int wr = NO == 256 ? st.wave : (st.wave & 1);
-                const int n = 64 * wr + st.lane;
-                cdma16(L.img, (uint32_t)((2 * (2 * ks) * L.img_rows + n) * 16),
-                       st.lds + Y::O_LEB + (l & 1) * 4096 + 64 * wr * 16);
+                dma16(img + ((2 * (2 * ks)) * NO + 64 * wr) * 16, st.voff16,
+                      st.lds0 + Y::O_LEB + (l & 1) * 4096 + 64 * wr * 16);
             } else if (st.lane < 16) {                   // one instruction, lanes 0-15 active
                 const int wb = NO == 256 ? st.wave - 4 : ((st.wave - 4) & 1);
-                cdma16(L.bias, (uint32_t)((64 * wb + 4 * st.lane) * 4),
-                       st.lds + Y::O_BIAS + ((l & 1) * 256 + 64 * wb) * 4);
+                dma16(reinterpret_cast<const char*>(L.bias) + 64 * wb * 4, st.voff16,
+                      st.lds0 + Y::O_BIAS + ((l & 1) * 256 + 64 * wb) * 4);
             } else {
                 // the other lanes of the bias instruction: masked off (the instruction is one
                 // vmcnt op for the wave either way)
@@ -904,147 +955,188 @@ __device__ __forceinline__ void dma_n(const ChainFwdArgs& p, State& st) {
     }
 }
 
-// the 8 consecutive encoding columns of this lane's k-chunk for k-step t (32 columns) of a
-// row, at exponent er -> fragment planes
-__device__ __forceinline__ void enc_frag(const float* row, int t, int g, int er, uint4& hi, uint4& lo) {
+// the 8 consecutive encoding columns 32 t + 8 g .. + 7 of a row (the encoding segments of the
+// chain images keep their natural column order) at scale s -> fragment planes
+__device__ __forceinline__ void enc_frag(const float* row, int t, int g, float s, uint4& hi, uint4& lo) {
     const float4* src = reinterpret_cast<const float4*>(row + 32 * t + 8 * g);
-    frag_from8(src[0], src[1], er, hi, lo);
+    const float4 a = src[0], b = src[1];
+    hi = make_uint4(mhi(a.x, a.y, s), mhi(a.z, a.w, s), mhi(b.x, b.y, s), mhi(b.z, b.w, s));
+    lo = make_uint4(mlo(a.x, a.y, s, hi.x), mlo(a.z, a.w, s, hi.y), mlo(b.x, b.y, s, hi.z), mlo(b.z, b.w, s, hi.w));
 }
 
-// training: the previous layer's output features 32 u + 8 g .. + 7 of the lane's row, rebuilt
-// from the fp16 pair this k-step feeds the MFMAs ((hi + lo) 2^-e: the value this layer
-// consumed, within 2^-22 relative of the f32 epilogue result) -> stored, its ReLU bits (word u,
-// bits 8 g ..) and its column maxima over the wave's 16 rows (a quad max by DPP, then LDS
-// atomics from the quads' first lanes).  The work is spread over the step's MFMA tiles (piece
-// j after tile j's MFMAs): the two waves of a SIMD reach their k-steps together, so short VALU
-// pieces between MFMA groups keep the matrix pipe fed where one block of VALU would not
-// (hi + lo) 2^-e from fp16 half K & 1 of the pair words: two v_fma_mix_f32 reading the fp16
-// halves in place, lo 2^-e then hi 2^-e + that -- both exact (power-of-two scale, the sum is
-// an f32), so the value is ldexp((float)hi + (float)lo, -e) bit for bit at half the VALU
-__device__ __forceinline__ float rebuilt(const uint4& ah, const uint4& al, int k, int er) {
-    const uint32_t h = (&ah.x)[k >> 1], l = (&al.x)[k >> 1];
-    const float s = __builtin_amdgcn_ldexpf(1.f, -er);
-    float t, v;
-    if (k & 1) {
-        asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(t) : "v"(l), "v"(s));
-        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(v) : "v"(h), "v"(s), "v"(t));
-    } else {
-        asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel_hi:[1,0,0]" : "=v"(t) : "v"(l), "v"(s));
-        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(v) : "v"(h), "v"(s), "v"(t));
-    }
-    return v;
-}
-typedef unsigned cu32x4 __attribute__((ext_vector_type(4)));
-// a float4 into a row-major [128 rows][W] f32 tile of one block through a buffer resource: the
-// lane's row / column byte offset in one VGPR, the block base in SGPRs, the k-step's column
-// offset an immediate -- no 64-bit per-lane address arithmetic per store
-template <int W>
-__device__ __forceinline__ void tile_store4(float* block_base, int voff, int imm_bytes, float a, float b, float c,
-                                            float d) {
-    const __amdgpu_buffer_rsrc_t r =
-        __builtin_amdgcn_make_buffer_rsrc((void*)block_base, (short)0, 128 * W * 4, 0x00020000);
-    const cu32x4 v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), __float_as_uint(d)};
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, imm_bytes, 0);
-}
-// max of |v| over the lane's quad as float bits (non-negative floats order like their bits):
-// v_and + two v_max_u32_dpp, no old-value moves or NaN canonicalisation
-__device__ __forceinline__ uint32_t quad_absmax_bits(float v) {
-    uint32_t b = __float_as_uint(v) & 0x7fffffffu;
-    b = max(b, (uint32_t)__builtin_amdgcn_mov_dpp((int)b, 0xB1, 0xF, 0xF, true));   // quad_perm [1,0,3,2]
-    b = max(b, (uint32_t)__builtin_amdgcn_mov_dpp((int)b, 0x4E, 0xF, 0xF, true));   // quad_perm [2,3,0,1]
-    return b;
-}
-template <int l, int u, int j, int ntj>
-__device__ __forceinline__ void save_piece(const ChainFwdArgs& p, State& st, const uint4& ah, const uint4& al,
-                                           uint32_t& bits) {
-    using Y = LY<true>;
-    const nerf_chain_layer& P = p.L[l - 1];
-    int rl = st.rl;
-    asm volatile("" : "+v"(rl));   // the row's address is rebuilt per piece, not kept live across layers
-    const size_t row = st.m0 + rl;
-    if constexpr (j == 1 || j == 2) {           // 4 features: store, ReLU bits
-        constexpr int k0 = 4 * (j - 1);
-        float v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = rebuilt(ah, al, k0 + k, st.er);
-        tile_store4<256>(P.out + st.m0 * 256, (rl * 256 + 8 * st.g) * 4, (32 * u + k0) * 4, v[0], v[1], v[2], v[3]);
-        {   // column maxima of these 4 features, from v
-            uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + Y::O_CMX) + ((l - 1) & 1) * 256 + 32 * u + 8 * st.g + k0;
-            uint32_t c[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) c[k] = quad_absmax_bits(v[k]);
-            if ((st.n & 3) == 0) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) atomicMax(cm + k, c[k]);
-            }
-        }
-        if constexpr (l - 1 != 8) {   // lf has no ReLU
-#pragma unroll
-            for (int k = 0; k < 4; ++k) bits |= (v[k] > 0.f ? 1u : 0u) << (k0 + k);
-            if constexpr (j == 2) {
-                const uint32_t w = rows_or(bits << (8 * st.g));
-                if constexpr (u & 1) st.mk1 = st.g == (u >> 1) ? w : st.mk1;
-                else st.mk0 = st.g == (u >> 1) ? w : st.mk0;
-                if constexpr (u == 7)
-                    *reinterpret_cast<uint2*>(P.mask + row * P.ldmask + 2 * st.g) = make_uint2(st.mk0, st.mk1);
-            }
-        }
-    }
-}
-
-// the next layer's A fragment for k-step t from the f32 tiles 2t, 2t + 1 at exponent st.er:
-// fp16 pairs, rows exchanged into the fragment layout ((A0 A1 A2 A3 | B0 B1 B2 B3) over the
-// 16-lane rows -> permlane32: (A0 A1 B0 B1 | A2 A3 B2 B3) -> permlane16: (A0 A2 B0 B2 | A1 A3
-// B1 B3): row r then holds its 8 consecutive features).  Two halves (split; exchange) so the
-// k-step can place them at two MFMA tiles
-struct SplitTmp { uint32_t ha0, la0, ha1, la1, hb0, lb0, hb1, lb1; };
-template <int t, bool MIX = true>
-__device__ __forceinline__ void split_a(State& st, SplitTmp& q) {
-    const int e = st.er;
+// k-step t's A fragment from tiles 2t, 2t + 1 of xs, in two halves (hi words, lo words)
+template <int t>
+__device__ __forceinline__ void split_hi(State& st) {
     const f32x4 A = st.xs[2 * t], B = st.xs[2 * t + 1];
-    csplit<MIX>(__builtin_amdgcn_ldexpf(A[0], e), __builtin_amdgcn_ldexpf(A[1], e), q.ha0, q.la0);
-    csplit<MIX>(__builtin_amdgcn_ldexpf(A[2], e), __builtin_amdgcn_ldexpf(A[3], e), q.ha1, q.la1);
-    csplit<MIX>(__builtin_amdgcn_ldexpf(B[0], e), __builtin_amdgcn_ldexpf(B[1], e), q.hb0, q.lb0);
-    csplit<MIX>(__builtin_amdgcn_ldexpf(B[2], e), __builtin_amdgcn_ldexpf(B[3], e), q.hb1, q.lb1);
+    const float s = st.ser;
+    st.act_hi[t] = make_uint4(mhi(A[0], A[1], s), mhi(A[2], A[3], s), mhi(B[0], B[1], s), mhi(B[2], B[3], s));
 }
 template <int t>
-__device__ __forceinline__ void split_b(State& st, const SplitTmp& q) {
-    const auto h0 = __builtin_amdgcn_permlane32_swap(q.ha0, q.hb0, false, false);
-    const auto h1 = __builtin_amdgcn_permlane32_swap(q.ha1, q.hb1, false, false);
-    const auto l0 = __builtin_amdgcn_permlane32_swap(q.la0, q.lb0, false, false);
-    const auto l1 = __builtin_amdgcn_permlane32_swap(q.la1, q.lb1, false, false);
-    const auto H0 = __builtin_amdgcn_permlane16_swap(h0[0], h0[1], false, false);
-    const auto H1 = __builtin_amdgcn_permlane16_swap(h1[0], h1[1], false, false);
-    const auto L0 = __builtin_amdgcn_permlane16_swap(l0[0], l0[1], false, false);
-    const auto L1 = __builtin_amdgcn_permlane16_swap(l1[0], l1[1], false, false);
-    st.act_hi[t] = make_uint4(H0[0], H1[0], H0[1], H1[1]);
-    st.act_lo[t] = make_uint4(L0[0], L1[0], L0[1], L1[1]);
+__device__ __forceinline__ void split_lo(State& st) {
+    const f32x4 A = st.xs[2 * t], B = st.xs[2 * t + 1];
+    const float s = st.ser;
+    const uint4 h = st.act_hi[t];
+    st.act_lo[t] = make_uint4(mlo(A[0], A[1], s, h.x), mlo(A[2], A[3], s, h.y), mlo(B[0], B[1], s, h.z),
+                              mlo(B[2], B[3], s, h.w));
 }
-// MFMA tiles of a k-step that carry the two split halves for the next k-step: the waves
-// sharing a SIMD (w, w + 4) take them half a step apart
-template <int ntj, bool second>
-constexpr int split_tile(int half) {
-    return ((second ? ntj / 2 : 0) + (ntj >= 16 ? kSplitTile : kSplitTile / 2) + half) % ntj;
+
+typedef unsigned cu32x4 __attribute__((ext_vector_type(4)));
+// a float4 into a row-major [128 rows][W] f32 tile of one block through a buffer resource: the
+// lane's row / column byte offset in one VGPR, the block base in SGPRs, the column offset an
+// immediate -- no 64-bit per-lane address arithmetic per store
+template <int W>
+__device__ __forceinline__ void tile_store4(float* block_base, int voff, int imm_bytes, const f32x4& x) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc((void*)block_base, (short)0, 128 * W * 4, 0x00020000);
+    const cu32x4 v = {__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]), __float_as_uint(x[3])};
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, imm_bytes, 0);
 }
-template <int l, int u, int j, int ntj, bool second, bool MIX>
-__device__ __forceinline__ void split_piece(State& st, SplitTmp& q) {
-    if constexpr (l > 0 && u + 1 < 8) {
-        if constexpr (j == split_tile<ntj, second>(0)) split_a<u + 1, MIX>(st, q);
-        if constexpr (j == split_tile<ntj, second>(1)) split_b<u + 1>(st, q);
+
+// column maxima of tile x's four features over the wave's 16 rows: max |x| over the lane
+// quad by two v_max_f32_dpp steps with |.| source modifiers (non-negative floats order as
+// their bits), then one LDS atomic max per quad leader.  The asm keeps the DPP hazard
+// explicit (a DPP source written by VALU needs two wait states: the s_nop; the second
+// step's sources are four instructions old) and the maxima out of the leaders' branch
+__device__ __forceinline__ void colmax4(const f32x4& x, uint32_t* cm, bool leader) {
+    float a0, a1, a2, a3;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %0, |%4|, |%4| quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_f32_dpp %1, |%5|, |%5| quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_f32_dpp %2, |%6|, |%6| quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_f32_dpp %3, |%7|, |%7| quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_f32_dpp %1, %1, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_f32_dpp %2, %2, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_f32_dpp %3, %3, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
+        : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
+        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]));
+    if (leader) {
+        atomicMax(cm + 0, __float_as_uint(a0));
+        atomicMax(cm + 1, __float_as_uint(a1));
+        atomicMax(cm + 2, __float_as_uint(a2));
+        atomicMax(cm + 3, __float_as_uint(a3));
     }
 }
 
-// weight fragments are read PF tiles ahead of their MFMAs (a ring of PF + 1 fragment pairs):
-// one tile gives a read the three MFMAs of the tile before it (~48 cycles x 2 waves) to land,
-// less than the LDS latency under eight waves' traffic
-template <bool TR>
-constexpr int pf_tiles() { return TR ? 1 : 3; }
+// the lane's ReLU bits of k-step t (features 32 t + 4 g + c -> bit 4 g + c, 32 t + 16 + 4 g +
+// c -> bit 16 + 4 g + c of word t) from the fp16 hi words of the pair: a value is kept by the
+// ReLU iff its hi half is non-zero (x >= +0, and hi = 0 exactly when x 2^e < 2^-25, i.e. when
+// the pair is (0, 0): the value the next layer consumed) -- v_pk_min_u16 gives two bits per
+// word, v_dot2_u32_u16 places them
+__device__ __forceinline__ uint32_t relu_word(const uint4& h, const State& st) {
+    uint32_t m0, m1, m2, m3;   // v_pk_min_u16 (the compiler would form min(x, 1) by compare + select)
+    asm("v_pk_min_u16 %0, %4, 1 op_sel_hi:[1,0]\n\t"
+        "v_pk_min_u16 %1, %5, 1 op_sel_hi:[1,0]\n\t"
+        "v_pk_min_u16 %2, %6, 1 op_sel_hi:[1,0]\n\t"
+        "v_pk_min_u16 %3, %7, 1 op_sel_hi:[1,0]"
+        : "=v"(m0), "=v"(m1), "=v"(m2), "=v"(m3) : "v"(h.x), "v"(h.y), "v"(h.z), "v"(h.w));
+    const u16x2 b0 = __builtin_bit_cast(u16x2, m0), b1 = __builtin_bit_cast(u16x2, m1);
+    const u16x2 b2 = __builtin_bit_cast(u16x2, m2), b3 = __builtin_bit_cast(u16x2, m3);
+    const uint32_t lo = __builtin_amdgcn_udot2(b1, st.rk1, __builtin_amdgcn_udot2(b0, st.rk0, 0u, false), false);
+    const uint32_t hi = __builtin_amdgcn_udot2(b3, st.rk1, __builtin_amdgcn_udot2(b2, st.rk0, 0u, false), false);
+    return lo | (hi << 16);
+}
 
-// tile j of a k-step (compile-time j, so the save pieces are placed between MFMA groups)
-template <int l, int u, bool TR, int j, int ntj, int nact>
+// Save pieces of the training kernels: tile pair t of xs (the previous epilogue's values,
+// features 32 t .. 32 t + 31) -- two float4 stores, the column maxima of each tile, the ReLU
+// word -- spread over the MFMA tiles of a k-step.  The placement (tile of each piece) for a
+// k-step of ntj tiles: pair 0 rides on k-step 0's first tiles, pair u + 1 on k-step u's later
+// tiles, behind its split (which it shares the xs registers with)
+enum Piece { P_SPLIT_HI_A, P_SPLIT_HI_B, P_SPLIT_LO_A, P_SPLIT_LO_B, P_STORE, P_CMAX_A, P_CMAX_B, P_RELU,
+             P0_STORE, P0_CMAX_A, P0_CMAX_B, P0_RELU };
+template <int ntj>
+constexpr int piece_tile(int piece) {
+    if constexpr (ntj == 16) {
+        constexpr int T[12] = {6, 7, 8, 9, 10, 11, 12, 13, 1, 2, 3, 4};
+        return T[piece];
+    } else {
+        constexpr int T[12] = {3, 3, 4, 4, 5, 6, 7, 7, 0, 1, 2, 2};
+        return T[piece];
+    }
+}
+// training: the save work of layer l's k-step u (the previous layer's output, P = p.L[l - 1]),
+// piece j of ntj
+template <int l, int u, int j, int ntj>
+__device__ __forceinline__ void save_pieces(const ChainFwdArgs& p, State& st) {
+    using Y = LY<true>;
+    if constexpr (l >= 1 && u < 8) {
+        const nerf_chain_layer& P = p.L[l - 1];
+        constexpr bool relu = l - 1 != 8;           // lf has no ReLU
+        constexpr int par = (l - 1) & 1;
+        // a per-piece opaque copy of the lane's LDS offsets (the compiler would otherwise keep
+        // every piece's address live across the chain)
+        // (the LDS offsets of the arrays are beyond a ds_* immediate: they ride in the base)
+        auto cm_at = [&](int t, int half) {
+            int o = Y::O_CMX + 16 * st.g;
+            asm volatile("" : "+v"(o));
+            return reinterpret_cast<uint32_t*>(st.lds + o) + par * 256 + 32 * t + 16 * half;
+        };
+        auto msk_at = [&](int t) {
+            int o = Y::O_MSK + 32 * st.rl;
+            asm volatile("" : "+v"(o));
+            return reinterpret_cast<uint32_t*>(st.lds + o) + par * 1024 + t;
+        };
+        const bool leader = (st.n & 3) == 0;
+        float* ob = P.out + st.m0 * 256;
+        if constexpr (u == 0) {
+            if constexpr (j == piece_tile<ntj>(P0_STORE)) {
+                tile_store4<256>(ob, st.vrow, 0, st.xs[0]);
+                tile_store4<256>(ob, st.vrow, 64, st.xs[1]);
+            }
+            if constexpr (j == piece_tile<ntj>(P0_CMAX_A)) colmax4(st.xs[0], cm_at(0, 0), leader);
+            if constexpr (j == piece_tile<ntj>(P0_CMAX_B)) colmax4(st.xs[1], cm_at(0, 1), leader);
+            if constexpr (relu && j == piece_tile<ntj>(P0_RELU)) atomicOr(msk_at(0), relu_word(st.act_hi[0], st));
+        }
+        if constexpr (u + 1 < 8) {
+            constexpr int t = u + 1;
+            if constexpr (j == piece_tile<ntj>(P_STORE)) {
+                tile_store4<256>(ob, st.vrow, 128 * t, st.xs[2 * t]);
+                tile_store4<256>(ob, st.vrow, 128 * t + 64, st.xs[2 * t + 1]);
+            }
+            if constexpr (j == piece_tile<ntj>(P_CMAX_A)) colmax4(st.xs[2 * t], cm_at(t, 0), leader);
+            if constexpr (j == piece_tile<ntj>(P_CMAX_B)) colmax4(st.xs[2 * t + 1], cm_at(t, 1), leader);
+            if constexpr (relu && j == piece_tile<ntj>(P_RELU)) atomicOr(msk_at(t), relu_word(st.act_hi[t], st));
+        }
+    }
+}
+
+// the next k-step's A fragment (tiles 2 (u + 1), 2 (u + 1) + 1 of the previous epilogue), in
+// four pieces
+template <int l, int u, int j, int ntj>
+__device__ __forceinline__ void split_pieces(State& st) {
+    if constexpr (l > 0 && u + 1 < 8) {
+        constexpr int t = u + 1;
+        const f32x4 A = st.xs[2 * t], B = st.xs[2 * t + 1];
+        const float s = st.ser;
+        if constexpr (j == piece_tile<ntj>(P_SPLIT_HI_A)) {
+            st.act_hi[t].x = mhi(A[0], A[1], s);
+            st.act_hi[t].y = mhi(A[2], A[3], s);
+        }
+        if constexpr (j == piece_tile<ntj>(P_SPLIT_HI_B)) {
+            st.act_hi[t].z = mhi(B[0], B[1], s);
+            st.act_hi[t].w = mhi(B[2], B[3], s);
+        }
+        if constexpr (j == piece_tile<ntj>(P_SPLIT_LO_A)) {
+            st.act_lo[t].x = mlo(A[0], A[1], s, st.act_hi[t].x);
+            st.act_lo[t].y = mlo(A[2], A[3], s, st.act_hi[t].y);
+        }
+        if constexpr (j == piece_tile<ntj>(P_SPLIT_LO_B)) {
+            st.act_lo[t].z = mlo(B[0], B[1], s, st.act_hi[t].z);
+            st.act_lo[t].w = mlo(B[2], B[3], s, st.act_hi[t].w);
+        }
+    }
+}
+
+// weight fragments are read PF tiles ahead of their MFMAs (a ring of PF + 1 fragment pairs)
+template <bool TR>
+constexpr int pf_tiles() { return TR ? 2 : 3; }
+
+// tile j of a k-step (compile-time j, so the pieces are placed between MFMA groups)
+template <int l, int u, bool TR, int j, int ntj>
 __device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, const uint4& ah, const uint4& al,
                                             const char* base, uint4 (&wh)[pf_tiles<TR>() + 1],
-                                            uint4 (&wl)[pf_tiles<TR>() + 1], uint32_t& bits, SplitTmp& q) {
+                                            uint4 (&wl)[pf_tiles<TR>() + 1]) {
     constexpr int PF = pf_tiles<TR>(), R = PF + 1;
     if constexpr (j < ntj) {
         if constexpr (j + PF < ntj) {
@@ -1055,17 +1147,17 @@ __device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, co
         st.acc[j] = mfma16(wh[j % R], al, st.acc[j]);   // hi . lo
         st.acc[j] = mfma16(wl[j % R], ah, st.acc[j]);   // lo . hi
         st.acc[j] = mfma16(wh[j % R], ah, st.acc[j]);   // hi . hi
-        if constexpr (TR && u < nact) save_piece<l, u, j, ntj>(p, st, ah, al, bits);
-        split_piece<l, u, j, ntj, false, !TR>(st, q);
+        split_pieces<l, u, j, ntj>(st);
+        if constexpr (TR) save_pieces<l, u, j, ntj>(p, st);
         __builtin_amdgcn_sched_barrier(0);
-        mstep_tiles<l, u, TR, j + 1, ntj, nact>(p, st, ah, al, base, wh, wl, bits, q);
+        mstep_tiles<l, u, TR, j + 1, ntj>(p, st, ah, al, base, wh, wl);
     }
 }
 
 // one 32-k MFMA step u of layer l (16-k steps TT, TT + 1): wait for its two slots, publish
 // them, refill the two slots step u - 1 read, 16 or 8 feature tiles x 3 products; training:
-// at the first step the column maxima of layer l - 2 leave LDS, and the steps from the
-// register tile save the previous layer's output (save_prev) beside the MFMAs
+// at the first step layer l - 2's column maxima and ReLU words leave LDS, and the steps from
+// the register tile save the previous layer's output beside the MFMAs
 template <int l, int u, bool TR>
 __device__ __forceinline__ void kstep(const ChainFwdArgs& p, State& st) {
     using Y = LY<TR>;
@@ -1086,13 +1178,18 @@ __device__ __forceinline__ void kstep(const ChainFwdArgs& p, State& st) {
             reinterpret_cast<float*>(st.lds + Y::O_EXP)[(l & 1) * 256 + st.tid] = __builtin_amdgcn_ldexpf(
                 1.f, -*reinterpret_cast<const int*>(st.lds + Y::O_LEB + (l & 1) * 4096 + st.tid * 16));
         if constexpr (TR && l >= 2) {
-            // layer l - 2's column maxima over the block's 128 rows (its 128-row group), complete
-            // since layer l - 1's last step: wave w stores features 32 w .. + 31 and clears them
+            // layer l - 2's column maxima over the block's 128 rows (its 128-row group) and its
+            // ReLU words, complete since layer l - 1's last step: wave w stores features 32 w ..
+            // + 31, lane (g, n) its row's words 2 g, 2 g + 1; both cleared for layer l
             if (st.lane < 32) {
                 uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + Y::O_CMX) + (l & 1) * 256 + 32 * st.wave + st.lane;
                 p.L[l - 2].cmax[(st.m0 / CROWS) * L_OUT[l - 2] + 32 * st.wave + st.lane] = __uint_as_float(*cm);
                 *cm = 0u;
             }
+            uint2* mw = reinterpret_cast<uint2*>(st.lds + Y::O_MSK + (l & 1) * 4096 + 32 * st.rl + 8 * st.g);
+            const nerf_chain_layer& Q = p.L[l - 2];
+            *reinterpret_cast<uint2*>(Q.mask + (st.m0 + st.rl) * Q.ldmask + 2 * st.g) = *mw;
+            *mw = make_uint2(0u, 0u);
         }
     }
     const uint4& ah = u < nact ? st.act_hi[u < nact ? u : 0] : st.enc_hi[u < nact ? 0 : u - nact];
@@ -1108,9 +1205,7 @@ __device__ __forceinline__ void kstep(const ChainFwdArgs& p, State& st) {
         wh[t] = *reinterpret_cast<const uint4*>(base + 256 * t);
         wl[t] = *reinterpret_cast<const uint4*>(base + 256 * t + SPLANE);
     }
-    uint32_t bits = 0;
-    SplitTmp q;
-    mstep_tiles<l, u, TR, 0, ntj, nact>(p, st, ah, al, base, wh, wl, bits, q);
+    mstep_tiles<l, u, TR, 0, ntj>(p, st, ah, al, base, wh, wl);
 }
 
 template <int l, int u, bool TR>
@@ -1142,7 +1237,7 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
     const float* le = reinterpret_cast<const float*>(st.lds + Y::O_EXP) + (l & 1) * 256 + g4;
     const float* lb = reinterpret_cast<const float*>(st.lds + Y::O_BIAS) + (l & 1) * 256 + g4;
     // unscale as (acc 2^-er) 2^-ew + b on packed-f32 ops: both scalings exact (powers of two
-    // in range: er <= 140 keeps 2^-er a float), one rounding, as ldexp(acc, -(er + ew)) + b
+    // in range), one rounding, as ldexp(acc, -(er + ew)) + b
     const float sr = __builtin_amdgcn_ldexpf(1.f, -st.er);
     const pf2 sr2 = {sr, sr};
     float rmx = 0.f, hs0 = 0.f, hs1 = 0.f, hs2 = 0.f;
@@ -1161,8 +1256,9 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
                                                   pf2{b4.z, b4.w});
         f32x4 x;
         x[0] = x01[0]; x[1] = x01[1]; x[2] = x23[0]; x[3] = x23[1];
-        if (relu) {
-            x[0] = fmaxf(x[0], 0.f); x[1] = fmaxf(x[1], 0.f); x[2] = fmaxf(x[2], 0.f); x[3] = fmaxf(x[3], 0.f);
+        if (relu) {   // as an integer max: every non-positive value (-0 included) becomes +0
+#pragma unroll
+            for (int c = 0; c < 4; ++c) x[c] = __int_as_float(max(__float_as_int(x[c]), 0));
         }
         st.xs[j] = x;
         rmx = fmaxf(rmx, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
@@ -1218,7 +1314,8 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
     }
     if constexpr (l < CNL - 1) {
         // next layer's A operand: row exponent over the row's 256 features (and the encoding
-        // the next layer joins), fp16 pairs, rows exchanged into the fragment layout
+        // the next layer joins), k-step 0's fp16 pairs now, the others during the next layer's
+        // k-steps (split_pieces)
         float m = fmaxf(rmx, __shfl_xor(rmx, 16, 64));
         m = fmaxf(m, __shfl_xor(m, 32, 64));
         const float* drec = st.fx + FX_ENCD + ENCD_REC * (st.rl / p.S);
@@ -1231,20 +1328,18 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
             }
         }
         if constexpr (l == 8) m = fmaxf(m, TR ? p.rd[st.m0 + st.rl] : drec[32]);
-        st.er = row_exp(m);
-        const int e = st.er;
-        // k-step 0's fragment now; the others during the next layer's k-steps (split_piece)
-        SplitTmp q;
-        split_a<0, !TR>(st, q);
-        split_b<0>(st, q);
+        st.er = chain_exp(m);
+        st.ser = __builtin_amdgcn_ldexpf(1.f, st.er);
+        split_hi<0>(st);
+        split_lo<0>(st);
         if constexpr (l == 3) {   // training: the encodings in HBM
             const float* er_row = TR ? p.enc_p + (st.m0 + st.rl) * 64
                                      : reinterpret_cast<const float*>(st.lds + Y::O_ENC) + st.rl * 64;
-            enc_frag(er_row, 0, st.g, e, st.enc_hi[0], st.enc_lo[0]);
-            enc_frag(er_row, 1, st.g, e, st.enc_hi[1], st.enc_lo[1]);
+            enc_frag(er_row, 0, st.g, st.ser, st.enc_hi[0], st.enc_lo[0]);
+            enc_frag(er_row, 1, st.g, st.ser, st.enc_hi[1], st.enc_lo[1]);
         }
         if constexpr (l == 8) {   // the view-direction encoding (27 columns + zeros)
-            enc_frag(TR ? p.enc_d + (st.m0 + st.rl) * 64 : drec, 0, st.g, e, st.enc_hi[0], st.enc_lo[0]);
+            enc_frag(TR ? p.enc_d + (st.m0 + st.rl) * 64 : drec, 0, st.g, st.ser, st.enc_hi[0], st.enc_lo[0]);
             st.enc_hi[1] = make_uint4(0u, 0u, 0u, 0u);
             st.enc_lo[1] = make_uint4(0u, 0u, 0u, 0u);
         }
@@ -1296,15 +1391,20 @@ __device__ __forceinline__ void encode_p(const ChainFwdArgs& p, State& st) {
 template <bool TR>
 __device__ __forceinline__ void init_state(State& st, char* smem) {
     st.lds = smem;
+    st.lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(clds_t*)smem);
     st.fx = reinterpret_cast<float*>(smem + LY<TR>::O_FX);
     st.tid = threadIdx.x;
     st.wave = __builtin_amdgcn_readfirstlane(st.tid >> 6);
     st.lane = st.tid & 63; st.n = st.lane & 15; st.g = st.lane >> 4;
     st.m0 = (size_t)blockIdx.x * CROWS;
     st.rl = 16 * st.wave + st.n;
+    st.voff16 = 16u * st.lane;
+    st.vrow = (st.rl * 256 + 4 * st.g) * 4;
     st.mk0 = st.mk1 = 0u;
+    st.rk0 = u16x2{(unsigned short)(1u << (4 * st.g)), (unsigned short)(2u << (4 * st.g))};
+    st.rk1 = u16x2{(unsigned short)(4u << (4 * st.g)), (unsigned short)(8u << (4 * st.g))};
     st.t_wait = st.t_bar = st.t_epi = st.t_pro = 0;
-    st.t_last = st.t_start = __builtin_amdgcn_s_memtime();
+    st.t_last = st.t_start = NERF_CHAIN_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
 }
 
 template <bool TR>
@@ -1338,10 +1438,11 @@ __global__ __launch_bounds__(512, 2) void k_render_fused2(ChainFwdArgs p) {
     __syncthreads();
     {
         const float* rp = reinterpret_cast<const float*>(smem + Y::O_RMX);
-        st.er = row_exp(fmaxf(fmaxf(rp[st.rl], rp[128 + st.rl]), fmaxf(rp[256 + st.rl], rp[384 + st.rl])));
+        st.er = chain_exp(fmaxf(fmaxf(rp[st.rl], rp[128 + st.rl]), fmaxf(rp[256 + st.rl], rp[384 + st.rl])));
+        st.ser = __builtin_amdgcn_ldexpf(1.f, st.er);
         const float* row = reinterpret_cast<const float*>(smem + Y::O_ENC) + st.rl * 64;
-        enc_frag(row, 0, st.g, st.er, st.enc_hi[0], st.enc_lo[0]);
-        enc_frag(row, 1, st.g, st.er, st.enc_hi[1], st.enc_lo[1]);
+        enc_frag(row, 0, st.g, st.ser, st.enc_hi[0], st.enc_lo[0]);
+        enc_frag(row, 1, st.g, st.ser, st.enc_hi[1], st.enc_lo[1]);
     }
     tick(p, st, &st.t_pro);
     chain_layers<false>(p, st);
@@ -1364,16 +1465,19 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_train2(ChainFwdArgs p) {
     init_state<true>(st, smem);
     // l0's A operand straight from HBM, before any LDS-DMA is in flight (the compiler waits
     // for ordinary loads with vmcnt(0))
-    st.er = row_exp(p.rp[st.m0 + st.rl]);
+    st.er = chain_exp(p.rp[st.m0 + st.rl]);
+    st.ser = __builtin_amdgcn_ldexpf(1.f, st.er);
     {
         const float* row = p.enc_p + (st.m0 + st.rl) * 64;
-        enc_frag(row, 0, st.g, st.er, st.enc_hi[0], st.enc_lo[0]);
-        enc_frag(row, 1, st.g, st.er, st.enc_hi[1], st.enc_lo[1]);
+        enc_frag(row, 0, st.g, st.ser, st.enc_hi[0], st.enc_lo[0]);
+        enc_frag(row, 1, st.g, st.ser, st.enc_hi[1], st.enc_lo[1]);
         opaque(st.enc_hi[0]); opaque(st.enc_lo[0]); opaque(st.enc_hi[1]); opaque(st.enc_lo[1]);
     }
     if (st.tid < 256) st.fx[FX_WD + st.tid] = p.wd[st.tid];
     for (int e = st.tid; e < 384; e += NTH) st.fx[FX_WC + e] = p.wc[e];
-    reinterpret_cast<uint32_t*>(smem + Y::O_CMX)[st.tid] = 0u;   // both column-max parities (512 words)
+    // both column-max parities (512 words) and both ReLU-word parities (2048 words) cleared
+    reinterpret_cast<uint32_t*>(smem + Y::O_CMX)[st.tid] = 0u;
+    reinterpret_cast<uint4*>(smem + Y::O_MSK)[st.tid] = make_uint4(0u, 0u, 0u, 0u);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     dma_n<0, 2 * Y::D, true>(p, st);
     tick(p, st, &st.t_pro);
@@ -1398,13 +1502,13 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_train2(ChainFwdArgs p) {
 // term d sigma_raw x w_density at the feature layer, official_nerf.py:66), masked by the
 // ReLU bits of the layer's input, is the next layer's dy.  A block keeps its 128 rows' dy
 // resident in registers as row-scaled fp16 pairs through all nine input gradients -- the
-// layer loop of k_mlp_chain_train2 with the weight-transpose images (rows = input features)
-// streaming through the LDS ring -- and saves every dy beside the next layer's MFMAs for the
-// weight gradients: f32 (rebuilt from the pair it consumed), per-128-row-group column maxima
-// and row maxima.  Against nine input-gradient launches this removes the read of every dy
-// (134 MB per 256-wide layer at 1024 x 128 samples), the in-kernel split of every A operand,
-// eight launch gaps and k_heads_dyr: the first dy (the colour layer's, dyr) is computed in
-// the prologue from graw4, fc_rgb and the colour layer's ReLU words (k_heads_dyr's
+// layer loop of k_mlp_chain_train2 with the weight-transpose chain images (rows = input
+// features, K in chain_perm order) streaming through the LDS ring -- and saves every dy beside
+// the next layer's MFMAs for the weight gradients: the f32 value, per-128-row-group column
+// maxima and row maxima.  Against nine input-gradient launches this removes the read of every
+// dy (134 MB per 256-wide layer at 1024 x 128 samples), the in-kernel split of every A
+// operand, eight launch gaps and k_heads_dyr: the first dy (the colour layer's, dyr) is
+// computed in the prologue from graw4, fc_rgb and the colour layer's ReLU words (k_heads_dyr's
 // arithmetic, render.hip).
 // Layer order i = 0..8: the colour layer (K = 128), lf, l7, ..., l1.  D_i is layer i's A
 // operand: D_0 = dyr, D_{i+1} = layer i's output; D_9 (the gradient at l0's output) is
@@ -1419,8 +1523,10 @@ using f2::NTH;
 using f2::SBYTES;
 using f2::SHALF;
 using f2::SPLANE;
+using f2::piece_tile;
 constexpr int NL = 9;
 constexpr int KS_[NL] = {8, 16, 16, 16, 16, 16, 16, 16, 16};   // 16-k steps: the layer's output width / 16
+constexpr int KPB[NL] = {320, 256, 256, 256, 256, 320, 256, 256, 256};   // W^T image rows (the layer's padded K)
 constexpr int kb(int i) { return i == 0 ? 0 : kb(i - 1) + KS_[i - 1]; }
 constexpr int CTB = kb(NL);
 constexpr int layer_of(int tt) { int i = 0; while (i + 1 < NL && kb(i + 1) <= tt) ++i; return i; }
@@ -1434,11 +1540,13 @@ constexpr int kfirst(int i) { return i == 0 ? 0 : kfirst(i - 1) + nks(i - 1); }
 constexpr int layer_of_k(int k) { int i = 0; while (i + 1 < NL && kfirst(i + 1) <= k) ++i; return i; }
 constexpr int tt_of_k(int k) { return kb(layer_of_k(k)) + 2 * (k - kfirst(layer_of_k(k))); }
 constexpr int dma_ops_k(int k) { return dma_count(tt_of_k(k) + 2 * D) + dma_count(tt_of_k(k) + 2 * D + 1); }
-// stores of 32-k step k, all issued after its DMAs: the two dy pieces, at a layer's first
-// step the previous dy's column maxima, at a layer's last step the epilogue's row-max store
+// stores of 32-k step k, all issued after its DMAs: the D_i pair stores (pairs 0 and 1 at u =
+// 0, pair u + 1 at u = 1 .. nks - 2), at a layer's first step the previous dy's column maxima,
+// at a layer's last step the epilogue's row-max store
 constexpr int st_ops_k(int k) {
     const int i = layer_of_k(k), u = k - kfirst(i);
-    return 2 + (u == 0 && i >= 1 ? 1 : 0) + (u == nks(i) - 1 && i < NL - 1 ? 1 : 0);
+    return (u == 0 ? 4 : (u + 1 < nks(i) ? 2 : 0)) + (u == 0 && i >= 1 ? 1 : 0) +
+           (u == nks(i) - 1 && i < NL - 1 ? 1 : 0);
 }
 // the counted wait of 32-k step k: for the DMAs issued D steps earlier (vmcnt counts loads,
 // stores and LDS-DMA together in issue order; ops left out only make a wait stricter)
@@ -1470,29 +1578,31 @@ __device__ __forceinline__ void dma(const nerf_chain_bwd& p, State& st) {
         constexpr int i = layer_of(TT);
         constexpr int s = TT - kb(i);
         constexpr int ks = KS_[i];
-        const uint16_t* img = p.wt_img[i];
-        const int rows = p.wt_img_rows[i];
-        char* slot = st.lds + O_RING + (TT % NSLOT) * SBYTES;
+        const char* img = reinterpret_cast<const char*>(p.wt_img[i]);
+        constexpr int rows = KPB[i];   // image rows (checked by the host entry)
+        const uint32_t slot = st.lds0 + O_RING + (TT % NSLOT) * SBYTES;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-            const int c = st.tid + NTH * q;             // 16-byte chunk of the step's 256 image rows
-            const int ph = c >> 8, n = c & 255;         // plane * 2 + k-half (wave-uniform), image row
-            const uint32_t off = (uint32_t)((((ph >> 1) * (2 * ks) + 2 * s + (ph & 1)) * rows + n) * 16);
-            cdma16(img, off, slot + ph * SHALF + (n - st.lane) * 16);
+            const int ph = (st.wave >> 2) + 2 * q;      // plane * 2 + k-half
+            const int n0 = 64 * (st.wave & 3);          // first image row of the wave's piece
+            const int chunk = (ph >> 1) * (2 * ks) + 2 * s + (ph & 1);
+            f2::dma16(img + (chunk * rows + n0) * 16, st.voff16, slot + ph * SHALF + n0 * 16);
         }
         if constexpr (s == 0) {
             if (st.wave < 4 || i == 0) {
                 // the weight-row exponents (plane 2, chunk 0 of each image row); the colour
                 // layer (its input f has no ReLU) repeats them on waves 4-7: same bytes, same place
                 const int w = st.wave & 3;
-                cdma16(img, (uint32_t)((2 * (2 * ks) * rows + 64 * w + st.lane) * 16),
-                       st.lds + O_LEB + (i & 1) * 4096 + 64 * w * 16);
+                f2::dma16(img + ((2 * (2 * ks)) * rows + 64 * w) * 16, st.voff16,
+                          st.lds0 + O_LEB + (i & 1) * 4096 + 64 * w * 16);
             } else {
                 // the block's ReLU words of the layer input: wave 4 + w rows 32 w .. 32 w + 31
+                // (two lanes per row, 16 bytes each)
                 const int w = st.wave - 4;
-                const int r = 32 * w + (st.lane >> 1);
-                cdma16(p.in_mask[i] + st.m0 * p.ld_in_mask[i], (uint32_t)((r * p.ld_in_mask[i] + 4 * (st.lane & 1)) * 4),
-                       st.lds + O_MASK + (i & 1) * 4096 + 32 * w * 32);
+                const int ld = p.ld_in_mask[i];
+                f2::dma16(reinterpret_cast<const char*>(p.in_mask[i] + (st.m0 + 32 * w) * ld),
+                          (uint32_t)(((st.lane >> 1) * ld + 4 * (st.lane & 1)) * 4),
+                          st.lds0 + O_MASK + (i & 1) * 4096 + 32 * w * 32);
             }
         }
     }
@@ -1505,27 +1615,62 @@ __device__ __forceinline__ void dma_n(const nerf_chain_bwd& p, State& st) {
     }
 }
 
-// D_i's features 32 u + 8 g + k0 .. + 3 of the lane's row, rebuilt from the pair this k-step
-// consumes: stored, and their column maxima over the wave's 16 rows (DPP quad max, then LDS
-// atomics from the quads' first lanes) into the parity-(i & 1) array
+// D_i's save work at layer i's k-step u, piece j: pair stores and the column maxima (parity
+// i & 1) of tiles 2t, 2t + 1 (pair 0 and 1 at u = 0, pair u + 1 later)
 template <int i, int u, int j>
-__device__ __forceinline__ void save_piece(const nerf_chain_bwd& p, State& st, const uint4& ah, const uint4& al) {
-    if constexpr (j == 1 || j == 2) {
-        constexpr int k0 = 4 * (j - 1);
-        int rl = st.rl;
-        asm volatile("" : "+v"(rl));
-        float v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = f2::rebuilt(ah, al, k0 + k, st.er);
-        constexpr int W = i == 0 ? 128 : 256;   // D_0 = dyr is 128 wide
-        f2::tile_store4<W>(p.dy[i] + st.m0 * W, (rl * W + 8 * st.g) * 4, (32 * u + k0) * 4, v[0], v[1], v[2], v[3]);
-        uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + O_CMX) + (i & 1) * 256 + 32 * u + 8 * st.g + k0;
-        uint32_t c[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) c[k] = f2::quad_absmax_bits(v[k]);
-        if ((st.n & 3) == 0) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) atomicMax(cm + k, c[k]);
+__device__ __forceinline__ void save_pieces(const nerf_chain_bwd& p, State& st) {
+    using f2::Piece;
+    constexpr int W = i == 0 ? 128 : 256;   // D_0 = dyr is 128 wide
+    constexpr int npair = W / 32;
+    auto cm_at = [&](int t, int half) {
+        int o = O_CMX + 16 * st.g;
+        asm volatile("" : "+v"(o));
+        return reinterpret_cast<uint32_t*>(st.lds + o) + (i & 1) * 256 + 32 * t + 16 * half;
+    };
+    const bool leader = (st.n & 3) == 0;
+    float* ob = p.dy[i] + st.m0 * W;
+    int vrow = st.vrow;
+    if constexpr (W != 256) vrow = (st.rl * W + 4 * st.g) * 4;
+    if constexpr (u == 0) {
+        if constexpr (j == piece_tile<16>(f2::P0_STORE)) {
+            f2::tile_store4<W>(ob, vrow, 0, st.xs[0]);
+            f2::tile_store4<W>(ob, vrow, 64, st.xs[1]);
+        }
+        if constexpr (j == piece_tile<16>(f2::P0_CMAX_A)) f2::colmax4(st.xs[0], cm_at(0, 0), leader);
+        if constexpr (j == piece_tile<16>(f2::P0_CMAX_B)) f2::colmax4(st.xs[1], cm_at(0, 1), leader);
+    }
+    if constexpr (u + 1 < npair) {
+        constexpr int t = u + 1;
+        if constexpr (j == piece_tile<16>(f2::P_STORE)) {
+            f2::tile_store4<W>(ob, vrow, 128 * t, st.xs[2 * t]);
+            f2::tile_store4<W>(ob, vrow, 128 * t + 64, st.xs[2 * t + 1]);
+        }
+        if constexpr (j == piece_tile<16>(f2::P_CMAX_A)) f2::colmax4(st.xs[2 * t], cm_at(t, 0), leader);
+        if constexpr (j == piece_tile<16>(f2::P_CMAX_B)) f2::colmax4(st.xs[2 * t + 1], cm_at(t, 1), leader);
+    }
+}
+
+template <int i, int u, int j>
+__device__ __forceinline__ void split_pieces(State& st) {
+    if constexpr (u + 1 < nks(i)) {
+        constexpr int t = u + 1;
+        const f2::f32x4 A = st.xs[2 * t], B = st.xs[2 * t + 1];
+        const float s = st.ser;
+        if constexpr (j == piece_tile<16>(f2::P_SPLIT_HI_A)) {
+            st.act_hi[t].x = f2::mhi(A[0], A[1], s);
+            st.act_hi[t].y = f2::mhi(A[2], A[3], s);
+        }
+        if constexpr (j == piece_tile<16>(f2::P_SPLIT_HI_B)) {
+            st.act_hi[t].z = f2::mhi(B[0], B[1], s);
+            st.act_hi[t].w = f2::mhi(B[2], B[3], s);
+        }
+        if constexpr (j == piece_tile<16>(f2::P_SPLIT_LO_A)) {
+            st.act_lo[t].x = f2::mlo(A[0], A[1], s, st.act_hi[t].x);
+            st.act_lo[t].y = f2::mlo(A[2], A[3], s, st.act_hi[t].y);
+        }
+        if constexpr (j == piece_tile<16>(f2::P_SPLIT_LO_B)) {
+            st.act_lo[t].z = f2::mlo(B[0], B[1], s, st.act_hi[t].z);
+            st.act_lo[t].w = f2::mlo(B[2], B[3], s, st.act_hi[t].w);
         }
     }
 }
@@ -1534,7 +1679,7 @@ constexpr int PF = 3;   // weight fragments read PF tiles ahead of their MFMAs (
 
 template <int i, int u, int j>
 __device__ __forceinline__ void tiles(const nerf_chain_bwd& p, State& st, const uint4& ah, const uint4& al,
-                                      const char* base, uint4 (&wh)[PF + 1], uint4 (&wl)[PF + 1], f2::SplitTmp& q) {
+                                      const char* base, uint4 (&wh)[PF + 1], uint4 (&wl)[PF + 1]) {
     constexpr int R = PF + 1;
     if constexpr (j < 16) {
         if constexpr (j + PF < 16) {
@@ -1545,15 +1690,10 @@ __device__ __forceinline__ void tiles(const nerf_chain_bwd& p, State& st, const 
         st.acc[j] = f2::mfma16(wh[j % R], al, st.acc[j]);   // hi . lo
         st.acc[j] = f2::mfma16(wl[j % R], ah, st.acc[j]);   // lo . hi
         st.acc[j] = f2::mfma16(wh[j % R], ah, st.acc[j]);   // hi . hi
-        save_piece<i, u, j>(p, st, ah, al);
-        // the next k-step's A fragment from the previous epilogue's f32 tiles (layer 0's are
-        // all split in the prologue)
-        if constexpr (i >= 1 && u + 1 < nks(i)) {
-            if constexpr (j == f2::split_tile<16, false>(0)) f2::split_a<u + 1>(st, q);
-            if constexpr (j == f2::split_tile<16, false>(1)) f2::split_b<u + 1>(st, q);
-        }
+        split_pieces<i, u, j>(st);
+        save_pieces<i, u, j>(p, st);
         __builtin_amdgcn_sched_barrier(0);
-        tiles<i, u, j + 1>(p, st, ah, al, base, wh, wl, q);
+        tiles<i, u, j + 1>(p, st, ah, al, base, wh, wl);
     }
 }
 
@@ -1595,8 +1735,7 @@ __device__ __forceinline__ void kstep(const nerf_chain_bwd& p, State& st) {
         wh[t] = *reinterpret_cast<const uint4*>(base + 256 * t);
         wl[t] = *reinterpret_cast<const uint4*>(base + 256 * t + SPLANE);
     }
-    f2::SplitTmp q;
-    tiles<i, u, 0>(p, st, ah, al, base, wh, wl, q);
+    tiles<i, u, 0>(p, st, ah, al, base, wh, wl);
 }
 
 template <int i, int u>
@@ -1608,8 +1747,8 @@ __device__ __forceinline__ void ksteps(const nerf_chain_bwd& p, State& st) {
 }
 
 // layer i: k-loop, then the epilogue -- unscale, the feature layer's rank-one term, the
-// input's ReLU mask -> D_{i+1} (features 16 j + 4 g + c of the lane's row), its row max and
-// the next A operand (k-step 0 now, the rest during the next layer's k-steps); the last
+// input's ReLU mask -> D_{i+1} (features 16 j + 4 g + c of the lane's row, tile layout), its
+// row max and k-step 0's A fragment (the rest during the next layer's k-steps); the last
 // layer stores D_9 and its column maxima here
 template <int i>
 __device__ __forceinline__ void layer(const nerf_chain_bwd& p, State& st) {
@@ -1643,25 +1782,17 @@ __device__ __forceinline__ void layer(const nerf_chain_bwd& p, State& st) {
             const float4 w4 = *reinterpret_cast<const float4*>(st.fx + f0);
             x[0] += st.gr0 * w4.x; x[1] += st.gr0 * w4.y; x[2] += st.gr0 * w4.z; x[3] += st.gr0 * w4.w;
         }
-        if constexpr (i >= 1) {
+        if constexpr (i >= 1) {   // the input's ReLU bits: all-ones / zero masks by a signed bit extract
             const uint32_t bits = mw[j >> 1] >> ((j & 1) * 16 + g4);
-            x[0] = (bits & 1u) ? x[0] : 0.f;
-            x[1] = (bits & 2u) ? x[1] : 0.f;
-            x[2] = (bits & 4u) ? x[2] : 0.f;
-            x[3] = (bits & 8u) ? x[3] : 0.f;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                x[c] = __int_as_float(__float_as_int(x[c]) & __builtin_amdgcn_sbfe((int)bits, c, 1));
         }
         st.xs[j] = x;
         rmx = fmaxf(rmx, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
         if constexpr (last) {
-            *reinterpret_cast<float4*>(p.dy[NL] + (st.m0 + st.rl) * p.lddy[NL] + f0) = make_float4(x[0], x[1], x[2], x[3]);
-            uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + O_CMX) + (NL & 1) * 256 + f0;
-            uint32_t c[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) c[k] = f2::quad_absmax_bits(x[k]);
-            if ((st.n & 3) == 0) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) atomicMax(cm + k, c[k]);
-            }
+            f2::tile_store4<256>(p.dy[NL] + st.m0 * 256, st.vrow, 64 * j, x);
+            f2::colmax4(x, reinterpret_cast<uint32_t*>(st.lds + O_CMX) + (NL & 1) * 256 + f0, (st.n & 3) == 0);
         }
     }
     // the row's max over its four 16-lane rows (lanes n, n + 16, n + 32, n + 48)
@@ -1669,10 +1800,10 @@ __device__ __forceinline__ void layer(const nerf_chain_bwd& p, State& st) {
     m = fmaxf(m, __shfl_xor(m, 32, 64));
     if (st.g == 0) p.dy_rmax[i + 1][st.m0 + st.rl] = m;
     if constexpr (!last) {
-        st.er = row_exp(m);
-        f2::SplitTmp q;
-        f2::split_a<0>(st, q);
-        f2::split_b<0>(st, q);
+        st.er = f2::chain_exp(m);
+        st.ser = __builtin_amdgcn_ldexpf(1.f, st.er);
+        f2::split_hi<0>(st);
+        f2::split_lo<0>(st);
     }
 }
 
@@ -1684,12 +1815,15 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_bwd(ChainBwdArgs args) {
     __shared__ __attribute__((aligned(16))) char smem[BYTES];
     State st;
     st.lds = smem;
+    st.lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(clds_t*)smem);
     st.fx = reinterpret_cast<float*>(smem + O_FX);
     st.tid = threadIdx.x;
     st.wave = __builtin_amdgcn_readfirstlane(st.tid >> 6);
     st.lane = st.tid & 63; st.n = st.lane & 15; st.g = st.lane >> 4;
     st.m0 = (size_t)blockIdx.x * CROWS;
     st.rl = 16 * st.wave + st.n;
+    st.voff16 = 16u * st.lane;
+    st.vrow = (st.rl * 256 + 4 * st.g) * 4;
     // head weights into LDS, both column-max parities cleared
     if (st.tid < 256) st.fx[st.tid] = p.wd[st.tid];
     for (int e = st.tid; e < 384; e += NTH) st.fx[256 + e] = p.wc[e];
@@ -1700,28 +1834,26 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_bwd(ChainBwdArgs args) {
     st.gr0 = gr.x;
     __syncthreads();
     // D_0 = dyr: (d rgb logits) . fc_rgb, gated by the colour layer's ReLU bits (render.hip
-    // k_heads_dyr), the lane's features 32 t + 8 g + e -- already the fragment layout
-    float d[4][8];
+    // k_heads_dyr), in the tile layout of an epilogue output: xs[j][c] = feature 16 j + 4 g + c
     float m = 0.f;
     const uint32_t mwr[4] = {mr.x, mr.y, mr.z, mr.w};
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int j = 0; j < 8; ++j)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int f = 32 * t + 8 * st.g + e;
+        for (int c = 0; c < 4; ++c) {
+            const int f = 16 * j + 4 * st.g + c;
             float v = fmaf(gr.w, st.fx[256 + 256 + f], fmaf(gr.z, st.fx[256 + 128 + f], gr.y * st.fx[256 + f]));
-            v = ((mwr[t] >> (8 * st.g + e)) & 1u) ? v : 0.f;
-            d[t][e] = v;
+            v = ((mwr[j >> 1] >> ((j & 1) * 16 + 4 * st.g + c)) & 1u) ? v : 0.f;
+            st.xs[j][c] = v;
             m = fmaxf(m, fabsf(v));
         }
     m = fmaxf(m, __shfl_xor(m, 16, 64));
     m = fmaxf(m, __shfl_xor(m, 32, 64));
     if (st.g == 0) p.dy_rmax[0][row] = m;
-    st.er = row_exp(m);
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-        frag_from8(make_float4(d[t][0], d[t][1], d[t][2], d[t][3]), make_float4(d[t][4], d[t][5], d[t][6], d[t][7]),
-                   st.er, st.act_hi[t], st.act_lo[t]);
+    st.er = f2::chain_exp(m);
+    st.ser = __builtin_amdgcn_ldexpf(1.f, st.er);
+    f2::split_hi<0>(st);
+    f2::split_lo<0>(st);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     dma_n<0, 2 * D>(p, st);
     layer<0>(p, st);
@@ -1743,7 +1875,6 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_bwd(ChainBwdArgs args) {
     const int par = tid >> 8, f = tid & 255;
     p.dy_cmax[NL - 1 + par][grp * 256 + f] = __uint_as_float(reinterpret_cast<const uint32_t*>(smem + O_CMX)[tid]);
 }
-
 }  // namespace nerf
 
 using namespace nerf;
@@ -1793,9 +1924,9 @@ extern "C" int nerf_mlp_chain_train(const float* enc_p, const float* enc_d, cons
     for (int l = 0; l < CNL; ++l) {
         const nerf_chain_layer& L = layers[l];
         NERF_CHECK(L.img && L.bias, "%s: layer %d needs its weight image and bias", __func__, l);
-        NERF_CHECK((((uintptr_t)L.bias) & 15u) == 0 && (((uintptr_t)L.img) & 15u) == 0 && L.img_rows >= L_OUT[l],
-                   "%s: layer %d: image / bias not 16-byte aligned or image rows %d < %d", __func__, l, L.img_rows,
-                   L_OUT[l]);
+        NERF_CHECK((((uintptr_t)L.bias) & 15u) == 0 && (((uintptr_t)L.img) & 15u) == 0 && L.img_rows == L_OUT[l],
+                   "%s: layer %d: image / bias not 16-byte aligned or chain image rows %d != %d", __func__, l,
+                   L.img_rows, L_OUT[l]);
         // every output is mandatory: the k-steps' vmcnt waits count these stores at compile time
         NERF_CHECK(L.out && L.ldo >= L_OUT[l] && L.ldo % 4 == 0 && (((uintptr_t)L.out) & 15u) == 0 &&
                        (l == CNL - 1 || L.ldo == 256),
@@ -1811,13 +1942,14 @@ extern "C" int nerf_mlp_chain_train(const float* enc_p, const float* enc_d, cons
     }
     a.wd = wd; a.bd = bd; a.wc = wc; a.bc = bc; a.raw4 = raw4;
     a.stamps = g_chain_stamps;
-    // algorithmic work per row: the ten linears (padded K: 64, 256 x 3, 320, 256 x 4, colour 320)
-    // + both heads; HBM: the two encodings read, every output (f32), ReLU word and raw4 written
+    // algorithmic work per row: the ten linears over their unpadded inputs (63, 256 x 3, 319,
+    // 256 x 4, colour 283) + both heads = 593 408 MACs; HBM: the two encodings
+    // read, every output (f32), ReLU word and raw4 written
     const double rows = (double)n_pad;
     prof_next(NERF_PROF_CHAIN_FWD, rows * (2 * 64 * 4 + 9 * 256 * 4 + 128 * 4 + 9 * 32 + 4 * 4));
     prof_begin(as_stream(stream));
     hipLaunchKernelGGL(k_mlp_chain_train2, dim3(n_pad / CROWS), dim3(f2::NTH), 0, as_stream(stream), a);
-    prof_end(as_stream(stream), 2.0 * rows * (256.0 * 64 + 7 * 256 * 256 + 256 * 320 + 128 * 320 + 4 * 256), 3);
+    prof_end(as_stream(stream), 2.0 * rows * (256.0 * 63 + 7 * 256 * 256 + 256 * 319 + 128 * 283 + 256 + 3 * 128), 3);
     return check_launch(__func__);
 }
 
@@ -1841,9 +1973,9 @@ extern "C" int nerf_render_eval_fused(const float* pts_o, const float* pts_d, co
     for (int l = 0; l < CNL; ++l) {
         const nerf_chain_layer& L = layers[l];
         NERF_CHECK(L.img && L.bias, "%s: layer %d needs its weight image and bias", __func__, l);
-        NERF_CHECK((((uintptr_t)L.bias) & 15u) == 0 && (((uintptr_t)L.img) & 15u) == 0 && L.img_rows >= L_OUT[l],
-                   "%s: layer %d: image / bias not 16-byte aligned or image rows %d < %d", __func__, l, L.img_rows,
-                   L_OUT[l]);
+        NERF_CHECK((((uintptr_t)L.bias) & 15u) == 0 && (((uintptr_t)L.img) & 15u) == 0 && L.img_rows == L_OUT[l],
+                   "%s: layer %d: image / bias not 16-byte aligned or chain image rows %d != %d", __func__, l,
+                   L.img_rows, L_OUT[l]);
         NERF_CHECK(L.out == nullptr && L.mask == nullptr && L.cmax == nullptr,
                    "%s: layer %d: the eval render saves no activations, masks or column maxima", __func__, l);
         a.L[l] = L;
@@ -1857,12 +1989,15 @@ extern "C" int nerf_render_eval_fused(const float* pts_o, const float* pts_d, co
     return check_launch(__func__);
 }
 
-// diagnostics: per-block phase cycles of the chain kernel (wait, barrier, MFMA section,
-// epilogue, total, end realtime) into a device buffer of (n_pad / 128) * 6 uint64; NULL off
+// diagnostics: per-block phase cycles of the chain kernels (wait, barrier, MFMA section,
+// epilogue, total, end realtime) into a device buffer of (n_pad / 128) * 6 uint64; NULL off.
+// The two-wave kernels stamp only in a NERF_CHAIN_STAMPS build (their production code has no
+// stamp instructions); the one-wave k_mlp_chain_fwd always can
 extern "C" int nerf_chain_debug_stamps(void* buf) {
     g_chain_stamps = reinterpret_cast<unsigned long long*>(buf);
     return NERF_OK;
 }
+extern "C" int nerf_chain_stamps_built(void) { return NERF_CHAIN_STAMPS; }
 
 extern "C" int nerf_mlp_chain_bwd(const nerf_chain_bwd* a, void* stream) {
     NERF_CHECK_PTR(a);
@@ -1875,8 +2010,9 @@ extern "C" int nerf_mlp_chain_bwd(const nerf_chain_bwd* a, void* stream) {
     NERF_CHECK_ALIGN16(p.graw4); NERF_CHECK_ALIGN16(p.wd);
     NERF_CHECK((((uintptr_t)p.hr_mask) & 15u) == 0 && p.ld_hr_mask % 4 == 0, "%s: hr_mask 16-byte rows", __func__);
     for (int i = 0; i < 9; ++i) {
-        NERF_CHECK(p.wt_img[i] && (((uintptr_t)p.wt_img[i]) & 15u) == 0 && p.wt_img_rows[i] >= 256,
-                   "%s: layer %d: weight-transpose image missing, unaligned or < 256 rows", __func__, i);
+        NERF_CHECK(p.wt_img[i] && (((uintptr_t)p.wt_img[i]) & 15u) == 0 && p.wt_img_rows[i] == b2::KPB[i],
+                   "%s: layer %d: weight-transpose chain image missing, unaligned or not %d rows", __func__, i,
+                   b2::KPB[i]);
         NERF_CHECK(i == 0 || (p.in_mask[i] && p.ld_in_mask[i] >= 8 && (((uintptr_t)p.in_mask[i]) & 15u) == 0 &&
                               p.ld_in_mask[i] % 4 == 0),
                    "%s: layer %d: the input's ReLU words (ld >= 8, 16-byte rows) are required", __func__, i);

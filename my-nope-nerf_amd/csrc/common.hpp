@@ -54,6 +54,14 @@ __device__ __forceinline__ int row_exp(float rmax) {
     return rmax == 0.f ? 0 : (ex ? 141 - ex : 140);
 }
 
+// the chain images' K order (nerf_pack_weights dst_cs / dst_cts): image column c of a 32-wide
+// k-step holds feature chain_perm(c) -- lane group g's eight k (c = 8 g + i) are features 4 g
+// + i (i < 4) and 16 + 4 g + i - 4 of the step, the tile layout of the 16x16x32 accumulators
+__host__ __device__ constexpr int chain_perm(int c) {
+    const int t = c >> 5, q = c & 31, g = q >> 3, i = q & 7;
+    return 32 * t + 4 * g + (i & 3) + (i >= 4 ? 16 : 0);
+}
+
 // GEMM arithmetic mode (nerf_gemm_set_precision), host side
 int gemm_precision();
 // several split-K slab reduces (nerf_slab_reduce without accumulate) in one launch

@@ -139,7 +139,7 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
     c.wc = a.wc;
     for (int i = 0; i < 9; ++i) {
         const int l = LR - i;
-        c.wt_img[i] = a.wt_img[l];
+        c.wt_img[i] = a.wt_cimg[l];   // the chain image: K in chain order (ABI 13)
         c.wt_img_rows[i] = KP[l];
         c.in_mask[i] = l == LR ? nullptr : a.mask[l - 1];
         c.ld_in_mask[i] = OUT_P[l - 1 < 0 ? 0 : l - 1] / 32;
@@ -340,6 +340,8 @@ int schedule(const nerf_field_bwd& a, void* stream, void* side_stream) {
     for (int l = 0; l < L; ++l) {
         NERF_CHECK(a.act[l] && a.wt[l] && a.wt_img[l] && a.gw[l] && a.gb[l], "%s: layer %d: missing tensor", __func__,
                    l);
+        NERF_CHECK(!a.bwd_chain || l == 0 || a.wt_cimg[l], "%s: layer %d: the input-gradient chain needs the chain "
+                   "image of W^T (wt_cimg)", __func__, l);
         NERF_CHECK((l == LF) == (a.mask[l] == nullptr), "%s: layer %d: ReLU words (none for the feature layer)",
                    __func__, l);
         NERF_CHECK((l == LR) == (a.cmax[l] == nullptr), "%s: layer %d: column maxima (none for the colour layer)",

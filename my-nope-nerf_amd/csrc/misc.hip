@@ -98,23 +98,28 @@ __device__ __forceinline__ void put_row_h(uint16_t* img, int N, int K, int r, F&
 }
 
 // fp16 pair images of the packed weights (GEMM precision mode 2): one wave per image row,
-// rows of dst_s then of dst_ts (block bx of nb)
+// rows of dst_s, dst_ts, then of the chain images dst_cs (the first perm_k columns in
+// chain_perm order) and dst_cts (every column in chain order) (block bx of nb)
 __device__ __forceinline__ void pack_h(const nerf_pack_desc& d, int bx, int nb) {
     const int rows_s = d.rows_s > d.rows ? d.rows_s : d.rows;
     const int ns = d.dst_s ? rows_s : 0, nt = d.dst_ts ? d.rows_t : 0;
+    const int ncs = d.dst_cs ? rows_s : 0, nct = d.dst_cts ? d.rows_t : 0;
     const int wave = (bx * blockDim.x + threadIdx.x) >> 6;
     const int nwaves = (nb * blockDim.x) >> 6;
-    for (int w = wave; w < ns + nt; w += nwaves) {
+    auto w_at = [&](int r, int c) { return (c < d.cols && r < d.rows) ? d.src[(size_t)r * d.cols + c] : 0.f; };
+    for (int w = wave; w < ns + nt + ncs + nct; w += nwaves) {
         if (w < ns) {
             const int r = w;
-            put_row_h(d.dst_s, rows_s, d.ld_dst, r, [&](int c) {
-                return (c < d.cols && r < d.rows) ? d.src[(size_t)r * d.cols + c] : 0.f;
-            });
-        } else {
+            put_row_h(d.dst_s, rows_s, d.ld_dst, r, [&](int c) { return w_at(r, c); });
+        } else if (w < ns + nt) {
             const int c = w - ns;   // dst_t row = source column c, its columns = source rows
-            put_row_h(d.dst_ts, d.rows_t, d.ld_t, c, [&](int r) {
-                return (c < d.cols && r < d.rows) ? d.src[(size_t)r * d.cols + c] : 0.f;
-            });
+            put_row_h(d.dst_ts, d.rows_t, d.ld_t, c, [&](int r) { return w_at(r, c); });
+        } else if (w < ns + nt + ncs) {
+            const int r = w - ns - nt;
+            put_row_h(d.dst_cs, rows_s, d.ld_dst, r, [&](int c) { return w_at(r, c < d.perm_k ? chain_perm(c) : c); });
+        } else {
+            const int c = w - ns - nt - ncs;
+            put_row_h(d.dst_cts, d.rows_t, d.ld_t, c, [&](int r) { return w_at(chain_perm(r), c); });
         }
     }
 }
@@ -131,25 +136,26 @@ __global__ __launch_bounds__(256) void k_pack(PackBatch pb) {
     else pack_h(d, blockIdx.x - PACK_F32, PACK_H);
 }
 
-// torch.optim.Adam (amsgrad=False, maximize=False), single-tensor formulation:
-//   g += wd*p; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2
-//   denom = sqrt(v)/sqrt(bc2) + eps;  p -= (lr/bc1) * m / denom
-// Hyper-parameters and the step count live in device memory (hyper = {step, lr, b1, b2,
-// eps, wd, -, ticket}) so a captured hipGraph replays correct bias corrections; an lr change
-// reaches a replay once the host pushes it into the device block (HipAdam.sync_hyper()
-// between replays).  Every workgroup uses step + 1; the last one to finish (ticket) stores it.
-// one element of torch's Adam (the foreach path, torch/optim/adam.py): om1 = 1 - beta1,
-// om2 = 1 - beta2 as torch passes them (Python doubles rounded once to f32; 1.f - 0.999f is
-// 1.3e-5 off 0.001)
+// torch.optim.Adam (amsgrad=False, maximize=False), the foreach formulation torch runs on GPU
+// tensors by default (torch/optim/adam.py _multi_tensor_adam), op for op:
+//   m.lerp_(g, 1 - b1); v.mul_(b2); v.addcmul_(g, g, 1 - b2); d = sqrt(v) / sqrt(bc2) + eps;
+//   p.addcdiv_(m, d, -lr / bc1)
+// with every scalar the f32 rounding of the Python double torch forms (1 - b1, 1 - b2,
+// sqrt(1 - b2^t), lr / (1 - b1^t)).  Hyper-parameters and the step count live in device
+// memory (hyper, 16 floats = {step, lr, b1, b2, eps, wd, 1 - b2, ticket, lr, b1, b2 as doubles
+// in slots 8-13, 1 - b1, doubles-valid flag}) so a captured hipGraph replays correct bias
+// corrections; an lr change reaches a replay once the host pushes it into the device block
+// (HipAdam.sync_hyper() between replays).  Every workgroup uses step + 1; the last one to
+// finish (ticket) stores it.
 __device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v, float om1, float b2, float om2,
                                           float eps, float wd, float sbc2, float step_size) {
-    if (wd != 0.f) g = g + wd * p;
-    const float mi = m + om1 * (g - m);          // exp_avg.lerp_(grad, 1 - beta1)
-    const float vi = v * b2 + om2 * g * g;       // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
+    if (wd != 0.f) g = __fmaf_rn(wd, p, g);                        // grad.add(param, alpha=wd)
+    const float mi = __fmaf_rn(om1, g - m, m);                       // exp_avg.lerp_(grad, 1 - beta1)
+    const float vi = __fmaf_rn(om2, __fmul_rn(g, g), __fmul_rn(v, b2));   // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
     m = mi;
     v = vi;
-    const float denom = sqrtf(vi) / sbc2 + eps;
-    p = p + (-step_size) * (mi / denom);         // addcdiv_(m, denom, value=-step_size)
+    const float denom = sqrtf(vi) / sbc2 + eps;                      // sqrt, div_(bc2 sqrt), add_(eps): three roundings
+    p = __fmaf_rn(-step_size, mi / denom, p);                        // addcdiv_(m, denom, value=-step_size)
     return p;
 }
 
@@ -159,15 +165,19 @@ constexpr int ADAM_BLOCKS = 512;
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float* __restrict__ g,
                                               float* __restrict__ m, float* __restrict__ v, int64_t n,
                                               float* __restrict__ hyper) {
-    const float step = hyper[0] + 1.f, lr = hyper[1], b1 = hyper[2], b2 = hyper[3], eps = hyper[4], wd = hyper[5];
-    // hyper[6]: 1 - beta2 from the host's doubles (0: derive it here, as before ABI 12); the
-    // bias corrections in double like torch's Python scalars (1 - beta2^t cancels: in f32
+    const float step = hyper[0] + 1.f, b2 = hyper[3], eps = hyper[4], wd = hyper[5];
+    // the scalars as torch forms them: from the host's doubles (slots 8-14, flag slot 15 = 1);
+    // the bias corrections in double like torch's Python scalars (1 - beta2^t cancels: in f32
     // it is ~1e-5 off at small t)
-    const float om2 = hyper[6] != 0.f ? hyper[6] : 1.f - b2;
-    const float om1 = (float)(1.0 - (double)b1);
-    const double bc1 = 1.0 - pow((double)b1, (double)step);
-    const float sbc2 = (float)sqrt(1.0 - pow(1.0 - (double)om2, (double)step));
-    const float step_size = (float)((double)lr / bc1);
+    const bool dbl = hyper[15] == 1.f;
+    const double* hd = reinterpret_cast<const double*>(hyper + 8);
+    const double lr_d = dbl ? hd[0] : (double)hyper[1], b1_d = dbl ? hd[1] : (double)hyper[2];
+    const double b2_d = dbl ? hd[2] : (double)b2;
+    const float om1 = dbl ? hyper[14] : (float)(1.0 - b1_d);
+    const float om2 = hyper[6] != 0.f ? hyper[6] : (float)(1.0 - b2_d);
+    const double bc1 = 1.0 - pow(b1_d, (double)step);
+    const float sbc2 = (float)sqrt(1.0 - pow(b2_d, (double)step));
+    const float step_size = (float)(lr_d / bc1);
     const int64_t n4 = n >> 2;
     float4* p4 = reinterpret_cast<float4*>(p);
     float4* m4 = reinterpret_cast<float4*>(m);
@@ -186,7 +196,7 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float
         for (int64_t i = n4 * 4; i < n; ++i) adam_one(p[i], g[i], m[i], v[i], om1, b2, om2, eps, wd, sbc2, step_size);
     __syncthreads();                              // this workgroup has read hyper[0]
     if (threadIdx.x == 0) {
-        unsigned* ticket = reinterpret_cast<unsigned*>(hyper + 7);
+        unsigned* ticket = reinterpret_cast<unsigned*>(hyper + 7);   // (hyper is 8-byte aligned: slots 8-13 doubles)
         if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
             hyper[0] = step;
             *ticket = 0u;
@@ -245,10 +255,20 @@ extern "C" int nerf_pack_weights(const nerf_pack_desc* descs, int n, void* strea
         NERF_CHECK(d.dst_ts == nullptr || (d.rows_t >= d.cols && d.ld_t >= d.rows && d.ld_t % 8 == 0),
                    "%s: descriptor %d: transposed split image needs rows_t >= cols, ld_t >= rows, ld_t %% 8 == 0",
                    __func__, i);
+        NERF_CHECK((d.dst_cs == nullptr && d.dst_cts == nullptr) ||
+                       (pb.f16 && d.perm_k >= 0 && d.perm_k % 32 == 0 && d.perm_k <= d.ld_dst && d.ld_dst % 8 == 0 &&
+                        d.ld_dst <= PACK_H_MAXK),
+                   "%s: descriptor %d: chain images need precision mode 2, perm_k %% 32 == 0 (<= ld_dst)", __func__, i);
+        NERF_CHECK(d.dst_cts == nullptr || (d.rows_t >= d.cols && d.ld_t >= d.rows && d.ld_t % 32 == 0 &&
+                                            d.ld_t <= PACK_H_MAXK),
+                   "%s: descriptor %d: the transposed chain image needs rows_t >= cols, ld_t >= rows, ld_t %% 32 == 0",
+                   __func__, i);
         pb.d[i] = d;
     }
     bool images = false;
-    for (int i = 0; i < n; ++i) images = images || descs[i].dst_s != nullptr || descs[i].dst_ts != nullptr;
+    for (int i = 0; i < n; ++i)
+        images = images || descs[i].dst_s != nullptr || descs[i].dst_ts != nullptr || descs[i].dst_cs != nullptr ||
+                 descs[i].dst_cts != nullptr;
     const int bx = PACK_F32 + ((pb.f16 && images) ? PACK_H : 0);
     hipLaunchKernelGGL(k_pack, dim3(bx, n), dim3(256), 0, as_stream(stream), pb);
     return check_launch(__func__);
@@ -261,6 +281,7 @@ extern "C" int nerf_adam_step(float* param, const float* grad, float* exp_avg, f
     NERF_CHECK(n > 0, "%s: n=%lld", __func__, (long long)n);
     NERF_CHECK((((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) & 15) == 0,
                "%s: buffers must be 16-byte aligned", __func__);
+    NERF_CHECK((((uintptr_t)hyper) & 7) == 0, "%s: hyper must be 8-byte aligned (doubles in slots 8-13)", __func__);
     int64_t blocks = (n / 4 + 255) / 256;
     if (blocks < 1) blocks = 1;
     if (blocks > ADAM_BLOCKS) blocks = ADAM_BLOCKS;

@@ -294,6 +294,13 @@ __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_pair(TNArgs p) {
 __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_pairs(TNPairs m) {
     __shared__ __attribute__((aligned(16))) char smem[wg::Cfg<256, 128>::BYTES];
     const int w = blockIdx.x, slot = w >> 3;
+    // LDS across the layer boundary: nothing here orders layer i + 1's first LDS write after
+    // layer i's last LDS reads.  It is the __syncthreads() inside layer i + 1's exponents()
+    // (block(), before any stage is put into the operand image) that keeps the load waves'
+    // stage-0 put out of the region the MFMA waves' tn_store_lds is still using for layer i's
+    // slab; a change that writes LDS before that barrier (hoisting the put, or the exponents'
+    // reads after the loads) must add a barrier here.  test_wgrad_multi_matches_single
+    // (n = 1 .. 4 and 8, tests/test_gpu_kernels.py) checks the slabs against one launch per layer.
     for (int i = 0; i < m.n; ++i)
         wg::block_any<256, 128>(m.a[i], smem, 0, slot & 1, (slot >> 1) * 8 + (w & 7), i & 1);
 }

@@ -36,7 +36,7 @@ _c_i64 = ctypes.c_int64
 class PackDesc(ctypes.Structure):
     _fields_ = [("src", _c_p), ("dst", _c_p), ("dst_t", _c_p), ("rows", _c_i), ("cols", _c_i),
                 ("ld_dst", _c_i), ("rows_t", _c_i), ("ld_t", _c_i), ("dst_s", _c_p), ("dst_ts", _c_p),
-                ("rows_s", _c_i)]
+                ("rows_s", _c_i), ("dst_cs", _c_p), ("dst_cts", _c_p), ("perm_k", _c_i)]
 
 
 class ProfKind(ctypes.Structure):
@@ -46,7 +46,7 @@ class ProfKind(ctypes.Structure):
 
 
 PROF_KINDS = ("fwd", "dx", "dw", "dw_narrow", "chain_fwd", "chain_bwd")   # NERF_PROF_FWD .. _CHAIN_BWD
-ABI_VERSION = 12                   # NERF_HIP_ABI_VERSION
+ABI_VERSION = 13                   # NERF_HIP_ABI_VERSION
 
 
 _P10 = _c_p * 10
@@ -57,7 +57,8 @@ class FieldBwd(ctypes.Structure):
     _fields_ = [("n_pad", _c_i), ("n_rays", _c_i), ("n_samples", _c_i), ("flags", _c_i), ("ray_grad", _c_i),
                 ("tail_main", _c_i), ("bwd_chain", _c_i), ("z", _c_p), ("raw4", _c_p), ("enc_p", _c_p), ("enc_d", _c_p),
                 ("enc_p_cmax", _c_p), ("enc_d_cmax", _c_p), ("act", _P10), ("mask", _P10), ("cmax", _P10),
-                ("pts_o", _c_p), ("pts_d", _c_p), ("view", _c_p), ("wt", _P10), ("wt_img", _P10), ("wd", _c_p),
+                ("pts_o", _c_p), ("pts_d", _c_p), ("view", _c_p), ("wt", _P10), ("wt_img", _P10), ("wt_cimg", _P10),
+                ("wd", _c_p),
                 ("wc", _c_p), ("g_rgb", _c_p), ("g_dist", _c_p), ("graw4", _c_p), ("gw", _P10), ("gb", _P10),
                 ("g_wd", _c_p), ("g_bd", _c_p), ("g_wc", _c_p), ("g_bc", _c_p), ("g_pts_o", _c_p), ("g_pts_d", _c_p),
                 ("g_view", _c_p), ("workspace", _c_p)]
@@ -116,6 +117,7 @@ _SIGS = {
     "nerf_pack_weights": ([ctypes.POINTER(PackDesc), _c_i, _c_p], _c_i),
     "nerf_mlp_chain_fwd": ([_c_p, _c_p, _c_p, _c_p, _c_i, ctypes.POINTER(ChainLayer), _c_p], _c_i),
     "nerf_chain_debug_stamps": ([_c_p], _c_i),
+    "nerf_chain_stamps_built": ([], _c_i),
     "nerf_mlp_chain_train": ([_c_p, _c_p, _c_p, _c_p, _c_i, ctypes.POINTER(ChainLayer), _c_p, _c_p, _c_p, _c_p, _c_p,
                               _c_p], _c_i),
     "nerf_render_eval_fused": ([_c_p, _c_p, _c_p, _c_i, _c_i, _c_f, _c_f, _c_i, ctypes.POINTER(ChainLayer), _c_p, _c_p,
@@ -417,10 +419,11 @@ def mlp_chain_train(enc_p, enc_d, enc_p_rmax, enc_d_rmax, n_pad, layers: Sequenc
 
 
 def adam_step(param, grad, exp_avg, exp_avg_sq, hyper):
-    """hyper: device float32 [8] = (step, lr, beta1, beta2, eps, weight_decay, -, ticket);
-    the update uses step + 1 and stores it back (ticket: zero-initialised counter)."""
-    if hyper.numel() < 8:
-        raise ValueError("adam_step: hyper needs 8 floats")
+    """hyper: device float32 [16] (model.optim.hyper_block: step, lr, beta1, beta2, eps,
+    weight_decay, 1 - beta2, ticket, lr / beta1 / beta2 as doubles, 1 - beta1, flag); the update
+    uses step + 1 and stores it back (ticket: zero-initialised counter)."""
+    if hyper.numel() < 16 or hyper.dtype != torch.float32:
+        raise ValueError("adam_step: hyper needs 16 float32 slots (ABI 13)")
     _call("nerf_adam_step", _ptr(param), _ptr(grad), _ptr(exp_avg), _ptr(exp_avg_sq), param.numel(),
           _ptr(hyper), _stream())
 

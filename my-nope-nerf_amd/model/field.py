@@ -103,6 +103,10 @@ class FieldRunner:
         # bf16x3 split images of w / wt: the B operands of GEMM precision mode 1
         self.ws = {l.name: _hip.split_image(l.out_p, l.kp, device) for l in self.layers}
         self.wts = {l.name: _hip.split_image(l.kp, l.out_p, device) for l in self.layers}
+        # precision mode 2's chain images (nerf_pack_desc dst_cs / dst_cts): the same fp16 pair
+        # form with K in the order the two-wave chains hold a layer's outputs (chain.hip)
+        self.wsc = {l.name: _hip.split_image(l.out_p, l.kp, device) for l in self.layers}
+        self.wtsc = {l.name: _hip.split_image(l.kp, l.out_p, device) for l in self.layers}
         # padded, 16-byte-aligned copies of every layer bias (the chain kernel loads them by
         # 16-byte LDS-DMA; HipAdam's flat parameter buffer leaves biases 4-byte aligned)
         self.bias_p = {l.name: z(l.out_p) for l in self.layers}
@@ -128,8 +132,12 @@ class FieldRunner:
             assert W.is_contiguous() and W.dtype == torch.float32
             ws = self.ws[l.name].data_ptr() if self.split else None
             wts = self.wts[l.name].data_ptr() if self.split else None
+            chain = self.h16 and self.D == 256 and self.HR == 128
+            wsc = self.wsc[l.name].data_ptr() if chain else None
+            wtsc = self.wtsc[l.name].data_ptr() if chain else None
             descs.append(_hip.PackDesc(W.data_ptr(), self.w[l.name].data_ptr(), self.wt[l.name].data_ptr(),
-                                       W.shape[0], W.shape[1], l.kp, l.kp, l.out_p, ws, wts, l.out_p))
+                                       W.shape[0], W.shape[1], l.kp, l.kp, l.out_p, ws, wts, l.out_p, wsc, wtsc,
+                                       l.k1 if l.name != "l0" else 0))
         for l in self.layers:
             b = l.linear.bias
             descs.append(_hip.PackDesc(b.data_ptr(), self.bias_p[l.name].data_ptr(), None, 1, b.shape[0], l.out_p, 0, 0))
@@ -194,7 +202,8 @@ class FieldRunner:
                         masks[l.name] = mo
                 y_cm = cm(l.out_p) if l.name != "lr" else None
                 cmaxes[l.name] = y_cm
-                ws = self.ws[l.name]
+                # the training chain reads the chain images, the one-wave eval chain the plain ones
+                ws = self.wsc[l.name] if keep else self.ws[l.name]
                 descs.append(_hip.ChainLayer(ws.data_ptr(), ws.shape[2], self.bias(l).data_ptr(),
                                              y.data_ptr() if y is not None else None, l.out_p,
                                              mo.data_ptr() if mo is not None else None, l.out_p // 32,
@@ -275,7 +284,7 @@ class FieldRunner:
         R = pts_o.shape[0]
         dev = pts_o.device
         self.pack()
-        descs = [_hip.ChainLayer(self.ws[l.name].data_ptr(), self.ws[l.name].shape[2], self.bias(l).data_ptr(),
+        descs = [_hip.ChainLayer(self.wsc[l.name].data_ptr(), self.wsc[l.name].shape[2], self.bias(l).data_ptr(),
                                  None, l.out_p, None, l.out_p // 32, None) for l in self.layers]
         e = lambda *sh: torch.empty(*sh, device=dev, dtype=torch.float32)
         rgb, dist, alpha, z = e(R, 3), e(R), e(R, S), e(R, S)
@@ -346,7 +355,7 @@ class FieldRunner:
             _hip._P10(*[P(masks.get(n)) for n in names]), _hip._P10(*[P(cms.get(n)) for n in names]),
             P(st["pts_o"]), P(st["pts_d"]), P(st["view"]),
             _hip._P10(*[self.wt[n].data_ptr() for n in names]), _hip._P10(*[self.wts[n].data_ptr() for n in names]),
-            self.wd.data_ptr(), self.wc.data_ptr(), P(g_rgb), P(g_dist), P(graw4),
+            _hip._P10(*[self.wtsc[n].data_ptr() for n in names]), self.wd.data_ptr(), self.wc.data_ptr(), P(g_rgb), P(g_dist), P(graw4),
             _hip._P10(*[G(l.linear.weight).data_ptr() for l in self.layers]),
             _hip._P10(*[G(l.linear.bias).data_ptr() for l in self.layers]),
             G(m.fc_density.weight).data_ptr(), G(m.fc_density.bias).data_ptr(), G(m.fc_rgb.weight).data_ptr(),

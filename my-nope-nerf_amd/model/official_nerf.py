@@ -114,6 +114,11 @@ class OfficialStaticNerf(nn.Module):
             raw = eval_points(self, p.reshape(-1, 3), torch.zeros_like(p).reshape(-1, 3))
             y = raw[:, 0:1]
             g = torch.autograd.grad(y, p, torch.ones_like(y), retain_graph=False)[0]
+            # that backward's parameter gradients are discarded (autograd.grad returns dp only):
+            # hand the data-parallel gradient buffer back, so the step's real backward writes
+            # into it in place instead of into a fresh flat that the all-reduce must copy
+            if self._runner is not None:
+                self._runner.release_grad_buffer()
             anchor = self.fc_density.bias
             if anchor.requires_grad:
                 g = _FirstOrderOnly.apply(g, anchor)

@@ -15,6 +15,20 @@ import torch
 from . import _hip
 
 
+def hyper_block(lr, beta1, beta2, eps, weight_decay, step=0.0):
+    """k_adam's hyper-parameter block as a CPU float32 [16] tensor: the scalars torch's Adam
+    forms from its Python doubles -- 1 - beta1 and 1 - beta2 rounded once to f32 (slots 14, 6),
+    lr / beta1 / beta2 kept as doubles (slots 8-13) for the bias corrections lr / (1 - beta1^t)
+    and sqrt(1 - beta2^t), which the kernel takes in double at the device step count."""
+    import numpy as np
+    b = np.zeros(16, dtype=np.float32)
+    b[:7] = (step, lr, beta1, beta2, eps, weight_decay, 1.0 - beta2)
+    b[8:14].view(np.float64)[:] = (lr, beta1, beta2)
+    b[14] = 1.0 - beta1
+    b[15] = 1.0
+    return torch.from_numpy(b)
+
+
 class HipAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
@@ -37,8 +51,10 @@ class HipAdam(torch.optim.Optimizer):
         self._params = ps
         self._m = torch.zeros_like(self._flat)
         self._v = torch.zeros_like(self._flat)
-        # {step, lr, beta1, beta2, eps, weight_decay, -, ticket} on the device (graph-replay safe)
-        self._hyper = torch.zeros(8, device=dev, dtype=torch.float32)
+        # the device block k_adam reads (graph-replay safe), 16 floats: {step, lr, beta1, beta2,
+        # eps, weight_decay, 1 - beta2, ticket, lr / beta1 / beta2 as doubles (slots 8-13),
+        # 1 - beta1, 1.0 = the doubles are valid}
+        self._hyper = torch.zeros(16, device=dev, dtype=torch.float32)
         self._hyper_host = None
         self._sync_hyper()
 
@@ -53,8 +69,7 @@ class HipAdam(torch.optim.Optimizer):
         g = self.param_groups[0]
         h = (float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]), float(g["weight_decay"]))
         if h != self._hyper_host:      # lr schedulers edit param_groups; push the change
-            # slot 6: 1 - beta2 from the Python doubles (torch's addcmul_ value), not 1.f - beta2_f32
-            self._hyper[1:7].copy_(torch.tensor(h + (1.0 - h[2],), dtype=torch.float32), non_blocking=False)
+            self._hyper[1:].copy_(hyper_block(*h)[1:], non_blocking=False)
             self._hyper_host = h
 
     def _flat_grad(self):

@@ -46,12 +46,16 @@ for step in "$@"; do
         wgh) RX=k_wgrad_pair; CT="TCC_HIT_sum TCC_MISS_sum"; CMD="$R/scripts/wgrad_bench.py --loop 20" ;;
         ch1) RX=k_mlp_chain; CT="$C1"; CMD="$BENCH" ;;
         ch2) RX=k_mlp_chain; CT="$C2"; CMD="$BENCH" ;;
+        ic) RX=k_mlp_chain; CT="SQ_WAVES SQ_IFETCH SQ_IFETCH_LEVEL SQ_WAIT_INST_ANY SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE"; CMD="$BENCH" ;;
         fetch) RX="$STEPRX"; CT="FETCH_SIZE"; CMD="$BENCH" ;;
         write) RX="$STEPRX"; CT="WRITE_SIZE"; CMD="$BENCH" ;;
         *) echo "unknown pmc set $step"; exit 2 ;;
       esac
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv --kernel-include-regex "$RX" --pmc $CT -d $OUT/pmc_${step#pmc:} -o run -- python3 $CMD > $OUT/pmc_${step#pmc:}.log 2>&1) || exit $?
       echo "pmc ok: ${step#pmc:}" ;;
+    list)
+      (cd /tmp && timeout -s KILL 60 rocprofv3 -L > $OUT/counters.txt 2>&1) || exit $?
+      echo "list ok" ;;
     py:*)
       args=${step#py:}
       (cd $R/scripts && timeout -k 10 300 python -u $args > $OUT/py_$(echo $args | tr ' /' '__' | cut -c1-60).txt 2>&1) || exit $?

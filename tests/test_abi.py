@@ -1,6 +1,7 @@
 """The C-ABI library loads and exports every symbol include/nerf_hip.h declares; the
 ctypes binding covers all of them; argument checks fail loudly (no GPU needed: these
 calls return before any HIP API call)."""
+import ctypes
 import os
 import re
 
@@ -36,7 +37,7 @@ def test_binding_covers_the_header():
 
 
 def test_abi_version_and_error_path(lib):
-    assert lib.nerf_hip_abi_version() == 12
+    assert lib.nerf_hip_abi_version() == 13
     rc = lib.nerf_linear_fwd(None, 256, 256, None, 0, 0, None, None, 0, None, None, 256, 128, 256, 1, None, 0,
                              None, None, None, None, None)
     assert rc == -1
@@ -74,3 +75,21 @@ def test_ops_refuse_cpu_tensors(lib):
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(ImportError, match="no CPU fallback"):
         _hip.load_library(str(tmp_path / "nope.so"))
+
+
+def test_chain_image_descriptor_checks(lib):
+    """ABI 13 chain images (nerf_pack_desc dst_cs / dst_cts): rejected outside precision mode 2
+    or with perm_k not a multiple of 32 -- argument checks only, no launch."""
+    src = ctypes.c_void_p(16)
+    old = lib.nerf_gemm_get_precision()
+    try:
+        lib.nerf_gemm_set_precision(2)
+        d = _hip.PackDesc(src, src, None, 256, 256, 256, 0, 0, src, None, 256, src, None, 48)
+        assert lib.nerf_pack_weights(ctypes.byref(d), 1, None) == -1
+        assert b"perm_k" in lib.nerf_hip_last_error()
+        lib.nerf_gemm_set_precision(0)
+        d = _hip.PackDesc(src, src, None, 256, 256, 256, 0, 0, None, None, 256, src, None, 256)
+        assert lib.nerf_pack_weights(ctypes.byref(d), 1, None) == -1
+        assert b"mode 2" in lib.nerf_hip_last_error()
+    finally:
+        lib.nerf_gemm_set_precision(old)

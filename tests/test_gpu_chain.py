@@ -90,12 +90,27 @@ def test_chain_eval_skips_intermediate_stores(dev, h16):
         os.environ.pop("NERF_CHAIN", None)
     os.environ["NERF_CHAIN"] = "0"
     try:
-        rgb0, dist0, _, _ = render_field_eval(net, o, d, -d, 0.01, 10.0, 64, 0, ray_chunk=200)
+        rgb0, dist0, _, z0 = render_field_eval(net, o, d, -d, 0.01, 10.0, 64, 0, ray_chunk=200)
     finally:
         os.environ.pop("NERF_CHAIN", None)
     torch.cuda.synchronize()
-    assert ((rgb1 - rgb0).abs().max() / rgb0.abs().max()).item() < 1e-5
-    assert ((dist1 - dist0).abs().max() / dist0.abs().max()).item() < 1e-5
+    # chain (the fused per-ray kernel at S = 64) and per-layer launches sum the K products in
+    # different orders (16x16x32 tiles in chain_perm order vs 32x32x16), so with the row-spread
+    # weights a ReLU decision near zero can move a ray by ~1e-5: the arbiter is the fp64 oracle,
+    # which the chain must track as closely as the per-layer path does
+    from oracle import nerf_oracle as orc
+    ref = orc.OracleNerf(hidden_dim=256).double()
+    ref.load_state_dict({k: v.detach().cpu().double() for k, v in net.state_dict().items()})
+    z = z0.cpu().double()
+    pts = b["o"].double()[:, None, :] + b["d"].double()[:, None, :] * z[..., None]
+    with torch.no_grad():
+        rgb_s, a_s = ref(pts.reshape(-1, 3), (-b["d"].double())[:, None, :].expand(512, 64, 3).reshape(-1, 3))
+        ro = orc.composite(a_s.reshape(512, 64), rgb_s.reshape(512, 64, 3), z)
+    for a1, a0, r in ((rgb1, rgb0, ro[0]), (dist1, dist0, ro[1])):
+        e1 = (a1.cpu().double() - r).abs().max().item()
+        e0 = (a0.cpu().double() - r).abs().max().item()
+        assert e1 <= 1.5 * e0 + 1e-6, (e1, e0)
+        assert ((a1 - a0).abs().max() / a0.abs().max()).item() < 5e-5
 
 
 def test_chain_gradients_match_per_layer(dev, h16):

@@ -3,11 +3,12 @@ schedule it replaces (FieldRunner.backward with NERF_NATIVE_BWD=0).  With the pe
 input gradients (NERF_BWD_CHAIN=0) it runs the same kernels in the same order, so every
 parameter gradient and every ray gradient must be bit-identical; with the input-gradient
 chain (nerf_mlp_chain_bwd, the default) the input gradients accumulate in another MFMA order
-and the saved dy are the fp16 pairs the chain consumed (within 2^-22 relative), so the
-gradients agree to 1e-5 relative L2 per tensor.  Training-size batches (Np >= 65536, where
-the native path runs), with and without ray gradients (pose learning), from the composite
-backward and from a given graw4 (eval_points); also under a tail of 0 and 3 deferred weight
-gradients, and with the chain under both weight-gradient schedules (NERF_WGRAD_SCHED 1 / 2)."""
+(16x16x32 tiles, K in chain order), so the gradients agree to 1e-5 relative L2 per tensor.
+Training-size batches (Np >= 65536, where the native path runs), with and without ray
+gradients (pose learning), from the composite backward and from a given graw4
+(eval_points); the per-layer schedule also under a tail of 0 and 3 deferred weight gradients
+(tail_main applies to it only), and the chain under both weight-gradient schedules
+(NERF_WGRAD_SCHED 1 / 2)."""
 import os
 
 import pytest
@@ -73,6 +74,8 @@ def _agree(a, b, chain):
 @pytest.mark.parametrize("ray_grad,R,S,tail", [(False, 1024, 128, None), (True, 1024, 128, None),
                                                (False, 600, 128, "0"), (True, 520, 128, "3")])
 def test_native_backward_bit_identical(dev, h16, ray_grad, R, S, tail, chain, sched):
+    if chain == "1" and tail is not None:
+        pytest.skip("tail_main applies to the per-layer schedule only (nerf_field_bwd)")
     net = _net(dev, seed=R)
     o, d, noise = _rays(R, S, seed=R + 1)
     runner = net.hip_runner()

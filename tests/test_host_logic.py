@@ -184,7 +184,13 @@ def test_hip_adam_hyper_block():
     assert h[1].item() == torch.tensor(1e-3).item() and h[2].item() == torch.tensor(0.9).item()
     assert h[6].item() == torch.tensor(1.0 - 0.999, dtype=torch.float32).item()
     assert h[6].item() != (1.0 - torch.tensor(0.999, dtype=torch.float32)).item()
+    # ABI 13: 1 - beta1 from the double too, and lr / beta1 / beta2 as doubles for the bias
+    # corrections (slots 8-13), flagged valid by slot 15
+    assert h[14].item() == torch.tensor(1.0 - 0.9, dtype=torch.float32).item()
+    assert h[14].item() != (1.0 - torch.tensor(0.9, dtype=torch.float32)).item()
+    assert h.cpu()[8:14].numpy().view("float64").tolist() == [1e-3, 0.9, 0.999] and h[15].item() == 1.0
     opt.param_groups[0]["lr"] = 5e-4
     opt.sync_hyper()
     assert opt._hyper[1].item() == torch.tensor(5e-4).item()
+    assert opt._hyper.cpu()[8:10].numpy().view("float64")[0] == 5e-4
     assert p.data.data_ptr() == opt._flat.data_ptr()     # parameters are views of the flat buffer
