@@ -639,16 +639,19 @@ def main():
         ach, peak, unit = ((d["hbm"]["achieved_gbs"], HBM_PEAK_GBS, "GB/s") if bound == "hbm" else
                            (d["mfma"]["achieved_tflops_f32eq"], d["mfma"]["peak_tflops_f32eq"], "TFLOP/s"))
         traffic, traffic_note = None, None
-        tpath = next((q for q in (os.path.join(ROOT, "profiles", r, "gemm_traffic.json") for r in ("r04", "r03", "r02"))
+        tpath = next((q for q in (os.path.join(ROOT, "profiles", r, "gemm_traffic.json") for r in ("r05", "r04"))
                       if os.path.exists(q)), "")
         if tpath and args.gemm_precision == "f16x3":
-            # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC
-            # passes (FETCH_SIZE x2 + WRITE_SIZE, the guide's gfx950 correction)
+            # HBM bytes per launch of the dominant kind from the committed rocprofv3 PMC passes
+            # (FETCH_SIZE x2 + WRITE_SIZE, the guide's gfx950 correction): the mean over the
+            # kind's launches, as per_kind's algorithmic bytes are
             t = json.load(open(tpath))
-            hit = [x for x in t.get("launches", []) if x.get("kind") == dom]
-            if hit:
-                traffic = hit[0]["bytes"]
-                traffic_note = hit[0].get("note")
+            kd = t.get("kinds", {}).get(dom)
+            if kd:
+                traffic = kd["bytes_per_launch"]
+                traffic_note = (f"{os.path.relpath(tpath, ROOT)}: mean over {kd['launches_profiled']} profiled "
+                                f"launches of the kind's kernels ({kd['read_bytes_per_launch'] / 1e6:.1f} MB read, "
+                                f"{kd['write_bytes_per_launch'] / 1e6:.1f} MB written per launch)")
         nt_fl, tn_fl = algorithmic_gemm_flops(net, RAYS * SAMPLES, split=True)
         fam_ms = sum(rec["ms"] for rec in kinds.values())
         fam_mfma = sum(rec["mfma_flops"] for rec in kinds.values())

@@ -777,39 +777,89 @@ constexpr int dma_count(int tt) {
     return tt >= CT ? 0 : (L_OUT[layer_of(tt)] == 256 ? 2 : 1) + (kbase(layer_of(tt)) == tt ? 1 : 0);
 }
 
-// the counted waits.  Every 32-k step k (global over the chain) waits for the DMAs issued D
-// steps earlier; vmcnt counts loads, stores and LDS-DMA together in issue order, so the count
-// is every vector-memory op the wave issued after them: the later steps' DMAs and, in the
-// training kernel, the stores each step issues after its DMAs (st_ops_k).  Ops left out of
-// the count only make a wait stricter.
+// The barrier of a 32-k step sits in the middle of the step before it.  32-k step k (global
+// over the chain, slot pair k % NPAIR) is published by barrier B_k, which every wave passes at
+// tile tb(k - 1) of step k - 1 (B_0 in the prologue) after waiting (vmcnt) for its own share of
+// step k's DMAs; right behind B_k a wave issues the DMAs of step k - 1 + NPAIR - 1 = k + NPAIR - 2
+// (the pair step k - 2 used: every wave is past it), and from tile tb + 1 on it reads step k's
+// first weight fragments while step k - 1's last MFMAs run.  A step therefore starts without a
+// barrier, without LDS latency and without DMA issue, and a layer's epilogue sits between two
+// barriers: the two waves of a SIMD leave it at their own pace (the older one first) and the
+// one ahead starts the next layer's MFMAs beside the other's epilogue VALU.
 constexpr int nks(int l) { return L_KS[l] / 2; }
 constexpr int kfirst(int l) { return l == 0 ? 0 : kfirst(l - 1) + nks(l - 1); }
 constexpr int layer_of_k(int k) { int l = 0; while (l + 1 < CNL && kfirst(l + 1) <= k) ++l; return l; }
 constexpr int tt_of_k(int k) { return kbase(layer_of_k(k)) + 2 * (k - kfirst(layer_of_k(k))); }
+constexpr int NK = kfirst(CNL);             // 32-k steps of the chain
 template <bool TR>
-constexpr int dma_ops_k(int k) {
-    return dma_count(tt_of_k(k) + 2 * LY<TR>::D) + dma_count(tt_of_k(k) + 2 * LY<TR>::D + 1);
-}
-// training, layer l >= 1, k-step u: the previous layer's output is saved two float4 stores per
+constexpr int npair() { return LY<TR>::NSLOT / 2; }
+// weight fragments are read PF tiles ahead of their MFMAs (a ring of PF + 1 fragment pairs that
+// runs on across steps and layers)
+#ifndef NERF_CHAIN_PF_TR
+#define NERF_CHAIN_PF_TR 2
+#endif
+template <bool TR>
+constexpr int pf_tiles() { return TR ? NERF_CHAIN_PF_TR : 3; }
+constexpr int ntj_k(int k) { return L_OUT[layer_of_k(k)] / 16; }
+// step -> first global tile and tile -> step, tabulated once (the templates ask per tile)
+struct TileMap {
+    int first[NK + 1];
+    int step[16 * NK];
+    constexpr TileMap() : first{}, step{} {
+        int g = 0;
+        for (int k = 0; k < NK; ++k) {
+            first[k] = g;
+            for (int j = 0; j < ntj_k(k); ++j) step[g + j] = k;
+            g += ntj_k(k);
+        }
+        first[NK] = g;
+    }
+};
+constexpr TileMap kTiles{};
+constexpr int gtile(int k) { return kTiles.first[k]; }
+constexpr int NG = gtile(NK);               // MFMA tiles of the chain
+constexpr int step_of_tile(int G) { return kTiles.step[G]; }
+// the tile of step k behind whose MFMAs (and save pieces) the wave waits, passes B_{k+1} and
+// issues DMAs: the last tile before the first read of step k + 1's fragments
+template <bool TR>
+constexpr int tb(int k) { return ntj_k(k) - pf_tiles<TR>() - 1; }
+// vector-memory ops of the DMAs of 32-k step m (two 16-k steps), and of those issued in step j
+constexpr int dma_step(int m) { return m >= NK ? 0 : dma_count(tt_of_k(m)) + dma_count(tt_of_k(m) + 1); }
+template <bool TR>
+constexpr int dma_in(int j) { return dma_step(j + npair<TR>() - 1); }
+// training, layer l >= 1, step u: the previous layer's output is saved two float4 stores per
 // tile pair (pairs 0 and 1 at u = 0, pair u + 1 at u = 1..6); at u = 0 of l >= 2 layer l - 2's
-// column maxima and ReLU words leave LDS (one store each)
+// column maxima and ReLU words leave LDS (one store each).  All before the step's barrier
 template <bool TR>
-constexpr int st_ops_k(int k) {
+constexpr int pre_st(int k) {
     const int l = layer_of_k(k), u = k - kfirst(l);
     if (!TR || l == 0) return 0;
     return u == 0 ? 4 + (l >= 2 ? 2 : 0) : (u <= 6 ? 2 : 0);
 }
+// the counted wait before B_{k+1} (at tile tb(k) of step k) for the DMAs of step k + 1, issued
+// behind B_{k + 3 - NPAIR} in step j0 = k + 2 - NPAIR (the prologue when negative): vmcnt counts
+// loads, stores and LDS-DMA together in issue order, so the count is every vector-memory op the
+// wave issued after them.  Ops left out of the count only make a wait stricter
 template <bool TR>
 constexpr int wait_n(int k) {
-    constexpr int D = LY<TR>::D;
-    int n = k >= D ? st_ops_k<TR>(k - D) : 0;
-    for (int i = (k - D + 1 > 0 ? k - D + 1 : 0); i < k; ++i) n += dma_ops_k<TR>(i) + st_ops_k<TR>(i);
-    if (k < D)
-        for (int t = 2 * k + 2; t < 2 * D; ++t) n += dma_count(t);
+    constexpr int P = npair<TR>();
+    const int j0 = k + 2 - P;
+    int n = 0;
+    if (j0 < 0)
+        for (int m = k + 2; m <= P - 2; ++m) n += dma_step(m);
+    for (int j = (j0 + 1 > 0 ? j0 + 1 : 0); j < k; ++j) n += pre_st<TR>(j) + dma_in<TR>(j);
+    return n + pre_st<TR>(k);
+}
+// the prologue's wait for step 0 (it issues the DMAs of steps 0 .. NPAIR - 2)
+template <bool TR>
+constexpr int wait_prologue() {
+    int n = 0;
+    for (int m = 1; m <= npair<TR>() - 2; ++m) n += dma_step(m);
     return n;
 }
-static_assert(wait_n<false>(5) == dma_count(kbase(1) + 6 + 2) + dma_count(kbase(1) + 6 + 3), "eval waits");
-static_assert(wait_n<false>(0) == dma_count(2) + dma_count(3), "eval waits");
+static_assert(wait_n<true>(0) == dma_step(2) && wait_n<true>(1) == dma_in<true>(0), "training waits");
+static_assert(wait_n<true>(5) == pre_st<true>(4) + dma_in<true>(4) + pre_st<true>(5), "training waits");
+static_assert(wait_n<false>(0) == 0 && wait_n<false>(7) == 0, "eval waits");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float pf2 __attribute__((ext_vector_type(2)));
@@ -827,6 +877,29 @@ __device__ __forceinline__ uint32_t rows_or(uint32_t v) {
     const uint32_t r = a[0] | a[1];
     const auto b = __builtin_amdgcn_permlane32_swap(r, r, false, false);
     return b[0] | b[1];
+}
+// max / sum over the four 16-lane rows (lanes n, n + 16, n + 32, n + 48) by permlane swaps: no
+// ds_bpermute and no lane-address registers (which the compiler would keep -- or spill --
+// across the chain).  rows_max takes non-negative floats (ordered as their bits)
+__device__ __forceinline__ float rows_max(float v) {
+    const uint32_t x = __float_as_uint(v);
+    const auto a = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    const uint32_t r = max((uint32_t)a[0], (uint32_t)a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(r, r, false, false);
+    return __uint_as_float(max((uint32_t)b[0], (uint32_t)b[1]));
+}
+__device__ __forceinline__ float rows_sum(float v) {
+    const uint32_t x = __float_as_uint(v);
+    const auto a = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    const float r = __uint_as_float(a[0]) + __uint_as_float(a[1]);   // own + the partner row's, as a shuffle sum
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(r), __float_as_uint(r), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+// a fresh copy of a lane value the compiler may not keep live (or spill) across the chain:
+// derived addresses are rebuilt from it where they are used
+__device__ __forceinline__ int fresh(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
 }
 // the chains' row exponent: row_exp capped at 127 so that 2^e is an f32 (rows below 2^-113
 // keep a smaller scale; nothing overflows)
@@ -874,11 +947,14 @@ struct State {
     u16x2 rk0, rk1;                     // ReLU-bit weights {1, 2} << 4 g, {4, 8} << 4 g (relu_word)
     unsigned long long t_wait, t_bar, t_epi, t_pro, t_last, t_start;   // diagnostics (stamps): cycles in the
                                                        // k-step waits, barriers, layer epilogues, prologue
+    int fr;                             // the lane's weight-fragment offset in a ring slot pair: slot
+                                        // g >> 1 of the pair, k-half g & 1, image row n (+ 16 j per tile)
     uint4 act_hi[8], act_lo[8];         // A operand: 8 k-steps of 32 (the 256 activations)
     uint4 enc_hi[2], enc_lo[2];         // encoding segment (64 columns) of the current layer
     f32x4 acc[16];                      // 16 rows x 256 outputs
     f32x4 xs[16];                       // the previous epilogue's outputs (tile layout), split into act
                                         // and saved during the next layer's k-steps
+    uint4 wh[4], wl[4];                 // weight-fragment ring (hi / lo planes), PF + 1 tiles
 };
 
 // diagnostics (nerf_chain_debug_stamps, NERF_CHAIN_STAMPS builds): cycles since the last tick
@@ -1055,6 +1131,12 @@ constexpr int piece_tile(int piece) {
         return T[piece];
     }
 }
+// the pieces that store (vector memory) run no later than the tile of the step's barrier, tb =
+// ntj - PF - 1 (the wait counts take every store of a step as issued before it): PF 2 in the
+// training forward (16- and 8-tile steps), 3 in the backward (16)
+static_assert(piece_tile<16>(P_STORE) <= 16 - 3 - 1 && piece_tile<16>(P0_STORE) <= 16 - 3 - 1 &&
+                  piece_tile<8>(P_STORE) <= 8 - 2 - 1 && piece_tile<8>(P0_STORE) <= 8 - 2 - 1,
+              "stores before the barrier");
 // training: the save work of layer l's k-step u (the previous layer's output, P = p.L[l - 1]),
 // piece j of ntj
 template <int l, int u, int j, int ntj>
@@ -1128,84 +1210,102 @@ __device__ __forceinline__ void split_pieces(State& st) {
     }
 }
 
-// weight fragments are read PF tiles ahead of their MFMAs (a ring of PF + 1 fragment pairs)
-template <bool TR>
-constexpr int pf_tiles() { return TR ? 2 : 3; }
-
-// tile j of a k-step (compile-time j, so the pieces are placed between MFMA groups)
-template <int l, int u, bool TR, int j, int ntj>
-__device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, const uint4& ah, const uint4& al,
-                                            const char* base, uint4 (&wh)[pf_tiles<TR>() + 1],
-                                            uint4 (&wl)[pf_tiles<TR>() + 1]) {
-    constexpr int PF = pf_tiles<TR>(), R = PF + 1;
-    if constexpr (j < ntj) {
-        if constexpr (j + PF < ntj) {
-            wh[(j + PF) % R] = *reinterpret_cast<const uint4*>(base + 256 * (j + PF));
-            wl[(j + PF) % R] = *reinterpret_cast<const uint4*>(base + 256 * (j + PF) + SPLANE);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        st.acc[j] = mfma16(wh[j % R], al, st.acc[j]);   // hi . lo
-        st.acc[j] = mfma16(wl[j % R], ah, st.acc[j]);   // lo . hi
-        st.acc[j] = mfma16(wh[j % R], ah, st.acc[j]);   // hi . hi
-        split_pieces<l, u, j, ntj>(st);
-        if constexpr (TR) save_pieces<l, u, j, ntj>(p, st);
-        __builtin_amdgcn_sched_barrier(0);
-        mstep_tiles<l, u, TR, j + 1, ntj>(p, st, ah, al, base, wh, wl);
+// global tile G's weight fragments (hi, lo) into ring entry G % (PF + 1): lane (g, n) reads
+// k-chunk g -- slot g >> 1 of the step's pair, k-half g & 1, image row 16 j + n -- one
+// ds_read_b128 per plane from the lane's base (two bases: slot pairs 0-1 and 2-3 of the ring)
+// with the rest an immediate offset
+template <int G, bool TR>
+__device__ __forceinline__ void frag_read(State& st) {
+    if constexpr (G < NG) {
+        using Y = LY<TR>;
+        constexpr int R = pf_tiles<TR>() + 1;
+        constexpr int k = step_of_tile(G), j = G - gtile(k), slot = tt_of_k(k) % Y::NSLOT;
+        static_assert(slot % 2 == 0, "a 32-k step's two slots are consecutive");
+        constexpr int off = Y::O_RING + (slot & 3) * SBYTES + 256 * j;
+        const char* b = st.lds + st.fr + (slot >= 4 ? 4 * SBYTES : 0);
+        st.wh[G % R] = *reinterpret_cast<const uint4*>(b + off);
+        st.wl[G % R] = *reinterpret_cast<const uint4*>(b + off + SPLANE);
+    }
+}
+template <int G0, int N, bool TR>
+__device__ __forceinline__ void frag_reads(State& st) {
+    if constexpr (N > 0) {
+        frag_read<G0, TR>(st);
+        frag_reads<G0 + 1, N - 1, TR>(st);
     }
 }
 
-// one 32-k MFMA step u of layer l (16-k steps TT, TT + 1): wait for its two slots, publish
-// them, refill the two slots step u - 1 read, 16 or 8 feature tiles x 3 products; training:
-// at the first step layer l - 2's column maxima and ReLU words leave LDS, and the steps from
-// the register tile save the previous layer's output beside the MFMAs
+// the work at the start of a layer's first step (behind its first tile's MFMAs): the layer's
+// weight-row exponents (landed with the step, published by its barrier) into the compact
+// array for the epilogue; training: layer l - 2's column maxima over the block's 128 rows
+// (its 128-row group) and its ReLU words, complete since layer l - 1's last step, leave LDS
+// -- wave w stores features 32 w .. + 31, lane (g, n) its row's words 2 g, 2 g + 1 -- and are
+// cleared for layer l's saves
+template <int l, bool TR>
+__device__ __forceinline__ void layer_start(const ChainFwdArgs& p, State& st) {
+    using Y = LY<TR>;
+    const int tid = fresh(st.tid);
+    if (tid < L_OUT[l])   // as the scale 2^-e of the weight row (exact)
+        reinterpret_cast<float*>(st.lds + Y::O_EXP)[(l & 1) * 256 + tid] = __builtin_amdgcn_ldexpf(
+            1.f, -*reinterpret_cast<const int*>(st.lds + Y::O_LEB + (l & 1) * 4096 + tid * 16));
+    if constexpr (TR && l >= 2) {
+        const int lane = tid & 63;
+        if (lane < 32) {
+            uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + Y::O_CMX) + (l & 1) * 256 + 32 * st.wave + lane;
+            p.L[l - 2].cmax[(st.m0 / CROWS) * L_OUT[l - 2] + 32 * st.wave + lane] = __uint_as_float(*cm);
+            *cm = 0u;
+        }
+        const int rl = 16 * st.wave + (lane & 15), g = lane >> 4;
+        uint2* mw = reinterpret_cast<uint2*>(st.lds + Y::O_MSK + (l & 1) * 4096 + 32 * rl + 8 * g);
+        const nerf_chain_layer& Q = p.L[l - 2];
+        *reinterpret_cast<uint2*>(Q.mask + (st.m0 + rl) * Q.ldmask + 2 * g) = *mw;
+        *mw = make_uint2(0u, 0u);
+    }
+}
+
+// tile j of 32-k step u of layer l: the read of tile j + PF's fragments, this tile's three
+// MFMA products, the pieces placed behind it, and at tile tb the wait, barrier B_{k+1} and the
+// DMAs of step k + NPAIR - 1 (one 16-k step at tb, the other at tb + 1)
+template <int l, int u, bool TR, int j, int ntj>
+__device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, const uint4& ah, const uint4& al) {
+    constexpr int PF = pf_tiles<TR>(), R = PF + 1;
+    constexpr int k = kfirst(l) + u, G = gtile(k) + j, T = tb<TR>(k);
+    if constexpr (j < ntj) {
+        // the next layer's first tiles are read after this layer's epilogue (kstep): the ring
+        // is not live across the epilogue's registers
+        if constexpr (G + PF < NG && layer_of_k(step_of_tile(G + PF)) == l) frag_read<G + PF, TR>(st);
+        __builtin_amdgcn_sched_barrier(0);
+        st.acc[j] = mfma16(st.wh[G % R], al, st.acc[j]);   // hi . lo
+        st.acc[j] = mfma16(st.wl[G % R], ah, st.acc[j]);   // lo . hi
+        st.acc[j] = mfma16(st.wh[G % R], ah, st.acc[j]);   // hi . hi
+        if constexpr (u == 0 && j == 0) layer_start<l, TR>(p, st);
+        split_pieces<l, u, j, ntj>(st);
+        if constexpr (TR) save_pieces<l, u, j, ntj>(p, st);
+        if constexpr (k + 1 < NK && j == T) {
+            tick(p, st, nullptr);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_n<TR>(k)) : "memory");
+            tick(p, st, &st.t_wait);
+            __syncthreads();
+            tick(p, st, &st.t_bar);
+            dma<tt_of_k(k + npair<TR>() - 1), TR>(p, st);
+        }
+        if constexpr (k + 1 < NK && j == T + 1) dma<tt_of_k(k + npair<TR>() - 1) + 1, TR>(p, st);
+        __builtin_amdgcn_sched_barrier(0);
+        mstep_tiles<l, u, TR, j + 1, ntj>(p, st, ah, al);
+    }
+}
+
+// one 32-k MFMA step u of layer l (16-k steps TT, TT + 1): 16 or 8 feature tiles x 3 products
+// over the fragments the ring already holds; the steps from the register tile split the next
+// step's A fragment and (training) save the previous layer's output beside the MFMAs
 template <int l, int u, bool TR>
 __device__ __forceinline__ void kstep(const ChainFwdArgs& p, State& st) {
-    using Y = LY<TR>;
-    constexpr int TT = kbase(l) + 2 * u;
     constexpr int nact = l == 0 ? 0 : 8;         // k-steps from the register tile, then the encoding
     constexpr int ntj = L_OUT[l] / 16;
-    tick(p, st, nullptr);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_n<TR>(kfirst(l) + u)) : "memory");
-    tick(p, st, &st.t_wait);
-    __syncthreads();
-    tick(p, st, &st.t_bar);
-    dma<TT + 2 * Y::D, TR>(p, st);
-    dma<TT + 2 * Y::D + 1, TR>(p, st);
-    if constexpr (u == 0) {
-        // this layer's exponents (landed with step TT) into the compact array; published to the
-        // epilogue by the next step's barrier (every layer has at least two 32-k steps)
-        if (st.tid < L_OUT[l])   // as the scale 2^-e of the weight row (exact)
-            reinterpret_cast<float*>(st.lds + Y::O_EXP)[(l & 1) * 256 + st.tid] = __builtin_amdgcn_ldexpf(
-                1.f, -*reinterpret_cast<const int*>(st.lds + Y::O_LEB + (l & 1) * 4096 + st.tid * 16));
-        if constexpr (TR && l >= 2) {
-            // layer l - 2's column maxima over the block's 128 rows (its 128-row group) and its
-            // ReLU words, complete since layer l - 1's last step: wave w stores features 32 w ..
-            // + 31, lane (g, n) its row's words 2 g, 2 g + 1; both cleared for layer l
-            if (st.lane < 32) {
-                uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + Y::O_CMX) + (l & 1) * 256 + 32 * st.wave + st.lane;
-                p.L[l - 2].cmax[(st.m0 / CROWS) * L_OUT[l - 2] + 32 * st.wave + st.lane] = __uint_as_float(*cm);
-                *cm = 0u;
-            }
-            uint2* mw = reinterpret_cast<uint2*>(st.lds + Y::O_MSK + (l & 1) * 4096 + 32 * st.rl + 8 * st.g);
-            const nerf_chain_layer& Q = p.L[l - 2];
-            *reinterpret_cast<uint2*>(Q.mask + (st.m0 + st.rl) * Q.ldmask + 2 * st.g) = *mw;
-            *mw = make_uint2(0u, 0u);
-        }
-    }
+    if constexpr (u == 0) frag_reads<gtile(kfirst(l)), pf_tiles<TR>(), TR>(st);   // published by B_k
     const uint4& ah = u < nact ? st.act_hi[u < nact ? u : 0] : st.enc_hi[u < nact ? 0 : u - nact];
     const uint4& al = u < nact ? st.act_lo[u < nact ? u : 0] : st.enc_lo[u < nact ? 0 : u - nact];
-    // lane (g, n) reads k-chunk g: slot of step TT + (g >> 1), k-half g & 1, image row 16 j + n
-    const char* s0 = st.lds + Y::O_RING + (TT % Y::NSLOT) * SBYTES;
-    const char* s1 = st.lds + Y::O_RING + ((TT + 1) % Y::NSLOT) * SBYTES;
-    const char* base = ((st.g >> 1) ? s1 : s0) + (st.g & 1) * SHALF + st.n * 16;
-    constexpr int PF = pf_tiles<TR>();
-    uint4 wh[PF + 1], wl[PF + 1];
-#pragma unroll
-    for (int t = 0; t < PF; ++t) {
-        wh[t] = *reinterpret_cast<const uint4*>(base + 256 * t);
-        wl[t] = *reinterpret_cast<const uint4*>(base + 256 * t + SPLANE);
-    }
-    mstep_tiles<l, u, TR, 0, ntj>(p, st, ah, al, base, wh, wl);
+    mstep_tiles<l, u, TR, 0, ntj>(p, st, ah, al);
 }
 
 template <int l, int u, bool TR>
@@ -1264,7 +1364,7 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
         rmx = fmaxf(rmx, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
         if constexpr (last_tr) {   // hr (the f32 epilogue value, as the per-layer kernel) and its ReLU words
             const nerf_chain_layer& L = p.L[l];
-            *reinterpret_cast<float4*>(L.out + (st.m0 + st.rl) * L.ldo + f0) = make_float4(x[0], x[1], x[2], x[3]);
+            tile_store4<128>(L.out + st.m0 * 128, (fresh(st.rl) * 128 + g4) * 4, 64 * j, x);
             mw |= ((x[0] > 0.f ? 1u : 0u) | (x[1] > 0.f ? 2u : 0u) | (x[2] > 0.f ? 4u : 0u) | (x[3] > 0.f ? 8u : 0u))
                   << ((j & 1) * 16 + g4);
             if (j & 1) {
@@ -1289,22 +1389,20 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
     }
     if constexpr (last_tr) {
         const nerf_chain_layer& L = p.L[l];
+        const int rl = fresh(st.rl);
         if (2 * st.g < L_OUT[l] / 32)
-            *reinterpret_cast<uint2*>(L.mask + (st.m0 + st.rl) * L.ldmask + 2 * st.g) = make_uint2(st.mk0, st.mk1);
+            *reinterpret_cast<uint2*>(L.mask + (st.m0 + rl) * L.ldmask + 2 * st.g) = make_uint2(st.mk0, st.mk1);
     }
     // the four 16-lane rows hold one sample's features: reduce across them (lanes n, n + 16,
     // n + 32, n + 48)
     if constexpr (head_d || head_c) {
         float* raw = st.fx + FX_RAW + 4 * st.rl;
-        hs0 += __shfl_xor(hs0, 16, 64);
-        hs0 += __shfl_xor(hs0, 32, 64);
+        hs0 = rows_sum(hs0);
         if constexpr (head_d) {
             if (st.g == 0) raw[0] = hs0 + p.bd[0];
         } else {
-            hs1 += __shfl_xor(hs1, 16, 64);
-            hs1 += __shfl_xor(hs1, 32, 64);
-            hs2 += __shfl_xor(hs2, 16, 64);
-            hs2 += __shfl_xor(hs2, 32, 64);
+            hs1 = rows_sum(hs1);
+            hs2 = rows_sum(hs2);
             if (st.g == 0) {
                 raw[1] = hs0 + p.bc[0];
                 raw[2] = hs1 + p.bc[1];
@@ -1316,8 +1414,7 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
         // next layer's A operand: row exponent over the row's 256 features (and the encoding
         // the next layer joins), k-step 0's fp16 pairs now, the others during the next layer's
         // k-steps (split_pieces)
-        float m = fmaxf(rmx, __shfl_xor(rmx, 16, 64));
-        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        float m = rows_max(rmx);
         const float* drec = st.fx + FX_ENCD + ENCD_REC * (st.rl / p.S);
         if constexpr (l == 3) {
             if constexpr (TR) {
@@ -1388,6 +1485,9 @@ __device__ __forceinline__ void encode_p(const ChainFwdArgs& p, State& st) {
     reinterpret_cast<float*>(st.lds + Y::O_RMX)[part * 128 + row] = m;
 }
 
+#ifndef NERF_CHAIN_PRIO
+#define NERF_CHAIN_PRIO 0     // 1: waves 4-7 (the second-dispatched half) at s_setprio 1 (MI355X_MICROARCH.md item 4)
+#endif
 template <bool TR>
 __device__ __forceinline__ void init_state(State& st, char* smem) {
     st.lds = smem;
@@ -1400,11 +1500,15 @@ __device__ __forceinline__ void init_state(State& st, char* smem) {
     st.rl = 16 * st.wave + st.n;
     st.voff16 = 16u * st.lane;
     st.vrow = (st.rl * 256 + 4 * st.g) * 4;
+    st.fr = (st.g >> 1) * SBYTES + (st.g & 1) * SHALF + st.n * 16;
     st.mk0 = st.mk1 = 0u;
     st.rk0 = u16x2{(unsigned short)(1u << (4 * st.g)), (unsigned short)(2u << (4 * st.g))};
     st.rk1 = u16x2{(unsigned short)(4u << (4 * st.g)), (unsigned short)(8u << (4 * st.g))};
     st.t_wait = st.t_bar = st.t_epi = st.t_pro = 0;
     st.t_last = st.t_start = NERF_CHAIN_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    if constexpr (NERF_CHAIN_PRIO) {
+        if (st.wave >= 4) __builtin_amdgcn_s_setprio(1);
+    }
 }
 
 template <bool TR>
@@ -1429,13 +1533,14 @@ __global__ __launch_bounds__(512, 2) void k_render_fused2(ChainFwdArgs p) {
     __shared__ __attribute__((aligned(16))) char smem[Y::BYTES];
     State st;
     init_state<false>(st, smem);
-    dma_n<0, 2 * Y::D, false>(p, st);
+    dma_n<0, 2 * (npair<false>() - 1), false>(p, st);   // steps 0 .. NPAIR - 2
     // head weights into LDS, then the samples and both encodings (beside the DMAs)
     if (st.tid < 256) st.fx[FX_WD + st.tid] = p.wd[st.tid];
     for (int e = st.tid; e < 384; e += NTH) st.fx[FX_WC + e] = p.wc[e];
     encode_p(p, st);
     fused_encode_d(p, st.fx, st.tid, st.m0);
-    __syncthreads();
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_prologue<false>()) : "memory");
+    __syncthreads();   // B_0 (and the encodings in LDS)
     {
         const float* rp = reinterpret_cast<const float*>(smem + Y::O_RMX);
         st.er = chain_exp(fmaxf(fmaxf(rp[st.rl], rp[128 + st.rl]), fmaxf(rp[256 + st.rl], rp[384 + st.rl])));
@@ -1479,7 +1584,9 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_train2(ChainFwdArgs p) {
     reinterpret_cast<uint32_t*>(smem + Y::O_CMX)[st.tid] = 0u;
     reinterpret_cast<uint4*>(smem + Y::O_MSK)[st.tid] = make_uint4(0u, 0u, 0u, 0u);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    dma_n<0, 2 * Y::D, true>(p, st);
+    dma_n<0, 2 * (npair<true>() - 1), true>(p, st);   // steps 0 .. NPAIR - 2
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_prologue<true>()) : "memory");
+    __syncthreads();   // B_0
     tick(p, st, &st.t_pro);
     chain_layers<true>(p, st);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1534,30 +1641,48 @@ constexpr bool first_step(int tt) { return tt < CTB && kb(layer_of(tt)) == tt; }
 // LDS-DMA instructions per wave at 16-k step tt: 2 ring pieces, +1 at a layer's first step
 // (waves 0-3 the weight-row exponents, waves 4-7 the block's ReLU words of the layer input)
 constexpr int dma_count(int tt) { return tt >= CTB ? 0 : 2 + (first_step(tt) ? 1 : 0); }
-constexpr int NSLOT = 8, D = NSLOT / 2 - 1;   // ring slots, 32-k steps in flight
+constexpr int NSLOT = 8, NPAIR = NSLOT / 2;   // ring slots (16-k), slot pairs (32-k steps)
 constexpr int nks(int i) { return KS_[i] / 2; }
 constexpr int kfirst(int i) { return i == 0 ? 0 : kfirst(i - 1) + nks(i - 1); }
 constexpr int layer_of_k(int k) { int i = 0; while (i + 1 < NL && kfirst(i + 1) <= k) ++i; return i; }
 constexpr int tt_of_k(int k) { return kb(layer_of_k(k)) + 2 * (k - kfirst(layer_of_k(k))); }
-constexpr int dma_ops_k(int k) { return dma_count(tt_of_k(k) + 2 * D) + dma_count(tt_of_k(k) + 2 * D + 1); }
-// stores of 32-k step k, all issued after its DMAs: the D_i pair stores (pairs 0 and 1 at u =
-// 0, pair u + 1 at u = 1 .. nks - 2), at a layer's first step the previous dy's column maxima,
-// at a layer's last step the epilogue's row-max store
-constexpr int st_ops_k(int k) {
+constexpr int NK = kfirst(NL);
+constexpr int PF = 3;   // weight fragments read PF tiles ahead of their MFMAs (the ring runs across steps)
+constexpr int NG = 16 * NK;                  // MFMA tiles (16 per step)
+constexpr int TB = 16 - PF - 1;              // the barrier tile of a step (f2::tb)
+constexpr int dma_step(int m) { return m >= NK ? 0 : dma_count(tt_of_k(m)) + dma_count(tt_of_k(m) + 1); }
+constexpr int dma_in(int j) { return dma_step(j + NPAIR - 1); }
+// stores of step k before its barrier: the D_i pair stores (pairs 0 and 1 at u = 0, pair u + 1
+// at u = 1 .. nks - 2), at a layer's first step the previous dy's column maxima; behind its
+// DMAs (post): at a layer's last step the epilogue's row-max store
+constexpr int pre_st(int k) {
     const int i = layer_of_k(k), u = k - kfirst(i);
-    return (u == 0 ? 4 : (u + 1 < nks(i) ? 2 : 0)) + (u == 0 && i >= 1 ? 1 : 0) +
-           (u == nks(i) - 1 && i < NL - 1 ? 1 : 0);
+    return (u == 0 ? 4 : (u + 1 < nks(i) ? 2 : 0)) + (u == 0 && i >= 1 ? 1 : 0);
 }
-// the counted wait of 32-k step k: for the DMAs issued D steps earlier (vmcnt counts loads,
-// stores and LDS-DMA together in issue order; ops left out only make a wait stricter)
+constexpr int post_st(int k) {
+    const int i = layer_of_k(k), u = k - kfirst(i);
+    return u == nks(i) - 1 && i < NL - 1 ? 1 : 0;
+}
+// the counted wait before B_{k+1} for step k + 1's DMAs, issued behind the barrier of step j0 =
+// k + 2 - NPAIR (f2::wait_n, plus the post stores)
 constexpr int wait_n(int k) {
-    int n = k >= D ? st_ops_k(k - D) : 0;
-    for (int i = (k - D + 1 > 0 ? k - D + 1 : 0); i < k; ++i) n += dma_ops_k(i) + st_ops_k(i);
-    if (k < D)
-        for (int t = 2 * k + 2; t < 2 * D; ++t) n += dma_count(t);
+    const int j0 = k + 2 - NPAIR;
+    int n = 0;
+    if (j0 < 0)
+        for (int m = k + 2; m <= NPAIR - 2; ++m) n += dma_step(m);
+    else
+        n += post_st(j0);
+    for (int j = (j0 + 1 > 0 ? j0 + 1 : 0); j < k; ++j) n += pre_st(j) + dma_in(j) + post_st(j);
+    return n + pre_st(k);
+}
+constexpr int wait_prologue() {
+    int n = 0;
+    for (int m = 1; m <= NPAIR - 2; ++m) n += dma_step(m);
     return n;
 }
-static_assert(wait_n(0) == dma_count(2) + dma_count(3) + dma_count(4) + dma_count(5), "prologue waits");
+static_assert(wait_n(0) == dma_step(2) + pre_st(0) && wait_prologue() == dma_step(1) + dma_step(2), "prologue waits");
+static_assert(wait_n(4) == post_st(2) + pre_st(3) + dma_in(3) + post_st(3) + pre_st(4), "waits");
+static_assert(f2::piece_tile<16>(f2::P_STORE) <= TB && f2::piece_tile<16>(f2::P0_STORE) <= TB, "stores before B");
 
 constexpr int O_RING = 0;
 constexpr int O_LEB = NSLOT * SBYTES;            // [2][256 rows][16 B] weight-row exponent chunks
@@ -1600,8 +1725,9 @@ __device__ __forceinline__ void dma(const nerf_chain_bwd& p, State& st) {
                 // (two lanes per row, 16 bytes each)
                 const int w = st.wave - 4;
                 const int ld = p.ld_in_mask[i];
+                const int lane = f2::fresh(st.lane);
                 f2::dma16(reinterpret_cast<const char*>(p.in_mask[i] + (st.m0 + 32 * w) * ld),
-                          (uint32_t)(((st.lane >> 1) * ld + 4 * (st.lane & 1)) * 4),
+                          (uint32_t)(((lane >> 1) * ld + 4 * (lane & 1)) * 4),
                           st.lds0 + O_MASK + (i & 1) * 4096 + 32 * w * 32);
             }
         }
@@ -1675,67 +1801,77 @@ __device__ __forceinline__ void split_pieces(State& st) {
     }
 }
 
-constexpr int PF = 3;   // weight fragments read PF tiles ahead of their MFMAs (f2::pf_tiles)
+// global tile G's weight fragments into ring entry G % (PF + 1) (f2::frag_read)
+template <int G>
+__device__ __forceinline__ void frag_read(State& st) {
+    if constexpr (G < NG) {
+        constexpr int R = PF + 1;
+        constexpr int k = G / 16, j = G % 16, slot = tt_of_k(k) % NSLOT;
+        static_assert(slot % 2 == 0, "a 32-k step's two slots are consecutive");
+        constexpr int off = O_RING + (slot & 3) * SBYTES + 256 * j;
+        const char* b = st.lds + st.fr + (slot >= 4 ? 4 * SBYTES : 0);
+        st.wh[G % R] = *reinterpret_cast<const uint4*>(b + off);
+        st.wl[G % R] = *reinterpret_cast<const uint4*>(b + off + SPLANE);
+    }
+}
+template <int G0, int N>
+__device__ __forceinline__ void frag_reads(State& st) {
+    if constexpr (N > 0) {
+        frag_read<G0>(st);
+        frag_reads<G0 + 1, N - 1>(st);
+    }
+}
+
+// behind layer i's first tile: its weight-row exponents (landed with the step) as the scales
+// 2^-e for its epilogue; D_{i-1}'s column maxima (complete since layer i-1's last step) out and
+// cleared -- D_0 is 128 wide: waves 4-7 store theirs to the scratch row (one store op per wave)
+template <int i>
+__device__ __forceinline__ void layer_start(const nerf_chain_bwd& p, State& st) {
+    const int tid = f2::fresh(st.tid);
+    if (tid < 256)
+        reinterpret_cast<float*>(st.lds + O_EXP)[(i & 1) * 256 + tid] = __builtin_amdgcn_ldexpf(
+            1.f, -*reinterpret_cast<const int*>(st.lds + O_LEB + (i & 1) * 4096 + tid * 16));
+    if constexpr (i >= 1) {
+        constexpr int W = i - 1 == 0 ? 128 : 256;
+        const int lane = tid & 63;
+        if (lane < 32) {
+            uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + O_CMX) + ((i - 1) & 1) * 256 + 32 * st.wave + lane;
+            float* dst = 32 * st.wave < W ? p.dy_cmax[i - 1] + (st.m0 / CROWS) * W + 32 * st.wave + lane
+                                          : p.scratch + 64 * st.wave + lane;
+            *dst = __uint_as_float(*cm);
+            *cm = 0u;
+        }
+    }
+}
 
 template <int i, int u, int j>
-__device__ __forceinline__ void tiles(const nerf_chain_bwd& p, State& st, const uint4& ah, const uint4& al,
-                                      const char* base, uint4 (&wh)[PF + 1], uint4 (&wl)[PF + 1]) {
+__device__ __forceinline__ void tiles(const nerf_chain_bwd& p, State& st, const uint4& ah, const uint4& al) {
     constexpr int R = PF + 1;
+    constexpr int k = kfirst(i) + u, G = 16 * k + j;
     if constexpr (j < 16) {
-        if constexpr (j + PF < 16) {
-            wh[(j + PF) % R] = *reinterpret_cast<const uint4*>(base + 256 * (j + PF));
-            wl[(j + PF) % R] = *reinterpret_cast<const uint4*>(base + 256 * (j + PF) + SPLANE);
-        }
+        if constexpr (G + PF < NG && layer_of_k((G + PF) / 16) == i) frag_read<G + PF>(st);   // (f2::mstep_tiles)
         __builtin_amdgcn_sched_barrier(0);
-        st.acc[j] = f2::mfma16(wh[j % R], al, st.acc[j]);   // hi . lo
-        st.acc[j] = f2::mfma16(wl[j % R], ah, st.acc[j]);   // lo . hi
-        st.acc[j] = f2::mfma16(wh[j % R], ah, st.acc[j]);   // hi . hi
+        st.acc[j] = f2::mfma16(st.wh[G % R], al, st.acc[j]);   // hi . lo
+        st.acc[j] = f2::mfma16(st.wl[G % R], ah, st.acc[j]);   // lo . hi
+        st.acc[j] = f2::mfma16(st.wh[G % R], ah, st.acc[j]);   // hi . hi
+        if constexpr (u == 0 && j == 0) layer_start<i>(p, st);
         split_pieces<i, u, j>(st);
         save_pieces<i, u, j>(p, st);
+        if constexpr (k + 1 < NK && j == TB) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_n(k)) : "memory");
+            __syncthreads();   // B_{k+1}
+            dma<tt_of_k(k + NPAIR - 1)>(p, st);
+        }
+        if constexpr (k + 1 < NK && j == TB + 1) dma<tt_of_k(k + NPAIR - 1) + 1>(p, st);
         __builtin_amdgcn_sched_barrier(0);
-        tiles<i, u, j + 1>(p, st, ah, al, base, wh, wl);
+        tiles<i, u, j + 1>(p, st, ah, al);
     }
 }
 
 template <int i, int u>
 __device__ __forceinline__ void kstep(const nerf_chain_bwd& p, State& st) {
-    constexpr int TT = kb(i) + 2 * u;
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_n(kfirst(i) + u)) : "memory");
-    __syncthreads();
-    dma<TT + 2 * D>(p, st);
-    dma<TT + 2 * D + 1>(p, st);
-    if constexpr (u == 0) {
-        // this layer's weight-row exponents (landed with step TT) as the scales 2^-e, read by
-        // its epilogue behind later barriers
-        if (st.tid < 256)
-            reinterpret_cast<float*>(st.lds + O_EXP)[(i & 1) * 256 + st.tid] = __builtin_amdgcn_ldexpf(
-                1.f, -*reinterpret_cast<const int*>(st.lds + O_LEB + (i & 1) * 4096 + st.tid * 16));
-        if constexpr (i >= 1) {
-            // D_{i-1}'s column maxima (complete since layer i-1's last step) out and cleared;
-            // D_0 is 128 wide: waves 4-7 store theirs to the scratch row (one store op per wave)
-            constexpr int W = i - 1 == 0 ? 128 : 256;
-            if (st.lane < 32) {
-                uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + O_CMX) + ((i - 1) & 1) * 256 + 32 * st.wave + st.lane;
-                float* dst = 32 * st.wave < W ? p.dy_cmax[i - 1] + (st.m0 / CROWS) * W + 32 * st.wave + st.lane
-                                              : p.scratch + 64 * st.wave + st.lane;
-                *dst = __uint_as_float(*cm);
-                *cm = 0u;
-            }
-        }
-    }
-    const uint4& ah = st.act_hi[u];
-    const uint4& al = st.act_lo[u];
-    // lane (g, n) reads k-chunk g: slot of step TT + (g >> 1), k-half g & 1, image row 16 j + n
-    const char* s0 = st.lds + O_RING + (TT % NSLOT) * SBYTES;
-    const char* s1 = st.lds + O_RING + ((TT + 1) % NSLOT) * SBYTES;
-    const char* base = ((st.g >> 1) ? s1 : s0) + (st.g & 1) * SHALF + st.n * 16;
-    uint4 wh[PF + 1], wl[PF + 1];
-#pragma unroll
-    for (int t = 0; t < PF; ++t) {
-        wh[t] = *reinterpret_cast<const uint4*>(base + 256 * t);
-        wl[t] = *reinterpret_cast<const uint4*>(base + 256 * t + SPLANE);
-    }
-    tiles<i, u, 0>(p, st, ah, al, base, wh, wl);
+    if constexpr (u == 0) frag_reads<16 * kfirst(i), PF>(st);
+    tiles<i, u, 0>(p, st, st.act_hi[u], st.act_lo[u]);
 }
 
 template <int i, int u>
@@ -1796,9 +1932,8 @@ __device__ __forceinline__ void layer(const nerf_chain_bwd& p, State& st) {
         }
     }
     // the row's max over its four 16-lane rows (lanes n, n + 16, n + 32, n + 48)
-    float m = fmaxf(rmx, __shfl_xor(rmx, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    if (st.g == 0) p.dy_rmax[i + 1][st.m0 + st.rl] = m;
+    const float m = f2::rows_max(rmx);
+    if (st.g == 0) p.dy_rmax[i + 1][st.m0 + f2::fresh(st.rl)] = m;
     if constexpr (!last) {
         st.er = f2::chain_exp(m);
         st.ser = __builtin_amdgcn_ldexpf(1.f, st.er);
@@ -1824,6 +1959,10 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_bwd(ChainBwdArgs args) {
     st.rl = 16 * st.wave + st.n;
     st.voff16 = 16u * st.lane;
     st.vrow = (st.rl * 256 + 4 * st.g) * 4;
+    st.fr = (st.g >> 1) * b2::SBYTES + (st.g & 1) * b2::SHALF + st.n * 16;
+    if constexpr (NERF_CHAIN_PRIO) {
+        if (st.wave >= 4) __builtin_amdgcn_s_setprio(1);
+    }
     // head weights into LDS, both column-max parities cleared
     if (st.tid < 256) st.fx[st.tid] = p.wd[st.tid];
     for (int e = st.tid; e < 384; e += NTH) st.fx[256 + e] = p.wc[e];
@@ -1847,15 +1986,16 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_bwd(ChainBwdArgs args) {
             st.xs[j][c] = v;
             m = fmaxf(m, fabsf(v));
         }
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    m = f2::rows_max(m);
     if (st.g == 0) p.dy_rmax[0][row] = m;
     st.er = f2::chain_exp(m);
     st.ser = __builtin_amdgcn_ldexpf(1.f, st.er);
     f2::split_hi<0>(st);
     f2::split_lo<0>(st);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    dma_n<0, 2 * D>(p, st);
+    dma_n<0, 2 * (NPAIR - 1)>(p, st);   // steps 0 .. NPAIR - 2
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_prologue()) : "memory");
+    __syncthreads();   // B_0
     layer<0>(p, st);
     layer<1>(p, st);
     layer<2>(p, st);
@@ -1928,10 +2068,9 @@ extern "C" int nerf_mlp_chain_train(const float* enc_p, const float* enc_d, cons
                    "%s: layer %d: image / bias not 16-byte aligned or chain image rows %d != %d", __func__, l,
                    L.img_rows, L_OUT[l]);
         // every output is mandatory: the k-steps' vmcnt waits count these stores at compile time
-        NERF_CHECK(L.out && L.ldo >= L_OUT[l] && L.ldo % 4 == 0 && (((uintptr_t)L.out) & 15u) == 0 &&
-                       (l == CNL - 1 || L.ldo == 256),
-                   "%s: layer %d: the training chain saves every layer output (ldo %d; 256 for l0..lf)", __func__, l,
-                   L.ldo);
+        NERF_CHECK(L.out && L.ldo == L_OUT[l] && (((uintptr_t)L.out) & 15u) == 0,
+                   "%s: layer %d: the training chain saves every layer output (ldo %d: 256 for l0..lf, 128 for the "
+                   "colour layer)", __func__, l, L.ldo);
         NERF_CHECK(l == 8 || (L.mask && L.ldmask >= L_OUT[l] / 32 && L.ldmask % 2 == 0 &&
                               (((uintptr_t)L.mask) & 7u) == 0),
                    "%s: layer %d: the ReLU words are mandatory (ldmask %d, even, 8-byte aligned)", __func__, l, L.ldmask);

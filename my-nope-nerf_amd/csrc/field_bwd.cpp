@@ -127,7 +127,8 @@ int weight_grad(const nerf_field_bwd& a, const Work& w, int l, const float* dy, 
 // reduce on the side stream behind an event, so a reduce runs beside the next layer's TN; the
 // ray gradients (pose learning) as three input-gradient GEMMs over the saved dy of the colour
 // layer, l4 and l0.  The head-weight partials were forked to the side stream before the chain.
-int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, void* stream, void* side_stream) {
+int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, void* stream, void* side_stream,
+                   bool heads_after) {
     const int np = a.n_pad;
     hipStream_t main = nerf::as_stream(stream), side = nerf::as_stream(side_stream);
     // D_0 = dyr, D_i = dx[10 - i]: the gradient at the output of layer 9 - i
@@ -152,6 +153,11 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
     c.scratch = w.scratch;
     c.n_pad = np;
     RC(nerf_mlp_chain_bwd(&c, stream));
+    if (heads_after) {   // (NERF_HEADS_PLACE=2, A/B only) the head-weight partials behind the chain
+        RC(nerf_heads_bwd_mode(2, graw4, a.act[7], D, a.act[LR], HR, nullptr, 0, D, a.wc, nullptr, 0, w.part, np,
+                               nullptr, nullptr, stream));
+        RC(nerf_heads_reduce(w.part, D, np, a.g_wd, a.g_bd, a.g_wc, a.g_bc, 0, stream));
+    }
     auto dy_of = [&](int l, const float*& dy, const float*& cm, const float*& rm) {
         if (l == LR) { dy = w.dyr; cm = w.dyr_cm; rm = w.dyr_rm; }
         else { dy = w.dx[l + 1]; cm = w.dx_cm[l + 1]; rm = w.dx_rm[l + 1]; }
@@ -362,16 +368,32 @@ int schedule(const nerf_field_bwd& a, void* stream, void* side_stream) {
         RC(nerf_composite_bwd(a.raw4, a.z, a.n_rays, a.n_samples, a.flags, a.g_rgb, a.g_dist, w.graw4, np, stream));
         graw4 = w.graw4;
     }
-    // heads: the head-weight partials (re-reading h8 and hr) on the side stream, dyr on main
-    RC(fork(main, side));
-    RC(nerf_heads_bwd_mode(2, graw4, a.act[7], D, a.act[LR], HR, nullptr, 0, D, a.wc, nullptr, 0, w.part, np, nullptr,
-                           nullptr, side_stream));
-    RC(nerf_heads_reduce(w.part, D, np, a.g_wd, a.g_bd, a.g_wc, a.g_bc, 0, side_stream));
+    // heads: the head-weight partials (re-reading h8 and hr).  With the input-gradient chain on
+    // the caller's stream BEFORE the chain (NERF_HEADS_PLACE 1, the default): beside it (0, the
+    // round-4 placement) the partials and their reduce stretch from ~45 to ~240 us sharing the
+    // CUs with the chain, and the step is 13 us slower (profiles/r05/heads_place_ab.json; 2 =
+    // after the chain: 7 us slower).  The per-layer schedule keeps them on the side stream
+    const char* hp = std::getenv("NERF_HEADS_PLACE");
+    const int heads_place = a.bwd_chain ? (hp ? std::atoi(hp) : 1) : 0;
+    auto heads = [&](hipStream_t s) -> int {
+        RC(nerf_heads_bwd_mode(2, graw4, a.act[7], D, a.act[LR], HR, nullptr, 0, D, a.wc, nullptr, 0, w.part, np,
+                               nullptr, nullptr, s));
+        return nerf_heads_reduce(w.part, D, np, a.g_wd, a.g_bd, a.g_wc, a.g_bc, 0, s);
+    };
+    if (heads_place == 0) {
+        RC(fork(main, side));
+        RC(heads(side));
+    } else if (heads_place == 1) {
+        RC(heads(main));
+    }
     if (!a.bwd_chain)
         RC(nerf_heads_bwd_mode(1, graw4, nullptr, 0, nullptr, 0, a.mask[LR], HR / 32, D, a.wc, w.dyr, HR, nullptr, np,
                                w.dyr_rm, w.dyr_cm, stream));
 
-    if (a.bwd_chain) return chain_schedule(a, w, graw4, stream, side_stream);
+    if (a.bwd_chain) {
+        if (heads_place != 2) return chain_schedule(a, w, graw4, stream, side_stream, false);
+        return chain_schedule(a, w, graw4, stream, side_stream, true);
+    }
 
     const float *dy = w.dyr, *dy_rm = w.dyr_rm, *dy_cm = w.dyr_cm;
     int deferred[L], nd = 0;

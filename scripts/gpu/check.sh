@@ -53,6 +53,13 @@ for step in "$@"; do
       esac
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv --kernel-include-regex "$RX" --pmc $CT -d $OUT/pmc_${step#pmc:} -o run -- python3 $CMD > $OUT/pmc_${step#pmc:}.log 2>&1) || exit $?
       echo "pmc ok: ${step#pmc:}" ;;
+    conv:*)
+      # the PSNR convergence study (tests/convergence_study.py, 8000 annealed steps): conv:<seeds>
+      seeds=$(echo ${step#conv:} | tr ',' ' ')
+      timeout -k 10 1100 python -u tests/convergence_study.py --steps 8000 --seeds $seeds --widths 256 --modes f32 f16x3 \
+        --window 1000 --every-late 100 --every 100 --lr-milestones 0.4 0.55 0.7 --lr-gamma 0.2 \
+        > $OUT/conv_$(echo $seeds | tr ' ' '_').jsonl 2> $OUT/conv_$(echo $seeds | tr ' ' '_').log || exit $?
+      tail -1 $OUT/conv_$(echo $seeds | tr ' ' '_').jsonl ;;
     list)
       (cd /tmp && timeout -s KILL 60 rocprofv3 -L > $OUT/counters.txt 2>&1) || exit $?
       echo "list ok" ;;

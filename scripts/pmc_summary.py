@@ -105,10 +105,25 @@ def main():
                                     "issuing": 4 * s.get("SQ_ACTIVE_INST_ANY", 0) / waves,
                                     "mfma_busy": s.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / waves}
         out.append(e)
+    # per GEMM kind (bench.py roofline.per_kind): mean HBM bytes over every launch of the kind's
+    # kernels -- the same launch set bench.py averages its algorithmic bytes over, so the two
+    # divide (a kind such as dw mixes launches of different sizes: l_f..l5, l4, l3..l1)
+    kinds = collections.defaultdict(lambda: {"read": 0.0, "write": 0.0, "launches": 0})
+    for k in sorted(fetch):
+        if k not in KINDS:
+            continue
+        kd = kinds[KINDS[k][0]]
+        kd["read"] += 2 * sum(fetch[k]["FETCH_SIZE"]) * 1024
+        kd["write"] += sum(write[k]["WRITE_SIZE"]) * 1024
+        kd["launches"] += len(fetch[k]["FETCH_SIZE"])
+    per_kind = {k: {"bytes_per_launch": (v["read"] + v["write"]) / v["launches"],
+                    "read_bytes_per_launch": v["read"] / v["launches"],
+                    "write_bytes_per_launch": v["write"] / v["launches"], "launches_profiled": v["launches"]}
+                for k, v in kinds.items()}
     print(json.dumps({"source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / --pmc WRITE_SIZE / SQ counters "
                                 "(separate passes) of `bench.py --steps 3 --warmup 2 --no-alt --no-cpu-baseline`, "
                                 "--kernel-include-regex 'k_gemm_(nt|tn)_x6|k_wgrad|k_mlp_chain'; FETCH_SIZE x2 (gfx950 correction)",
-                      "launches": out}, indent=1))
+                      "launches": out, "kinds": per_kind}, indent=1))
 
 
 if __name__ == "__main__":
