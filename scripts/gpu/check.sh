@@ -46,6 +46,8 @@ for step in "$@"; do
         wgh) RX=k_wgrad_pair; CT="TCC_HIT_sum TCC_MISS_sum"; CMD="$R/scripts/wgrad_bench.py --loop 20" ;;
         ch1) RX=k_mlp_chain; CT="$C1"; CMD="$BENCH" ;;
         ch2) RX=k_mlp_chain; CT="$C2"; CMD="$BENCH" ;;
+        ch3) RX=k_mlp_chain; CT="SQ_WAVES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_VALU_MFMA_COEXEC_CYCLES SQ_BUSY_CYCLES"; CMD="$BENCH" ;;
+        ch4) RX=k_mlp_chain; CT="SQ_WAVES SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_MISC SQ_INSTS_LDS_ATOMIC SQ_INSTS_LDS_LOAD SQ_INSTS_LDS_STORE"; CMD="$BENCH" ;;
         ic) RX=k_mlp_chain; CT="SQ_WAVES SQ_IFETCH SQ_IFETCH_LEVEL SQ_WAIT_INST_ANY SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE"; CMD="$BENCH" ;;
         fetch) RX="$STEPRX"; CT="FETCH_SIZE"; CMD="$BENCH" ;;
         write) RX="$STEPRX"; CT="WRITE_SIZE"; CMD="$BENCH" ;;
