@@ -40,8 +40,9 @@ extern "C" {
  * and the depth-prior distortion (nerf_depth_affine(_bwd)), 7 nerf_linear_fwd_heads, 8 nerf_heads_bwd_mode,
  * 9 precision mode 2 as the default, 10 nerf_mlp_chain_train, 11 nerf_linear_bwd_weight_seg and
  * nerf_field_backward, 12 nerf_mlp_chain_bwd, nerf_field_bwd.bwd_chain, TN policy 8 and the
- * Adam hyper slot 6 (1 - beta2). */
-#define NERF_HIP_ABI_VERSION 13
+ * Adam hyper slot 6 (1 - beta2), 13 the chain images (nerf_pack_desc dst_cs / dst_cts, nerf_field_bwd
+ * wt_cimg) and torch-exact Adam, 14 nerf_linear_bwd_weight_jobs and nerf_pair_backward's 12P gXY. */
+#define NERF_HIP_ABI_VERSION 14
 int nerf_hip_abi_version(void);
 const char* nerf_hip_last_error(void);
 
@@ -157,6 +158,23 @@ typedef struct nerf_wgrad_job {   /* (slab columns from 0, ldslab >= 256) */
     const float* dy_cmax; const float* x_cmax;
 } nerf_wgrad_job;
 int nerf_linear_bwd_weight_multi(const nerf_wgrad_job* jobs, int n, int m, int splits, void* stream);
+
+/* Weight gradients of several shapes in one launch (ABI 14; the chain backward's weight-gradient
+ * schedule 3, field_bwd.cpp): job i is nerf_linear_bwd_weight(dy_i, lddy_i, nout_i, x_i, ldx_i,
+ * kin_i, m, splits_i, slab_i, ldslab_i, col0_i, bslab_i, dy_cmax_i, x_cmax_i), and the slabs are
+ * those calls' bit for bit.  With S = `splits` (a multiple of 8) the shapes are 256 x 256 at S
+ * splits, 256 x 64 at S or 2 S, 128 x 256 and 128 x 64 at 2 S; in precision mode 2 under TN
+ * policy 8, with every job's column maxima and 128-row multiples per split, ONE launch of 2 S
+ * blocks walks the jobs in order (k_wgrad_jobs); otherwise the n calls. */
+typedef struct nerf_wgrad_tile_job {
+    const float* dy; int lddy; int nout;
+    const float* x; int ldx; int kin;
+    int splits;
+    float* slab; int ldslab; int col0;
+    float* bslab;
+    const float* dy_cmax; const float* x_cmax;
+} nerf_wgrad_tile_job;
+int nerf_linear_bwd_weight_jobs(const nerf_wgrad_tile_job* jobs, int n, int m, int splits, void* stream);
 
 /* ---------------------------------------------------------------------------
  * The training backward of the field in one host call (ABI 11): FieldRunner.backward's
@@ -569,7 +587,8 @@ int nerf_pair_forward(const float* d1, const float* d2, int h, int w, const floa
                       const float* s1, float nl, const float* img1, const float* img2, float* work, int* nn,
                       float* out3, void* stream);
 /* Backward: upstream scalars go_pc / go_rgbs (device, optional) -> g_d1, g_d2 [P] (optional),
- * g13 = {dR (9, row-major), dt (3), ds1}; gXY: scratch [6P] floats; part13: scratch
+ * g13 = {dR (9, row-major), dt (3), ds1}; gXY: scratch [12P] floats, 8-byte aligned (ABI 14: the
+ * gathered-point chamfer gradients as 6P int64 fixed-point sums, order-independent); part13: scratch
  * [13 * ceil(P / 256)] floats.  rgbs_detach_scale: detach_rgbs_scale (training.py:372-375). */
 int nerf_pair_backward(const float* d1, const float* d2, int h, int w, const float* K, const float* Rt,
                        const float* s1, float nl, const float* img1, const float* img2, int rgbs_detach_scale,

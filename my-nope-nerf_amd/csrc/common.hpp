@@ -74,7 +74,13 @@ struct SlabJobDesc {
     float* gb;
 };
 int slab_reduce_jobs(const SlabJobDesc* d, int n, hipStream_t s);
+// the chain backward's head-weight partials (render.hip k_heads_part: hidden 256, colour 128) into
+// `part` (heads_part_blocks(n) x 644 floats) and the two slab-reduce jobs that finish them
+int heads_part_blocks(int n);
+int heads_partials(const float* graw4, const float* h8, int ld8, const float* hr, int ldr, int n, float* part,
+                   float* gwd, float* gbd, float* gwc, float* gbc, SlabJobDesc (&jobs)[2], hipStream_t s);
 constexpr int kWgradPairsMax = 8;
+constexpr int kWgradJobsMax = 8;   // jobs of one k_wgrad_jobs launch
 // two 256 x 64 weight gradients over the position encoding in one launch (l4's enc_p segment and
 // l0, nerf_linear_bwd_weight's arguments each): a's splits first, then b's, on the 4-wave kernel
 int wgrad_narrow_pair(const float* dy_a, int lddy_a, const float* x_a, int ldx_a, int splits_a, float* slab_a,

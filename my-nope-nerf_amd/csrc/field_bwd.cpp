@@ -42,7 +42,7 @@ struct Carve {
 };
 
 struct Work {
-    float *graw4, *dyr, *dyr_rm, *dyr_cm, *part, *scratch;
+    float *graw4, *dyr, *dyr_rm, *dyr_cm, *part, *hpart, *scratch;
     float *dx[L], *dx_rm[L], *dx_cm[L];   // dx[l]: gradient w.r.t. layer l's first input (l = 1..9)
     float *genc_p0, *genc_p4, *genc_d;
     float *slab[L], *bslab[L];
@@ -56,6 +56,7 @@ size_t carve(char* base, int np, int ray_grad, Work& w) {
     w.dyr_rm = c.take(np);
     w.dyr_cm = c.take((size_t)(np / 128) * HR);
     w.part = c.take((size_t)nerf_heads_part_size(D, np));
+    w.hpart = c.take((size_t)nerf::heads_part_blocks(np) * (256 + 384 + 4));
     w.scratch = c.take(512);
     for (int l = 1; l < L; ++l) {
         w.dx[l] = c.take((size_t)np * K1[l]);
@@ -128,7 +129,7 @@ int weight_grad(const nerf_field_bwd& a, const Work& w, int l, const float* dy, 
 // ray gradients (pose learning) as three input-gradient GEMMs over the saved dy of the colour
 // layer, l4 and l0.  The head-weight partials were forked to the side stream before the chain.
 int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, void* stream, void* side_stream,
-                   bool heads_after) {
+                   bool heads_after, const nerf::SlabJobDesc* extra, int n_extra) {
     const int np = a.n_pad;
     hipStream_t main = nerf::as_stream(stream), side = nerf::as_stream(side_stream);
     // D_0 = dyr, D_i = dx[10 - i]: the gradient at the output of layer 9 - i
@@ -162,10 +163,72 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
         if (l == LR) { dy = w.dyr; cm = w.dyr_cm; rm = w.dyr_rm; }
         else { dy = w.dx[l + 1]; cm = w.dx_cm[l + 1]; rm = w.dx_rm[l + 1]; }
     };
-    // the weight-gradient schedule: 1 (the default) as measured in r04n; 2 the balanced one
-    // (NERF_WGRAD_SCHED=2: one eight-layer launch, the encoding segments of l4 and l0 together)
+    // the weight-gradient schedule (NERF_WGRAD_SCHED): 3 (the default) two k_wgrad_jobs launches,
+    // 2.062 vs 2.093 ms/step for 1 (profiles/r05/wgrad_sched_ab.json); 1 the round-4 schedule (r04n);
+    // 2 one eight-layer launch with the encoding segments of l4 and l0 together (= 1 in-step)
     const char* ws = std::getenv("NERF_WGRAD_SCHED");
-    if (ws && std::atoi(ws) == 2) {
+    const int sched = ws ? std::atoi(ws) : 3;
+    if (sched == 3) {
+        // every weight gradient as a job of one of two k_wgrad_jobs launches (2 S blocks, S the
+        // 256 x 256 layers' split count; the narrow tiles fill the same grid instead of a launch
+        // of their own): the colour layer's two segments + l_f .. l5, then l4's two segments +
+        // l3 .. l1 + l0.  Same splits and slab columns as schedule 1, so the same slabs.  The
+        // first launch's slab reduces run on the side stream beside the second launch, the
+        // second's on the caller's stream at the end.
+        nerf::SlabJobDesc jobs[nerf::kSlabJobsMax];
+        int nj = 0;
+        for (int e = 0; e < n_extra; ++e) jobs[nj++] = extra[e];   // the head-weight reduces ride in the first batch
+        auto flush = [&](hipStream_t s) -> int {
+            if (s != main) RC(fork(main, s));
+            RC(nerf::slab_reduce_jobs(jobs, nj, s));
+            nj = 0;
+            return NERF_OK;
+        };
+        auto job = [&](int l) {
+            jobs[nj++] = nerf::SlabJobDesc{w.slab[l], w.splits[l], OUT_P[l], KP[l], NREF[l], KREF[l], w.bslab[l], a.gw[l],
+                                           a.gb[l]};
+        };
+        auto enc_rows = [&](int l) -> int {
+            if (!a.ray_grad) return NERF_OK;
+            const float *dy, *cm, *rm;
+            dy_of(l, dy, cm, rm);
+            const int op = OUT_P[l];
+            const int k0 = l == 0 ? 0 : K1[l];
+            float* out = l == LR ? w.genc_d : l == 4 ? w.genc_p4 : w.genc_p0;
+            return nerf_linear_bwd_data(dy, op, op, a.wt[l] + (size_t)k0 * op, a.wt_img[l] + (size_t)k0 * 8, KP[l], nullptr,
+                                        0, nullptr, nullptr, 0, out, 64, np, 64, rm, nullptr, nullptr, stream);
+        };
+        nerf_wgrad_tile_job tj[nerf::kWgradJobsMax];
+        int nt = 0;
+        // layer l's main segment (x = its input; l0: enc_p) and, for l4 / the colour layer, the
+        // 64-wide encoding segment at slab column K1[l]
+        auto tiles = [&](int l) {
+            const float *dy, *cm, *rm;
+            dy_of(l, dy, cm, rm);
+            const int op = OUT_P[l];
+            const float* x = l == 0 ? a.enc_p : a.act[l - 1];
+            const float* xcm = l == 0 ? a.enc_p_cmax : a.cmax[l - 1];
+            tj[nt++] = nerf_wgrad_tile_job{dy, op, op, x, K1[l], K1[l], w.splits[l], w.slab[l], KP[l], 0, w.bslab[l], cm, xcm};
+            if (SEG[l])
+                tj[nt++] = nerf_wgrad_tile_job{dy, op, op, SEG[l] == 1 ? a.enc_p : a.enc_d, 64, 64, w.splits[l], w.slab[l],
+                                               KP[l], K1[l], nullptr, cm, SEG[l] == 1 ? a.enc_p_cmax : a.enc_d_cmax};
+            job(l);
+        };
+        auto launch = [&]() -> int {
+            RC(nerf_linear_bwd_weight_jobs(tj, nt, np, w.splits[LF], stream));
+            nt = 0;
+            return NERF_OK;
+        };
+        for (int l : {LR, LF, 7, 6, 5}) tiles(l);
+        RC(launch());
+        RC(flush(side));
+        RC(enc_rows(LR));
+        for (int l : {4, 3, 2, 1, 0}) tiles(l);
+        RC(launch());
+        RC(flush(main));
+        RC(enc_rows(4));
+        RC(enc_rows(0));
+    } else if (sched == 2) {
         // the weight gradients back to back on the caller's stream (each needs only the chain's
         // saved dy): the colour layer's two segments (f, enc_d) as two launches; l_f .. l1 -- with
         // l4's h3 segment -- as ONE launch (k_wgrad_pairs: a block walks the eight 256 x 256
@@ -173,8 +236,9 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
         // reduces: every layer but l4 and l0 on the side stream after the eight-layer launch (beside
         // the last one), l4's and l0's on the caller's stream at the end (a cross-stream event costs
         // ~7 us of idle on the stream that records it; one fork per layer was ~80 us per step)
-        nerf::SlabJobDesc jobs[L];
+        nerf::SlabJobDesc jobs[nerf::kSlabJobsMax];
         int nj = 0;
+        for (int e = 0; e < n_extra; ++e) jobs[nj++] = extra[e];   // the head-weight reduces ride in the first batch
         auto flush = [&](hipStream_t s) -> int {
             if (s != main) RC(fork(main, s));
             RC(nerf::slab_reduce_jobs(jobs, nj, s));
@@ -239,8 +303,9 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
         // after l5's (beside l4 .. l1's), l4 .. l1 on the side stream after l1's (beside l0's),
         // l0's on the caller's stream at the end (a cross-stream event costs ~7 us of idle on the
         // stream that records it, and the join another; one fork per layer was ~80 us per step)
-        nerf::SlabJobDesc jobs[L];
+        nerf::SlabJobDesc jobs[nerf::kSlabJobsMax];
         int nj = 0;
+        for (int e = 0; e < n_extra; ++e) jobs[nj++] = extra[e];   // the head-weight reduces ride in the first batch
         auto flush = [&](hipStream_t s) -> int {
             if (s != main) RC(fork(main, s));
             RC(nerf::slab_reduce_jobs(jobs, nj, s));
@@ -369,10 +434,13 @@ int schedule(const nerf_field_bwd& a, void* stream, void* side_stream) {
         graw4 = w.graw4;
     }
     // heads: the head-weight partials (re-reading h8 and hr).  With the input-gradient chain on
-    // the caller's stream BEFORE the chain (NERF_HEADS_PLACE 1, the default): beside it (0, the
-    // round-4 placement) the partials and their reduce stretch from ~45 to ~240 us sharing the
-    // CUs with the chain, and the step is 13 us slower (profiles/r05/heads_place_ab.json; 2 =
-    // after the chain: 7 us slower).  The per-layer schedule keeps them on the side stream
+    // the caller's stream BEFORE the chain: NERF_HEADS_PLACE 1 (the default) by k_heads_bwd mode 2
+    // + k_heads_reduce (~70 + 13 us in-step), 3 by k_heads_part (16-byte buffer loads, 4x the
+    // waves: ~62 us in-step) with the reduces in the first slab batch (2.066 vs 2.058 ms/step,
+    // profiles/r05/heads_part_ab.json); beside the chain (0, the round-4 placement) the partials and their reduce stretch
+    // to ~240 us sharing the CUs with the chain, and the step is 13 us slower than 1
+    // (profiles/r05/heads_place_ab.json; 2 = after the chain: 7 us slower).  The per-layer
+    // schedule keeps them on the side stream
     const char* hp = std::getenv("NERF_HEADS_PLACE");
     const int heads_place = a.bwd_chain ? (hp ? std::atoi(hp) : 1) : 0;
     auto heads = [&](hipStream_t s) -> int {
@@ -380,19 +448,26 @@ int schedule(const nerf_field_bwd& a, void* stream, void* side_stream) {
                                nullptr, nullptr, s));
         return nerf_heads_reduce(w.part, D, np, a.g_wd, a.g_bd, a.g_wc, a.g_bc, 0, s);
     };
+    // NERF_HEADS_PLACE 3 (the default with the chain): the partials by k_heads_part (16-byte loads,
+    // 4x the waves) before the chain, their reduces in the weight gradients' first slab batch
+    nerf::SlabJobDesc hjobs[2];
+    int n_hjobs = 0;
     if (heads_place == 0) {
         RC(fork(main, side));
         RC(heads(side));
     } else if (heads_place == 1) {
         RC(heads(main));
+    } else if (heads_place == 3) {
+        RC(nerf::heads_partials(graw4, a.act[7], D, a.act[LR], HR, np, w.hpart, a.g_wd, a.g_bd, a.g_wc, a.g_bc, hjobs,
+                                main));
+        n_hjobs = 2;
     }
     if (!a.bwd_chain)
         RC(nerf_heads_bwd_mode(1, graw4, nullptr, 0, nullptr, 0, a.mask[LR], HR / 32, D, a.wc, w.dyr, HR, nullptr, np,
                                w.dyr_rm, w.dyr_cm, stream));
 
     if (a.bwd_chain) {
-        if (heads_place != 2) return chain_schedule(a, w, graw4, stream, side_stream, false);
-        return chain_schedule(a, w, graw4, stream, side_stream, true);
+        return chain_schedule(a, w, graw4, stream, side_stream, heads_place == 2, hjobs, n_hjobs);
     }
 
     const float *dy = w.dyr, *dy_rm = w.dyr_rm, *dy_cm = w.dyr_cm;

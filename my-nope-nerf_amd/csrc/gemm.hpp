@@ -649,6 +649,14 @@ struct TNPairs {
     int n;
 };
 void launch_wgrad_pairs(const TNPairs& m, int splits, hipStream_t s);
+// a job list of weight-gradient tiles of several shapes in one launch (k_wgrad_jobs)
+enum WgradJobKind : int { WJ_PAIR = 0, WJ_WIDE = 1, WJ_ENC = 2, WJ_ENC_HALF = 3, WJ_ENC128 = 4 };
+struct TNJobs {
+    TNArgs a[kWgradJobsMax];
+    int kind[kWgradJobsMax];
+    int n;
+};
+void launch_wgrad_jobs(const TNJobs& m, int splits, hipStream_t s);
 void launch_wgrad_two(const TNArgs& a, int na, const TNArgs& b, int nb, hipStream_t s);
 
 }  // namespace nerf

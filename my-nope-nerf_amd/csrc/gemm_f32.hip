@@ -593,6 +593,53 @@ extern "C" int nerf_linear_bwd_weight_multi(const nerf_wgrad_job* j, int n, int 
     return check_launch("k_wgrad_pairs");
 }
 
+// weight gradients of several shapes in one launch (k_wgrad_jobs): each job's shape and split
+// count against the launch's S (2 S blocks) pick its tile kind; anything else runs per job
+extern "C" int nerf_linear_bwd_weight_jobs(const nerf_wgrad_tile_job* j, int n, int m, int splits, void* stream) {
+    NERF_CHECK_PTR(j);
+    hipStream_t s = as_stream(stream);
+    NERF_CHECK(n >= 1 && n <= kWgradJobsMax, "%s: %d jobs (1..%d)", __func__, n, kWgradJobsMax);
+    const int pol = g_tn_policy ? g_tn_policy : kTnDefault;
+    bool fused = g_precision == 2 && pol == 8 && splits > 0 && splits % 8 == 0;
+    TNJobs tj{};
+    double bytes = 0.0, flops = 0.0;
+    for (int i = 0; i < n && fused; ++i) {
+        const nerf_wgrad_tile_job& q = j[i];
+        const bool twice = q.splits == 2 * splits, once = q.splits == splits;
+        int kind = -1;
+        if (q.nout == 256 && q.kin == 256 && once) kind = WJ_PAIR;
+        else if (q.nout == 128 && q.kin == 256 && twice) kind = WJ_WIDE;
+        else if (q.nout == 256 && q.kin == 64 && twice) kind = WJ_ENC;
+        else if (q.nout == 256 && q.kin == 64 && once) kind = WJ_ENC_HALF;
+        else if (q.nout == 128 && q.kin == 64 && twice) kind = WJ_ENC128;
+        fused = kind >= 0 && q.dy_cmax && q.x_cmax && m % q.splits == 0 && (m / q.splits) % 128 == 0 &&
+                wgrad_supported(q.nout, q.kin, q.splits, m / q.splits);
+        if (!fused) break;
+        int rc = tn_args(__func__, q.dy, q.lddy, q.nout, q.x, q.ldx, q.kin, m, q.splits, q.slab, q.ldslab, q.col0,
+                         q.bslab, q.dy_cmax, q.x_cmax, tj.a[i]);
+        if (rc) return rc;
+        tj.kind[i] = kind;
+        // dy counted once per layer: a second segment over the same dy (col0 > 0) adds its x only
+        bytes += 4.0 * m * (q.kin + (q.col0 == 0 ? q.nout : 0)) + 4.0 * q.nout * q.kin + (q.bslab ? 4.0 * q.nout : 0.0);
+        flops += 2.0 * m * q.nout * q.kin;
+    }
+    if (!fused) {
+        for (int i = 0; i < n; ++i) {
+            const nerf_wgrad_tile_job& q = j[i];
+            int rc = nerf_linear_bwd_weight(q.dy, q.lddy, q.nout, q.x, q.ldx, q.kin, m, q.splits, q.slab, q.ldslab,
+                                            q.col0, q.bslab, q.dy_cmax, q.x_cmax, s);
+            if (rc) return rc;
+        }
+        return NERF_OK;
+    }
+    tj.n = n;
+    prof_next(NERF_PROF_DW, bytes);
+    prof_begin(s);
+    launch_wgrad_jobs(tj, splits, s);
+    prof_end(s, flops, 3);
+    return check_launch("k_wgrad_jobs");
+}
+
 namespace nerf {
 int wgrad_narrow_pair(const float* dy_a, int lddy_a, const float* x_a, int ldx_a, int splits_a, float* slab_a,
                       int ldslab_a, int col0_a, float* bslab_a, const float* dcm_a, const float* xcm_a,

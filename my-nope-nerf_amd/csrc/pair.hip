@@ -9,7 +9,7 @@
 //   forward : k_pair_points (P points: pc1, pc2, X, Y, reprojection + rgb_s partials),
 //             k_nn_part (both chamfer directions, query x chunk grid), k_nn_final (argmin over
 //             chunks + |X - Y[nn]| partials), k_pair_reduce (one workgroup, fixed order);
-//   backward: k_pair_bwd_scatter (the gathered-point chamfer gradients, atomics),
+//   backward: k_pair_bwd_scatter (the gathered-point chamfer gradients, 64-bit fixed-point atomics),
 //             k_pair_bwd_points (per-point gradients -> d1, d2 and R, t, scale partials),
 //             k_pair_bwd_reduce.
 // Sizes are tiny (47 x 155 = 7285 points at V_KITTI): the budget is launches, and the NN
@@ -267,29 +267,38 @@ __global__ __launch_bounds__(256) void k_pair_reduce(const float* __restrict__ d
 
 // ---------------------------------------------------------------------------- backward
 // chamfer terms whose gradient lands on a gathered point: d|X_i - Y_a(i)| / dY_a(i) and
-// d|Y_j - X_b(j)| / dX_b(j) (scatter-add, float atomics)
+// d|Y_j - X_b(j)| / dX_b(j), scatter-added as 64-bit fixed point: each term is g * u with
+// u = -(Q_i - R_j) / |Q_i - R_j| in [-1, 1], and u * 2^48 (rounded) is added by an integer
+// atomic.  Integer sums do not depend on the order the atomics land in, so the gradient is the
+// same bits on every run (float atomics are not: a resumed run would drift from the uninterrupted
+// one in the last bit); the scale g = go_pc / P is applied once per point when the sums are read
+// (pair_scattered).  2^48 per term: a point gathered by all 2 P terms still fits in 63 bits.
+constexpr double kPairFix = 281474976710656.0;   // 2^48
 __global__ __launch_bounds__(PT) void k_pair_bwd_scatter(const float* __restrict__ X, const float* __restrict__ Y,
                                                          int P, const int* __restrict__ nn,
-                                                         const float* __restrict__ go_pc, float* __restrict__ gX,
-                                                         float* __restrict__ gY) {
+                                                         unsigned long long* __restrict__ gX,
+                                                         unsigned long long* __restrict__ gY) {
     const int i = blockIdx.x * PT + threadIdx.x;
     if (i >= P) return;
-    const float g = *go_pc / (float)P;
 #pragma unroll
     for (int z = 0; z < 2; ++z) {
         const float* Q = z == 0 ? X : Y;
         const float* Rf = z == 0 ? Y : X;
-        float* gR = z == 0 ? gY : gX;
+        unsigned long long* gR = z == 0 ? gY : gX;
         const int j = nn[z * P + i];
         const float dx = Q[3 * i] - Rf[3 * j], dy = Q[3 * i + 1] - Rf[3 * j + 1], dz = Q[3 * i + 2] - Rf[3 * j + 2];
         const float d = sqrtf(dx * dx + dy * dy + dz * dz);
         if (d > 0.f) {
-            const float f = g / d;
-            atomicAdd(&gR[3 * j], -f * dx);
-            atomicAdd(&gR[3 * j + 1], -f * dy);
-            atomicAdd(&gR[3 * j + 2], -f * dz);
+            atomicAdd(&gR[3 * j], (unsigned long long)llrint((double)(-dx / d) * kPairFix));
+            atomicAdd(&gR[3 * j + 1], (unsigned long long)llrint((double)(-dy / d) * kPairFix));
+            atomicAdd(&gR[3 * j + 2], (unsigned long long)llrint((double)(-dz / d) * kPairFix));
         }
     }
+}
+
+// a point's scattered chamfer gradient: its fixed-point sum times g (one rounding to float)
+__device__ __forceinline__ float pair_scattered(const unsigned long long* s, int k, double g) {
+    return (float)((double)(long long)s[k] * (g / kPairFix));
 }
 
 // per point: the direct chamfer terms plus the scattered ones -> dX_i, dY_i; the rgb_s term
@@ -300,7 +309,8 @@ __global__ __launch_bounds__(PT) void k_pair_bwd_points(PairArgs a, const float*
                                                         const float* __restrict__ go_pc,
                                                         const float* __restrict__ go_rgbs,
                                                         const float* __restrict__ red_out,
-                                                        const float* __restrict__ gX, const float* __restrict__ gY,
+                                                        const unsigned long long* __restrict__ gX,
+                                                        const unsigned long long* __restrict__ gY,
                                                         float* __restrict__ g_d1, float* __restrict__ g_d2,
                                                         float* __restrict__ part) {
     __shared__ float red[PT / 64][13];
@@ -319,8 +329,12 @@ __global__ __launch_bounds__(PT) void k_pair_bwd_points(PairArgs a, const float*
         unproject_pt(m.Kinv, x, y, a.d2[i], pc2);
         // dX_i, dY_i: own terms + scattered terms
         float gx[3], gy[3];
+        const double gsc = (double)gpc;   // the scatter's g
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { gx[k] = gX ? gX[3 * i + k] : 0.f; gy[k] = gY ? gY[3 * i + k] : 0.f; }
+        for (int k = 0; k < 3; ++k) {
+            gx[k] = gX ? pair_scattered(gX + 3 * i, k, gsc) : 0.f;
+            gy[k] = gY ? pair_scattered(gY + 3 * i, k, gsc) : 0.f;
+        }
         if (go_pc) {
 #pragma unroll
             for (int z = 0; z < 2; ++z) {
@@ -500,13 +514,14 @@ extern "C" int nerf_pair_backward(const float* d1, const float* d2, int h, int w
     const int nb = (P + PT - 1) / PT;
     const float* X = work;
     const float* Y = X + 3 * (size_t)P;
-    float* gX = gXY;
-    float* gY = gXY + 3 * (size_t)P;
+    NERF_CHECK(((uintptr_t)gXY & 7u) == 0, "%s: gXY must be 8-byte aligned (64-bit fixed-point sums)", __func__);
+    unsigned long long* gX = reinterpret_cast<unsigned long long*>(gXY);
+    unsigned long long* gY = gX + 3 * (size_t)P;
     hipStream_t s = as_stream(stream);
-    hipMemsetAsync(gXY, 0, 6 * (size_t)P * sizeof(float), s);
-    if (go_pc != nullptr) hipLaunchKernelGGL(k_pair_bwd_scatter, dim3(nb), dim3(PT), 0, s, X, Y, P, nn, go_pc, gX, gY);
+    (void)hipMemsetAsync(gXY, 0, 6 * (size_t)P * sizeof(unsigned long long), s);
+    if (go_pc != nullptr) hipLaunchKernelGGL(k_pair_bwd_scatter, dim3(nb), dim3(PT), 0, s, X, Y, P, nn, gX, gY);
     hipLaunchKernelGGL(k_pair_bwd_points, dim3(nb), dim3(PT), 0, s, a, X, Y, nn, go_pc, go_rgbs, out3,
-                       (const float*)gX, (const float*)gY, g_d1, g_d2, part13);
+                       (const unsigned long long*)gX, (const unsigned long long*)gY, g_d1, g_d2, part13);
     hipLaunchKernelGGL(k_pair_bwd_reduce, dim3(1), dim3(64), 0, s, (const float*)part13, nb, g13);
     return check_launch(__func__);
 }

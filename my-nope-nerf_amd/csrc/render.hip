@@ -1060,6 +1060,130 @@ extern "C" int nerf_heads_bwd(const float* graw4, const float* h8, int ld8, cons
                                dyr_cmax, stream);
 }
 
+// The head-weight partials of the chain backward (hidden 256, colour width 128): per 128-row
+// block, the density head's sum_s graw4[s].x h8[s][:] (256), the colour head's sum_s graw4[s].c
+// hr[s][:] (3 x 128) and the bias sums sum_s graw4[s] (4) -- k_heads_bwd mode 2's sums in another
+// order, laid out as slabs for nerf::slab_reduce_jobs (the reduce then rides in the weight
+// gradients' batch).  Each wave walks 32 rows with 16-byte loads: an h8 row per wave instruction
+// (lane: columns 4 lane .. + 3), two hr rows per instruction (half-wave h: the rows of parity h);
+// 1024 blocks x 4 waves at cfg2 (the mode-2 kernel's 1024 waves of 4-byte loads ran at ~2.8 TB/s
+// in-step).  Sums in a fixed order: the gradients are the same bits on every run.
+constexpr int HP_RPW = 32;                    // rows per wave
+constexpr int HP_ROWS = 4 * HP_RPW;           // rows per block
+__global__ __launch_bounds__(256, 4) void k_heads_part(const float* __restrict__ graw4, const float* __restrict__ h8,
+                                                    int ld8, const float* __restrict__ hr, int ldr, int n,
+                                                    float* __restrict__ wdp, float* __restrict__ wcp,
+                                                    float* __restrict__ bdp, float* __restrict__ bcp) {
+    __shared__ float4 red[4][4][64];   // [wave][wd, wc r, wc g, wc b][lane]
+    __shared__ float4 rb[4];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int half = lane >> 5, l32 = lane & 31;
+    const int r0 = blockIdx.x * HP_ROWS + wave * HP_RPW;
+    float4 awd = make_float4(0.f, 0.f, 0.f, 0.f), ac[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) ac[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto fma4 = [](float g, const float4& v, float4& a) {
+        a.x = fmaf(g, v.x, a.x); a.y = fmaf(g, v.y, a.y); a.z = fmaf(g, v.z, a.z); a.w = fmaf(g, v.w, a.w);
+    };
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    // the wave's rows as buffer resources: row offsets in SGPRs, the lane's column (and for hr
+    // its row parity) in one VGPR each -- few address registers, so every load of a batch can be
+    // in flight at once
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)(h8 + (size_t)r0 * ld8), (short)0,
+                                                                        HP_RPW * ld8 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)(hr + (size_t)r0 * ldr), (short)0,
+                                                                        HP_RPW * ldr * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)(graw4 + 4 * (size_t)r0), (short)0,
+                                                                        HP_RPW * 16, 0x00020000);
+    const int vh = 16 * lane, vr = half * ldr * 4 + 16 * l32, vg = half * 16;
+    auto ld4 = [](const __amdgpu_buffer_rsrc_t& r, int v, int so) {
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        const u4 t = __builtin_amdgcn_raw_buffer_load_b128(r, v, so, 0);
+        return make_float4(__uint_as_float(t.x), __uint_as_float(t.y), __uint_as_float(t.z), __uint_as_float(t.w));
+    };
+#pragma unroll 1
+    for (int t = 0; t < HP_RPW; t += 8) {
+        float4 hv[8], rv[4], gc[4];
+        float gh[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            hv[u] = ld4(rh, vh, (t + u) * ld8 * 4);
+            gh[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, 0, (t + u) * 16, 0));
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            rv[u] = ld4(rr, vr, (t + 2 * u) * ldr * 4);
+            gc[u] = ld4(rg, vg, (t + 2 * u) * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) fma4(gh[u], hv[u], awd);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            fma4(gc[u].y, rv[u], ac[0]);
+            fma4(gc[u].z, rv[u], ac[1]);
+            fma4(gc[u].w, rv[u], ac[2]);
+        }
+    }
+    // the colour sums of the two row parities (lanes l32 and l32 + 32), then the bias sums (lane
+    // l: row r0 + l of the wave's 32; a butterfly in a fixed order)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        ac[c].x += __shfl_xor(ac[c].x, 32, 64); ac[c].y += __shfl_xor(ac[c].y, 32, 64);
+        ac[c].z += __shfl_xor(ac[c].z, 32, 64); ac[c].w += __shfl_xor(ac[c].w, 32, 64);
+    }
+    float4 b = lane < HP_RPW ? *reinterpret_cast<const float4*>(graw4 + 4 * (size_t)(r0 + lane)) : z4;
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) {
+        b.x += __shfl_xor(b.x, o, 64); b.y += __shfl_xor(b.y, o, 64);
+        b.z += __shfl_xor(b.z, o, 64); b.w += __shfl_xor(b.w, o, 64);
+    }
+    red[wave][0][lane] = awd;
+    red[wave][1][lane] = ac[0];
+    red[wave][2][lane] = ac[1];
+    red[wave][3][lane] = ac[2];
+    if (lane == 0) rb[wave] = b;
+    __syncthreads();
+    const int k = threadIdx.x >> 6, e = lane;   // thread: section k (wd, r, g, b), lane e
+    float4 v = red[0][k][e];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+        const float4 q = red[w][k][e];
+        v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+    }
+    const size_t blk = blockIdx.x;
+    if (k == 0) *reinterpret_cast<float4*>(wdp + blk * 256 + 4 * e) = v;
+    else if (e < 32) *reinterpret_cast<float4*>(wcp + blk * 384 + (k - 1) * 128 + 4 * e) = v;
+    if (threadIdx.x == 0) {
+        float4 q = rb[0];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) { q.x += rb[w].x; q.y += rb[w].y; q.z += rb[w].z; q.w += rb[w].w; }
+        bdp[blk] = q.x;
+        bcp[blk * 3 + 0] = q.y; bcp[blk * 3 + 1] = q.z; bcp[blk * 3 + 2] = q.w;
+    }
+}
+
+namespace nerf {
+int heads_part_blocks(int n) { return (n + HP_ROWS - 1) / HP_ROWS; }   // (the kernel takes n % HP_ROWS == 0)
+// the partial slabs of k_heads_part and the two slab-reduce jobs that finish them (gw / gb: the
+// density head's [1][256] + [1], the colour head's [3][128] + [3])
+int heads_partials(const float* graw4, const float* h8, int ld8, const float* hr, int ldr, int n, float* part,
+                   float* gwd, float* gbd, float* gwc, float* gbc, SlabJobDesc (&jobs)[2], hipStream_t s) {
+    NERF_CHECK_PTR(graw4); NERF_CHECK_PTR(h8); NERF_CHECK_PTR(hr); NERF_CHECK_PTR(part);
+    NERF_CHECK(n > 0 && n % HP_ROWS == 0 && ld8 % 4 == 0 && ldr % 4 == 0 && ld8 >= 256 && ldr >= 128,
+               "%s: n %d (a multiple of %d), ld8 %d, ldr %d", __func__, n, HP_ROWS, ld8, ldr);
+    NERF_CHECK_ALIGN16(graw4); NERF_CHECK_ALIGN16(h8); NERF_CHECK_ALIGN16(hr); NERF_CHECK_ALIGN16(part);
+    const int nb = heads_part_blocks(n);
+    float* wdp = part;
+    float* wcp = wdp + (size_t)nb * 256;
+    float* bdp = wcp + (size_t)nb * 384;
+    float* bcp = bdp + nb;
+    hipLaunchKernelGGL(k_heads_part, dim3(nb), dim3(256), 0, s, graw4, h8, ld8, hr, ldr, n, wdp, wcp, bdp, bcp);
+    jobs[0] = SlabJobDesc{wdp, nb, 1, 256, 1, 256, bdp, gwd, gbd};
+    jobs[1] = SlabJobDesc{wcp, nb, 3, 128, 3, 128, bcp, gwc, gbc};
+    return check_launch(__func__);
+}
+}  // namespace nerf
+
 extern "C" int nerf_heads_reduce(const float* part, int hidden, int n_pad, float* gwd, float* gbd,
                                  float* gwc, float* gbc, int accumulate, void* stream) {
     NERF_CHECK_PTR(part); NERF_CHECK_PTR(gwd); NERF_CHECK_PTR(gbd); NERF_CHECK_PTR(gwc); NERF_CHECK_PTR(gbc);

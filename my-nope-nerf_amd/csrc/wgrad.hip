@@ -92,19 +92,26 @@ __device__ __forceinline__ void put_strip(char* d, int plane_bytes, const float 
 // BIAS: the load waves also sum the dy columns (the bias gradient; one column tile per split)
 // par: which exponent set (consecutive layers of one launch alternate, so a layer's exponents
 // can be written while the previous layer's epilogue still reads its own)
-template <int BO, int BK, bool BIAS>
+// AUX: the LDS offset of the column exponents and bias partials (a kernel that runs tiles of
+// several shapes puts them past the largest main region, so one shape's exponents never land in
+// the region another shape's epilogue is still staging its slab through)
+template <int BO, int BK, bool BIAS, int AUX = Cfg<BO, BK>::MAIN>
 __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int jt, int split, int par) {
     using C = Cfg<BO, BK>;
     constexpr int CA = C::CA, CB = C::CB, TM = C::TM, TN = C::TN;
-    const int tid = threadIdx.x;
+    // an opaque copy: nothing derived from the thread index is hoisted out of a kernel's job loop
+    // (k_wgrad_jobs: the shapes' hoisted lane offsets would stay live together and spill)
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int j0 = jt * BK;
     const size_t s0 = (size_t)split * p.rows_per_split;
     const int nst = p.rows_per_split / KS;
-    int* lea = reinterpret_cast<int*>(smem + C::MAIN) + par * (BO + BK);   // the tile's column exponents
+    static_assert(AUX >= C::MAIN, "aux region");
+    int* lea = reinterpret_cast<int*>(smem + AUX) + par * (BO + BK);   // the tile's column exponents
     int* leb = lea + BO;
-    float* lbias = reinterpret_cast<float*>(smem + C::MAIN) + 2 * (BO + BK);   // [4 load waves][BO] bias partials
+    float* lbias = reinterpret_cast<float*>(smem + AUX) + 2 * (BO + BK);   // [4 load waves][BO] bias partials
     // the column exponents: every thread its share (one round trip to the producers' group
     // maxima), in both roles -- the load waves issue their first NS stages before theirs
     auto exponents = [&]() {
@@ -272,11 +279,16 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
 }
 
 // the block of column tile jt, with the bias sums where the layer wants them (column tile 0)
-template <int BO, int BK>
+template <int BO, int BK, int AUX = Cfg<BO, BK>::MAIN>
 __device__ __forceinline__ void block_any(const TNArgs& p, char* smem, int o0, int jt, int split, int par = 0) {
-    if (jt == 0 && p.bslab != nullptr) block<BO, BK, true>(p, smem, o0, jt, split, par);
-    else block<BO, BK, false>(p, smem, o0, jt, split, par);
+    if (jt == 0 && p.bslab != nullptr) block<BO, BK, true, AUX>(p, smem, o0, jt, split, par);
+    else block<BO, BK, false, AUX>(p, smem, o0, jt, split, par);
 }
+
+// the LDS of a kernel that runs tiles of every shape (k_wgrad_jobs)
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+constexpr int JOBS_AUX = cmax(cmax(Cfg<256, 128>::MAIN, Cfg<128, 256>::MAIN), cmax(Cfg<256, 64>::MAIN, Cfg<128, 64>::MAIN));
+constexpr int JOBS_BYTES = JOBS_AUX + cmax(2 * (256 + 128) * 4 + 4 * 256 * 4, 2 * (128 + 256) * 4 + 4 * 128 * 4);
 
 }  // namespace wg
 
@@ -303,6 +315,49 @@ __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_pairs(TNPairs m) {
     // (n = 1 .. 4 and 8, tests/test_gpu_kernels.py) checks the slabs against one launch per layer.
     for (int i = 0; i < m.n; ++i)
         wg::block_any<256, 128>(m.a[i], smem, 0, slot & 1, (slot >> 1) * 8 + (w & 7), i & 1);
+}
+
+// every weight gradient of a backward group in one launch (TN schedule 3, field_bwd.cpp): a job
+// list walked in order by 2 S blocks (S = the 256 x 256 layers' split count, a multiple of 8),
+// block w on XCD w % 8 with column tile jt = (w >> 3) & 1 of split sp = (w >> 4) * 8 + w % 8:
+//   WJ_PAIR      256 x 256 over S splits: column tile jt of split sp (k_wgrad_pair's tiles);
+//   WJ_WIDE      128 x 256 over 2 S splits (the colour layer over f): the whole tile of split 2 sp + jt;
+//   WJ_ENC       256 x 64 over 2 S splits (l0 over enc_p): split 2 sp + jt;
+//   WJ_ENC_HALF  256 x 64 over S splits (l4 over enc_p): output rows 128 jt .. + 127 of split sp
+//                (the XCD pair shares the split's enc_p rows through L2);
+//   WJ_ENC128    128 x 64 over 2 S splits (the colour layer over enc_d): split 2 sp + jt.
+// The jobs run grouped by shape (128 x 256, 128 x 64, 256 x 256, 256 x 64), each group in list
+// order.  The splits and slab columns are those of the per-layer launches, so are the slabs, bit
+// for bit.
+// Each job's exponents alternate between the two sets of one aux region past every shape's main
+// region (JOBS_AUX), so the barrier in a job's exponents() orders it after the previous job's
+// epilogue as in k_wgrad_pairs.
+// SH: the shapes compiled in (bit 0 128 x 256, bit 1 128 x 64, bit 2 256 x 64; 256 x 256 always):
+// with all four in one kernel the register allocation spills, with any three it does not
+template <int SH>
+__global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_jobs(TNJobs m) {
+    __shared__ __attribute__((aligned(16))) char smem[wg::JOBS_BYTES];
+    constexpr int A = wg::JOBS_AUX;
+    const int w = blockIdx.x, q = w >> 3;
+    const int jt = q & 1, sp = (q >> 1) * 8 + (w & 7);
+    // one loop per tile shape: the jobs run grouped by shape in this order, each group in list
+    // order; the exponent set alternates per job run (c)
+    int c = 0;
+    if constexpr (SH & 1)
+        for (int i = 0; i < m.n; ++i)
+            if (m.kind[i] == WJ_WIDE) wg::block_any<128, 256, A>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
+    if constexpr (SH & 2)
+        for (int i = 0; i < m.n; ++i) {
+            const int k = m.kind[i];
+            if (k == WJ_ENC128 || k == WJ_ENC_HALF)
+                wg::block_any<128, 64, A>(m.a[i], smem, k == WJ_ENC_HALF ? 128 * jt : 0, 0,
+                                          k == WJ_ENC_HALF ? sp : 2 * sp + jt, c++ & 1);
+        }
+    for (int i = 0; i < m.n; ++i)
+        if (m.kind[i] == WJ_PAIR) wg::block_any<256, 128, A>(m.a[i], smem, 0, jt, sp, c++ & 1);
+    if constexpr (SH & 4)
+        for (int i = 0; i < m.n; ++i)
+            if (m.kind[i] == WJ_ENC) wg::block_any<256, 64, A>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
 }
 
 // two layers' 256 x 64 tiles in one launch: a's splits (blocks 0 .. na - 1), then b's (l4's
@@ -363,6 +418,23 @@ void launch_wgrad_two(const TNArgs& a, int na, const TNArgs& b, int nb, hipStrea
 
 void launch_wgrad_pairs(const TNPairs& m, int splits, hipStream_t s) {
     hipLaunchKernelGGL(k_wgrad_pairs, dim3(2 * splits), dim3(wg::NTH), 0, s, m);
+}
+
+void launch_wgrad_jobs(const TNJobs& m, int splits, hipStream_t s) {
+    int sh = 0;
+    for (int i = 0; i < m.n; ++i)
+        sh |= m.kind[i] == WJ_WIDE ? 1 : m.kind[i] == WJ_ENC128 || m.kind[i] == WJ_ENC_HALF ? 2 : m.kind[i] == WJ_ENC ? 4 : 0;
+    const dim3 g(2 * splits), b(wg::NTH);
+    switch (sh) {
+    case 0: hipLaunchKernelGGL(k_wgrad_jobs<0>, g, b, 0, s, m); break;
+    case 1: hipLaunchKernelGGL(k_wgrad_jobs<1>, g, b, 0, s, m); break;
+    case 2: hipLaunchKernelGGL(k_wgrad_jobs<2>, g, b, 0, s, m); break;
+    case 3: hipLaunchKernelGGL(k_wgrad_jobs<3>, g, b, 0, s, m); break;
+    case 4: hipLaunchKernelGGL(k_wgrad_jobs<4>, g, b, 0, s, m); break;
+    case 5: hipLaunchKernelGGL(k_wgrad_jobs<5>, g, b, 0, s, m); break;
+    case 6: hipLaunchKernelGGL(k_wgrad_jobs<6>, g, b, 0, s, m); break;
+    default: hipLaunchKernelGGL(k_wgrad_jobs<7>, g, b, 0, s, m); break;   // (spills; no schedule uses it)
+    }
 }
 
 void launch_wgrad_seg(const TNArgs& pm, const TNArgs& ps, int nout, int splits, hipStream_t s) {

@@ -46,7 +46,7 @@ class ProfKind(ctypes.Structure):
 
 
 PROF_KINDS = ("fwd", "dx", "dw", "dw_narrow", "chain_fwd", "chain_bwd")   # NERF_PROF_FWD .. _CHAIN_BWD
-ABI_VERSION = 13                   # NERF_HIP_ABI_VERSION
+ABI_VERSION = 14                   # NERF_HIP_ABI_VERSION
 
 
 _P10 = _c_p * 10
@@ -68,6 +68,13 @@ class WgradJob(ctypes.Structure):
     """nerf_wgrad_job (include/nerf_hip.h): one 256 x 256 layer of nerf_linear_bwd_weight_multi."""
     _fields_ = [("dy", _c_p), ("lddy", _c_i), ("x", _c_p), ("ldx", _c_i), ("slab", _c_p), ("ldslab", _c_i),
                 ("bslab", _c_p), ("dy_cmax", _c_p), ("x_cmax", _c_p)]
+
+
+class WgradTileJob(ctypes.Structure):
+    """nerf_wgrad_tile_job (include/nerf_hip.h): one weight gradient of nerf_linear_bwd_weight_jobs."""
+    _fields_ = [("dy", _c_p), ("lddy", _c_i), ("nout", _c_i), ("x", _c_p), ("ldx", _c_i), ("kin", _c_i),
+                ("splits", _c_i), ("slab", _c_p), ("ldslab", _c_i), ("col0", _c_i), ("bslab", _c_p),
+                ("dy_cmax", _c_p), ("x_cmax", _c_p)]
 
 
 class ChainBwd(ctypes.Structure):
@@ -100,6 +107,7 @@ _SIGS = {
     "nerf_linear_bwd_weight_seg": ([_c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p, _c_i, _c_p,
                                     _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_linear_bwd_weight_multi": ([_c_p, _c_i, _c_i, _c_i, _c_p], _c_i),
+    "nerf_linear_bwd_weight_jobs": ([_c_p, _c_i, _c_i, _c_i, _c_p], _c_i),
     "nerf_linear_bwd_weight_splits": ([_c_i, _c_i, _c_i], _c_i),
     "nerf_field_bwd_workspace_bytes": ([_c_i, _c_i], ctypes.c_size_t),
     "nerf_field_backward": ([_c_p, _c_p, _c_p], _c_i),
@@ -310,6 +318,18 @@ def linear_bwd_weight_multi(layers, m, splits):
         j.dy, j.lddy, j.x, j.ldx = _ptr(dy), _ld(dy), _ptr(x), _ld(x)
         j.slab, j.ldslab, j.bslab, j.dy_cmax, j.x_cmax = _ptr(slab), 256, _ptr(bslab), _ptr(dcm), _ptr(xcm)
     _call("nerf_linear_bwd_weight_multi", ctypes.addressof(jobs), len(layers), m, splits, _stream())
+
+
+def linear_bwd_weight_jobs(jobs, m, splits):
+    """Weight gradients of several shapes in one launch of 2 * splits blocks (mode 2, TN policy 8):
+    jobs is a list of (dy, nout, x, kin, job_splits, slab, ldslab, col0, bslab, dy_cmax, x_cmax), each
+    as linear_bwd_weight(dy, nout, x, kin, m, job_splits, slab, ldslab, col0, bslab, dy_cmax, x_cmax)
+    would write it."""
+    arr = (WgradTileJob * len(jobs))()
+    for j, (dy, nout, x, kin, sp, slab, ldslab, col0, bslab, dcm, xcm) in zip(arr, jobs):
+        j.dy, j.lddy, j.nout, j.x, j.ldx, j.kin, j.splits = _ptr(dy), _ld(dy), nout, _ptr(x), _ld(x), kin, sp
+        j.slab, j.ldslab, j.col0, j.bslab, j.dy_cmax, j.x_cmax = _ptr(slab), ldslab, col0, _ptr(bslab), _ptr(dcm), _ptr(xcm)
+    _call("nerf_linear_bwd_weight_jobs", ctypes.addressof(arr), len(jobs), m, splits, _stream())
 
 
 def bwd_weight_splits(nout, kin, m) -> int:

@@ -47,7 +47,7 @@ class _PairTerms(torch.autograd.Function):
         P = h * w
         nb = (P + 255) // 256
         c = lambda g: None if g is None else g.detach().float().contiguous()
-        gxy = torch.empty(6 * P, device=dev, dtype=torch.float32)
+        gxy = torch.empty(12 * P, device=dev, dtype=torch.float32)   # 6 P int64 fixed-point sums (ABI 14)
         part = torch.empty(13 * nb, device=dev, dtype=torch.float32)
         g13 = torch.empty(13, device=dev, dtype=torch.float32)
         want = ctx.needs_input_grad

@@ -32,8 +32,11 @@ SETTINGS = {
     "dw_two_launch": (0, 0, {"NERF_DW_SEG": "0"}),
     "python_bwd": (0, 0, {"NERF_NATIVE_BWD": "0"}),
     "wgrad2": (0, 0, {"NERF_WGRAD_SCHED": "2"}),
+    "wgrad3": (0, 0, {"NERF_WGRAD_SCHED": "3"}),
     "heads_before": (0, 0, {"NERF_HEADS_PLACE": "1"}),
     "heads_after": (0, 0, {"NERF_HEADS_PLACE": "2"}),
+    "heads_part": (0, 0, {"NERF_HEADS_PLACE": "3"}),
+    "wgrad1": (0, 0, {"NERF_WGRAD_SCHED": "1"}),
 }
 ENV_KEYS = ("NERF_TAIL_MAIN", "NERF_HEADS_SIDE", "NERF_CHAIN", "NERF_DW_SEG", "NERF_NATIVE_BWD", "NERF_WGRAD_SCHED",
             "NERF_HEADS_PLACE")

@@ -37,7 +37,7 @@ def test_binding_covers_the_header():
 
 
 def test_abi_version_and_error_path(lib):
-    assert lib.nerf_hip_abi_version() == 13
+    assert lib.nerf_hip_abi_version() == 14
     rc = lib.nerf_linear_fwd(None, 256, 256, None, 0, 0, None, None, 0, None, None, 256, 128, 256, 1, None, 0,
                              None, None, None, None, None)
     assert rc == -1
@@ -62,6 +62,11 @@ def test_abi_version_and_error_path(lib):
     rc = lib.nerf_linear_bwd_weight_multi(ctypes.addressof(jobs), 0, 131072, 128, None)
     assert rc == -1
     rc = lib.nerf_linear_bwd_weight_multi(None, 2, 131072, 128, None)
+    assert rc == -1
+    tjobs = (_hip.WgradTileJob * 9)()
+    rc = lib.nerf_linear_bwd_weight_jobs(ctypes.addressof(tjobs), 9, 131072, 128, None)
+    assert rc == -1 and b"jobs" in lib.nerf_hip_last_error()
+    rc = lib.nerf_linear_bwd_weight_jobs(None, 2, 131072, 128, None)
     assert rc == -1
 
 

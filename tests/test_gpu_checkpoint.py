@@ -65,6 +65,60 @@ def test_resume_is_bit_identical(dev, tmp_path, hidden, rays):
         assert torch.equal(p.detach(), want[n]), (n, (p.detach() - want[n]).abs().max().item())
 
 
+def _cfg3_trainer(dev):
+    """Config 3 (pose + distortion learned, pc + rgb_s losses) as bench.cfg3_setup builds it,
+    with the three optimizers of train.py:59, :100, :118."""
+    from model.synthetic import vkitti_pair_scene
+    cfg = make_cfg(hidden=256, S=128)
+    t = cfg["training"]
+    t["n_training_points"] = 1024
+    t["annealing_epochs"], t["scheduling_start"] = 2000, 0
+    datas, c2w = vkitti_pair_scene(dev)
+    torch.manual_seed(42)
+    net = mdl.OfficialStaticNerf(cfg)
+    nn_model = mdl.get_model(mdl.Renderer(net, cfg["rendering"], device=dev), cfg, device=dev)
+    opt = HipAdam(nn_model.parameters(), lr=1e-3)
+    pose = mdl.LearnPose(2, True, True, cfg, init_c2w=c2w.clone()).to(dev)
+    distn = mdl.Learn_Distortion(2, True, True, cfg).to(dev)
+    opt_pose = torch.optim.Adam(pose.parameters(), lr=5e-4, fused=True)
+    opt_dist = torch.optim.Adam(distn.parameters(), lr=5e-4, fused=True)
+    tr = mdl.Trainer(nn_model, opt, t, device=dev, optimizer_pose=opt_pose, pose_param_net=pose,
+                     optimizer_distortion=opt_dist, distortion_net=distn)
+    mods = {"model.pt": (nn_model, opt), "model_pose.pt": (pose, opt_pose),
+            "model_distortion.pt": (distn, opt_dist)}
+    return tr, datas, mods
+
+
+def test_resume_cfg3_with_pose_and_distortion_files(dev, tmp_path):
+    """Config 3 resume: model.pt, model_pose.pt and model_distortion.pt written as train.py:
+    255-262 writes them (each module with its optimizer), loaded into a fresh config-3 trainer
+    (train.py:62, :101, :119); the next step (the other camera) leaves the field, the learned
+    poses and the distortion parameters bit for bit where the uninterrupted run leaves them."""
+    tr, datas, mods = _cfg3_trainer(dev)
+    k = 3
+    for i in range(k):
+        tr.train_step(datas[i % 2], it=i + 1, epoch=0, scheduling_start=0)
+    for name, (m, o) in mods.items():
+        mdl.CheckpointIO(str(tmp_path), model=m, optimizer=o).save(name, epoch_it=0, it=k)
+    rng = (torch.get_rng_state(), torch.cuda.get_rng_state(dev))
+    tr.train_step(datas[k % 2], it=k + 1, epoch=0, scheduling_start=0)
+    torch.cuda.synchronize()
+    want = {name: {n: p.detach().clone() for n, p in m.named_parameters()} for name, (m, _) in mods.items()}
+
+    tr2, _, mods2 = _cfg3_trainer(dev)
+    for name, (m, o) in mods2.items():
+        scalars = mdl.CheckpointIO(str(tmp_path), model=m, optimizer=o).load(name, device=dev)
+        assert scalars["it"] == k and scalars["epoch_it"] == 0
+    torch.set_rng_state(rng[0])
+    torch.cuda.set_rng_state(rng[1], dev)
+    tr2.train_step(datas[k % 2], it=k + 1, epoch=0, scheduling_start=0)
+    torch.cuda.synchronize()
+    for name, (m, _) in mods2.items():
+        assert want[name], name
+        for n, p in m.named_parameters():
+            assert torch.equal(p.detach(), want[name][n]), (name, n, (p.detach() - want[name][n]).abs().max().item())
+
+
 def test_torch_adam_state_steps_like_torch_adam(dev):
     """A torch.optim.Adam state (the reference's optimizer, train.py:59) loaded into HipAdam:
     one HIP step from it equals torch Adam's step from the same state bit for bit."""

@@ -292,6 +292,58 @@ def test_wgrad_multi_matches_single(dev, n, m, splits):
         _hip.gemm_set_precision(prev)
 
 
+@pytest.mark.parametrize("which,m,S", [("colour+trunk", 131072, 128), ("l4+trunk+l0", 131072, 128),
+                                        ("colour+trunk", 32768, 32), ("l4+trunk+l0", 32768, 32)])
+def test_wgrad_jobs_matches_single(dev, which, m, S):
+    """nerf_linear_bwd_weight_jobs (k_wgrad_jobs: 2 S blocks walk tiles of four shapes -- the
+    TN schedule 3 launches of the field backward) against one nerf_linear_bwd_weight per job
+    with the same splits and slab columns: every slab and bias partial bit-identical."""
+    prev = _hip.gemm_get_precision()
+    _hip.gemm_set_precision(2)
+    try:
+        g = torch.Generator().manual_seed(m + len(which))
+        jobs = []
+
+        def layer(nout, kin, sp, x2=None, sp2=None, bias=True):
+            dy = _rand(m, nout, g=g).to(dev)
+            x = _rand(m, kin, g=g).clamp_min(0).to(dev)
+            dy[:, 3] *= 1e-5
+            ld = kin + (64 if x2 is not None else 0)
+            slab = torch.full((sp * nout * ld,), float("nan"), device=dev)
+            bslab = torch.full((sp * nout,), float("nan"), device=dev) if bias else None
+            jobs.append((dy, nout, x, kin, sp, slab, ld, 0, bslab, _cm(dy), _cm(x)))
+            if x2 is not None:
+                e = _rand(m, 64, g=g).to(dev)
+                jobs.append((dy, nout, e, 64, sp, slab, ld, kin, None, _cm(dy), _cm(e)))
+
+        if which == "colour+trunk":
+            layer(128, 256, 2 * S, x2=True)          # the colour layer over [f | enc_d]
+            for _ in range(4):
+                layer(256, 256, S)                   # l_f .. l5
+        else:
+            layer(256, 256, S, x2=True)              # l4 over [h3 | enc_p]: the enc_p tile per output half
+            for _ in range(3):
+                layer(256, 256, S)                   # l3 .. l1
+            layer(256, 64, 2 * S)                    # l0 over enc_p
+        want = []
+        for dy, nout, x, kin, sp, slab, ld, col0, bslab, dcm, xcm in jobs:
+            if col0 == 0:
+                want.append((torch.full_like(slab, float("nan")),
+                             None if bslab is None else torch.full_like(bslab, float("nan"))))
+            s1, b1 = want[-1]
+            _hip.linear_bwd_weight(dy, nout, x, kin, m, sp, s1, ld, col0, b1 if col0 == 0 else None,
+                                   dy_cmax=dcm, x_cmax=xcm)
+        _hip.linear_bwd_weight_jobs(jobs, m, S)
+        torch.cuda.synchronize()
+        got = [(slab, bslab) for (_, _, _, _, _, slab, _, col0, bslab, _, _) in jobs if col0 == 0]
+        assert len(got) == len(want)
+        for (slab, bslab), (s1, b1) in zip(got, want):
+            assert torch.equal(slab, s1)
+            assert (bslab is None and b1 is None) or torch.equal(bslab, b1)
+    finally:
+        _hip.gemm_set_precision(prev)
+
+
 def test_slab_reduce_accumulate(dev):
     """nerf_slab_reduce with accumulate=1 adds onto the existing gradient (train.py's
     gradient accumulation across render calls); split sums in a fixed order."""
