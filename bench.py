@@ -118,8 +118,9 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 KIND_NAMES = {
     "fwd": "forward NT (nerf_linear_fwd)",
     "dx": "input-gradient NT (nerf_linear_bwd_data)",
-    "dw": "weight-gradient TN of the 256-output layers (nerf_linear_bwd_weight[_seg]: l1-l3, l5-l7, lf, and l4 "
-          "over [h3 | enc_p] in one launch; algorithmic bytes exclude the split-K slabs)",
+    "dw": "weight-gradient TN (f16x3 default: every layer's, as the two nerf_linear_bwd_weight_jobs launches of TN "
+          "schedule 3 -- [colour f | enc_d, l_f, l7, l6, l5] and [l3, l2, l1, l4 h3 | enc_p, l0]; other modes: the "
+          "256-output layers; algorithmic bytes: dy once per layer + x + dW, the split-K slabs excluded)",
     "dw_narrow": "narrow weight-gradient TN (l0 over enc_p; the colour layer over [f | enc_d] in one launch)",
     "chain_fwd": "training forward chain (nerf_mlp_chain_train: ten linears + heads, every output saved, one launch)",
     "chain_bwd": "input-gradient chain (nerf_mlp_chain_bwd: dyr + nine input gradients, every dy saved, one launch)",
@@ -127,8 +128,8 @@ KIND_NAMES = {
 KERNEL = {
     "f16x3": {"fwd": "k_gemm_nt_x6<128,256,2,2,0,true,true,2> (fp16 pair, 3 products)",
               "dx": "k_gemm_nt_x6<128,256,2,2,1,true,true,2> (fp16 pair, 3 products)",
-              "dw": "k_wgrad_pair + k_wgrad_seg<256,128,2,64> (XCD-paired 256x128 column tiles, 4 waves; fp16 "
-                    "pair, 3 products)",
+              "dw": "k_wgrad_jobs<3> + k_wgrad_jobs<6> (a job list of 256x128 / 128x256 / 128x64 / 256x64 tiles "
+                    "on 256 XCD-paired blocks, 4 MFMA + 4 load waves; fp16 pair, 3 products)",
               "dw_narrow": "k_wgrad_one<256,64> + k_wgrad_seg<128,256,1,64> (4 waves; fp16 pair, 3 products)",
               "chain_fwd": "k_mlp_chain_train2 (8 waves x 16 rows, 16x16x32 f16 MFMA; fp16 pair, 3 products)",
               "chain_bwd": "k_mlp_chain_bwd (8 waves x 16 rows, 16x16x32 f16 MFMA; fp16 pair, 3 products)"},

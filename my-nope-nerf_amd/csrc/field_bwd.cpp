@@ -223,7 +223,7 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
         RC(launch());
         RC(flush(side));
         RC(enc_rows(LR));
-        for (int l : {4, 3, 2, 1, 0}) tiles(l);
+        for (int l : {3, 2, 1, 4, 0}) tiles(l);   // l4's h3 job the last 256 x 256 one: its enc_p job follows
         RC(launch());
         RC(flush(main));
         RC(enc_rows(4));

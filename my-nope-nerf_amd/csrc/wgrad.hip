@@ -326,8 +326,7 @@ __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_pairs(TNPairs m) {
 //   WJ_ENC_HALF  256 x 64 over S splits (l4 over enc_p): output rows 128 jt .. + 127 of split sp
 //                (the XCD pair shares the split's enc_p rows through L2);
 //   WJ_ENC128    128 x 64 over 2 S splits (the colour layer over enc_d): split 2 sp + jt.
-// The jobs run grouped by shape (128 x 256, 128 x 64, 256 x 256, 256 x 64), each group in list
-// order.  The splits and slab columns are those of the per-layer launches, so are the slabs, bit
+// The jobs run grouped by shape (see the kernel for the order), each group in list order.  The splits and slab columns are those of the per-layer launches, so are the slabs, bit
 // for bit.
 // Each job's exponents alternate between the two sets of one aux region past every shape's main
 // region (JOBS_AUX), so the barrier in a job's exponents() orders it after the previous job's
@@ -340,21 +339,34 @@ __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_jobs(TNJobs m) {
     constexpr int A = wg::JOBS_AUX;
     const int w = blockIdx.x, q = w >> 3;
     const int jt = q & 1, sp = (q >> 1) * 8 + (w & 7);
-    // one loop per tile shape: the jobs run grouped by shape in this order, each group in list
-    // order; the exponent set alternates per job run (c)
+    // one loop per tile shape, each group in list order; the exponent set alternates per job run
+    // (c).  The order keeps a layer's second segment right behind its first (the same dy rows;
+    // measured: 20 of l4's 134 MB dy re-read come from the MALL, gpurun_out/r05q): with a 128 x 256
+    // job (the colour layer)
+    // 128 x 256, 128 x 64, 256 x 256; otherwise 256 x 256 (l4's h3 job last in the list), 128 x 64
+    // (l4's enc_p), 256 x 64
     int c = 0;
-    if constexpr (SH & 1)
+    auto pairs = [&]() {
         for (int i = 0; i < m.n; ++i)
-            if (m.kind[i] == WJ_WIDE) wg::block_any<128, 256, A>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
-    if constexpr (SH & 2)
+            if (m.kind[i] == WJ_PAIR) wg::block_any<256, 128, A>(m.a[i], smem, 0, jt, sp, c++ & 1);
+    };
+    auto narrow = [&]() {
         for (int i = 0; i < m.n; ++i) {
             const int k = m.kind[i];
             if (k == WJ_ENC128 || k == WJ_ENC_HALF)
                 wg::block_any<128, 64, A>(m.a[i], smem, k == WJ_ENC_HALF ? 128 * jt : 0, 0,
                                           k == WJ_ENC_HALF ? sp : 2 * sp + jt, c++ & 1);
         }
-    for (int i = 0; i < m.n; ++i)
-        if (m.kind[i] == WJ_PAIR) wg::block_any<256, 128, A>(m.a[i], smem, 0, jt, sp, c++ & 1);
+    };
+    if constexpr (SH & 1) {
+        for (int i = 0; i < m.n; ++i)
+            if (m.kind[i] == WJ_WIDE) wg::block_any<128, 256, A>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
+        if constexpr (SH & 2) narrow();
+        pairs();
+    } else {
+        pairs();
+        if constexpr (SH & 2) narrow();
+    }
     if constexpr (SH & 4)
         for (int i = 0; i < m.n; ++i)
             if (m.kind[i] == WJ_ENC) wg::block_any<256, 64, A>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
