@@ -7,11 +7,11 @@
 
 namespace nerf {
 
-// One thread per sample, 128 samples (one 128-row group) per block.  Each row is built in
+// Four threads per sample, 128 samples (one 128-row group) per block.  Each row is built in
 // LDS (65-float stride: the per-thread scalar writes are conflict-free) and then copied out
 // as whole 256-byte rows, 16 lanes x float4 per row: a thread-per-row float4 store touches 64
 // rows' lines per wave instruction, which held the 67 MB of encodings at ~1.5 TB/s.
-constexpr int ENC_ROWS = 128, ENC_LD = 65;
+constexpr int ENC_ROWS = 128, ENC_LD = 65, ENC_THREADS = 4 * ENC_ROWS;
 
 // encode_position (official_nerf.py:99-119) of one sample into its LDS row; returns max |.|
 template <int L, int W>
@@ -39,9 +39,9 @@ __device__ __forceinline__ float encode3_lds(const float x[3], float* row) {
 
 // the block's 128 LDS rows -> rows m0 .. m0 + 127 of a [n][64] encoding, coalesced
 __device__ __forceinline__ void enc_copy_out(const float* lds, float* dst, size_t m0) {
-#pragma unroll 4
-    for (int it = 0; it < ENC_ROWS * 16 / ENC_ROWS; ++it) {
-        const int idx = it * ENC_ROWS + threadIdx.x;
+#pragma unroll
+    for (int it = 0; it < ENC_ROWS * 16 / ENC_THREADS; ++it) {
+        const int idx = it * ENC_THREADS + threadIdx.x;
         const int row = idx >> 4, c4 = (idx & 15) * 4;
         const float* src = lds + row * ENC_LD + c4;
         *reinterpret_cast<float4*>(dst + (m0 + row) * 64 + c4) = make_float4(src[0], src[1], src[2], src[3]);
@@ -53,9 +53,9 @@ __device__ __forceinline__ void enc_copy_out(const float* lds, float* dst, size_
 // past the last sample are zeros
 __device__ __forceinline__ void enc_copy_out_rays(const float* rec, float* dst, size_t m0, int S, int r0,
                                                   int total) {
-#pragma unroll 4
-    for (int it = 0; it < 16; ++it) {
-        const int idx = it * ENC_ROWS + threadIdx.x;
+#pragma unroll
+    for (int it = 0; it < ENC_ROWS * 16 / ENC_THREADS; ++it) {
+        const int idx = it * ENC_THREADS + threadIdx.x;
         const int row = idx >> 4, c4 = (idx & 15) * 4;
         const int s = (int)m0 + row;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -67,7 +67,11 @@ __device__ __forceinline__ void enc_copy_out_rays(const float* rec, float* dst, 
     }
 }
 
-__global__ __launch_bounds__(ENC_ROWS) void k_encode_samples(const float* __restrict__ po, const float* __restrict__ pd,
+// 128 samples per block, four threads per sample (part = threadIdx.x >> 7, wave-uniform): part 0
+// the coordinates and frequencies 0-2, part 1 3-5, part 2 6-7, part 3 8-9 of the position
+// encoding (official_nerf.py:99-119) -- the per-thread sincosf chain a quarter as long and four
+// times the waves to hide it (one thread per sample: ~32 us per cfg2 step)
+__global__ __launch_bounds__(ENC_THREADS) void k_encode_samples(const float* __restrict__ po, const float* __restrict__ pd,
                                  const float* __restrict__ view, const float* __restrict__ noise,
                                  int R, int S, int n_pad, float nz, float fz,
                                  float* __restrict__ z_out, float* __restrict__ enc_p,
@@ -77,11 +81,13 @@ __global__ __launch_bounds__(ENC_ROWS) void k_encode_samples(const float* __rest
     static_assert(ENC_P == 64 && ENC_D == 64, "row copies assume 64-wide encodings");
     __shared__ float rows[ENC_ROWS * ENC_LD];
     __shared__ float wm[2][6];
-    __shared__ float lmd[ENC_ROWS];   // max |enc_d| per ray slot
+    __shared__ uint32_t lmdu[ENC_ROWS];   // max |enc_d| per ray slot (float bits)
+    __shared__ float lmp[4][ENC_ROWS];   // max |enc_p| per part and row
     const size_t m0 = (size_t)blockIdx.x * ENC_ROWS;
-    const int s = (int)m0 + threadIdx.x;
+    const int row = threadIdx.x & (ENC_ROWS - 1), part = threadIdx.x >> 7;
+    const int s = (int)m0 + row;
     const int total = R * S;
-    float* lrow = rows + threadIdx.x * ENC_LD;
+    float* lrow = rows + row * ENC_LD;
     float ax[3] = {0.f, 0.f, 0.f}, av[3] = {0.f, 0.f, 0.f};   // |coordinates| (column bounds)
     float x[3] = {0.f, 0.f, 0.f}, v[3] = {0.f, 0.f, 0.f};
     const bool live = s < total;
@@ -102,45 +108,81 @@ __global__ __launch_bounds__(ENC_ROWS) void k_encode_samples(const float* __rest
             av[c] = fabsf(v[c]);
         }
     }
-    // position encoding rows (padding rows: zeros, max 0)
+    // this part's columns of the position encoding row (padding rows: zeros, max 0)
     float mp = 0.f;
-    if (live) mp = encode3_lds<10, ENC_P>(x, lrow);
-    else for (int c = 0; c < ENC_P; ++c) lrow[c] = 0.f;
-    if (s < n_pad) {
-        z_out[s] = z;
-        if (rmax_p) rmax_p[s] = mp;
+    const int lv0 = part == 0 ? 0 : part == 1 ? 3 : part == 2 ? 6 : 8;
+    const int lv1 = part == 0 ? 3 : part == 1 ? 6 : part == 2 ? 8 : 10;
+    if (part == 0) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { lrow[c] = x[c]; mp = fmaxf(mp, fabsf(x[c])); }
     }
+    if (part == 3) lrow[63] = 0.f;
+    for (int lv = lv0; lv < lv1; ++lv) {
+        const float f = (float)(1 << lv);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float sn = 0.f, co = 0.f;
+            if (live) sincosf(f * x[c], &sn, &co);
+            lrow[3 + 6 * lv + c] = sn;
+            lrow[6 + 6 * lv + c] = co;
+            mp = fmaxf(mp, fmaxf(fabsf(sn), fabsf(co)));
+        }
+    }
+    lmp[part][row] = mp;
+    if (part == 0) lmdu[row] = 0u;
+    if (part == 0 && s < n_pad) z_out[s] = z;
     __syncthreads();
+    if (part == 0 && s < n_pad && rmax_p)
+        rmax_p[s] = fmaxf(fmaxf(lmp[0][row], lmp[1][row]), fmaxf(lmp[2][row], lmp[3][row]));
     enc_copy_out(rows, enc_p, m0);
     __syncthreads();
     // the view-direction encoding is per ray (official_nerf.py:87 encodes the ray's direction,
     // repeated over its samples): the block's first sample of each ray encodes it once into
     // that ray's LDS record (slot r - r0 < 128), the copy-out repeats it per sample row --
     // the same sincosf on the same input, so enc_d is bit-identical to a per-sample encode
+    // one thread per (ray slot, column), so the slot's sincosf run side by side: the values of
+    // encode3_lds<4, ENC_D> (the same sincosf on the same input), its max by an LDS max on the
+    // bits (non-negative floats order like their bits)
     const int r0 = (int)(m0 / (size_t)S);
-    if (live && (s % S == 0 || threadIdx.x == 0)) {
-        const int slot = s / S - r0;
-        lmd[slot] = encode3_lds<4, ENC_D>(v, rows + slot * ENC_LD);
+    const int nslot = (int)m0 < total ? min((int)((m0 + ENC_ROWS - 1) / (size_t)S), R - 1) - r0 + 1 : 0;
+    for (int idx = threadIdx.x; idx < nslot * 64; idx += ENC_THREADS) {
+        const int slot = idx >> 6, col = idx & 63;
+        float val = 0.f;
+        if (col < 3) {
+            val = view[3 * (size_t)(r0 + slot) + col];
+        } else if (col < 3 + 6 * 4) {
+            const int lv = (col - 3) / 6, w = (col - 3) % 6, c = w % 3;
+            float sn, co;
+            sincosf((float)(1 << lv) * view[3 * (size_t)(r0 + slot) + c], &sn, &co);
+            val = w < 3 ? sn : co;
+        }
+        rows[slot * ENC_LD + col] = val;
+        atomicMax(&lmdu[slot], __float_as_uint(fabsf(val)));
     }
     __syncthreads();
-    const float md = live ? lmd[s / S - r0] : 0.f;
-    if (s < n_pad && rmax_d) rmax_d[s] = md;
+    if (part == 0) {
+        const float md = live ? __uint_as_float(lmdu[s / S - r0]) : 0.f;
+        if (s < n_pad && rmax_d) rmax_d[s] = md;
+    }
     enc_copy_out_rays(rows, enc_d, m0, S, r0, total);
     if (cmax_p != nullptr) {
-        // per 128-row group (this block): exact max of the coordinate columns (wave max, then
-        // the two waves in LDS), 1 for the sin / cos columns (|sin|, |cos| <= 1), 0 for the pad
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) {
-                ax[c] = fmaxf(ax[c], __shfl_xor(ax[c], off, 64));
-                av[c] = fmaxf(av[c], __shfl_xor(av[c], off, 64));
-            }
-        }
+        // per 128-row group (this block): exact max of the coordinate columns (wave max over the
+        // part-0 waves, then the two waves in LDS), 1 for the sin / cos columns (|sin|, |cos| <=
+        // 1), 0 for the pad
         const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-        if (l == 0)
+        if (part == 0) {
 #pragma unroll
-            for (int c = 0; c < 3; ++c) { wm[w][c] = ax[c]; wm[w][3 + c] = av[c]; }
+            for (int c = 0; c < 3; ++c) {
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    ax[c] = fmaxf(ax[c], __shfl_xor(ax[c], off, 64));
+                    av[c] = fmaxf(av[c], __shfl_xor(av[c], off, 64));
+                }
+            }
+            if (l == 0)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) { wm[w][c] = ax[c]; wm[w][3 + c] = av[c]; }
+        }
         __syncthreads();
         if (w == 0) {
             float vp, vd;
@@ -955,7 +997,7 @@ extern "C" int nerf_encode_samples(const float* pts_o, const float* pts_d, const
     NERF_CHECK(n_rays > 0 && n_samples > 0 && (int64_t)n_rays * n_samples <= n_pad,
                "%s: n_pad=%d < R*S=%lld", __func__, n_pad, (long long)n_rays * n_samples);
     NERF_CHECK(n_pad % ENC_ROWS == 0, "%s: n_pad=%d must be a multiple of %d", __func__, n_pad, ENC_ROWS);
-    hipLaunchKernelGGL(k_encode_samples, dim3(n_pad / ENC_ROWS), dim3(ENC_ROWS), 0, as_stream(stream), pts_o, pts_d,
+    hipLaunchKernelGGL(k_encode_samples, dim3(n_pad / ENC_ROWS), dim3(ENC_THREADS), 0, as_stream(stream), pts_o, pts_d,
                        view, noise, n_rays, n_samples, n_pad, near_z, far_z, z, enc_p, enc_d, enc_p_rmax,
                        enc_d_rmax, enc_p_cmax, enc_d_cmax);
     return check_launch(__func__);
