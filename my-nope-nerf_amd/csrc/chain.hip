@@ -1074,7 +1074,11 @@ __device__ __forceinline__ void tile_store4(float* block_base, int voff, int imm
 }
 
 #ifndef NERF_CHAIN_COLMAX_ROW
-#define NERF_CHAIN_COLMAX_ROW 0   // 1: column maxima reduced over the whole 16-lane row before the LDS atomic
+// 1 (the default): column maxima reduced over the whole 16-lane row (two more DPP row_ror steps)
+// before one LDS atomic per row instead of one per quad: forward chain 556-558 vs 563-565 us,
+// input-gradient chain 504 vs 510 us, cfg2 step 2.076 vs 2.091 ms in three interleaved rounds
+// (profiles/r05/colmax_row_ab.txt); 0 keeps the quad atomics
+#define NERF_CHAIN_COLMAX_ROW 1
 #endif
 // column maxima of tile x's four features over the wave's 16 rows: max |x| over the lane
 // quad by two v_max_f32_dpp steps with |.| source modifiers (non-negative floats order as
