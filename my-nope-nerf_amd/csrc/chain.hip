@@ -1140,6 +1140,21 @@ __device__ __forceinline__ uint32_t relu_word(const uint4& h, const State& st) {
     return lo | (hi << 16);
 }
 
+#ifndef NERF_CHAIN_RELU_ROWS
+#define NERF_CHAIN_RELU_ROWS 0   // 1: the row's four lane words ORed by permlane swaps, one plain LDS store per row
+                                 // (forward chain 557-559 vs 546-550 us: slower, profiles/r05/chain_variants_ab.txt)
+#endif
+// a row's ReLU word of k-step t into LDS: an atomic OR from each of the row's four lanes, or
+// (NERF_CHAIN_RELU_ROWS) the OR over the four 16-lane rows and one store from row 0's lane
+__device__ __forceinline__ void relu_put(uint32_t* a, uint32_t w, const State& st) {
+    if constexpr (NERF_CHAIN_RELU_ROWS) {
+        const uint32_t r = rows_or(w);
+        if (st.g == 0) *a = r;
+    } else {
+        atomicOr(a, w);
+    }
+}
+
 // Save pieces of the training kernels: tile pair t of xs (the previous epilogue's values,
 // features 32 t .. 32 t + 31) -- two float4 stores, the column maxima of each tile, the ReLU
 // word -- spread over the MFMA tiles of a k-step.  The placement (tile of each piece) for a
@@ -1200,7 +1215,7 @@ __device__ __forceinline__ void save_pieces(const ChainFwdArgs& p, State& st) {
             }
             if constexpr (CM && j == piece_tile<ntj, WV>(P0_CMAX_A)) colmax4(st.xs[0], cm_at(0, 0), leader);
             if constexpr (CM && j == piece_tile<ntj, WV>(P0_CMAX_B)) colmax4(st.xs[1], cm_at(0, 1), leader);
-            if constexpr (RW && j == piece_tile<ntj, WV>(P0_RELU)) atomicOr(msk_at(0), relu_word(st.act_hi[0], st));
+            if constexpr (RW && j == piece_tile<ntj, WV>(P0_RELU)) relu_put(msk_at(0), relu_word(st.act_hi[0], st), st);
         }
         if constexpr (u + 1 < 8) {
             constexpr int t = u + 1;
@@ -1210,7 +1225,7 @@ __device__ __forceinline__ void save_pieces(const ChainFwdArgs& p, State& st) {
             }
             if constexpr (CM && j == piece_tile<ntj, WV>(P_CMAX_A)) colmax4(st.xs[2 * t], cm_at(t, 0), leader);
             if constexpr (CM && j == piece_tile<ntj, WV>(P_CMAX_B)) colmax4(st.xs[2 * t + 1], cm_at(t, 1), leader);
-            if constexpr (RW && j == piece_tile<ntj, WV>(P_RELU)) atomicOr(msk_at(t), relu_word(st.act_hi[t], st));
+            if constexpr (RW && j == piece_tile<ntj, WV>(P_RELU)) relu_put(msk_at(t), relu_word(st.act_hi[t], st), st);
         }
     }
 }
