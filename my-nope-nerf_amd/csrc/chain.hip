@@ -1709,7 +1709,10 @@ constexpr int kfirst(int i) { return i == 0 ? 0 : kfirst(i - 1) + nks(i - 1); }
 constexpr int layer_of_k(int k) { int i = 0; while (i + 1 < NL && kfirst(i + 1) <= k) ++i; return i; }
 constexpr int tt_of_k(int k) { return kb(layer_of_k(k)) + 2 * (k - kfirst(layer_of_k(k))); }
 constexpr int NK = kfirst(NL);
-constexpr int PF = 3;   // weight fragments read PF tiles ahead of their MFMAs (the ring runs across steps)
+#ifndef NERF_CHAIN_PF_BWD
+#define NERF_CHAIN_PF_BWD 3
+#endif
+constexpr int PF = NERF_CHAIN_PF_BWD;   // weight fragments read PF tiles ahead of their MFMAs (the ring runs across steps)
 constexpr int NG = 16 * NK;                  // MFMA tiles (16 per step)
 constexpr int TB = 16 - PF - 1;              // the barrier tile of a step (f2::tb)
 constexpr int dma_step(int m) { return m >= NK ? 0 : dma_count(tt_of_k(m)) + dma_count(tt_of_k(m) + 1); }

@@ -909,13 +909,14 @@ __global__ __launch_bounds__(256) void k_composite16_bwd(const float* __restrict
 // ---------------------------------------------------------------------------
 // gradient back to the ray inputs (pose / ray learning)
 // ---------------------------------------------------------------------------
-// One workgroup per ray, four waves over its samples, lane = encoding column: every load of
+// One workgroup per ray, EB_WAVES waves over its samples, lane = encoding column: every load of
 // a gradient row is one coalesced 256-byte wave access (a lane-per-sample layout reads 64
 // lines per instruction).  Column k of encode_position (official_nerf.py:99-119) is x_c
 // (k < 3) or sin / cos(2^i x_c) (k = 3 + 6 i + c, + 3 for cos); its derivative w.r.t. x_c
 // is 1, 2^i cos, -2^i sin.  A lane accumulates G[s][k] d_k(x(s)) over its samples (and the
 // same times z_s for the direction gradient, x = o + d z); the view encoding is constant per
 // ray, so its columns are summed first and scaled once.  The per-component sums meet in LDS.
+constexpr int EB_WAVES = 16;   // waves per ray (8 samples each at S = 128: 4 waves of 32 ran ~31 us per cfg3 step)
 struct EncCol {
     int c;        // input component, -1 for a padding column
     float f;      // 2^i (1 for the identity columns)
@@ -938,13 +939,13 @@ __device__ __forceinline__ float enc_dfac(const EncCol& e, float x) {
     return e.kind == 1 ? e.f * cs : -e.f * sn;
 }
 
-__global__ __launch_bounds__(256) void k_encode_bwd(const float* __restrict__ po, const float* __restrict__ pd,
+__global__ __launch_bounds__(64 * EB_WAVES) void k_encode_bwd(const float* __restrict__ po, const float* __restrict__ pd,
                                                     const float* __restrict__ view, const float* __restrict__ zv,
                                                     const float* __restrict__ gp, const float* __restrict__ gp2,
                                                     const float* __restrict__ gd,
                                                     int R, int S, float* __restrict__ g_po,
                                                     float* __restrict__ g_pd, float* __restrict__ g_view) {
-    __shared__ float red[4][3][3];   // [wave][o / d / view][component]
+    __shared__ float red[EB_WAVES][3][3];   // [wave][o / d / view][component]
     const int ray = blockIdx.x;
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const EncCol ep = enc_col(lane, 10), ed = enc_col(lane, 4);
@@ -953,7 +954,7 @@ __global__ __launch_bounds__(256) void k_encode_bwd(const float* __restrict__ po
     float ao = 0.f, ad = 0.f, sv = 0.f;
     const size_t base = (size_t)ray * S;
 #pragma unroll 4
-    for (int i = w; i < S; i += 4) {
+    for (int i = w; i < S; i += EB_WAVES) {
         const size_t s = base + i;
         const float z = zv[s];
         float g = gp[s * ENC_P + lane];
@@ -975,7 +976,9 @@ __global__ __launch_bounds__(256) void k_encode_bwd(const float* __restrict__ po
     __syncthreads();
     if (threadIdx.x < 9) {
         const int k = threadIdx.x / 3, c = threadIdx.x % 3;
-        const float v = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
+        float v = red[0][k][c];
+#pragma unroll
+        for (int q = 1; q < EB_WAVES; ++q) v += red[q][k][c];   // waves in order
         (k == 0 ? g_po : k == 1 ? g_pd : g_view)[3 * ray + c] = v;
     }
 }
@@ -1298,7 +1301,7 @@ extern "C" int nerf_encode_bwd(const float* pts_o, const float* pts_d, const flo
     NERF_CHECK_PTR(genc_p); NERF_CHECK_PTR(genc_d);
     NERF_CHECK_PTR(g_pts_o); NERF_CHECK_PTR(g_pts_d); NERF_CHECK_PTR(g_view);
     NERF_CHECK(n_rays > 0 && n_samples > 0, "%s: empty input", __func__);
-    hipLaunchKernelGGL(k_encode_bwd, dim3(n_rays), dim3(256), 0, as_stream(stream), pts_o, pts_d, view, z,
+    hipLaunchKernelGGL(k_encode_bwd, dim3(n_rays), dim3(64 * EB_WAVES), 0, as_stream(stream), pts_o, pts_d, view, z,
                        genc_p, genc_p2, genc_d, n_rays, n_samples, g_pts_o, g_pts_d, g_view);
     return check_launch(__func__);
 }
