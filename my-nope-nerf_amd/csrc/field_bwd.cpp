@@ -434,15 +434,17 @@ int schedule(const nerf_field_bwd& a, void* stream, void* side_stream) {
         graw4 = w.graw4;
     }
     // heads: the head-weight partials (re-reading h8 and hr).  With the input-gradient chain on
-    // the caller's stream BEFORE the chain: NERF_HEADS_PLACE 1 (the default) by k_heads_bwd mode 2
-    // + k_heads_reduce (~70 + 13 us in-step), 3 by k_heads_part (16-byte buffer loads, 4x the
+    // the caller's stream BEFORE the chain: NERF_HEADS_PLACE 5 (the default) k_heads_bwd mode 2
+    // there and k_heads_reduce (11 blocks, ~13 us) forked to the side stream beside the chain
+    // (2.009 vs 2.030 ms/step, profiles/r05/heads_reduce_side_ab.json); 1 both on the caller's
+    // stream (~70 + 13 us in-step); 3 by k_heads_part (16-byte buffer loads, 4x the
     // waves: ~62 us in-step) with the reduces in the first slab batch (2.066 vs 2.058 ms/step,
     // profiles/r05/heads_part_ab.json); beside the chain (0, the round-4 placement) the partials and their reduce stretch
     // to ~240 us sharing the CUs with the chain, and the step is 13 us slower than 1
     // (profiles/r05/heads_place_ab.json; 2 = after the chain: 7 us slower).  The per-layer
     // schedule keeps them on the side stream
     const char* hp = std::getenv("NERF_HEADS_PLACE");
-    const int heads_place = a.bwd_chain ? (hp ? std::atoi(hp) : 1) : 0;
+    const int heads_place = a.bwd_chain ? (hp ? std::atoi(hp) : 5) : 0;
     auto heads = [&](hipStream_t s) -> int {
         RC(nerf_heads_bwd_mode(2, graw4, a.act[7], D, a.act[LR], HR, nullptr, 0, D, a.wc, nullptr, 0, w.part, np,
                                nullptr, nullptr, s));
@@ -457,6 +459,12 @@ int schedule(const nerf_field_bwd& a, void* stream, void* side_stream) {
         RC(heads(side));
     } else if (heads_place == 1) {
         RC(heads(main));
+    } else if (heads_place == 5) {
+        // the partials before the chain, their reduce (11 blocks) forked to the side stream
+        RC(nerf_heads_bwd_mode(2, graw4, a.act[7], D, a.act[LR], HR, nullptr, 0, D, a.wc, nullptr, 0, w.part, np,
+                               nullptr, nullptr, main));
+        RC(fork(main, side));
+        RC(nerf_heads_reduce(w.part, D, np, a.g_wd, a.g_bd, a.g_wc, a.g_bc, 0, side));
     } else if (heads_place == 3) {
         RC(nerf::heads_partials(graw4, a.act[7], D, a.act[LR], HR, np, w.hpart, a.g_wd, a.g_bd, a.g_wc, a.g_bc, hjobs,
                                 main));

@@ -37,6 +37,7 @@ SETTINGS = {
     "heads_after": (0, 0, {"NERF_HEADS_PLACE": "2"}),
     "heads_part": (0, 0, {"NERF_HEADS_PLACE": "3"}),
     "wgrad1": (0, 0, {"NERF_WGRAD_SCHED": "1"}),
+    "heads_reduce_side": (0, 0, {"NERF_HEADS_PLACE": "5"}),
 }
 ENV_KEYS = ("NERF_TAIL_MAIN", "NERF_HEADS_SIDE", "NERF_CHAIN", "NERF_DW_SEG", "NERF_NATIVE_BWD", "NERF_WGRAD_SCHED",
             "NERF_HEADS_PLACE")
