@@ -172,9 +172,8 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
         // every weight gradient as a job of one of two k_wgrad_jobs launches (2 S blocks, S the
         // 256 x 256 layers' split count; the narrow tiles fill the same grid instead of a launch
         // of their own): the colour layer's two segments + l_f .. l5, then l4's two segments +
-        // l3 .. l1 + l0.  Same splits and slab columns as schedule 1, so the same slabs.  The
-        // first launch's slab reduces run on the side stream beside the second launch, the
-        // second's on the caller's stream at the end.
+        // l3 .. l1 + l0.  Same splits and slab columns as schedule 1, so the same slabs.  Each
+        // launch's slab reduces follow it on the caller's stream.
         nerf::SlabJobDesc jobs[nerf::kSlabJobsMax];
         int nj = 0;
         for (int e = 0; e < n_extra; ++e) jobs[nj++] = extra[e];   // the head-weight reduces ride in the first batch
@@ -221,7 +220,12 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
         };
         for (int l : {LR, LF, 7, 6, 5}) tiles(l);
         RC(launch());
-        RC(flush(side));
+        // NERF_WGRAD_BATCH1: 1 (the default) the first batch on the caller's stream between the two
+        // launches; 0 on the side stream (it can only start once the second launch frees CUs).
+        // Eager the two are within noise (2.029 vs 2.037 ms/step); replayed as a hipGraph the
+        // side-stream branch costs ~55 us per step (2.093 vs 2.039 ms, profiles/r05/batch1_ab.json)
+        const char* b1 = std::getenv("NERF_WGRAD_BATCH1");
+        RC(flush(b1 && std::atoi(b1) == 0 ? side : main));
         RC(enc_rows(LR));
         for (int l : {3, 2, 1, 4, 0}) tiles(l);   // l4's h3 job the last 256 x 256 one: its enc_p job follows
         RC(launch());

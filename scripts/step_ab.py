@@ -38,9 +38,10 @@ SETTINGS = {
     "heads_part": (0, 0, {"NERF_HEADS_PLACE": "3"}),
     "wgrad1": (0, 0, {"NERF_WGRAD_SCHED": "1"}),
     "heads_reduce_side": (0, 0, {"NERF_HEADS_PLACE": "5"}),
+    "batch1_main": (0, 0, {"NERF_WGRAD_BATCH1": "1"}),
 }
 ENV_KEYS = ("NERF_TAIL_MAIN", "NERF_HEADS_SIDE", "NERF_CHAIN", "NERF_DW_SEG", "NERF_NATIVE_BWD", "NERF_WGRAD_SCHED",
-            "NERF_HEADS_PLACE")
+            "NERF_HEADS_PLACE", "NERF_WGRAD_BATCH1")
 
 
 def main():
