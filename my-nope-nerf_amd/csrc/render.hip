@@ -294,6 +294,13 @@ __global__ __launch_bounds__(256) void k_heads_fwd(const float* __restrict__ h8,
     }
 }
 
+#ifndef NERF_HEADS_NT
+#define NERF_HEADS_NT 0   // A/B builds: 1 = the head partials' h8 / hr loads non-temporal
+#endif
+__device__ __forceinline__ float heads_ld(const float* a) {
+    if constexpr (NERF_HEADS_NT) return __builtin_nontemporal_load(a);
+    else return *a;
+}
 // part layout per block: [wd: 64*NH][wc: 3*64*NR][bd, bc0, bc1, bc2]
 // MODE bit 0: dyr and its row / column maxima (the input-gradient chain waits for these);
 // bit 1: the head-weight / bias partials (read h8 and hr; nothing downstream waits for them
@@ -343,13 +350,13 @@ __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ gra
             const float4 gr = *reinterpret_cast<const float4*>(graw4 + 4 * s);
             if constexpr (MODE & 2) {
 #pragma unroll
-                for (int q = 0; q < NH; ++q) awd[q] = fmaf(gr.x, h8[s * ld8 + lane + 64 * q], awd[q]);
+                for (int q = 0; q < NH; ++q) awd[q] = fmaf(gr.x, heads_ld(h8 + s * ld8 + lane + 64 * q), awd[q]);
             }
             float dmax = 0.f;
 #pragma unroll
             for (int q = 0; q < NR; ++q) {
                 static_assert(!MB || MODE == 1, "mask-bit gate: dyr-only mode");
-                const float x = MB ? 0.f : hr[s * ldr + lane + 64 * q];
+                const float x = MB ? 0.f : heads_ld(hr + s * ldr + lane + 64 * q);
                 const bool on = MB ? ((hmask[s * ldm + ((lane + 64 * q) >> 5)] >> (lane & 31)) & 1u) != 0 : x > 0.f;
                 if constexpr (MODE & 1) {
                     // explicit fmas: every MODE instantiation rounds identically

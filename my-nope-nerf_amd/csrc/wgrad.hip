@@ -65,19 +65,26 @@ typedef unsigned wg_u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned wg_u32x2 __attribute__((ext_vector_type(2)));
 // (named components: subscripting the builtin's vector with an unrolled index miscompiles to
 // one dword load on this toolchain)
-template <int C>
+// POL: the buffer instruction's cache-policy bits (2 = nt)
+template <int C, int POL = 0>
 __device__ __forceinline__ void load_row(float (&v)[C], const __amdgpu_buffer_rsrc_t& r, int voff, int soff) {
     if constexpr (C == 4) {
-        const wg_u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+        const wg_u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, POL);
         v[0] = __uint_as_float(t.x); v[1] = __uint_as_float(t.y);
         v[2] = __uint_as_float(t.z); v[3] = __uint_as_float(t.w);
     } else if constexpr (C == 2) {
-        const wg_u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+        const wg_u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, POL);
         v[0] = __uint_as_float(t.x); v[1] = __uint_as_float(t.y);
     } else {
-        v[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+        v[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, POL));
     }
 }
+#ifndef NERF_WG_POL_DY
+#define NERF_WG_POL_DY 0   // A/B builds: cache policy of the dy / x stage loads
+#endif
+#ifndef NERF_WG_POL_X
+#define NERF_WG_POL_X 0
+#endif
 
 // 8 rows of one column, scaled by 2^e -> one 16-byte fragment chunk per plane
 __device__ __forceinline__ void put_strip(char* d, int plane_bytes, const float (&v)[8], int e) {
@@ -137,8 +144,8 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
             const int r0 = KS * t + 8 * lw;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                load_row<CA>(va[U][i], rdy, va_off, (r0 + i) * p.lddy * 4);
-                load_row<CB>(vb[U][i], rx, vb_off, (r0 + i) * p.ldx * 4);
+                load_row<CA, NERF_WG_POL_DY>(va[U][i], rdy, va_off, (r0 + i) * p.lddy * 4);
+                load_row<CB, NERF_WG_POL_X>(vb[U][i], rx, vb_off, (r0 + i) * p.ldx * 4);
             }
         };
         unroll<NS>([&](auto u) { load(u, decltype(u)::value); });

@@ -67,7 +67,7 @@ for step in "$@"; do
       echo "list ok" ;;
     py:*)
       args=${step#py:}
-      (cd $R/scripts && timeout -k 10 300 python -u $args > $OUT/py_$(echo $args | tr ' /' '__' | cut -c1-60).txt 2>&1) || exit $?
+      (cd $R/scripts && timeout -k 10 1000 python -u $args > $OUT/py_$(echo $args | tr ' /' '__' | cut -c1-60).txt 2>&1) || exit $?
       echo "py ok: $args" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
