@@ -294,8 +294,11 @@ __global__ __launch_bounds__(256) void k_heads_fwd(const float* __restrict__ h8,
     }
 }
 
+// the head partials' h8 / hr loads non-temporal (1, the default: cfg2 step 2.021 vs 2.035 ms in
+// three interleaved rounds, profiles/r05/nt_loads_ab.txt; the same hint on the weight-gradient
+// stage loads made those 9-27 % slower)
 #ifndef NERF_HEADS_NT
-#define NERF_HEADS_NT 0   // A/B builds: 1 = the head partials' h8 / hr loads non-temporal
+#define NERF_HEADS_NT 1
 #endif
 __device__ __forceinline__ float heads_ld(const float* a) {
     if constexpr (NERF_HEADS_NT) return __builtin_nontemporal_load(a);
