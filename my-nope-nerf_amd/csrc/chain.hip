@@ -933,8 +933,14 @@ __device__ __forceinline__ uint32_t mlo(float x0, float x1, float s, uint32_t h)
 }
 // 16 bytes per lane from (g + voff) into LDS at lds + 16 lane; g and lds wave-uniform (SGPRs:
 // the address arithmetic is scalar), voff the lane's 16-byte offset
+#ifndef NERF_CHAIN_DMA_NT
+#define NERF_CHAIN_DMA_NT 0   // A/B builds: 1 = the weight LDS-DMA loads non-temporal
+#endif
 __device__ __forceinline__ void dma16(const void* g, uint32_t voff, uint32_t lds) {
-    asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(g), "s"(lds) : "memory", "m0");
+    if constexpr (NERF_CHAIN_DMA_NT)
+        asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1 nt" ::"v"(voff), "s"(g), "s"(lds) : "memory", "m0");
+    else
+        asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(g), "s"(lds) : "memory", "m0");
 }
 
 struct State {
@@ -1062,6 +1068,14 @@ __device__ __forceinline__ void split_lo(State& st) {
 }
 
 typedef unsigned cu32x4 __attribute__((ext_vector_type(4)));
+// cache-policy bits of the training chains' saved-output stores: 2 = nt (the default): forward
+// chain 525-536 vs 550-554 us, input-gradient chain 493-498 vs 507-510 us, cfg2 step 1.999 vs
+// 2.047 ms in three interleaved rounds (profiles/r05/chain_nt_ab.txt) -- the 1.3 GB each chain
+// writes no longer displaces the weight stream every block re-reads; 0 = the default policy.
+// The same hint on the weight LDS-DMA loads (NERF_CHAIN_DMA_NT) made both chains ~20 % slower
+#ifndef NERF_CHAIN_ST_POL
+#define NERF_CHAIN_ST_POL 2
+#endif
 // a float4 into a row-major [128 rows][W] f32 tile of one block through a buffer resource: the
 // lane's row / column byte offset in one VGPR, the block base in SGPRs, the column offset an
 // immediate -- no 64-bit per-lane address arithmetic per store
@@ -1070,7 +1084,7 @@ __device__ __forceinline__ void tile_store4(float* block_base, int voff, int imm
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc((void*)block_base, (short)0, 128 * W * 4, 0x00020000);
     const cu32x4 v = {__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]), __float_as_uint(x[3])};
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, imm_bytes, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, imm_bytes, NERF_CHAIN_ST_POL);
 }
 
 #ifndef NERF_CHAIN_COLMAX_ROW
