@@ -37,6 +37,19 @@ __device__ __forceinline__ float encode3_lds(const float x[3], float* row) {
     return m;
 }
 
+#ifndef NERF_ENC_NT
+#define NERF_ENC_NT 0   // A/B builds: 1 = the encodings' stores non-temporal (the forward chain reads them
+                        // next: 538-543 vs 526-530 us, slower; profiles/r05/nt_loads_ab.txt)
+#endif
+__device__ __forceinline__ void enc_st4(float* d, const float4& v) {
+    if constexpr (NERF_ENC_NT) {
+        typedef float enc_f4 __attribute__((ext_vector_type(4)));
+        const enc_f4 q = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(q, reinterpret_cast<enc_f4*>(d));
+    } else {
+        *reinterpret_cast<float4*>(d) = v;
+    }
+}
 // the block's 128 LDS rows -> rows m0 .. m0 + 127 of a [n][64] encoding, coalesced
 __device__ __forceinline__ void enc_copy_out(const float* lds, float* dst, size_t m0) {
 #pragma unroll
@@ -44,7 +57,7 @@ __device__ __forceinline__ void enc_copy_out(const float* lds, float* dst, size_
         const int idx = it * ENC_THREADS + threadIdx.x;
         const int row = idx >> 4, c4 = (idx & 15) * 4;
         const float* src = lds + row * ENC_LD + c4;
-        *reinterpret_cast<float4*>(dst + (m0 + row) * 64 + c4) = make_float4(src[0], src[1], src[2], src[3]);
+        enc_st4(dst + (m0 + row) * 64 + c4, make_float4(src[0], src[1], src[2], src[3]));
     }
 }
 
@@ -63,7 +76,7 @@ __device__ __forceinline__ void enc_copy_out_rays(const float* rec, float* dst, 
             const float* src = rec + (s / S - r0) * ENC_LD + c4;
             v = make_float4(src[0], src[1], src[2], src[3]);
         }
-        *reinterpret_cast<float4*>(dst + (m0 + row) * 64 + c4) = v;
+        enc_st4(dst + (m0 + row) * 64 + c4, v);
     }
 }
 
