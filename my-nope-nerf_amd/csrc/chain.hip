@@ -795,12 +795,22 @@ constexpr int NK = kfirst(CNL);             // 32-k steps of the chain
 template <bool TR>
 constexpr int npair() { return LY<TR>::NSLOT / 2; }
 // weight fragments are read PF tiles ahead of their MFMAs (a ring of PF + 1 fragment pairs that
-// runs on across steps and layers)
-#ifndef NERF_CHAIN_PF_TR
-#define NERF_CHAIN_PF_TR 2
+// runs on across steps and layers): 2 in the training forward (3 measured no faster,
+// profiles/r05/chain_variants_ab.txt), 3 in the eval kernel.  NERF_CHAIN_PF_EVAL (diagnostic
+// builds) sets the eval depth; the ring holds at most PF_MAX + 1 entries (State::wh / wl), and a
+// step of 8 tiles must keep its barrier tile tb >= 0 (static_asserts below): round 5's PF 4
+// eval build indexed wh[4] of a 4-entry ring -- a register array read out of bounds, hence
+// its non-finite frame (profiles/r06/pf_eval4.txt)
+#ifndef NERF_CHAIN_PF_EVAL
+#define NERF_CHAIN_PF_EVAL 3
 #endif
 template <bool TR>
-constexpr int pf_tiles() { return TR ? NERF_CHAIN_PF_TR : 3; }
+constexpr int pf_tiles() { return TR ? 2 : NERF_CHAIN_PF_EVAL; }
+constexpr int PF_BWD = 3;                   // the input-gradient chain (b2::PF; 2 measured no change)
+constexpr int PF_MAX = 4;                   // fragment-ring entries - 1 (State::wh / wl)
+static_assert(pf_tiles<true>() >= 1 && pf_tiles<true>() <= PF_MAX && pf_tiles<false>() >= 1 &&
+                  pf_tiles<false>() <= PF_MAX && PF_BWD <= PF_MAX,
+              "the weight-fragment ring holds PF_MAX + 1 entries");
 constexpr int ntj_k(int k) { return L_OUT[layer_of_k(k)] / 16; }
 // step -> first global tile and tile -> step, tabulated once (the templates ask per tile)
 struct TileMap {
@@ -824,13 +834,18 @@ constexpr int step_of_tile(int G) { return kTiles.step[G]; }
 // issues DMAs: the last tile before the first read of step k + 1's fragments
 template <bool TR>
 constexpr int tb(int k) { return ntj_k(k) - pf_tiles<TR>() - 1; }
+// every step's barrier tile exists (the 8-tile colour-layer steps bound PF at 6), and in the
+// training forward the save stores (issued no later than tb: piece_tile) precede it
+constexpr bool tb_ok() {
+    for (int k = 0; k < NK; ++k)
+        if (tb<true>(k) < 0 || tb<false>(k) < 0) return false;
+    return true;
+}
+static_assert(tb_ok(), "a step's barrier tile tb = ntj - PF - 1 must exist");
 // vector-memory ops of the DMAs of 32-k step m (two 16-k steps), and of those issued in step j
 constexpr int dma_step(int m) { return m >= NK ? 0 : dma_count(tt_of_k(m)) + dma_count(tt_of_k(m) + 1); }
 template <bool TR>
 constexpr int dma_in(int j) { return dma_step(j + npair<TR>() - 1); }
-#ifndef NERF_CHAIN_ABLATE
-#define NERF_CHAIN_ABLATE 0   // diagnostic builds only (results wrong): 1 no column maxima, 2 no ReLU words, 4 no saved outputs
-#endif
 // training, layer l >= 1, step u: the previous layer's output is saved two float4 stores per
 // tile pair (pairs 0 and 1 at u = 0, pair u + 1 at u = 1..6); at u = 0 of l >= 2 layer l - 2's
 // column maxima and ReLU words leave LDS (one store each).  All before the step's barrier
@@ -838,7 +853,6 @@ template <bool TR>
 constexpr int pre_st(int k) {
     const int l = layer_of_k(k), u = k - kfirst(l);
     if (!TR || l == 0) return 0;
-    if (NERF_CHAIN_ABLATE & 4) return u == 0 && l >= 2 ? 2 : 0;
     return u == 0 ? 4 + (l >= 2 ? 2 : 0) : (u <= 6 ? 2 : 0);
 }
 // the counted wait before B_{k+1} (at tile tb(k) of step k) for the DMAs of step k + 1, issued
@@ -933,14 +947,9 @@ __device__ __forceinline__ uint32_t mlo(float x0, float x1, float s, uint32_t h)
 }
 // 16 bytes per lane from (g + voff) into LDS at lds + 16 lane; g and lds wave-uniform (SGPRs:
 // the address arithmetic is scalar), voff the lane's 16-byte offset
-#ifndef NERF_CHAIN_DMA_NT
-#define NERF_CHAIN_DMA_NT 0   // A/B builds: 1 = the weight LDS-DMA loads non-temporal
-#endif
+// (the nt hint on these loads made both training chains ~20 % slower, profiles/r05/nt_loads_ab.txt)
 __device__ __forceinline__ void dma16(const void* g, uint32_t voff, uint32_t lds) {
-    if constexpr (NERF_CHAIN_DMA_NT)
-        asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1 nt" ::"v"(voff), "s"(g), "s"(lds) : "memory", "m0");
-    else
-        asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(g), "s"(lds) : "memory", "m0");
+    asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(g), "s"(lds) : "memory", "m0");
 }
 
 struct State {
@@ -965,7 +974,7 @@ struct State {
     f32x4 acc[16];                      // 16 rows x 256 outputs
     f32x4 xs[16];                       // the previous epilogue's outputs (tile layout), split into act
                                         // and saved during the next layer's k-steps
-    uint4 wh[4], wl[4];                 // weight-fragment ring (hi / lo planes), PF + 1 tiles
+    uint4 wh[PF_MAX + 1], wl[PF_MAX + 1];   // weight-fragment ring (hi / lo planes), PF + 1 tiles
 };
 
 // diagnostics (nerf_chain_debug_stamps, NERF_CHAIN_STAMPS builds): cycles since the last tick
@@ -1068,14 +1077,11 @@ __device__ __forceinline__ void split_lo(State& st) {
 }
 
 typedef unsigned cu32x4 __attribute__((ext_vector_type(4)));
-// cache-policy bits of the training chains' saved-output stores: 2 = nt (the default): forward
+// the training chains' saved-output stores are non-temporal (cache-policy bits 2): forward
 // chain 525-536 vs 550-554 us, input-gradient chain 493-498 vs 507-510 us, cfg2 step 1.999 vs
 // 2.047 ms in three interleaved rounds (profiles/r05/chain_nt_ab.txt) -- the 1.3 GB each chain
-// writes no longer displaces the weight stream every block re-reads; 0 = the default policy.
-// The same hint on the weight LDS-DMA loads (NERF_CHAIN_DMA_NT) made both chains ~20 % slower
-#ifndef NERF_CHAIN_ST_POL
-#define NERF_CHAIN_ST_POL 2
-#endif
+// writes no longer displaces the weight stream every block re-reads
+constexpr int ST_POL = 2;
 // a float4 into a row-major [128 rows][W] f32 tile of one block through a buffer resource: the
 // lane's row / column byte offset in one VGPR, the block base in SGPRs, the column offset an
 // immediate -- no 64-bit per-lane address arithmetic per store
@@ -1084,21 +1090,17 @@ __device__ __forceinline__ void tile_store4(float* block_base, int voff, int imm
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc((void*)block_base, (short)0, 128 * W * 4, 0x00020000);
     const cu32x4 v = {__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]), __float_as_uint(x[3])};
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, imm_bytes, NERF_CHAIN_ST_POL);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, imm_bytes, ST_POL);
 }
 
-#ifndef NERF_CHAIN_COLMAX_ROW
-// 1 (the default): column maxima reduced over the whole 16-lane row (two more DPP row_ror steps)
-// before one LDS atomic per row instead of one per quad: forward chain 556-558 vs 563-565 us,
-// input-gradient chain 504 vs 510 us, cfg2 step 2.076 vs 2.091 ms in three interleaved rounds
-// (profiles/r05/colmax_row_ab.txt); 0 keeps the quad atomics
-#define NERF_CHAIN_COLMAX_ROW 1
-#endif
 // column maxima of tile x's four features over the wave's 16 rows: max |x| over the lane
 // quad by two v_max_f32_dpp steps with |.| source modifiers (non-negative floats order as
-// their bits), then one LDS atomic max per quad leader.  The asm keeps the DPP hazard
-// explicit (a DPP source written by VALU needs two wait states: the s_nop; the second
-// step's sources are four instructions old) and the maxima out of the leaders' branch
+// their bits), the quads combined by two row_ror steps, then one LDS atomic max per row
+// leader (lane n == 0) -- against one atomic per quad: forward chain 556-558 vs 563-565 us,
+// input-gradient chain 504 vs 510 us, cfg2 step 2.076 vs 2.091 ms in three interleaved rounds
+// (profiles/r05/colmax_row_ab.txt).  The asm keeps the DPP hazard explicit (a DPP source
+// written by VALU needs two wait states: the s_nop; the later steps' sources are four
+// instructions old) and the maxima out of the leaders' branch
 __device__ __forceinline__ void colmax4(const f32x4& x, uint32_t* cm, bool leader) {
     float a0, a1, a2, a3;
     asm volatile(
@@ -1113,9 +1115,9 @@ __device__ __forceinline__ void colmax4(const f32x4& x, uint32_t* cm, bool leade
         "v_max_f32_dpp %3, %3, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
         : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
         : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]));
-    if constexpr (NERF_CHAIN_COLMAX_ROW) {
+    {
         // the max over all 16 lanes of the row (quads combined by row_ror 4, 8): one atomic per
-        // row and feature, no address conflicts (the caller's leader is then lane n == 0)
+        // row and feature, no address conflicts
         asm volatile(
             "v_max_f32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
             "v_max_f32_dpp %1, %1, %1 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
@@ -1154,19 +1156,11 @@ __device__ __forceinline__ uint32_t relu_word(const uint4& h, const State& st) {
     return lo | (hi << 16);
 }
 
-#ifndef NERF_CHAIN_RELU_ROWS
-#define NERF_CHAIN_RELU_ROWS 0   // 1: the row's four lane words ORed by permlane swaps, one plain LDS store per row
-                                 // (forward chain 557-559 vs 546-550 us: slower, profiles/r05/chain_variants_ab.txt)
-#endif
-// a row's ReLU word of k-step t into LDS: an atomic OR from each of the row's four lanes, or
-// (NERF_CHAIN_RELU_ROWS) the OR over the four 16-lane rows and one store from row 0's lane
-__device__ __forceinline__ void relu_put(uint32_t* a, uint32_t w, const State& st) {
-    if constexpr (NERF_CHAIN_RELU_ROWS) {
-        const uint32_t r = rows_or(w);
-        if (st.g == 0) *a = r;
-    } else {
-        atomicOr(a, w);
-    }
+// a row's ReLU word of k-step t into LDS: an atomic OR from each of the row's four lanes (the
+// OR over the four 16-lane rows by permlane swaps and one plain store per row was slower:
+// forward chain 557-559 vs 546-550 us, profiles/r05/chain_variants_ab.txt)
+__device__ __forceinline__ void relu_put(uint32_t* a, uint32_t w, const State&) {
+    atomicOr(a, w);
 }
 
 // Save pieces of the training kernels: tile pair t of xs (the previous epilogue's values,
@@ -1176,29 +1170,27 @@ __device__ __forceinline__ void relu_put(uint32_t* a, uint32_t w, const State& s
 // tiles, behind its split (which it shares the xs registers with)
 enum Piece { P_SPLIT_HI_A, P_SPLIT_HI_B, P_SPLIT_LO_A, P_SPLIT_LO_B, P_STORE, P_CMAX_A, P_CMAX_B, P_RELU,
              P0_STORE, P0_CMAX_A, P0_CMAX_B, P0_RELU };
-// WV = 1 (NERF_CHAIN_STAGGER builds: waves 4-7 run their own copy of the chain): the pieces sit
-// at the tiles the other half's leave free, so one wave's VALU meets its SIMD partner's MFMAs
-template <int ntj, int WV = 0>
+// (a staggered table for waves 4-7, their pieces at the tiles waves 0-3 leave free, ran 4 %
+// slower: profiles/r05/chain_variants_ab.txt)
+template <int ntj>
 constexpr int piece_tile(int piece) {
     if constexpr (ntj == 16) {
-        constexpr int T[2][12] = {{6, 7, 8, 9, 10, 11, 12, 13, 1, 2, 3, 4}, {0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 11, 12}};
-        return T[WV][piece];
+        constexpr int T[12] = {6, 7, 8, 9, 10, 11, 12, 13, 1, 2, 3, 4};
+        return T[piece];
     } else {
-        constexpr int T[2][12] = {{3, 3, 4, 4, 5, 6, 7, 7, 0, 1, 2, 2}, {0, 0, 1, 1, 2, 3, 4, 4, 5, 6, 7, 7}};
-        return T[WV][piece];
+        constexpr int T[12] = {3, 3, 4, 4, 5, 6, 7, 7, 0, 1, 2, 2};
+        return T[piece];
     }
 }
 // the pieces that store (vector memory) run no later than the tile of the step's barrier, tb =
 // ntj - PF - 1 (the wait counts take every store of a step as issued before it): PF 2 in the
 // training forward (16- and 8-tile steps), 3 in the backward (16)
 static_assert(piece_tile<16>(P_STORE) <= 16 - 3 - 1 && piece_tile<16>(P0_STORE) <= 16 - 3 - 1 &&
-                  piece_tile<8>(P_STORE) <= 8 - 2 - 1 && piece_tile<8>(P0_STORE) <= 8 - 2 - 1 &&
-                  piece_tile<16, 1>(P_STORE) <= 16 - 3 - 1 && piece_tile<16, 1>(P0_STORE) <= 16 - 3 - 1 &&
-                  piece_tile<8, 1>(P_STORE) <= 8 - 2 - 1 && piece_tile<8, 1>(P0_STORE) <= 8 - 2 - 1,
+                  piece_tile<8>(P_STORE) <= 8 - 2 - 1 && piece_tile<8>(P0_STORE) <= 8 - 2 - 1,
               "stores before the barrier");
 // training: the save work of layer l's k-step u (the previous layer's output, P = p.L[l - 1]),
 // piece j of ntj
-template <int l, int u, int j, int ntj, int WV>
+template <int l, int u, int j, int ntj>
 __device__ __forceinline__ void save_pieces(const ChainFwdArgs& p, State& st) {
     using Y = LY<true>;
     if constexpr (l >= 1 && u < 8) {
@@ -1218,53 +1210,52 @@ __device__ __forceinline__ void save_pieces(const ChainFwdArgs& p, State& st) {
             asm volatile("" : "+v"(o));
             return reinterpret_cast<uint32_t*>(st.lds + o) + par * 1024 + t;
         };
-        const bool leader = NERF_CHAIN_COLMAX_ROW ? st.n == 0 : (st.n & 3) == 0;
+        const bool leader = st.n == 0;
         float* ob = P.out + st.m0 * 256;
-        constexpr bool CM = !(NERF_CHAIN_ABLATE & 1), RW = relu && !(NERF_CHAIN_ABLATE & 2),
-                       SV = !(NERF_CHAIN_ABLATE & 4);
+        constexpr bool CM = true, RW = relu, SV = true;
         if constexpr (u == 0) {
-            if constexpr (SV && j == piece_tile<ntj, WV>(P0_STORE)) {
+            if constexpr (SV && j == piece_tile<ntj>(P0_STORE)) {
                 tile_store4<256>(ob, st.vrow, 0, st.xs[0]);
                 tile_store4<256>(ob, st.vrow, 64, st.xs[1]);
             }
-            if constexpr (CM && j == piece_tile<ntj, WV>(P0_CMAX_A)) colmax4(st.xs[0], cm_at(0, 0), leader);
-            if constexpr (CM && j == piece_tile<ntj, WV>(P0_CMAX_B)) colmax4(st.xs[1], cm_at(0, 1), leader);
-            if constexpr (RW && j == piece_tile<ntj, WV>(P0_RELU)) relu_put(msk_at(0), relu_word(st.act_hi[0], st), st);
+            if constexpr (CM && j == piece_tile<ntj>(P0_CMAX_A)) colmax4(st.xs[0], cm_at(0, 0), leader);
+            if constexpr (CM && j == piece_tile<ntj>(P0_CMAX_B)) colmax4(st.xs[1], cm_at(0, 1), leader);
+            if constexpr (RW && j == piece_tile<ntj>(P0_RELU)) relu_put(msk_at(0), relu_word(st.act_hi[0], st), st);
         }
         if constexpr (u + 1 < 8) {
             constexpr int t = u + 1;
-            if constexpr (SV && j == piece_tile<ntj, WV>(P_STORE)) {
+            if constexpr (SV && j == piece_tile<ntj>(P_STORE)) {
                 tile_store4<256>(ob, st.vrow, 128 * t, st.xs[2 * t]);
                 tile_store4<256>(ob, st.vrow, 128 * t + 64, st.xs[2 * t + 1]);
             }
-            if constexpr (CM && j == piece_tile<ntj, WV>(P_CMAX_A)) colmax4(st.xs[2 * t], cm_at(t, 0), leader);
-            if constexpr (CM && j == piece_tile<ntj, WV>(P_CMAX_B)) colmax4(st.xs[2 * t + 1], cm_at(t, 1), leader);
-            if constexpr (RW && j == piece_tile<ntj, WV>(P_RELU)) relu_put(msk_at(t), relu_word(st.act_hi[t], st), st);
+            if constexpr (CM && j == piece_tile<ntj>(P_CMAX_A)) colmax4(st.xs[2 * t], cm_at(t, 0), leader);
+            if constexpr (CM && j == piece_tile<ntj>(P_CMAX_B)) colmax4(st.xs[2 * t + 1], cm_at(t, 1), leader);
+            if constexpr (RW && j == piece_tile<ntj>(P_RELU)) relu_put(msk_at(t), relu_word(st.act_hi[t], st), st);
         }
     }
 }
 
 // the next k-step's A fragment (tiles 2 (u + 1), 2 (u + 1) + 1 of the previous epilogue), in
 // four pieces
-template <int l, int u, int j, int ntj, int WV>
+template <int l, int u, int j, int ntj>
 __device__ __forceinline__ void split_pieces(State& st) {
     if constexpr (l > 0 && u + 1 < 8) {
         constexpr int t = u + 1;
         const f32x4 A = st.xs[2 * t], B = st.xs[2 * t + 1];
         const float s = st.ser;
-        if constexpr (j == piece_tile<ntj, WV>(P_SPLIT_HI_A)) {
+        if constexpr (j == piece_tile<ntj>(P_SPLIT_HI_A)) {
             st.act_hi[t].x = mhi(A[0], A[1], s);
             st.act_hi[t].y = mhi(A[2], A[3], s);
         }
-        if constexpr (j == piece_tile<ntj, WV>(P_SPLIT_HI_B)) {
+        if constexpr (j == piece_tile<ntj>(P_SPLIT_HI_B)) {
             st.act_hi[t].z = mhi(B[0], B[1], s);
             st.act_hi[t].w = mhi(B[2], B[3], s);
         }
-        if constexpr (j == piece_tile<ntj, WV>(P_SPLIT_LO_A)) {
+        if constexpr (j == piece_tile<ntj>(P_SPLIT_LO_A)) {
             st.act_lo[t].x = mlo(A[0], A[1], s, st.act_hi[t].x);
             st.act_lo[t].y = mlo(A[2], A[3], s, st.act_hi[t].y);
         }
-        if constexpr (j == piece_tile<ntj, WV>(P_SPLIT_LO_B)) {
+        if constexpr (j == piece_tile<ntj>(P_SPLIT_LO_B)) {
             st.act_lo[t].z = mlo(B[0], B[1], s, st.act_hi[t].z);
             st.act_lo[t].w = mlo(B[2], B[3], s, st.act_hi[t].w);
         }
@@ -1327,7 +1318,7 @@ __device__ __forceinline__ void layer_start(const ChainFwdArgs& p, State& st) {
 // tile j of 32-k step u of layer l: the read of tile j + PF's fragments, this tile's three
 // MFMA products, the pieces placed behind it, and at tile tb the wait, barrier B_{k+1} and the
 // DMAs of step k + NPAIR - 1 (one 16-k step at tb, the other at tb + 1)
-template <int l, int u, bool TR, int j, int ntj, int WV>
+template <int l, int u, bool TR, int j, int ntj>
 __device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, const uint4& ah, const uint4& al) {
     constexpr int PF = pf_tiles<TR>(), R = PF + 1;
     constexpr int k = kfirst(l) + u, G = gtile(k) + j, T = tb<TR>(k);
@@ -1340,8 +1331,8 @@ __device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, co
         st.acc[j] = mfma16(st.wl[G % R], ah, st.acc[j]);   // lo . hi
         st.acc[j] = mfma16(st.wh[G % R], ah, st.acc[j]);   // hi . hi
         if constexpr (u == 0 && j == 0) layer_start<l, TR>(p, st);
-        split_pieces<l, u, j, ntj, WV>(st);
-        if constexpr (TR) save_pieces<l, u, j, ntj, WV>(p, st);
+        split_pieces<l, u, j, ntj>(st);
+        if constexpr (TR) save_pieces<l, u, j, ntj>(p, st);
         if constexpr (k + 1 < NK && j == T) {
             tick(p, st, nullptr);
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_n<TR>(k)) : "memory");
@@ -1352,35 +1343,35 @@ __device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, co
         }
         if constexpr (k + 1 < NK && j == T + 1) dma<tt_of_k(k + npair<TR>() - 1) + 1, TR>(p, st);
         __builtin_amdgcn_sched_barrier(0);
-        mstep_tiles<l, u, TR, j + 1, ntj, WV>(p, st, ah, al);
+        mstep_tiles<l, u, TR, j + 1, ntj>(p, st, ah, al);
     }
 }
 
 // one 32-k MFMA step u of layer l (16-k steps TT, TT + 1): 16 or 8 feature tiles x 3 products
 // over the fragments the ring already holds; the steps from the register tile split the next
 // step's A fragment and (training) save the previous layer's output beside the MFMAs
-template <int l, int u, bool TR, int WV>
+template <int l, int u, bool TR>
 __device__ __forceinline__ void kstep(const ChainFwdArgs& p, State& st) {
     constexpr int nact = l == 0 ? 0 : 8;         // k-steps from the register tile, then the encoding
     constexpr int ntj = L_OUT[l] / 16;
     if constexpr (u == 0) frag_reads<gtile(kfirst(l)), pf_tiles<TR>(), TR>(st);   // published by B_k
     const uint4& ah = u < nact ? st.act_hi[u < nact ? u : 0] : st.enc_hi[u < nact ? 0 : u - nact];
     const uint4& al = u < nact ? st.act_lo[u < nact ? u : 0] : st.enc_lo[u < nact ? 0 : u - nact];
-    mstep_tiles<l, u, TR, 0, ntj, WV>(p, st, ah, al);
+    mstep_tiles<l, u, TR, 0, ntj>(p, st, ah, al);
 }
 
-template <int l, int u, bool TR, int WV>
+template <int l, int u, bool TR>
 __device__ __forceinline__ void ksteps(const ChainFwdArgs& p, State& st) {
     if constexpr (2 * u < L_KS[l]) {
-        kstep<l, u, TR, WV>(p, st);
-        ksteps<l, u + 1, TR, WV>(p, st);
+        kstep<l, u, TR>(p, st);
+        ksteps<l, u + 1, TR>(p, st);
     }
 }
 
 // layer l: k-loop, epilogue (feature f = 16 j + 4 g + i of the lane's sample), heads, next A.
 // Training: the colour layer stores its f32 output and ReLU words here (no later layer
 // consumes it; every other layer's are saved by the next layer's k-steps)
-template <int l, bool TR, int WV>
+template <int l, bool TR>
 __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
     using Y = LY<TR>;
     constexpr int ntj = L_OUT[l] / 16;
@@ -1389,7 +1380,7 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
     constexpr bool last_tr = TR && l == CNL - 1;
 #pragma unroll
     for (int j = 0; j < 16; ++j) st.acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    ksteps<l, 0, TR, WV>(p, st);
+    ksteps<l, 0, TR>(p, st);
     tick(p, st, nullptr);
     // the lane's feature offset, opaque per layer: otherwise the exponent / bias addresses of
     // the even (odd) layers are computed once and kept live -- spilled -- across the chain
@@ -1548,10 +1539,7 @@ __device__ __forceinline__ void encode_p(const ChainFwdArgs& p, State& st) {
 
 // waves 4-7 (the second-dispatched half, the arbitration loser) at s_setprio 1 for the whole
 // chain (MI355X_MICROARCH.md "Two waves per SIMD" item 4): -0.5 % per cfg2 step in two
-// interleaved library A/Bs (profiles/r05/chain_variants_ab.txt); 0 keeps equal priorities
-#ifndef NERF_CHAIN_PRIO
-#define NERF_CHAIN_PRIO 1
-#endif
+// interleaved library A/Bs (profiles/r05/chain_variants_ab.txt)
 template <bool TR>
 __device__ __forceinline__ void init_state(State& st, char* smem) {
     st.lds = smem;
@@ -1570,35 +1558,21 @@ __device__ __forceinline__ void init_state(State& st, char* smem) {
     st.rk1 = u16x2{(unsigned short)(4u << (4 * st.g)), (unsigned short)(8u << (4 * st.g))};
     st.t_wait = st.t_bar = st.t_epi = st.t_pro = 0;
     st.t_last = st.t_start = NERF_CHAIN_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-    if constexpr (NERF_CHAIN_PRIO) {
-        if (st.wave >= 4) __builtin_amdgcn_s_setprio(1);
-    }
+    if (st.wave >= 4) __builtin_amdgcn_s_setprio(1);
 }
 
-template <bool TR, int WV>
-__device__ __forceinline__ void chain_layers_wv(const ChainFwdArgs& p, State& st) {
-    layer<0, TR, WV>(p, st);
-    layer<1, TR, WV>(p, st);
-    layer<2, TR, WV>(p, st);
-    layer<3, TR, WV>(p, st);
-    layer<4, TR, WV>(p, st);
-    layer<5, TR, WV>(p, st);
-    layer<6, TR, WV>(p, st);
-    layer<7, TR, WV>(p, st);
-    layer<8, TR, WV>(p, st);
-    layer<9, TR, WV>(p, st);
-}
-#ifndef NERF_CHAIN_STAGGER
-#define NERF_CHAIN_STAGGER 0   // 1: waves 4-7 run a copy of the chain with the staggered piece table
-#endif
 template <bool TR>
 __device__ __forceinline__ void chain_layers(const ChainFwdArgs& p, State& st) {
-    if constexpr (NERF_CHAIN_STAGGER) {
-        if (st.wave >= 4) chain_layers_wv<TR, 1>(p, st);
-        else chain_layers_wv<TR, 0>(p, st);
-    } else {
-        chain_layers_wv<TR, 0>(p, st);
-    }
+    layer<0, TR>(p, st);
+    layer<1, TR>(p, st);
+    layer<2, TR>(p, st);
+    layer<3, TR>(p, st);
+    layer<4, TR>(p, st);
+    layer<5, TR>(p, st);
+    layer<6, TR>(p, st);
+    layer<7, TR>(p, st);
+    layer<8, TR>(p, st);
+    layer<9, TR>(p, st);
 }
 
 }  // namespace f2
@@ -1723,10 +1697,7 @@ constexpr int kfirst(int i) { return i == 0 ? 0 : kfirst(i - 1) + nks(i - 1); }
 constexpr int layer_of_k(int k) { int i = 0; while (i + 1 < NL && kfirst(i + 1) <= k) ++i; return i; }
 constexpr int tt_of_k(int k) { return kb(layer_of_k(k)) + 2 * (k - kfirst(layer_of_k(k))); }
 constexpr int NK = kfirst(NL);
-#ifndef NERF_CHAIN_PF_BWD
-#define NERF_CHAIN_PF_BWD 3
-#endif
-constexpr int PF = NERF_CHAIN_PF_BWD;   // weight fragments read PF tiles ahead of their MFMAs (the ring runs across steps)
+constexpr int PF = f2::PF_BWD;   // weight fragments read PF tiles ahead of their MFMAs (the ring runs across steps)
 constexpr int NG = 16 * NK;                  // MFMA tiles (16 per step)
 constexpr int TB = 16 - PF - 1;              // the barrier tile of a step (f2::tb)
 constexpr int dma_step(int m) { return m >= NK ? 0 : dma_count(tt_of_k(m)) + dma_count(tt_of_k(m) + 1); }
@@ -1822,7 +1793,7 @@ __device__ __forceinline__ void dma_n(const nerf_chain_bwd& p, State& st) {
 
 // D_i's save work at layer i's k-step u, piece j: pair stores and the column maxima (parity
 // i & 1) of tiles 2t, 2t + 1 (pair 0 and 1 at u = 0, pair u + 1 later)
-template <int i, int u, int j, int WV>
+template <int i, int u, int j>
 __device__ __forceinline__ void save_pieces(const nerf_chain_bwd& p, State& st) {
     using f2::Piece;
     constexpr int W = i == 0 ? 128 : 256;   // D_0 = dyr is 128 wide
@@ -1832,48 +1803,48 @@ __device__ __forceinline__ void save_pieces(const nerf_chain_bwd& p, State& st) 
         asm volatile("" : "+v"(o));
         return reinterpret_cast<uint32_t*>(st.lds + o) + (i & 1) * 256 + 32 * t + 16 * half;
     };
-    const bool leader = NERF_CHAIN_COLMAX_ROW ? st.n == 0 : (st.n & 3) == 0;
+    const bool leader = st.n == 0;
     float* ob = p.dy[i] + st.m0 * W;
     int vrow = st.vrow;
     if constexpr (W != 256) vrow = (st.rl * W + 4 * st.g) * 4;
     if constexpr (u == 0) {
-        if constexpr (j == piece_tile<16, WV>(f2::P0_STORE)) {
+        if constexpr (j == piece_tile<16>(f2::P0_STORE)) {
             f2::tile_store4<W>(ob, vrow, 0, st.xs[0]);
             f2::tile_store4<W>(ob, vrow, 64, st.xs[1]);
         }
-        if constexpr (j == piece_tile<16, WV>(f2::P0_CMAX_A)) f2::colmax4(st.xs[0], cm_at(0, 0), leader);
-        if constexpr (j == piece_tile<16, WV>(f2::P0_CMAX_B)) f2::colmax4(st.xs[1], cm_at(0, 1), leader);
+        if constexpr (j == piece_tile<16>(f2::P0_CMAX_A)) f2::colmax4(st.xs[0], cm_at(0, 0), leader);
+        if constexpr (j == piece_tile<16>(f2::P0_CMAX_B)) f2::colmax4(st.xs[1], cm_at(0, 1), leader);
     }
     if constexpr (u + 1 < npair) {
         constexpr int t = u + 1;
-        if constexpr (j == piece_tile<16, WV>(f2::P_STORE)) {
+        if constexpr (j == piece_tile<16>(f2::P_STORE)) {
             f2::tile_store4<W>(ob, vrow, 128 * t, st.xs[2 * t]);
             f2::tile_store4<W>(ob, vrow, 128 * t + 64, st.xs[2 * t + 1]);
         }
-        if constexpr (j == piece_tile<16, WV>(f2::P_CMAX_A)) f2::colmax4(st.xs[2 * t], cm_at(t, 0), leader);
-        if constexpr (j == piece_tile<16, WV>(f2::P_CMAX_B)) f2::colmax4(st.xs[2 * t + 1], cm_at(t, 1), leader);
+        if constexpr (j == piece_tile<16>(f2::P_CMAX_A)) f2::colmax4(st.xs[2 * t], cm_at(t, 0), leader);
+        if constexpr (j == piece_tile<16>(f2::P_CMAX_B)) f2::colmax4(st.xs[2 * t + 1], cm_at(t, 1), leader);
     }
 }
 
-template <int i, int u, int j, int WV>
+template <int i, int u, int j>
 __device__ __forceinline__ void split_pieces(State& st) {
     if constexpr (u + 1 < nks(i)) {
         constexpr int t = u + 1;
         const f2::f32x4 A = st.xs[2 * t], B = st.xs[2 * t + 1];
         const float s = st.ser;
-        if constexpr (j == piece_tile<16, WV>(f2::P_SPLIT_HI_A)) {
+        if constexpr (j == piece_tile<16>(f2::P_SPLIT_HI_A)) {
             st.act_hi[t].x = f2::mhi(A[0], A[1], s);
             st.act_hi[t].y = f2::mhi(A[2], A[3], s);
         }
-        if constexpr (j == piece_tile<16, WV>(f2::P_SPLIT_HI_B)) {
+        if constexpr (j == piece_tile<16>(f2::P_SPLIT_HI_B)) {
             st.act_hi[t].z = f2::mhi(B[0], B[1], s);
             st.act_hi[t].w = f2::mhi(B[2], B[3], s);
         }
-        if constexpr (j == piece_tile<16, WV>(f2::P_SPLIT_LO_A)) {
+        if constexpr (j == piece_tile<16>(f2::P_SPLIT_LO_A)) {
             st.act_lo[t].x = f2::mlo(A[0], A[1], s, st.act_hi[t].x);
             st.act_lo[t].y = f2::mlo(A[2], A[3], s, st.act_hi[t].y);
         }
-        if constexpr (j == piece_tile<16, WV>(f2::P_SPLIT_LO_B)) {
+        if constexpr (j == piece_tile<16>(f2::P_SPLIT_LO_B)) {
             st.act_lo[t].z = f2::mlo(B[0], B[1], s, st.act_hi[t].z);
             st.act_lo[t].w = f2::mlo(B[2], B[3], s, st.act_hi[t].w);
         }
@@ -1923,7 +1894,7 @@ __device__ __forceinline__ void layer_start(const nerf_chain_bwd& p, State& st) 
     }
 }
 
-template <int i, int u, int j, int WV>
+template <int i, int u, int j>
 __device__ __forceinline__ void tiles(const nerf_chain_bwd& p, State& st, const uint4& ah, const uint4& al) {
     constexpr int R = PF + 1;
     constexpr int k = kfirst(i) + u, G = 16 * k + j;
@@ -1934,8 +1905,8 @@ __device__ __forceinline__ void tiles(const nerf_chain_bwd& p, State& st, const 
         st.acc[j] = f2::mfma16(st.wl[G % R], ah, st.acc[j]);   // lo . hi
         st.acc[j] = f2::mfma16(st.wh[G % R], ah, st.acc[j]);   // hi . hi
         if constexpr (u == 0 && j == 0) layer_start<i>(p, st);
-        split_pieces<i, u, j, WV>(st);
-        save_pieces<i, u, j, WV>(p, st);
+        split_pieces<i, u, j>(st);
+        save_pieces<i, u, j>(p, st);
         if constexpr (k + 1 < NK && j == TB) {
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_n(k)) : "memory");
             __syncthreads();   // B_{k+1}
@@ -1943,21 +1914,21 @@ __device__ __forceinline__ void tiles(const nerf_chain_bwd& p, State& st, const 
         }
         if constexpr (k + 1 < NK && j == TB + 1) dma<tt_of_k(k + NPAIR - 1) + 1>(p, st);
         __builtin_amdgcn_sched_barrier(0);
-        tiles<i, u, j + 1, WV>(p, st, ah, al);
+        tiles<i, u, j + 1>(p, st, ah, al);
     }
 }
 
-template <int i, int u, int WV>
+template <int i, int u>
 __device__ __forceinline__ void kstep(const nerf_chain_bwd& p, State& st) {
     if constexpr (u == 0) frag_reads<16 * kfirst(i), PF>(st);
-    tiles<i, u, 0, WV>(p, st, st.act_hi[u], st.act_lo[u]);
+    tiles<i, u, 0>(p, st, st.act_hi[u], st.act_lo[u]);
 }
 
-template <int i, int u, int WV>
+template <int i, int u>
 __device__ __forceinline__ void ksteps(const nerf_chain_bwd& p, State& st) {
     if constexpr (u < nks(i)) {
-        kstep<i, u, WV>(p, st);
-        ksteps<i, u + 1, WV>(p, st);
+        kstep<i, u>(p, st);
+        ksteps<i, u + 1>(p, st);
     }
 }
 
@@ -1965,12 +1936,12 @@ __device__ __forceinline__ void ksteps(const nerf_chain_bwd& p, State& st) {
 // input's ReLU mask -> D_{i+1} (features 16 j + 4 g + c of the lane's row, tile layout), its
 // row max and k-step 0's A fragment (the rest during the next layer's k-steps); the last
 // layer stores D_9 and its column maxima here
-template <int i, int WV>
+template <int i>
 __device__ __forceinline__ void layer(const nerf_chain_bwd& p, State& st) {
     constexpr bool last = i == NL - 1;
 #pragma unroll
     for (int j = 0; j < 16; ++j) st.acc[j] = f2::f32x4{0.f, 0.f, 0.f, 0.f};
-    ksteps<i, 0, WV>(p, st);
+    ksteps<i, 0>(p, st);
     int g4 = 4 * st.g;
     asm volatile("" : "+v"(g4));
     const float* le = reinterpret_cast<const float*>(st.lds + O_EXP) + (i & 1) * 256 + g4;
@@ -2007,8 +1978,7 @@ __device__ __forceinline__ void layer(const nerf_chain_bwd& p, State& st) {
         rmx = fmaxf(rmx, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
         if constexpr (last) {
             f2::tile_store4<256>(p.dy[NL] + st.m0 * 256, st.vrow, 64 * j, x);
-            f2::colmax4(x, reinterpret_cast<uint32_t*>(st.lds + O_CMX) + (NL & 1) * 256 + f0,
-                        NERF_CHAIN_COLMAX_ROW ? st.n == 0 : (st.n & 3) == 0);
+            f2::colmax4(x, reinterpret_cast<uint32_t*>(st.lds + O_CMX) + (NL & 1) * 256 + f0, st.n == 0);
         }
     }
     // the row's max over its four 16-lane rows (lanes n, n + 16, n + 32, n + 48)
@@ -2022,17 +1992,16 @@ __device__ __forceinline__ void layer(const nerf_chain_bwd& p, State& st) {
     }
 }
 
-template <int WV>
 __device__ __forceinline__ void layers(const nerf_chain_bwd& p, State& st) {
-    layer<0, WV>(p, st);
-    layer<1, WV>(p, st);
-    layer<2, WV>(p, st);
-    layer<3, WV>(p, st);
-    layer<4, WV>(p, st);
-    layer<5, WV>(p, st);
-    layer<6, WV>(p, st);
-    layer<7, WV>(p, st);
-    layer<8, WV>(p, st);
+    layer<0>(p, st);
+    layer<1>(p, st);
+    layer<2>(p, st);
+    layer<3>(p, st);
+    layer<4>(p, st);
+    layer<5>(p, st);
+    layer<6>(p, st);
+    layer<7>(p, st);
+    layer<8>(p, st);
 }
 
 }  // namespace b2
@@ -2053,9 +2022,7 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_bwd(ChainBwdArgs args) {
     st.voff16 = 16u * st.lane;
     st.vrow = (st.rl * 256 + 4 * st.g) * 4;
     st.fr = (st.g >> 1) * b2::SBYTES + (st.g & 1) * b2::SHALF + st.n * 16;
-    if constexpr (NERF_CHAIN_PRIO) {
-        if (st.wave >= 4) __builtin_amdgcn_s_setprio(1);
-    }
+    if (st.wave >= 4) __builtin_amdgcn_s_setprio(1);
     // head weights into LDS, both column-max parities cleared
     if (st.tid < 256) st.fx[st.tid] = p.wd[st.tid];
     for (int e = st.tid; e < 384; e += NTH) st.fx[256 + e] = p.wc[e];
@@ -2089,12 +2056,7 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_bwd(ChainBwdArgs args) {
     dma_n<0, 2 * (NPAIR - 1)>(p, st);   // steps 0 .. NPAIR - 2
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_prologue()) : "memory");
     __syncthreads();   // B_0
-    if constexpr (NERF_CHAIN_STAGGER) {
-        if (st.wave >= 4) layers<1>(p, st);
-        else layers<0>(p, st);
-    } else {
-        layers<0>(p, st);
-    }
+    layers(p, st);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // D_8's (parity 0, saved by layer 8's k-steps) and D_9's (parity 1, the last epilogue)

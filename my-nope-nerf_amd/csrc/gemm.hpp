@@ -55,10 +55,6 @@ struct NTArgs {
 };
 
 __device__ __forceinline__ void store_out4(float* dst, const float4& x) { *reinterpret_cast<float4*>(dst) = x; }
-#ifndef NERF_SLAB_NT
-#define NERF_SLAB_NT 0   // A/B builds: 1 = the split-K slab stores of the TN epilogue non-temporal
-                         // (weight gradients 368-373 vs 329-333 us per launch: slower, profiles/r05/chain_nt_ab.txt)
-#endif
 
 // max |a| over row m of the (one or two segment) A operand
 __device__ __forceinline__ float a_rowmax(const NTArgs& p, int m) {
@@ -624,11 +620,8 @@ __device__ __forceinline__ void tn_store_lds(const TNArgs& p, f32x16 (&acc)[TM][
             v.w = __builtin_amdgcn_ldexpf(v.w, -(ea + eb.w));
         }
         float* d = slab + (size_t)(o0 + wm0 + rl) * p.ldslab + p.col0 + j0 + wn0 + c4;
-        if constexpr (NERF_SLAB_NT) {
-            typedef float slab_f4 __attribute__((ext_vector_type(4)));
-            const slab_f4 q = {v.x, v.y, v.z, v.w};
-            __builtin_nontemporal_store(q, reinterpret_cast<slab_f4*>(d));
-        } else {
+        {   // (plain stores: non-temporal slab stores made the weight gradients slower, 368-373 vs
+            // 329-333 us per launch, profiles/r05/chain_nt_ab.txt)
             store_out4(d, v);
         }
     });

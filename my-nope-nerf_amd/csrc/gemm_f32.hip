@@ -266,11 +266,8 @@ struct SlabJob {
     float* gb;
     int accumulate;
 };
-// the slab reduce's loads non-temporal (1, the default: the slabs are read once; cfg2 step 2.020
-// vs 2.030 ms, per round -0.5 / -1.9 / -14 us, profiles/r05/reduce_nt_ab.txt)
-#ifndef NERF_REDUCE_NT
-#define NERF_REDUCE_NT 1
-#endif
+// the slab reduce's loads are non-temporal (the slabs are read once; cfg2 step 2.020 vs 2.030
+// ms, per round -0.5 / -1.9 / -14 us, profiles/r05/reduce_nt_ab.txt)
 // one block of the reduce: block `blk` of job j (weight blocks, then bias blocks)
 __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int blk, float4 (&part)[SR_GROUPS][16]) {
     const int l16 = threadIdx.x & 15, grp = threadIdx.x >> 4;
@@ -296,12 +293,10 @@ __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int blk, flo
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const float* a = src + (size_t)(q + SR_GROUPS * u) * st + c0;
-                    if constexpr (NERF_REDUCE_NT) {
+                    {
                         typedef float sr_f4 __attribute__((ext_vector_type(4)));
                         const sr_f4 t = __builtin_nontemporal_load(reinterpret_cast<const sr_f4*>(a));
                         v[u] = make_float4(t.x, t.y, t.z, t.w);
-                    } else {
-                        v[u] = *reinterpret_cast<const float4*>(a);
                     }
                 }
 #pragma unroll

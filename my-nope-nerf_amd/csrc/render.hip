@@ -37,18 +37,10 @@ __device__ __forceinline__ float encode3_lds(const float x[3], float* row) {
     return m;
 }
 
-#ifndef NERF_ENC_NT
-#define NERF_ENC_NT 0   // A/B builds: 1 = the encodings' stores non-temporal (the forward chain reads them
-                        // next: 538-543 vs 526-530 us, slower; profiles/r05/nt_loads_ab.txt)
-#endif
+// (plain stores: the forward chain reads the encodings next; non-temporal ones made it slower,
+// 538-543 vs 526-530 us, profiles/r05/nt_loads_ab.txt)
 __device__ __forceinline__ void enc_st4(float* d, const float4& v) {
-    if constexpr (NERF_ENC_NT) {
-        typedef float enc_f4 __attribute__((ext_vector_type(4)));
-        const enc_f4 q = {v.x, v.y, v.z, v.w};
-        __builtin_nontemporal_store(q, reinterpret_cast<enc_f4*>(d));
-    } else {
-        *reinterpret_cast<float4*>(d) = v;
-    }
+    *reinterpret_cast<float4*>(d) = v;
 }
 // the block's 128 LDS rows -> rows m0 .. m0 + 127 of a [n][64] encoding, coalesced
 __device__ __forceinline__ void enc_copy_out(const float* lds, float* dst, size_t m0) {
@@ -307,15 +299,11 @@ __global__ __launch_bounds__(256) void k_heads_fwd(const float* __restrict__ h8,
     }
 }
 
-// the head partials' h8 / hr loads non-temporal (1, the default: cfg2 step 2.021 vs 2.035 ms in
-// three interleaved rounds, profiles/r05/nt_loads_ab.txt; the same hint on the weight-gradient
-// stage loads made those 9-27 % slower)
-#ifndef NERF_HEADS_NT
-#define NERF_HEADS_NT 1
-#endif
+// the head partials' h8 / hr loads are non-temporal: cfg2 step 2.021 vs 2.035 ms in three
+// interleaved rounds, profiles/r05/nt_loads_ab.txt (the same hint on the weight-gradient stage
+// loads made those 9-27 % slower)
 __device__ __forceinline__ float heads_ld(const float* a) {
-    if constexpr (NERF_HEADS_NT) return __builtin_nontemporal_load(a);
-    else return *a;
+    return __builtin_nontemporal_load(a);
 }
 // part layout per block: [wd: 64*NH][wc: 3*64*NR][bd, bc0, bc1, bc2]
 // MODE bit 0: dyr and its row / column maxima (the input-gradient chain waits for these);

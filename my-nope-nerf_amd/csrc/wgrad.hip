@@ -79,12 +79,8 @@ __device__ __forceinline__ void load_row(float (&v)[C], const __amdgpu_buffer_rs
         v[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, POL));
     }
 }
-#ifndef NERF_WG_POL_DY
-#define NERF_WG_POL_DY 0   // A/B builds: cache policy of the dy / x stage loads (nt on x: +9 %, on both:
-#endif                     // +27 % per launch, profiles/r05/nt_loads_ab.txt)
-#ifndef NERF_WG_POL_X
-#define NERF_WG_POL_X 0
-#endif
+// (the stage loads keep the default cache policy: nt on x made a launch 9 % slower, on dy and x
+// 27 %, profiles/r05/nt_loads_ab.txt)
 
 // 8 rows of one column, scaled by 2^e -> one 16-byte fragment chunk per plane
 __device__ __forceinline__ void put_strip(char* d, int plane_bytes, const float (&v)[8], int e) {
@@ -144,8 +140,8 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
             const int r0 = KS * t + 8 * lw;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                load_row<CA, NERF_WG_POL_DY>(va[U][i], rdy, va_off, (r0 + i) * p.lddy * 4);
-                load_row<CB, NERF_WG_POL_X>(vb[U][i], rx, vb_off, (r0 + i) * p.ldx * 4);
+                load_row<CA>(va[U][i], rdy, va_off, (r0 + i) * p.lddy * 4);
+                load_row<CB>(vb[U][i], rx, vb_off, (r0 + i) * p.ldx * 4);
             }
         };
         unroll<NS>([&](auto u) { load(u, decltype(u)::value); });
