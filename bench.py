@@ -28,10 +28,12 @@ replay from the sampler's device step counter) -- and "value" is the faster; "ex
 > 3 ms (slow core) of Python enqueue per step from the timed region, which on a slow host
 is longer than the GPU's step.  N > 1 runs eager.
 
-"roofline" names the GEMM kind with the most time per step (per_kind lists all three)
+"roofline" names the GEMM kind with the most time per step (per_kind lists all of them)
 and prices it against BOTH ceilings: its MFMA work at the dense MFMA rate of the
 arithmetic that ran, and its algorithmic HBM bytes at 8 TB/s; "bound" is the ceiling
-with the larger ideal time.
+with the larger ideal time.  "roofline.dominant_kernel" prices the longest single in-step
+kernel (the training forward chain) the same way, so that the figure stays comparable
+across rounds whichever kind has the most time per step.
 
     python bench.py --gpus N     (N > 1 without WORLD_SIZE: spawns N ranks itself)
 """
@@ -639,20 +641,39 @@ def main():
         bound = d["binding"]
         ach, peak, unit = ((d["hbm"]["achieved_gbs"], HBM_PEAK_GBS, "GB/s") if bound == "hbm" else
                            (d["mfma"]["achieved_tflops_f32eq"], d["mfma"]["peak_tflops_f32eq"], "TFLOP/s"))
-        traffic, traffic_note = None, None
-        tpath = next((q for q in (os.path.join(ROOT, "profiles", r, "gemm_traffic.json") for r in ("r05", "r04"))
-                      if os.path.exists(q)), "")
-        if tpath and args.gemm_precision == "f16x3":
-            # HBM bytes per launch of the dominant kind from the committed rocprofv3 PMC passes
-            # (FETCH_SIZE x2 + WRITE_SIZE, the guide's gfx950 correction): the mean over the
-            # kind's launches, as per_kind's algorithmic bytes are
-            t = json.load(open(tpath))
-            kd = t.get("kinds", {}).get(dom)
-            if kd:
-                traffic = kd["bytes_per_launch"]
-                traffic_note = (f"{os.path.relpath(tpath, ROOT)}: mean over {kd['launches_profiled']} profiled "
-                                f"launches of the kind's kernels ({kd['read_bytes_per_launch'] / 1e6:.1f} MB read, "
-                                f"{kd['write_bytes_per_launch'] / 1e6:.1f} MB written per launch)")
+        tpath = next((q for q in (os.path.join(ROOT, "profiles", r, "gemm_traffic.json")
+                                  for r in ("r06", "r05", "r04")) if os.path.exists(q)), "")
+        tkinds = json.load(open(tpath)).get("kinds", {}) if tpath and args.gemm_precision == "f16x3" else {}
+
+        def kind_traffic(k):
+            # HBM bytes per launch of kind k from the committed rocprofv3 PMC passes (FETCH_SIZE x2 +
+            # WRITE_SIZE, the guide's gfx950 correction): the mean over the kind's launches, as
+            # per_kind's algorithmic bytes are
+            kd = tkinds.get(k)
+            if not kd:
+                return None, None
+            return kd["bytes_per_launch"], (
+                f"{os.path.relpath(tpath, ROOT)}: mean over {kd['launches_profiled']} profiled launches of the "
+                f"kind's kernels ({kd['read_bytes_per_launch'] / 1e6:.1f} MB read, "
+                f"{kd['write_bytes_per_launch'] / 1e6:.1f} MB written per launch)")
+
+        traffic, traffic_note = kind_traffic(dom)
+        # the longest single in-step kernel (the training forward chain since round 4), priced
+        # against its own binding ceiling: comparable across rounds whichever kind has the most
+        # time per step
+        dk = max(per_kind, key=lambda k: per_kind[k]["avg_launch_us"])
+        dkr = per_kind[dk]
+        dk_hbm = dkr["binding"] == "hbm"
+        dk_traffic, dk_note = kind_traffic(dk)
+        dominant = {"kind": dk, "kernel": dkr["kernel"], "bound": dkr["binding"],
+                    "avg_launch_us": dkr["avg_launch_us"],
+                    "achieved": dkr["hbm"]["achieved_gbs"] if dk_hbm else dkr["mfma"]["achieved_tflops_f32eq"],
+                    "peak": HBM_PEAK_GBS if dk_hbm else dkr["mfma"]["peak_tflops_f32eq"],
+                    "unit": "GB/s" if dk_hbm else "TFLOP/s",
+                    "frac": dkr["hbm"]["frac"] if dk_hbm else dkr["mfma"]["frac"],
+                    "algorithmic_mbytes_per_launch": dkr["mbytes_per_launch"],
+                    "gflop_per_launch": dkr["gflop_per_launch"],
+                    "traffic": dk_traffic, "traffic_note": dk_note}
         nt_fl, tn_fl = algorithmic_gemm_flops(net, RAYS * SAMPLES, split=True)
         fam_ms = sum(rec["ms"] for rec in kinds.values())
         fam_mfma = sum(rec["mfma_flops"] for rec in kinds.values())
@@ -666,6 +687,7 @@ def main():
                                    d["mfma"]["achieved_tflops_f32eq"], "mfma_peak_tflops_f32eq":
                                    d["mfma"]["peak_tflops_f32eq"]} if bound == "hbm" else
                                   {"hbm_frac": d["hbm"]["frac"], "hbm_achieved_gbs": d["hbm"]["achieved_gbs"]}),
+                "dominant_kernel": dominant,
                 "per_kind": per_kind,
                 "family": {"gemm_ms_per_step": gemm_ms / args.steps, "union_ms_per_step": gemm_union_ms / args.steps,
                            "launches_per_step": gemm_launches / args.steps,

@@ -454,8 +454,8 @@ int schedule(const nerf_field_bwd& a, void* stream, void* side_stream) {
                                nullptr, nullptr, s));
         return nerf_heads_reduce(w.part, D, np, a.g_wd, a.g_bd, a.g_wc, a.g_bc, 0, s);
     };
-    // NERF_HEADS_PLACE 3 (the default with the chain): the partials by k_heads_part (16-byte loads,
-    // 4x the waves) before the chain, their reduces in the weight gradients' first slab batch
+    // NERF_HEADS_PLACE 3 (an A/B option; 5 is the default): the partials by k_heads_part (16-byte
+    // loads, 4x the waves) before the chain, their reduces in the weight gradients' first slab batch
     nerf::SlabJobDesc hjobs[2];
     int n_hjobs = 0;
     if (heads_place == 0) {

@@ -272,14 +272,22 @@ __global__ __launch_bounds__(256) void k_pair_reduce(const float* __restrict__ d
 // atomic.  Integer sums do not depend on the order the atomics land in, so the gradient is the
 // same bits on every run (float atomics are not: a resumed run would drift from the uninterrupted
 // one in the last bit); the scale g = go_pc / P is applied once per point when the sums are read
-// (pair_scattered).  2^48 per term: a point gathered by all 2 P terms still fits in 63 bits.
-constexpr double kPairFix = 281474976710656.0;   // 2^48
+// (pair_scattered).  The scale: a point of one cloud gathers at most the other cloud's P terms,
+// each |u| 2^e <= 2^e, so P 2^e < 2^63 needs e <= 62 - ceil(log2 P): 2^48 up to P = 2^14
+// (every V_KITTI depth grid; cfg3's P = 7 285), smaller beyond (pair_fix_scale)
+__host__ __device__ inline double pair_fix_scale(int P) {
+    int b = 0;
+    while (b < 31 && (1LL << b) < (long long)P) ++b;
+    const int e = 62 - b < 48 ? 62 - b : 48;
+    return (double)(1LL << e);
+}
 __global__ __launch_bounds__(PT) void k_pair_bwd_scatter(const float* __restrict__ X, const float* __restrict__ Y,
                                                          int P, const int* __restrict__ nn,
                                                          unsigned long long* __restrict__ gX,
                                                          unsigned long long* __restrict__ gY) {
     const int i = blockIdx.x * PT + threadIdx.x;
     if (i >= P) return;
+    const double fix = pair_fix_scale(P);
 #pragma unroll
     for (int z = 0; z < 2; ++z) {
         const float* Q = z == 0 ? X : Y;
@@ -289,16 +297,16 @@ __global__ __launch_bounds__(PT) void k_pair_bwd_scatter(const float* __restrict
         const float dx = Q[3 * i] - Rf[3 * j], dy = Q[3 * i + 1] - Rf[3 * j + 1], dz = Q[3 * i + 2] - Rf[3 * j + 2];
         const float d = sqrtf(dx * dx + dy * dy + dz * dz);
         if (d > 0.f) {
-            atomicAdd(&gR[3 * j], (unsigned long long)llrint((double)(-dx / d) * kPairFix));
-            atomicAdd(&gR[3 * j + 1], (unsigned long long)llrint((double)(-dy / d) * kPairFix));
-            atomicAdd(&gR[3 * j + 2], (unsigned long long)llrint((double)(-dz / d) * kPairFix));
+            atomicAdd(&gR[3 * j], (unsigned long long)llrint((double)(-dx / d) * fix));
+            atomicAdd(&gR[3 * j + 1], (unsigned long long)llrint((double)(-dy / d) * fix));
+            atomicAdd(&gR[3 * j + 2], (unsigned long long)llrint((double)(-dz / d) * fix));
         }
     }
 }
 
 // a point's scattered chamfer gradient: its fixed-point sum times g (one rounding to float)
-__device__ __forceinline__ float pair_scattered(const unsigned long long* s, int k, double g) {
-    return (float)((double)(long long)s[k] * (g / kPairFix));
+__device__ __forceinline__ float pair_scattered(const unsigned long long* s, int k, double g, double fix) {
+    return (float)((double)(long long)s[k] * (g / fix));
 }
 
 // per point: the direct chamfer terms plus the scattered ones -> dX_i, dY_i; the rgb_s term
@@ -332,8 +340,8 @@ __global__ __launch_bounds__(PT) void k_pair_bwd_points(PairArgs a, const float*
         const double gsc = (double)gpc;   // the scatter's g
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            gx[k] = gX ? pair_scattered(gX + 3 * i, k, gsc) : 0.f;
-            gy[k] = gY ? pair_scattered(gY + 3 * i, k, gsc) : 0.f;
+            gx[k] = gX ? pair_scattered(gX + 3 * i, k, gsc, pair_fix_scale(P)) : 0.f;
+            gy[k] = gY ? pair_scattered(gY + 3 * i, k, gsc, pair_fix_scale(P)) : 0.f;
         }
         if (go_pc) {
 #pragma unroll
@@ -454,6 +462,7 @@ static int fill_args(PairArgs& a, const float* d1, const float* d2, int h, int w
     NERF_CHECK_PTR(d1); NERF_CHECK_PTR(d2); NERF_CHECK_PTR(K16); NERF_CHECK_PTR(Rt16);
     NERF_CHECK(h > 1 && w > 1, "nerf_pair: resolution %dx%d", h, w);
     NERF_CHECK((img1 == nullptr) == (img2 == nullptr), "nerf_pair: img1 and img2 go together");
+    NERF_CHECK((long long)h * w < (1LL << 28), "nerf_pair: %dx%d points", h, w);
     a.d1 = d1; a.d2 = d2; a.h = h; a.w = w; a.P = h * w;
     a.Kg = K16; a.Rtg = Rt16; a.s1g = s1; a.nl = nl;
     a.img1 = img1; a.img2 = img2; a.rgbs_detach_scale = rgbs_detach_scale;

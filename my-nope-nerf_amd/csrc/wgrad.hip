@@ -98,7 +98,12 @@ __device__ __forceinline__ void put_strip(char* d, int plane_bytes, const float 
 // AUX: the LDS offset of the column exponents and bias partials (a kernel that runs tiles of
 // several shapes puts them past the largest main region, so one shape's exponents never land in
 // the region another shape's epilogue is still staging its slab through)
-template <int BO, int BK, bool BIAS, int AUX = Cfg<BO, BK>::MAIN>
+// SET: ints per exponent set.  A kernel that runs tiles of several shapes passes one stride for
+// all of them (JOBS_SET): the next job's exponents() writes its set while the previous job's
+// epilogue may still read the other set's lea / leb, so the two sets must not overlap whatever
+// the two jobs' shapes (with a per-shape stride BO + BK, a 128 x 64 job's set 1 overlapped a
+// 256 x 128 job's set 0)
+template <int BO, int BK, bool BIAS, int AUX = Cfg<BO, BK>::MAIN, int SET = BO + BK>
 __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int jt, int split, int par) {
     using C = Cfg<BO, BK>;
     constexpr int CA = C::CA, CB = C::CB, TM = C::TM, TN = C::TN;
@@ -112,9 +117,10 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
     const size_t s0 = (size_t)split * p.rows_per_split;
     const int nst = p.rows_per_split / KS;
     static_assert(AUX >= C::MAIN, "aux region");
-    int* lea = reinterpret_cast<int*>(smem + AUX) + par * (BO + BK);   // the tile's column exponents
+    static_assert(SET >= BO + BK, "an exponent set holds BO + BK ints");
+    int* lea = reinterpret_cast<int*>(smem + AUX) + par * SET;   // the tile's column exponents
     int* leb = lea + BO;
-    float* lbias = reinterpret_cast<float*>(smem + AUX) + 2 * (BO + BK);   // [4 load waves][BO] bias partials
+    float* lbias = reinterpret_cast<float*>(smem + AUX) + 2 * SET;   // [4 load waves][BO] bias partials
     // the column exponents: every thread its share (one round trip to the producers' group
     // maxima), in both roles -- the load waves issue their first NS stages before theirs
     auto exponents = [&]() {
@@ -282,16 +288,19 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
 }
 
 // the block of column tile jt, with the bias sums where the layer wants them (column tile 0)
-template <int BO, int BK, int AUX = Cfg<BO, BK>::MAIN>
+template <int BO, int BK, int AUX = Cfg<BO, BK>::MAIN, int SET = BO + BK>
 __device__ __forceinline__ void block_any(const TNArgs& p, char* smem, int o0, int jt, int split, int par = 0) {
-    if (jt == 0 && p.bslab != nullptr) block<BO, BK, true, AUX>(p, smem, o0, jt, split, par);
-    else block<BO, BK, false, AUX>(p, smem, o0, jt, split, par);
+    if (jt == 0 && p.bslab != nullptr) block<BO, BK, true, AUX, SET>(p, smem, o0, jt, split, par);
+    else block<BO, BK, false, AUX, SET>(p, smem, o0, jt, split, par);
 }
 
-// the LDS of a kernel that runs tiles of every shape (k_wgrad_jobs)
+// the LDS of a kernel that runs tiles of every shape (k_wgrad_jobs): the main regions, then two
+// exponent sets of JOBS_SET ints (the widest shape's BO + BK) and the bias partials
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int JOBS_AUX = cmax(cmax(Cfg<256, 128>::MAIN, Cfg<128, 256>::MAIN), cmax(Cfg<256, 64>::MAIN, Cfg<128, 64>::MAIN));
-constexpr int JOBS_BYTES = JOBS_AUX + cmax(2 * (256 + 128) * 4 + 4 * 256 * 4, 2 * (128 + 256) * 4 + 4 * 128 * 4);
+constexpr int JOBS_SET = cmax(cmax(256 + 128, 128 + 256), cmax(256 + 64, 128 + 64));
+constexpr int JOBS_BYTES = JOBS_AUX + 2 * JOBS_SET * 4 + 4 * 256 * 4;
+static_assert(JOBS_SET == 384, "exponent sets");
 
 }  // namespace wg
 
@@ -332,8 +341,9 @@ __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_pairs(TNPairs m) {
 // The jobs run grouped by shape (see the kernel for the order), each group in list order.  The splits and slab columns are those of the per-layer launches, so are the slabs, bit
 // for bit.
 // Each job's exponents alternate between the two sets of one aux region past every shape's main
-// region (JOBS_AUX), so the barrier in a job's exponents() orders it after the previous job's
-// epilogue as in k_wgrad_pairs.
+// region (JOBS_AUX), at one stride for every shape (JOBS_SET), so a job's exponents never land
+// on the set the previous job's epilogue still reads, and the barrier in a job's exponents()
+// orders the rest of it after that epilogue as in k_wgrad_pairs.
 // SH: the shapes compiled in (bit 0 128 x 256, bit 1 128 x 64, bit 2 256 x 64; 256 x 256 always):
 // with all four in one kernel the register allocation spills, with any three it does not
 template <int SH>
@@ -351,19 +361,19 @@ __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_jobs(TNJobs m) {
     int c = 0;
     auto pairs = [&]() {
         for (int i = 0; i < m.n; ++i)
-            if (m.kind[i] == WJ_PAIR) wg::block_any<256, 128, A>(m.a[i], smem, 0, jt, sp, c++ & 1);
+            if (m.kind[i] == WJ_PAIR) wg::block_any<256, 128, A, wg::JOBS_SET>(m.a[i], smem, 0, jt, sp, c++ & 1);
     };
     auto narrow = [&]() {
         for (int i = 0; i < m.n; ++i) {
             const int k = m.kind[i];
             if (k == WJ_ENC128 || k == WJ_ENC_HALF)
-                wg::block_any<128, 64, A>(m.a[i], smem, k == WJ_ENC_HALF ? 128 * jt : 0, 0,
+                wg::block_any<128, 64, A, wg::JOBS_SET>(m.a[i], smem, k == WJ_ENC_HALF ? 128 * jt : 0, 0,
                                           k == WJ_ENC_HALF ? sp : 2 * sp + jt, c++ & 1);
         }
     };
     if constexpr (SH & 1) {
         for (int i = 0; i < m.n; ++i)
-            if (m.kind[i] == WJ_WIDE) wg::block_any<128, 256, A>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
+            if (m.kind[i] == WJ_WIDE) wg::block_any<128, 256, A, wg::JOBS_SET>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
         if constexpr (SH & 2) narrow();
         pairs();
     } else {
@@ -372,7 +382,7 @@ __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_jobs(TNJobs m) {
     }
     if constexpr (SH & 4)
         for (int i = 0; i < m.n; ++i)
-            if (m.kind[i] == WJ_ENC) wg::block_any<256, 64, A>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
+            if (m.kind[i] == WJ_ENC) wg::block_any<256, 64, A, wg::JOBS_SET>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
 }
 
 // two layers' 256 x 64 tiles in one launch: a's splits (blocks 0 .. na - 1), then b's (l4's

@@ -110,7 +110,10 @@ def test_chain_eval_skips_intermediate_stores(dev, h16):
         e1 = (a1.cpu().double() - r).abs().max().item()
         e0 = (a0.cpu().double() - r).abs().max().item()
         assert e1 <= 1.5 * e0 + 1e-6, (e1, e0)
-        assert ((a1 - a0).abs().max() / a0.abs().max()).item() < 5e-5
+        # the oracle check above is the main one; the cross-path bound is what is measured
+        # (round 6: tightened from 5e-5, the value is in the message when it fails)
+        rel = ((a1 - a0).abs().max() / a0.abs().max()).item()
+        assert rel < 2e-5, rel
 
 
 def test_chain_gradients_match_per_layer(dev, h16):
