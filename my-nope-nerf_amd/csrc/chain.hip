@@ -842,6 +842,23 @@ constexpr bool tb_ok() {
     return true;
 }
 static_assert(tb_ok(), "a step's barrier tile tb = ntj - PF - 1 must exist");
+// The second half of the block (waves 4-7, one per SIMD) places its wait, barrier and DMA issue
+// LAG tiles earlier in each step than the first half: s_barrier counts arrivals, not program
+// positions, so both halves still meet at every B_k, but from B_1 on waves 4-7 run LAG tiles of
+// work behind their SIMD partners -- a layer epilogue (VALU only) of one half meets the other
+// half's MFMAs instead of the partner's epilogue.  Legal for any lag that keeps tb_lag >= 0: a
+// wave passing B_{k+1} (at its tile tb or tb_lag of step k) is past step k - 1, whose slots the
+// DMAs behind B_{k+1} refill, and reads step k + 1's fragments only after it.  (Eval kernel:
+// its waits are vmcnt(0); the training kernels count stores per position, wait_n.)
+#ifndef NERF_CHAIN_LAG
+#define NERF_CHAIN_LAG 0
+#endif
+template <bool TR>
+constexpr int tb_lag(int k) {
+    if (TR) return tb<TR>(k);
+    const int lag = ntj_k(k) == 16 ? NERF_CHAIN_LAG : NERF_CHAIN_LAG / 2;
+    return tb<TR>(k) - lag < 0 ? 0 : tb<TR>(k) - lag;
+}
 // vector-memory ops of the DMAs of 32-k step m (two 16-k steps), and of those issued in step j
 constexpr int dma_step(int m) { return m >= NK ? 0 : dma_count(tt_of_k(m)) + dma_count(tt_of_k(m) + 1); }
 template <bool TR>
@@ -957,6 +974,7 @@ struct State {
     uint32_t lds0;                      // LDS address of the block's buffer (wave-uniform)
     float* fx;
     int tid, wave, lane, n, g;          // n = lane & 15 (the lane's sample in the wave), g = lane >> 4
+    bool lag;                           // waves 4-7 (wave-uniform): the half whose barrier tile is tb_lag
     size_t m0;
     int rl;                             // the lane's row in the block (16 wave + n)
     uint32_t voff16;                    // 16 lane: the lane's offset in a 16-byte-per-lane LDS-DMA
@@ -1333,15 +1351,27 @@ __device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, co
         if constexpr (u == 0 && j == 0) layer_start<l, TR>(p, st);
         split_pieces<l, u, j, ntj>(st);
         if constexpr (TR) save_pieces<l, u, j, ntj>(p, st);
-        if constexpr (k + 1 < NK && j == T) {
+        constexpr int TL = tb_lag<TR>(k);
+        // the wait, B_{k+1} and the first DMA half; the second half a tile later (one branch on
+        // the wave-uniform half where the two halves' tiles differ)
+        auto sync = [&]() {
             tick(p, st, nullptr);
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_n<TR>(k)) : "memory");
             tick(p, st, &st.t_wait);
             __syncthreads();
             tick(p, st, &st.t_bar);
             dma<tt_of_k(k + npair<TR>() - 1), TR>(p, st);
+        };
+        auto dma2 = [&]() { dma<tt_of_k(k + npair<TR>() - 1) + 1, TR>(p, st); };
+        if constexpr (k + 1 < NK && TL == T) {
+            if constexpr (j == T) sync();
+            if constexpr (j == T + 1) dma2();
+        } else if constexpr (k + 1 < NK) {
+            if constexpr (j == TL) { if (st.lag) sync(); }
+            if constexpr (j == TL + 1) { if (st.lag) dma2(); }
+            if constexpr (j == T) { if (!st.lag) sync(); }
+            if constexpr (j == T + 1) { if (!st.lag) dma2(); }
         }
-        if constexpr (k + 1 < NK && j == T + 1) dma<tt_of_k(k + npair<TR>() - 1) + 1, TR>(p, st);
         __builtin_amdgcn_sched_barrier(0);
         mstep_tiles<l, u, TR, j + 1, ntj>(p, st, ah, al);
     }
@@ -1547,6 +1577,7 @@ __device__ __forceinline__ void init_state(State& st, char* smem) {
     st.fx = reinterpret_cast<float*>(smem + LY<TR>::O_FX);
     st.tid = threadIdx.x;
     st.wave = __builtin_amdgcn_readfirstlane(st.tid >> 6);
+    st.lag = st.wave >= 4;
     st.lane = st.tid & 63; st.n = st.lane & 15; st.g = st.lane >> 4;
     st.m0 = (size_t)blockIdx.x * CROWS;
     st.rl = 16 * st.wave + st.n;
