@@ -853,10 +853,13 @@ static_assert(tb_ok(), "a step's barrier tile tb = ntj - PF - 1 must exist");
 #ifndef NERF_CHAIN_LAG
 #define NERF_CHAIN_LAG 0
 #endif
+#ifndef NERF_CHAIN_LAG_TR
+#define NERF_CHAIN_LAG_TR 0
+#endif
 template <bool TR>
 constexpr int tb_lag(int k) {
-    if (TR) return tb<TR>(k);
-    const int lag = ntj_k(k) == 16 ? NERF_CHAIN_LAG : NERF_CHAIN_LAG / 2;
+    const int L = TR ? NERF_CHAIN_LAG_TR : NERF_CHAIN_LAG;
+    const int lag = ntj_k(k) == 16 ? L : L / 2;
     return tb<TR>(k) - lag < 0 ? 0 : tb<TR>(k) - lag;
 }
 // vector-memory ops of the DMAs of 32-k step m (two 16-k steps), and of those issued in step j
@@ -967,6 +970,12 @@ __device__ __forceinline__ uint32_t mlo(float x0, float x1, float s, uint32_t h)
 // (the nt hint on these loads made both training chains ~20 % slower, profiles/r05/nt_loads_ab.txt)
 __device__ __forceinline__ void dma16(const void* g, uint32_t voff, uint32_t lds) {
     asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(g), "s"(lds) : "memory", "m0");
+}
+// a wave-uniform address the compiler cannot prove uniform (behind a branch on the wave's half)
+__device__ __forceinline__ const char* uni(const char* a) {
+    const uint64_t v = (uint64_t)(uintptr_t)a;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<const char*>((uintptr_t)(((uint64_t)hi << 32) | lo));
 }
 
 struct State {
@@ -1201,11 +1210,77 @@ constexpr int piece_tile(int piece) {
     }
 }
 // the pieces that store (vector memory) run no later than the tile of the step's barrier, tb =
-// ntj - PF - 1 (the wait counts take every store of a step as issued before it): PF 2 in the
-// training forward (16- and 8-tile steps), 3 in the backward (16)
+// ntj - PF - 1 (the first half's wait counts take every store of a step as issued before it):
+// PF 2 in the training forward (16- and 8-tile steps), 3 in the backward (16)
 static_assert(piece_tile<16>(P_STORE) <= 16 - 3 - 1 && piece_tile<16>(P0_STORE) <= 16 - 3 - 1 &&
                   piece_tile<8>(P_STORE) <= 8 - 2 - 1 && piece_tile<8>(P0_STORE) <= 8 - 2 - 1,
               "stores before the barrier");
+
+// Position-based wait counts (either half, any barrier tile): the vector-memory ops of the
+// training forward at tile j of step k -- layer_start's two stores, the save pieces' pair
+// stores -- in program order before that tile's wait / DMA issue
+struct StoreTab {   // [step][tile] stores of the training forward, tiles and DMA ops per step (tabulated)
+    unsigned char n[NK][16];
+    int ntj[NK], dma[NK];
+    constexpr StoreTab() : n{}, ntj{}, dma{} {
+        for (int k = 0; k < NK; ++k) {
+            ntj[k] = ntj_k(k);
+            dma[k] = dma_step(k);
+        }
+        for (int k = 0; k < NK; ++k) {
+            const int l = layer_of_k(k), u = k - kfirst(l), ntj = ntj_k(k);
+            if (l == 0) continue;
+            const int p0 = ntj == 16 ? piece_tile<16>(P0_STORE) : piece_tile<8>(P0_STORE);
+            const int ps = ntj == 16 ? piece_tile<16>(P_STORE) : piece_tile<8>(P_STORE);
+            if (u == 0 && l >= 2) n[k][0] += 2;
+            if (u == 0) n[k][p0] += 2;
+            if (u + 1 < 8) n[k][ps] += 2;
+        }
+    }
+};
+constexpr StoreTab kStores{};
+template <bool TR>
+constexpr int stores_at(int k, int j) { return TR ? kStores.n[k][j] : 0; }
+template <bool TR, bool H>
+constexpr int tbh(int k) {
+    const int t = kStores.ntj[k] - pf_tiles<TR>() - 1;
+    if (!H) return t;
+    const int L = TR ? NERF_CHAIN_LAG_TR : NERF_CHAIN_LAG;
+    const int lag = kStores.ntj[k] == 16 ? L : L / 2;
+    return t - lag < 0 ? 0 : t - lag;
+}
+// the wait of half H before B_{k+1} (tile tbh(k) of step k) for step k + 1's DMAs, which it
+// issued at tiles tbh(j0), tbh(j0) + 1 of step j0 = k + 2 - NPAIR (the prologue when j0 < 0):
+// every vector-memory op issued after them -- stores of step j0 past that tile, all ops of the
+// steps in between, stores of step k up to its barrier tile (ops left out only make a wait
+// stricter: the epilogues' encoding / row-max loads are not counted)
+template <bool TR, bool H>
+constexpr int wait_h(int k) {
+    constexpr int P = npair<TR>();
+    const int j0 = k + 2 - P;
+    int n = 0;
+    if (j0 < 0) {
+        for (int m = k + 2; m <= P - 2; ++m) n += kStores.dma[m];
+    } else {
+        for (int j = tbh<TR, H>(j0) + 2; j < kStores.ntj[j0]; ++j) n += stores_at<TR>(j0, j);
+    }
+    for (int s = (j0 + 1 > 0 ? j0 + 1 : 0); s < k; ++s) {
+        for (int j = 0; j < kStores.ntj[s]; ++j) n += stores_at<TR>(s, j);
+        n += s + P - 1 < NK ? kStores.dma[s + P - 1] : 0;
+    }
+    for (int j = 0; j <= tbh<TR, H>(k); ++j) n += stores_at<TR>(k, j);
+    return n;
+}
+template <bool TR>
+constexpr bool wait_h_consistent() {
+    for (int k = 0; k + 1 < NK; ++k) {
+        if (tbh<TR, false>(k) != tb<TR>(k) || tbh<TR, true>(k) != tb_lag<TR>(k)) return false;
+        if (wait_h<TR, false>(k) != wait_n<TR>(k)) return false;
+        if (wait_h<TR, true>(k) > 63 || wait_h<TR, false>(k) > 63) return false;   // the vmcnt field
+    }
+    return true;
+}
+static_assert(wait_h_consistent<true>() && wait_h_consistent<false>(), "position-based waits");
 // training: the save work of layer l's k-step u (the previous layer's output, P = p.L[l - 1]),
 // piece j of ntj
 template <int l, int u, int j, int ntj>
@@ -1354,22 +1429,24 @@ __device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, co
         constexpr int TL = tb_lag<TR>(k);
         // the wait, B_{k+1} and the first DMA half; the second half a tile later (one branch on
         // the wave-uniform half where the two halves' tiles differ)
-        auto sync = [&]() {
+        auto sync = [&](auto hc) {
             tick(p, st, nullptr);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_n<TR>(k)) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_h<TR, decltype(hc)::value>(k)) : "memory");
             tick(p, st, &st.t_wait);
             __syncthreads();
             tick(p, st, &st.t_bar);
             dma<tt_of_k(k + npair<TR>() - 1), TR>(p, st);
         };
         auto dma2 = [&]() { dma<tt_of_k(k + npair<TR>() - 1) + 1, TR>(p, st); };
+        constexpr std::false_type lead{};
+        constexpr std::true_type lagh{};
         if constexpr (k + 1 < NK && TL == T) {
-            if constexpr (j == T) sync();
+            if constexpr (j == T) sync(lead);
             if constexpr (j == T + 1) dma2();
         } else if constexpr (k + 1 < NK) {
-            if constexpr (j == TL) { if (st.lag) sync(); }
+            if constexpr (j == TL) { if (st.lag) sync(lagh); }
             if constexpr (j == TL + 1) { if (st.lag) dma2(); }
-            if constexpr (j == T) { if (!st.lag) sync(); }
+            if constexpr (j == T) { if (!st.lag) sync(lead); }
             if constexpr (j == T + 1) { if (!st.lag) dma2(); }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -1764,6 +1841,54 @@ constexpr int wait_prologue() {
 static_assert(wait_n(0) == dma_step(2) + pre_st(0) && wait_prologue() == dma_step(1) + dma_step(2), "prologue waits");
 static_assert(wait_n(4) == post_st(2) + pre_st(3) + dma_in(3) + post_st(3) + pre_st(4), "waits");
 static_assert(f2::piece_tile<16>(f2::P_STORE) <= TB && f2::piece_tile<16>(f2::P0_STORE) <= TB, "stores before B");
+// waves 4-7 at barrier tile TB - LAG (f2::tb_lag), with position-based waits (f2::wait_h)
+#ifndef NERF_CHAIN_LAG_BWD
+#define NERF_CHAIN_LAG_BWD 0
+#endif
+constexpr int TBL = TB - NERF_CHAIN_LAG_BWD < 0 ? 0 : TB - NERF_CHAIN_LAG_BWD;
+// the DMA operands as provably wave-uniform values: behind the half's branches the compiler
+// otherwise loses their uniformity and the "s" constraints of dma16 fail to assemble
+__device__ __forceinline__ const char* bu(const char* a) { return TBL != TB ? f2::uni(a) : a; }
+__device__ __forceinline__ uint32_t bu(uint32_t a) { return TBL != TB ? __builtin_amdgcn_readfirstlane(a) : a; }
+struct StoreTab {   // [step][tile] stores before the tile's wait / DMA issue, [step] the epilogue's after it
+    unsigned char n[NK][16], post[NK];
+    int dma[NK];
+    constexpr StoreTab() : n{}, post{}, dma{} {
+        for (int k = 0; k < NK; ++k) {
+            const int i = layer_of_k(k), u = k - kfirst(i);
+            dma[k] = dma_step(k);
+            if (u == 0 && i >= 1) n[k][0] += 1;                                   // layer_start
+            if (u == 0) n[k][f2::piece_tile<16>(f2::P0_STORE)] += 2;
+            if (u + 1 < nks(i)) n[k][f2::piece_tile<16>(f2::P_STORE)] += 2;
+            post[k] = post_st(k);
+        }
+    }
+};
+constexpr StoreTab kStores{};
+template <bool H>
+constexpr int wait_h(int k) {
+    constexpr int T = H ? TBL : TB;
+    const int j0 = k + 2 - NPAIR;
+    int n = 0;
+    if (j0 < 0) {
+        for (int m = k + 2; m <= NPAIR - 2; ++m) n += kStores.dma[m];
+    } else {
+        for (int j = T + 2; j < 16; ++j) n += kStores.n[j0][j];
+        n += kStores.post[j0];
+    }
+    for (int s = (j0 + 1 > 0 ? j0 + 1 : 0); s < k; ++s) {
+        for (int j = 0; j < 16; ++j) n += kStores.n[s][j];
+        n += kStores.post[s] + (s + NPAIR - 1 < NK ? kStores.dma[s + NPAIR - 1] : 0);
+    }
+    for (int j = 0; j <= T; ++j) n += kStores.n[k][j];
+    return n;
+}
+constexpr bool wait_h_consistent() {
+    for (int k = 0; k + 1 < NK; ++k)
+        if (wait_h<false>(k) != wait_n(k) || wait_h<true>(k) > 63) return false;
+    return true;
+}
+static_assert(wait_h_consistent(), "position-based waits");
 
 constexpr int O_RING = 0;
 constexpr int O_LEB = NSLOT * SBYTES;            // [2][256 rows][16 B] weight-row exponent chunks
@@ -1792,14 +1917,14 @@ __device__ __forceinline__ void dma(const nerf_chain_bwd& p, State& st) {
             const int ph = (st.wave >> 2) + 2 * q;      // plane * 2 + k-half
             const int n0 = 64 * (st.wave & 3);          // first image row of the wave's piece
             const int chunk = (ph >> 1) * (2 * ks) + 2 * s + (ph & 1);
-            f2::dma16(img + (chunk * rows + n0) * 16, st.voff16, slot + ph * SHALF + n0 * 16);
+            f2::dma16(bu(img + (chunk * rows + n0) * 16), st.voff16, bu(slot + ph * SHALF + n0 * 16));
         }
         if constexpr (s == 0) {
             if (st.wave < 4 || i == 0) {
                 // the weight-row exponents (plane 2, chunk 0 of each image row); the colour
                 // layer (its input f has no ReLU) repeats them on waves 4-7: same bytes, same place
                 const int w = st.wave & 3;
-                f2::dma16(img + ((2 * (2 * ks)) * rows + 64 * w) * 16, st.voff16,
+                f2::dma16(bu(img + ((2 * (2 * ks)) * rows + 64 * w) * 16), st.voff16,
                           st.lds0 + O_LEB + (i & 1) * 4096 + 64 * w * 16);
             } else {
                 // the block's ReLU words of the layer input: wave 4 + w rows 32 w .. 32 w + 31
@@ -1807,7 +1932,7 @@ __device__ __forceinline__ void dma(const nerf_chain_bwd& p, State& st) {
                 const int w = st.wave - 4;
                 const int ld = p.ld_in_mask[i];
                 const int lane = f2::fresh(st.lane);
-                f2::dma16(reinterpret_cast<const char*>(p.in_mask[i] + (st.m0 + 32 * w) * ld),
+                f2::dma16(bu(reinterpret_cast<const char*>(p.in_mask[i] + (st.m0 + 32 * w) * ld)),
                           (uint32_t)(((lane >> 1) * ld + 4 * (lane & 1)) * 4),
                           st.lds0 + O_MASK + (i & 1) * 4096 + 32 * w * 32);
             }
@@ -1938,12 +2063,23 @@ __device__ __forceinline__ void tiles(const nerf_chain_bwd& p, State& st, const 
         if constexpr (u == 0 && j == 0) layer_start<i>(p, st);
         split_pieces<i, u, j>(st);
         save_pieces<i, u, j>(p, st);
-        if constexpr (k + 1 < NK && j == TB) {
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_n(k)) : "memory");
+        auto sync = [&](auto hc) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_h<decltype(hc)::value>(k)) : "memory");
             __syncthreads();   // B_{k+1}
             dma<tt_of_k(k + NPAIR - 1)>(p, st);
+        };
+        auto dma2 = [&]() { dma<tt_of_k(k + NPAIR - 1) + 1>(p, st); };
+        constexpr std::false_type lead{};
+        constexpr std::true_type lagh{};
+        if constexpr (k + 1 < NK && TBL == TB) {
+            if constexpr (j == TB) sync(lead);
+            if constexpr (j == TB + 1) dma2();
+        } else if constexpr (k + 1 < NK) {
+            if constexpr (j == TBL) { if (st.lag) sync(lagh); }
+            if constexpr (j == TBL + 1) { if (st.lag) dma2(); }
+            if constexpr (j == TB) { if (!st.lag) sync(lead); }
+            if constexpr (j == TB + 1) { if (!st.lag) dma2(); }
         }
-        if constexpr (k + 1 < NK && j == TB + 1) dma<tt_of_k(k + NPAIR - 1) + 1>(p, st);
         __builtin_amdgcn_sched_barrier(0);
         tiles<i, u, j + 1>(p, st, ah, al);
     }
@@ -2047,6 +2183,7 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_bwd(ChainBwdArgs args) {
     st.fx = reinterpret_cast<float*>(smem + O_FX);
     st.tid = threadIdx.x;
     st.wave = __builtin_amdgcn_readfirstlane(st.tid >> 6);
+    st.lag = st.wave >= 4;
     st.lane = st.tid & 63; st.n = st.lane & 15; st.g = st.lane >> 4;
     st.m0 = (size_t)blockIdx.x * CROWS;
     st.rl = 16 * st.wave + st.n;
