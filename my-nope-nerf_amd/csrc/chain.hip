@@ -755,6 +755,33 @@ constexpr int FX_WD = 0, FX_WC = 256;   // fc_density weight [256], fc_rgb weigh
 // MFMAs has three k-steps to complete before a wait counts it, see wait_n), the column
 // maxima of the block's 128-row group ([2 parities][256] uint, LDS atomic max) and its ReLU
 // words ([2 parities][128 rows][8] uint, LDS atomic or)
+// Column maxima in LDS: CMQ copies of the [2 parities][256] array.  CMQ = 1: the max over the
+// 16-lane row by four DPP steps, one LDS atomic per row; CMQ = 2 / 4: over 8 / 4 lanes by three /
+// two DPP steps, one atomic per 8 / 4 lanes into copy n >> 3 / n >> 2 -- copies CMS words apart, so
+// the leaders' atomics of one instruction hit distinct banks -- and the copies are combined when the
+// maxima leave LDS
+#ifndef NERF_CHAIN_CMQ
+#define NERF_CHAIN_CMQ 1
+#endif
+#ifndef NERF_CHAIN_CMQ_BWD
+#define NERF_CHAIN_CMQ_BWD NERF_CHAIN_CMQ
+#endif
+constexpr int CMS = 513;                                     // words per copy (both parities + 1)
+constexpr int cm_words(int q) { return q == 1 ? 512 : q * CMS; }
+// the max of word w (parity * 256 + feature) over the q copies
+template <int Q>
+__device__ __forceinline__ uint32_t cm_read(const uint32_t* cm, int w) {
+    uint32_t m = cm[w];
+#pragma unroll
+    for (int c = 1; c < Q; ++c) m = max(m, cm[c * CMS + w]);
+    return m;
+}
+template <int Q>
+__device__ __forceinline__ void cm_clear(uint32_t* cm, int w) {
+#pragma unroll
+    for (int c = 0; c < Q; ++c) cm[c * CMS + w] = 0u;
+}
+
 template <bool TR>
 struct LY {
     static constexpr int NSLOT = TR ? 8 : 6;
@@ -765,7 +792,7 @@ struct LY {
     static constexpr int O_BIAS = O_EXP + 2 * 256 * 4;        // [2][256] float
     static constexpr int O_ENC = O_BIAS + 2 * 256 * 4;        // eval: [128][64] float position encodings
     static constexpr int O_CMX = O_ENC;                       // training: [2][256] uint column maxima
-    static constexpr int O_MSK = O_CMX + 2 * 256 * 4;         // training: [2][128][8] uint ReLU words
+    static constexpr int O_MSK = O_CMX + cm_words(NERF_CHAIN_CMQ) * 4;   // training: [2][128][8] uint ReLU words
     static constexpr int O_RMX = O_ENC + 128 * 64 * 4;        // eval: [4][128] row maxima
     static constexpr int O_FX = TR ? O_MSK + 2 * 128 * 32 : O_RMX + 4 * 128 * 4;   // head weights, raw4, ...
     static constexpr int FX_FLOATS = TR ? FX_ENCD : FX_ENCD + (CROWS / 2) * ENCD_REC;
@@ -842,26 +869,6 @@ constexpr bool tb_ok() {
     return true;
 }
 static_assert(tb_ok(), "a step's barrier tile tb = ntj - PF - 1 must exist");
-// The second half of the block (waves 4-7, one per SIMD) places its wait, barrier and DMA issue
-// LAG tiles earlier in each step than the first half: s_barrier counts arrivals, not program
-// positions, so both halves still meet at every B_k, but from B_1 on waves 4-7 run LAG tiles of
-// work behind their SIMD partners -- a layer epilogue (VALU only) of one half meets the other
-// half's MFMAs instead of the partner's epilogue.  Legal for any lag that keeps tb_lag >= 0: a
-// wave passing B_{k+1} (at its tile tb or tb_lag of step k) is past step k - 1, whose slots the
-// DMAs behind B_{k+1} refill, and reads step k + 1's fragments only after it.  (Eval kernel:
-// its waits are vmcnt(0); the training kernels count stores per position, wait_n.)
-#ifndef NERF_CHAIN_LAG
-#define NERF_CHAIN_LAG 0
-#endif
-#ifndef NERF_CHAIN_LAG_TR
-#define NERF_CHAIN_LAG_TR 0
-#endif
-template <bool TR>
-constexpr int tb_lag(int k) {
-    const int L = TR ? NERF_CHAIN_LAG_TR : NERF_CHAIN_LAG;
-    const int lag = ntj_k(k) == 16 ? L : L / 2;
-    return tb<TR>(k) - lag < 0 ? 0 : tb<TR>(k) - lag;
-}
 // vector-memory ops of the DMAs of 32-k step m (two 16-k steps), and of those issued in step j
 constexpr int dma_step(int m) { return m >= NK ? 0 : dma_count(tt_of_k(m)) + dma_count(tt_of_k(m) + 1); }
 template <bool TR>
@@ -971,19 +978,12 @@ __device__ __forceinline__ uint32_t mlo(float x0, float x1, float s, uint32_t h)
 __device__ __forceinline__ void dma16(const void* g, uint32_t voff, uint32_t lds) {
     asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(g), "s"(lds) : "memory", "m0");
 }
-// a wave-uniform address the compiler cannot prove uniform (behind a branch on the wave's half)
-__device__ __forceinline__ const char* uni(const char* a) {
-    const uint64_t v = (uint64_t)(uintptr_t)a;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return reinterpret_cast<const char*>((uintptr_t)(((uint64_t)hi << 32) | lo));
-}
 
 struct State {
     char* lds;
     uint32_t lds0;                      // LDS address of the block's buffer (wave-uniform)
     float* fx;
     int tid, wave, lane, n, g;          // n = lane & 15 (the lane's sample in the wave), g = lane >> 4
-    bool lag;                           // waves 4-7 (wave-uniform): the half whose barrier tile is tb_lag
     size_t m0;
     int rl;                             // the lane's row in the block (16 wave + n)
     uint32_t voff16;                    // 16 lane: the lane's offset in a 16-byte-per-lane LDS-DMA
@@ -1128,6 +1128,7 @@ __device__ __forceinline__ void tile_store4(float* block_base, int voff, int imm
 // (profiles/r05/colmax_row_ab.txt).  The asm keeps the DPP hazard explicit (a DPP source
 // written by VALU needs two wait states: the s_nop; the later steps' sources are four
 // instructions old) and the maxima out of the leaders' branch
+template <int Q = 1>
 __device__ __forceinline__ void colmax4(const f32x4& x, uint32_t* cm, bool leader) {
     float a0, a1, a2, a3;
     asm volatile(
@@ -1142,7 +1143,15 @@ __device__ __forceinline__ void colmax4(const f32x4& x, uint32_t* cm, bool leade
         "v_max_f32_dpp %3, %3, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
         : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
         : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]));
-    {
+    if constexpr (Q == 2) {
+        asm volatile(
+            "v_max_f32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+            "v_max_f32_dpp %1, %1, %1 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+            "v_max_f32_dpp %2, %2, %2 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+            "v_max_f32_dpp %3, %3, %3 row_ror:4 row_mask:0xf bank_mask:0xf"
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
+    }
+    if constexpr (Q == 1) {
         // the max over all 16 lanes of the row (quads combined by row_ror 4, 8): one atomic per
         // row and feature, no address conflicts
         asm volatile(
@@ -1196,91 +1205,33 @@ __device__ __forceinline__ void relu_put(uint32_t* a, uint32_t w, const State&) 
 // k-step of ntj tiles: pair 0 rides on k-step 0's first tiles, pair u + 1 on k-step u's later
 // tiles, behind its split (which it shares the xs registers with)
 enum Piece { P_SPLIT_HI_A, P_SPLIT_HI_B, P_SPLIT_LO_A, P_SPLIT_LO_B, P_STORE, P_CMAX_A, P_CMAX_B, P_RELU,
-             P0_STORE, P0_CMAX_A, P0_CMAX_B, P0_RELU };
+             P0_STORE, P0_CMAX_A, P0_CMAX_B, P0_RELU, P_STORE_B, P0_STORE_B };
+#ifndef NERF_CHAIN_DMA2
+#define NERF_CHAIN_DMA2 1      // A/B: the second 16-k step's DMAs DMA2 tiles after the barrier tile
+#endif
+#ifndef NERF_CHAIN_STSPLIT
+#define NERF_CHAIN_STSPLIT 0   // A/B: the second store of a pair STSPLIT tiles after the first
+#endif
 // (a staggered table for waves 4-7, their pieces at the tiles waves 0-3 leave free, ran 4 %
 // slower: profiles/r05/chain_variants_ab.txt)
 template <int ntj>
 constexpr int piece_tile(int piece) {
     if constexpr (ntj == 16) {
-        constexpr int T[12] = {6, 7, 8, 9, 10, 11, 12, 13, 1, 2, 3, 4};
+        constexpr int T[14] = {6, 7, 8, 9, 10, 11, 12, 13, 1, 2, 3, 4, 10 + NERF_CHAIN_STSPLIT, 1 + NERF_CHAIN_STSPLIT};
         return T[piece];
     } else {
-        constexpr int T[12] = {3, 3, 4, 4, 5, 6, 7, 7, 0, 1, 2, 2};
+        constexpr int T[14] = {3, 3, 4, 4, 5, 6, 7, 7, 0, 1, 2, 2, 5, NERF_CHAIN_STSPLIT ? 1 : 0};
         return T[piece];
     }
 }
 // the pieces that store (vector memory) run no later than the tile of the step's barrier, tb =
-// ntj - PF - 1 (the first half's wait counts take every store of a step as issued before it):
-// PF 2 in the training forward (16- and 8-tile steps), 3 in the backward (16)
+// ntj - PF - 1 (the wait counts take every store of a step as issued before it): PF 2 in the
+// training forward (16- and 8-tile steps), 3 in the backward (16)
 static_assert(piece_tile<16>(P_STORE) <= 16 - 3 - 1 && piece_tile<16>(P0_STORE) <= 16 - 3 - 1 &&
-                  piece_tile<8>(P_STORE) <= 8 - 2 - 1 && piece_tile<8>(P0_STORE) <= 8 - 2 - 1,
+                  piece_tile<8>(P_STORE) <= 8 - 2 - 1 && piece_tile<8>(P0_STORE) <= 8 - 2 - 1 &&
+                  piece_tile<16>(P_STORE_B) <= 16 - 3 - 1 && piece_tile<16>(P0_STORE_B) <= 16 - 3 - 1 &&
+                  piece_tile<8>(P_STORE_B) <= 8 - 2 - 1 && piece_tile<8>(P0_STORE_B) <= 8 - 2 - 1,
               "stores before the barrier");
-
-// Position-based wait counts (either half, any barrier tile): the vector-memory ops of the
-// training forward at tile j of step k -- layer_start's two stores, the save pieces' pair
-// stores -- in program order before that tile's wait / DMA issue
-struct StoreTab {   // [step][tile] stores of the training forward, tiles and DMA ops per step (tabulated)
-    unsigned char n[NK][16];
-    int ntj[NK], dma[NK];
-    constexpr StoreTab() : n{}, ntj{}, dma{} {
-        for (int k = 0; k < NK; ++k) {
-            ntj[k] = ntj_k(k);
-            dma[k] = dma_step(k);
-        }
-        for (int k = 0; k < NK; ++k) {
-            const int l = layer_of_k(k), u = k - kfirst(l), ntj = ntj_k(k);
-            if (l == 0) continue;
-            const int p0 = ntj == 16 ? piece_tile<16>(P0_STORE) : piece_tile<8>(P0_STORE);
-            const int ps = ntj == 16 ? piece_tile<16>(P_STORE) : piece_tile<8>(P_STORE);
-            if (u == 0 && l >= 2) n[k][0] += 2;
-            if (u == 0) n[k][p0] += 2;
-            if (u + 1 < 8) n[k][ps] += 2;
-        }
-    }
-};
-constexpr StoreTab kStores{};
-template <bool TR>
-constexpr int stores_at(int k, int j) { return TR ? kStores.n[k][j] : 0; }
-template <bool TR, bool H>
-constexpr int tbh(int k) {
-    const int t = kStores.ntj[k] - pf_tiles<TR>() - 1;
-    if (!H) return t;
-    const int L = TR ? NERF_CHAIN_LAG_TR : NERF_CHAIN_LAG;
-    const int lag = kStores.ntj[k] == 16 ? L : L / 2;
-    return t - lag < 0 ? 0 : t - lag;
-}
-// the wait of half H before B_{k+1} (tile tbh(k) of step k) for step k + 1's DMAs, which it
-// issued at tiles tbh(j0), tbh(j0) + 1 of step j0 = k + 2 - NPAIR (the prologue when j0 < 0):
-// every vector-memory op issued after them -- stores of step j0 past that tile, all ops of the
-// steps in between, stores of step k up to its barrier tile (ops left out only make a wait
-// stricter: the epilogues' encoding / row-max loads are not counted)
-template <bool TR, bool H>
-constexpr int wait_h(int k) {
-    constexpr int P = npair<TR>();
-    const int j0 = k + 2 - P;
-    int n = 0;
-    if (j0 < 0) {
-        for (int m = k + 2; m <= P - 2; ++m) n += kStores.dma[m];
-    } else {
-        for (int j = tbh<TR, H>(j0) + 2; j < kStores.ntj[j0]; ++j) n += stores_at<TR>(j0, j);
-    }
-    for (int s = (j0 + 1 > 0 ? j0 + 1 : 0); s < k; ++s) {
-        for (int j = 0; j < kStores.ntj[s]; ++j) n += stores_at<TR>(s, j);
-        n += s + P - 1 < NK ? kStores.dma[s + P - 1] : 0;
-    }
-    for (int j = 0; j <= tbh<TR, H>(k); ++j) n += stores_at<TR>(k, j);
-    return n;
-}
-template <bool TR>
-constexpr bool wait_h_consistent() {
-    for (int k = 0; k + 1 < NK; ++k) {
-        if (tbh<TR, false>(k) != tb<TR>(k) || tbh<TR, true>(k) != tb_lag<TR>(k)) return false;
-        if (wait_h<TR, false>(k) != wait_n<TR>(k)) return false;
-        if (wait_h<TR, true>(k) > 63 || wait_h<TR, false>(k) > 63) return false;   // the vmcnt field
-    }
-    return true;
-}
-static_assert(wait_h_consistent<true>() && wait_h_consistent<false>(), "position-based waits");
 // training: the save work of layer l's k-step u (the previous layer's output, P = p.L[l - 1]),
 // piece j of ntj
 template <int l, int u, int j, int ntj>
@@ -1293,8 +1244,9 @@ __device__ __forceinline__ void save_pieces(const ChainFwdArgs& p, State& st) {
         // a per-piece opaque copy of the lane's LDS offsets (the compiler would otherwise keep
         // every piece's address live across the chain)
         // (the LDS offsets of the arrays are beyond a ds_* immediate: they ride in the base)
+        constexpr int Q = NERF_CHAIN_CMQ;
         auto cm_at = [&](int t, int half) {
-            int o = Y::O_CMX + 16 * st.g;
+            int o = Y::O_CMX + 16 * st.g + (Q == 1 ? 0 : 4 * CMS * (st.n >> (Q == 2 ? 3 : 2)));
             asm volatile("" : "+v"(o));
             return reinterpret_cast<uint32_t*>(st.lds + o) + par * 256 + 32 * t + 16 * half;
         };
@@ -1303,26 +1255,23 @@ __device__ __forceinline__ void save_pieces(const ChainFwdArgs& p, State& st) {
             asm volatile("" : "+v"(o));
             return reinterpret_cast<uint32_t*>(st.lds + o) + par * 1024 + t;
         };
-        const bool leader = st.n == 0;
+        const bool leader = (st.n & (16 / Q - 1)) == 0;
         float* ob = P.out + st.m0 * 256;
         constexpr bool CM = true, RW = relu, SV = true;
         if constexpr (u == 0) {
-            if constexpr (SV && j == piece_tile<ntj>(P0_STORE)) {
-                tile_store4<256>(ob, st.vrow, 0, st.xs[0]);
-                tile_store4<256>(ob, st.vrow, 64, st.xs[1]);
-            }
-            if constexpr (CM && j == piece_tile<ntj>(P0_CMAX_A)) colmax4(st.xs[0], cm_at(0, 0), leader);
-            if constexpr (CM && j == piece_tile<ntj>(P0_CMAX_B)) colmax4(st.xs[1], cm_at(0, 1), leader);
+            if constexpr (SV && j == piece_tile<ntj>(P0_STORE)) tile_store4<256>(ob, st.vrow, 0, st.xs[0]);
+            if constexpr (SV && j == piece_tile<ntj>(P0_STORE_B)) tile_store4<256>(ob, st.vrow, 64, st.xs[1]);
+            if constexpr (CM && j == piece_tile<ntj>(P0_CMAX_A)) colmax4<Q>(st.xs[0], cm_at(0, 0), leader);
+            if constexpr (CM && j == piece_tile<ntj>(P0_CMAX_B)) colmax4<Q>(st.xs[1], cm_at(0, 1), leader);
             if constexpr (RW && j == piece_tile<ntj>(P0_RELU)) relu_put(msk_at(0), relu_word(st.act_hi[0], st), st);
         }
         if constexpr (u + 1 < 8) {
             constexpr int t = u + 1;
-            if constexpr (SV && j == piece_tile<ntj>(P_STORE)) {
-                tile_store4<256>(ob, st.vrow, 128 * t, st.xs[2 * t]);
+            if constexpr (SV && j == piece_tile<ntj>(P_STORE)) tile_store4<256>(ob, st.vrow, 128 * t, st.xs[2 * t]);
+            if constexpr (SV && j == piece_tile<ntj>(P_STORE_B))
                 tile_store4<256>(ob, st.vrow, 128 * t + 64, st.xs[2 * t + 1]);
-            }
-            if constexpr (CM && j == piece_tile<ntj>(P_CMAX_A)) colmax4(st.xs[2 * t], cm_at(t, 0), leader);
-            if constexpr (CM && j == piece_tile<ntj>(P_CMAX_B)) colmax4(st.xs[2 * t + 1], cm_at(t, 1), leader);
+            if constexpr (CM && j == piece_tile<ntj>(P_CMAX_A)) colmax4<Q>(st.xs[2 * t], cm_at(t, 0), leader);
+            if constexpr (CM && j == piece_tile<ntj>(P_CMAX_B)) colmax4<Q>(st.xs[2 * t + 1], cm_at(t, 1), leader);
             if constexpr (RW && j == piece_tile<ntj>(P_RELU)) relu_put(msk_at(t), relu_word(st.act_hi[t], st), st);
         }
     }
@@ -1396,9 +1345,11 @@ __device__ __forceinline__ void layer_start(const ChainFwdArgs& p, State& st) {
     if constexpr (TR && l >= 2) {
         const int lane = tid & 63;
         if (lane < 32) {
-            uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + Y::O_CMX) + (l & 1) * 256 + 32 * st.wave + lane;
-            p.L[l - 2].cmax[(st.m0 / CROWS) * L_OUT[l - 2] + 32 * st.wave + lane] = __uint_as_float(*cm);
-            *cm = 0u;
+            uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + Y::O_CMX);
+            const int cw = (l & 1) * 256 + 32 * st.wave + lane;
+            p.L[l - 2].cmax[(st.m0 / CROWS) * L_OUT[l - 2] + 32 * st.wave + lane] =
+                __uint_as_float(cm_read<NERF_CHAIN_CMQ>(cm, cw));
+            cm_clear<NERF_CHAIN_CMQ>(cm, cw);
         }
         const int rl = 16 * st.wave + (lane & 15), g = lane >> 4;
         uint2* mw = reinterpret_cast<uint2*>(st.lds + Y::O_MSK + (l & 1) * 4096 + 32 * rl + 8 * g);
@@ -1426,29 +1377,15 @@ __device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, co
         if constexpr (u == 0 && j == 0) layer_start<l, TR>(p, st);
         split_pieces<l, u, j, ntj>(st);
         if constexpr (TR) save_pieces<l, u, j, ntj>(p, st);
-        constexpr int TL = tb_lag<TR>(k);
-        // the wait, B_{k+1} and the first DMA half; the second half a tile later (one branch on
-        // the wave-uniform half where the two halves' tiles differ)
-        auto sync = [&](auto hc) {
+        if constexpr (k + 1 < NK && j == T) {
             tick(p, st, nullptr);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_h<TR, decltype(hc)::value>(k)) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_n<TR>(k)) : "memory");
             tick(p, st, &st.t_wait);
             __syncthreads();
             tick(p, st, &st.t_bar);
             dma<tt_of_k(k + npair<TR>() - 1), TR>(p, st);
-        };
-        auto dma2 = [&]() { dma<tt_of_k(k + npair<TR>() - 1) + 1, TR>(p, st); };
-        constexpr std::false_type lead{};
-        constexpr std::true_type lagh{};
-        if constexpr (k + 1 < NK && TL == T) {
-            if constexpr (j == T) sync(lead);
-            if constexpr (j == T + 1) dma2();
-        } else if constexpr (k + 1 < NK) {
-            if constexpr (j == TL) { if (st.lag) sync(lagh); }
-            if constexpr (j == TL + 1) { if (st.lag) dma2(); }
-            if constexpr (j == T) { if (!st.lag) sync(lead); }
-            if constexpr (j == T + 1) { if (!st.lag) dma2(); }
         }
+        if constexpr (k + 1 < NK && j == T + NERF_CHAIN_DMA2) dma<tt_of_k(k + npair<TR>() - 1) + 1, TR>(p, st);
         __builtin_amdgcn_sched_barrier(0);
         mstep_tiles<l, u, TR, j + 1, ntj>(p, st, ah, al);
     }
@@ -1654,7 +1591,6 @@ __device__ __forceinline__ void init_state(State& st, char* smem) {
     st.fx = reinterpret_cast<float*>(smem + LY<TR>::O_FX);
     st.tid = threadIdx.x;
     st.wave = __builtin_amdgcn_readfirstlane(st.tid >> 6);
-    st.lag = st.wave >= 4;
     st.lane = st.tid & 63; st.n = st.lane & 15; st.g = st.lane >> 4;
     st.m0 = (size_t)blockIdx.x * CROWS;
     st.rl = 16 * st.wave + st.n;
@@ -1739,7 +1675,7 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_train2(ChainFwdArgs p) {
     if (st.tid < 256) st.fx[FX_WD + st.tid] = p.wd[st.tid];
     for (int e = st.tid; e < 384; e += NTH) st.fx[FX_WC + e] = p.wc[e];
     // both column-max parities (512 words) and both ReLU-word parities (2048 words) cleared
-    reinterpret_cast<uint32_t*>(smem + Y::O_CMX)[st.tid] = 0u;
+    for (int e = st.tid; e < cm_words(NERF_CHAIN_CMQ); e += NTH) reinterpret_cast<uint32_t*>(smem + Y::O_CMX)[e] = 0u;
     reinterpret_cast<uint4*>(smem + Y::O_MSK)[st.tid] = make_uint4(0u, 0u, 0u, 0u);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     dma_n<0, 2 * (npair<true>() - 1), true>(p, st);   // steps 0 .. NPAIR - 2
@@ -1757,7 +1693,7 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_train2(ChainFwdArgs p) {
         *reinterpret_cast<float4*>(p.raw4 + (m0 + tid) * 4) = *reinterpret_cast<const float4*>(st.fx + FX_RAW + 4 * tid);
     else if (tid < CROWS + 256)
         p.L[8].cmax[(m0 / CROWS) * L_OUT[8] + tid - CROWS] =
-            __uint_as_float(reinterpret_cast<const uint32_t*>(smem + Y::O_CMX)[(8 & 1) * 256 + tid - CROWS]);
+            __uint_as_float(cm_read<NERF_CHAIN_CMQ>(reinterpret_cast<const uint32_t*>(smem + Y::O_CMX), (8 & 1) * 256 + tid - CROWS));
 }
 
 // ---------------------------------------------------------------------------
@@ -1840,62 +1776,17 @@ constexpr int wait_prologue() {
 }
 static_assert(wait_n(0) == dma_step(2) + pre_st(0) && wait_prologue() == dma_step(1) + dma_step(2), "prologue waits");
 static_assert(wait_n(4) == post_st(2) + pre_st(3) + dma_in(3) + post_st(3) + pre_st(4), "waits");
-static_assert(f2::piece_tile<16>(f2::P_STORE) <= TB && f2::piece_tile<16>(f2::P0_STORE) <= TB, "stores before B");
-// waves 4-7 at barrier tile TB - LAG (f2::tb_lag), with position-based waits (f2::wait_h)
-#ifndef NERF_CHAIN_LAG_BWD
-#define NERF_CHAIN_LAG_BWD 0
-#endif
-constexpr int TBL = TB - NERF_CHAIN_LAG_BWD < 0 ? 0 : TB - NERF_CHAIN_LAG_BWD;
-// the DMA operands as provably wave-uniform values: behind the half's branches the compiler
-// otherwise loses their uniformity and the "s" constraints of dma16 fail to assemble
-__device__ __forceinline__ const char* bu(const char* a) { return TBL != TB ? f2::uni(a) : a; }
-__device__ __forceinline__ uint32_t bu(uint32_t a) { return TBL != TB ? __builtin_amdgcn_readfirstlane(a) : a; }
-struct StoreTab {   // [step][tile] stores before the tile's wait / DMA issue, [step] the epilogue's after it
-    unsigned char n[NK][16], post[NK];
-    int dma[NK];
-    constexpr StoreTab() : n{}, post{}, dma{} {
-        for (int k = 0; k < NK; ++k) {
-            const int i = layer_of_k(k), u = k - kfirst(i);
-            dma[k] = dma_step(k);
-            if (u == 0 && i >= 1) n[k][0] += 1;                                   // layer_start
-            if (u == 0) n[k][f2::piece_tile<16>(f2::P0_STORE)] += 2;
-            if (u + 1 < nks(i)) n[k][f2::piece_tile<16>(f2::P_STORE)] += 2;
-            post[k] = post_st(k);
-        }
-    }
-};
-constexpr StoreTab kStores{};
-template <bool H>
-constexpr int wait_h(int k) {
-    constexpr int T = H ? TBL : TB;
-    const int j0 = k + 2 - NPAIR;
-    int n = 0;
-    if (j0 < 0) {
-        for (int m = k + 2; m <= NPAIR - 2; ++m) n += kStores.dma[m];
-    } else {
-        for (int j = T + 2; j < 16; ++j) n += kStores.n[j0][j];
-        n += kStores.post[j0];
-    }
-    for (int s = (j0 + 1 > 0 ? j0 + 1 : 0); s < k; ++s) {
-        for (int j = 0; j < 16; ++j) n += kStores.n[s][j];
-        n += kStores.post[s] + (s + NPAIR - 1 < NK ? kStores.dma[s + NPAIR - 1] : 0);
-    }
-    for (int j = 0; j <= T; ++j) n += kStores.n[k][j];
-    return n;
-}
-constexpr bool wait_h_consistent() {
-    for (int k = 0; k + 1 < NK; ++k)
-        if (wait_h<false>(k) != wait_n(k) || wait_h<true>(k) > 63) return false;
-    return true;
-}
-static_assert(wait_h_consistent(), "position-based waits");
+static_assert(f2::piece_tile<16>(f2::P_STORE) <= TB && f2::piece_tile<16>(f2::P0_STORE) <= TB &&
+                  f2::piece_tile<16>(f2::P_STORE_B) <= TB && f2::piece_tile<16>(f2::P0_STORE_B) <= TB,
+              "stores before B");
 
 constexpr int O_RING = 0;
 constexpr int O_LEB = NSLOT * SBYTES;            // [2][256 rows][16 B] weight-row exponent chunks
 constexpr int O_EXP = O_LEB + 2 * 256 * 16;      // [2][256] float 2^-e of the weight rows
 constexpr int O_MASK = O_EXP + 2 * 256 * 4;      // [2][128 rows][8 words] ReLU words of the layer input
 constexpr int O_CMX = O_MASK + 2 * 128 * 32;     // [2][256] uint column maxima (LDS atomics)
-constexpr int O_FX = O_CMX + 2 * 256 * 4;        // fc_density [256], fc_rgb [3][128]
+constexpr int CMQ = NERF_CHAIN_CMQ_BWD;          // column-max copies (f2::cm_words)
+constexpr int O_FX = O_CMX + f2::cm_words(CMQ) * 4;   // fc_density [256], fc_rgb [3][128]
 constexpr int BYTES = O_FX + (256 + 384) * 4;
 static_assert(BYTES <= 160 * 1024, "LDS");
 
@@ -1917,14 +1808,14 @@ __device__ __forceinline__ void dma(const nerf_chain_bwd& p, State& st) {
             const int ph = (st.wave >> 2) + 2 * q;      // plane * 2 + k-half
             const int n0 = 64 * (st.wave & 3);          // first image row of the wave's piece
             const int chunk = (ph >> 1) * (2 * ks) + 2 * s + (ph & 1);
-            f2::dma16(bu(img + (chunk * rows + n0) * 16), st.voff16, bu(slot + ph * SHALF + n0 * 16));
+            f2::dma16(img + (chunk * rows + n0) * 16, st.voff16, slot + ph * SHALF + n0 * 16);
         }
         if constexpr (s == 0) {
             if (st.wave < 4 || i == 0) {
                 // the weight-row exponents (plane 2, chunk 0 of each image row); the colour
                 // layer (its input f has no ReLU) repeats them on waves 4-7: same bytes, same place
                 const int w = st.wave & 3;
-                f2::dma16(bu(img + ((2 * (2 * ks)) * rows + 64 * w) * 16), st.voff16,
+                f2::dma16(img + ((2 * (2 * ks)) * rows + 64 * w) * 16, st.voff16,
                           st.lds0 + O_LEB + (i & 1) * 4096 + 64 * w * 16);
             } else {
                 // the block's ReLU words of the layer input: wave 4 + w rows 32 w .. 32 w + 31
@@ -1932,7 +1823,7 @@ __device__ __forceinline__ void dma(const nerf_chain_bwd& p, State& st) {
                 const int w = st.wave - 4;
                 const int ld = p.ld_in_mask[i];
                 const int lane = f2::fresh(st.lane);
-                f2::dma16(bu(reinterpret_cast<const char*>(p.in_mask[i] + (st.m0 + 32 * w) * ld)),
+                f2::dma16(reinterpret_cast<const char*>(p.in_mask[i] + (st.m0 + 32 * w) * ld),
                           (uint32_t)(((lane >> 1) * ld + 4 * (lane & 1)) * 4),
                           st.lds0 + O_MASK + (i & 1) * 4096 + 32 * w * 32);
             }
@@ -1955,30 +1846,26 @@ __device__ __forceinline__ void save_pieces(const nerf_chain_bwd& p, State& st) 
     constexpr int W = i == 0 ? 128 : 256;   // D_0 = dyr is 128 wide
     constexpr int npair = W / 32;
     auto cm_at = [&](int t, int half) {
-        int o = O_CMX + 16 * st.g;
+        int o = O_CMX + 16 * st.g + (CMQ == 1 ? 0 : 4 * f2::CMS * (st.n >> (CMQ == 2 ? 3 : 2)));
         asm volatile("" : "+v"(o));
         return reinterpret_cast<uint32_t*>(st.lds + o) + (i & 1) * 256 + 32 * t + 16 * half;
     };
-    const bool leader = st.n == 0;
+    const bool leader = (st.n & (16 / CMQ - 1)) == 0;
     float* ob = p.dy[i] + st.m0 * W;
     int vrow = st.vrow;
     if constexpr (W != 256) vrow = (st.rl * W + 4 * st.g) * 4;
     if constexpr (u == 0) {
-        if constexpr (j == piece_tile<16>(f2::P0_STORE)) {
-            f2::tile_store4<W>(ob, vrow, 0, st.xs[0]);
-            f2::tile_store4<W>(ob, vrow, 64, st.xs[1]);
-        }
-        if constexpr (j == piece_tile<16>(f2::P0_CMAX_A)) f2::colmax4(st.xs[0], cm_at(0, 0), leader);
-        if constexpr (j == piece_tile<16>(f2::P0_CMAX_B)) f2::colmax4(st.xs[1], cm_at(0, 1), leader);
+        if constexpr (j == piece_tile<16>(f2::P0_STORE)) f2::tile_store4<W>(ob, vrow, 0, st.xs[0]);
+        if constexpr (j == piece_tile<16>(f2::P0_STORE_B)) f2::tile_store4<W>(ob, vrow, 64, st.xs[1]);
+        if constexpr (j == piece_tile<16>(f2::P0_CMAX_A)) f2::colmax4<CMQ>(st.xs[0], cm_at(0, 0), leader);
+        if constexpr (j == piece_tile<16>(f2::P0_CMAX_B)) f2::colmax4<CMQ>(st.xs[1], cm_at(0, 1), leader);
     }
     if constexpr (u + 1 < npair) {
         constexpr int t = u + 1;
-        if constexpr (j == piece_tile<16>(f2::P_STORE)) {
-            f2::tile_store4<W>(ob, vrow, 128 * t, st.xs[2 * t]);
-            f2::tile_store4<W>(ob, vrow, 128 * t + 64, st.xs[2 * t + 1]);
-        }
-        if constexpr (j == piece_tile<16>(f2::P_CMAX_A)) f2::colmax4(st.xs[2 * t], cm_at(t, 0), leader);
-        if constexpr (j == piece_tile<16>(f2::P_CMAX_B)) f2::colmax4(st.xs[2 * t + 1], cm_at(t, 1), leader);
+        if constexpr (j == piece_tile<16>(f2::P_STORE)) f2::tile_store4<W>(ob, vrow, 128 * t, st.xs[2 * t]);
+        if constexpr (j == piece_tile<16>(f2::P_STORE_B)) f2::tile_store4<W>(ob, vrow, 128 * t + 64, st.xs[2 * t + 1]);
+        if constexpr (j == piece_tile<16>(f2::P_CMAX_A)) f2::colmax4<CMQ>(st.xs[2 * t], cm_at(t, 0), leader);
+        if constexpr (j == piece_tile<16>(f2::P_CMAX_B)) f2::colmax4<CMQ>(st.xs[2 * t + 1], cm_at(t, 1), leader);
     }
 }
 
@@ -2041,11 +1928,12 @@ __device__ __forceinline__ void layer_start(const nerf_chain_bwd& p, State& st) 
         constexpr int W = i - 1 == 0 ? 128 : 256;
         const int lane = tid & 63;
         if (lane < 32) {
-            uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + O_CMX) + ((i - 1) & 1) * 256 + 32 * st.wave + lane;
+            uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + O_CMX);
+            const int cw = ((i - 1) & 1) * 256 + 32 * st.wave + lane;
             float* dst = 32 * st.wave < W ? p.dy_cmax[i - 1] + (st.m0 / CROWS) * W + 32 * st.wave + lane
                                           : p.scratch + 64 * st.wave + lane;
-            *dst = __uint_as_float(*cm);
-            *cm = 0u;
+            *dst = __uint_as_float(f2::cm_read<CMQ>(cm, cw));
+            f2::cm_clear<CMQ>(cm, cw);
         }
     }
 }
@@ -2063,23 +1951,12 @@ __device__ __forceinline__ void tiles(const nerf_chain_bwd& p, State& st, const 
         if constexpr (u == 0 && j == 0) layer_start<i>(p, st);
         split_pieces<i, u, j>(st);
         save_pieces<i, u, j>(p, st);
-        auto sync = [&](auto hc) {
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_h<decltype(hc)::value>(k)) : "memory");
+        if constexpr (k + 1 < NK && j == TB) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_n(k)) : "memory");
             __syncthreads();   // B_{k+1}
             dma<tt_of_k(k + NPAIR - 1)>(p, st);
-        };
-        auto dma2 = [&]() { dma<tt_of_k(k + NPAIR - 1) + 1>(p, st); };
-        constexpr std::false_type lead{};
-        constexpr std::true_type lagh{};
-        if constexpr (k + 1 < NK && TBL == TB) {
-            if constexpr (j == TB) sync(lead);
-            if constexpr (j == TB + 1) dma2();
-        } else if constexpr (k + 1 < NK) {
-            if constexpr (j == TBL) { if (st.lag) sync(lagh); }
-            if constexpr (j == TBL + 1) { if (st.lag) dma2(); }
-            if constexpr (j == TB) { if (!st.lag) sync(lead); }
-            if constexpr (j == TB + 1) { if (!st.lag) dma2(); }
         }
+        if constexpr (k + 1 < NK && j == TB + NERF_CHAIN_DMA2) dma<tt_of_k(k + NPAIR - 1) + 1>(p, st);
         __builtin_amdgcn_sched_barrier(0);
         tiles<i, u, j + 1>(p, st, ah, al);
     }
@@ -2145,7 +2022,13 @@ __device__ __forceinline__ void layer(const nerf_chain_bwd& p, State& st) {
         rmx = fmaxf(rmx, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
         if constexpr (last) {
             f2::tile_store4<256>(p.dy[NL] + st.m0 * 256, st.vrow, 64 * j, x);
-            f2::colmax4(x, reinterpret_cast<uint32_t*>(st.lds + O_CMX) + (NL & 1) * 256 + f0, st.n == 0);
+            if constexpr (CMQ == 1)
+                f2::colmax4(x, reinterpret_cast<uint32_t*>(st.lds + O_CMX) + (NL & 1) * 256 + f0, st.n == 0);
+            else
+                f2::colmax4<CMQ>(x, reinterpret_cast<uint32_t*>(st.lds + O_CMX + 16 * st.g +
+                                                                 4 * f2::CMS * (st.n >> (CMQ == 2 ? 3 : 2))) +
+                                        (NL & 1) * 256 + 16 * j,
+                                 (st.n & (16 / CMQ - 1)) == 0);
         }
     }
     // the row's max over its four 16-lane rows (lanes n, n + 16, n + 32, n + 48)
@@ -2183,7 +2066,6 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_bwd(ChainBwdArgs args) {
     st.fx = reinterpret_cast<float*>(smem + O_FX);
     st.tid = threadIdx.x;
     st.wave = __builtin_amdgcn_readfirstlane(st.tid >> 6);
-    st.lag = st.wave >= 4;
     st.lane = st.tid & 63; st.n = st.lane & 15; st.g = st.lane >> 4;
     st.m0 = (size_t)blockIdx.x * CROWS;
     st.rl = 16 * st.wave + st.n;
@@ -2194,7 +2076,7 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_bwd(ChainBwdArgs args) {
     // head weights into LDS, both column-max parities cleared
     if (st.tid < 256) st.fx[st.tid] = p.wd[st.tid];
     for (int e = st.tid; e < 384; e += NTH) st.fx[256 + e] = p.wc[e];
-    reinterpret_cast<uint32_t*>(smem + O_CMX)[st.tid] = 0u;
+    for (int e = st.tid; e < f2::cm_words(CMQ); e += NTH) reinterpret_cast<uint32_t*>(smem + O_CMX)[e] = 0u;
     const size_t row = st.m0 + st.rl;
     const float4 gr = *reinterpret_cast<const float4*>(p.graw4 + row * 4);
     const uint4 mr = *reinterpret_cast<const uint4*>(p.hr_mask + row * p.ld_hr_mask);
@@ -2233,7 +2115,8 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_bwd(ChainBwdArgs args) {
     asm volatile("" : "+v"(tid));
     const size_t grp = (size_t)blockIdx.x;
     const int par = tid >> 8, f = tid & 255;
-    p.dy_cmax[NL - 1 + par][grp * 256 + f] = __uint_as_float(reinterpret_cast<const uint32_t*>(smem + O_CMX)[tid]);
+    p.dy_cmax[NL - 1 + par][grp * 256 + f] =
+        __uint_as_float(f2::cm_read<CMQ>(reinterpret_cast<const uint32_t*>(smem + O_CMX), tid));
 }
 }  // namespace nerf
 
