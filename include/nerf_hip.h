@@ -41,8 +41,10 @@ extern "C" {
  * 9 precision mode 2 as the default, 10 nerf_mlp_chain_train, 11 nerf_linear_bwd_weight_seg and
  * nerf_field_backward, 12 nerf_mlp_chain_bwd, nerf_field_bwd.bwd_chain, TN policy 8 and the
  * Adam hyper slot 6 (1 - beta2), 13 the chain images (nerf_pack_desc dst_cs / dst_cts, nerf_field_bwd
- * wt_cimg) and torch-exact Adam, 14 nerf_linear_bwd_weight_jobs and nerf_pair_backward's 12P gXY. */
-#define NERF_HIP_ABI_VERSION 14
+ * wt_cimg) and torch-exact Adam, 14 nerf_linear_bwd_weight_jobs and nerf_pair_backward's 12P gXY,
+ * 15 the chain images' compact exponent arrays (nerf_pack_desc dst_cs / dst_cts) and
+ * nerf_linear_bwd_weight_job_groups. */
+#define NERF_HIP_ABI_VERSION 15
 int nerf_hip_abi_version(void);
 const char* nerf_hip_last_error(void);
 
@@ -175,6 +177,13 @@ typedef struct nerf_wgrad_tile_job {
     const float* dy_cmax; const float* x_cmax;
 } nerf_wgrad_tile_job;
 int nerf_linear_bwd_weight_jobs(const nerf_wgrad_tile_job* jobs, int n, int m, int splits, void* stream);
+/* The same with the jobs in n_groups block groups (ABI 15): job i runs on group[i]'s own range of
+ * 2 S blocks (one launch of n_groups x 2 S blocks), so two job lists share the chip side by side
+ * at half the split count each -- half the split-K slab bytes for the same work.  The slabs are
+ * those of the per-job calls at each job's split count, bit for bit; group == NULL with
+ * n_groups == 1 is nerf_linear_bwd_weight_jobs. */
+int nerf_linear_bwd_weight_job_groups(const nerf_wgrad_tile_job* jobs, const int* group, int n, int m, int splits,
+                                      int n_groups, void* stream);
 
 /* ---------------------------------------------------------------------------
  * The training backward of the field in one host call (ABI 11): FieldRunner.backward's
@@ -442,7 +451,9 @@ int nerf_encode_bwd(const float* pts_o, const float* pts_d, const float* view, c
  * chain order: within each 32 columns, image column 8 g + i holds column 4 g + i (i < 4) or
  * 16 + 4 g + i - 4 (i >= 4) of the 32 (common.hpp chain_perm), the order in which the
  * 16x16x32 MFMA accumulators of the two-wave chains hold a layer's outputs.  perm_k % 32 == 0,
- * ld_t % 32 == 0 when dst_cts is given. */
+ * ld_t % 32 == 0 when dst_cts is given.  Since ABI 15 the chain images also hold every row's
+ * exponent in a compact int32 array at plane 2's chunk 1 (u16 index ((2*K/8 + 1)*rows + 2 r)),
+ * which the chain kernels load with one 1 KB LDS-DMA per layer. */
 #define NERF_MAX_PACK 24
 typedef struct {
     const float* src;

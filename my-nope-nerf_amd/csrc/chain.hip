@@ -333,6 +333,57 @@ __device__ __forceinline__ void fused_encode_d(const ChainFwdArgs& p, float* fx,
     for (int c = 27; c < 32; ++c) rec[c] = 0.f;
     rec[32] = m;
 }
+// the same records spread over threads t0 .. t0 + nt - 1 (nt a multiple of 64): sixteen lanes
+// (one DPP row) per ray, lane i < 12 one (level i / 3, coordinate i % 3) sin / cos pair, lane 12
+// the direction itself, the record's max by a row reduction -- the same values as
+// fused_encode_d, 12 sincosf deep on one thread there, one here
+// the direction of the ray whose record lane u of the range works on in pass rb (zero past the
+// rays): loaded before the prologue's LDS-DMAs for pass 0
+__device__ __forceinline__ void encd_load(const ChainFwdArgs& p, int u, int nt, size_t m0, int rb, float (&d)[3]) {
+    const int nr = CROWS / p.S;
+    const int r = rb + (u >> 4);
+    const size_t ray = m0 / (size_t)p.S + r;
+    const bool live = u >= 0 && u < nt && r < nr && ray < (size_t)p.R;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d[c] = live ? p.view[3 * ray + c] : 0.f;
+}
+__device__ __forceinline__ void fused_encode_d_rows(const ChainFwdArgs& p, float* fx, int tid, int t0, int nt,
+                                                    size_t m0, const float (&d0)[3]) {
+    const int nr = CROWS / p.S;
+    const int u = tid - t0;
+    if (u < 0 || u >= nt) return;
+    const int i = u & 15;
+    for (int rb = 0; rb < nr; rb += nt / 16) {   // block-uniform trip count: the row shuffles stay converged
+        const int r = rb + (u >> 4);
+        float dv[3] = {d0[0], d0[1], d0[2]};
+        if (rb > 0) encd_load(p, u, nt, m0, rb, dv);
+        float m = 0.f;
+        if (r < nr) {
+            float* rec = fx + FX_ENCD + ENCD_REC * r;
+            if (i < 12) {
+                const int lv = i / 3, c = i % 3;
+                const float d = c == 0 ? dv[0] : c == 1 ? dv[1] : dv[2];
+                float sn, cs;
+                sincosf((float)(1 << lv) * d, &sn, &cs);
+                rec[3 + 6 * lv + c] = sn;
+                rec[6 + 6 * lv + c] = cs;
+                m = fmaxf(fabsf(sn), fabsf(cs));
+            } else if (i == 12) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    rec[c] = dv[c];
+                    m = fmaxf(m, fabsf(dv[c]));
+                }
+            } else if (i == 13) {
+#pragma unroll
+                for (int c = 27; c < 32; ++c) rec[c] = 0.f;
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        if (r < nr && i == 0) fx[FX_ENCD + ENCD_REC * r + 32] = m;
+    }
+}
 // this lane's 4 encoding k-steps (8-feature chunks 16 s + 8 hf .. + 7; columns >= 32 zero)
 __device__ __forceinline__ void enc_d_frags(ChainState& st, const float* rec) {
     const float4* src = reinterpret_cast<const float4*>(rec);
@@ -764,7 +815,7 @@ constexpr int FX_WD = 0, FX_WC = 256;   // fc_density weight [256], fc_rgb weigh
 #define NERF_CHAIN_CMQ 1
 #endif
 #ifndef NERF_CHAIN_CMQ_BWD
-#define NERF_CHAIN_CMQ_BWD NERF_CHAIN_CMQ
+#define NERF_CHAIN_CMQ_BWD 4
 #endif
 constexpr int CMS = 513;                                     // words per copy (both parities + 1)
 constexpr int cm_words(int q) { return q == 1 ? 512 : q * CMS; }
@@ -782,19 +833,26 @@ __device__ __forceinline__ void cm_clear(uint32_t* cm, int w) {
     for (int c = 0; c < Q; ++c) cm[c * CMS + w] = 0u;
 }
 
+// words per row of the training forward's ReLU-word array: 8, or 9 (A/B) so that the rows' OR
+// atomics of one instruction (16 rows, stride 8 words: 4-way bank conflicts) hit distinct banks
+#ifndef NERF_CHAIN_MSKW
+#define NERF_CHAIN_MSKW 8
+#endif
+constexpr int MSKW = NERF_CHAIN_MSKW;
+
 template <bool TR>
 struct LY {
     static constexpr int NSLOT = TR ? 8 : 6;
     static constexpr int D = NSLOT / 2 - 1;                   // 32-k steps in flight
     static constexpr int O_RING = 0;
-    static constexpr int O_LEB = NSLOT * SBYTES;              // [2][256][16 B] weight-row exponent chunks
-    static constexpr int O_EXP = O_LEB + 2 * 256 * 16;        // [2][256] float: 2^-(weight-row exponent)
+    static constexpr int O_LEB = NSLOT * SBYTES;              // [2][256] int weight-row exponents (compact array)
+    static constexpr int O_EXP = O_LEB + 2 * 256 * 4;         // [2][256] float: 2^-(weight-row exponent)
     static constexpr int O_BIAS = O_EXP + 2 * 256 * 4;        // [2][256] float
     static constexpr int O_ENC = O_BIAS + 2 * 256 * 4;        // eval: [128][64] float position encodings
     static constexpr int O_CMX = O_ENC;                       // training: [2][256] uint column maxima
-    static constexpr int O_MSK = O_CMX + cm_words(NERF_CHAIN_CMQ) * 4;   // training: [2][128][8] uint ReLU words
+    static constexpr int O_MSK = O_CMX + cm_words(NERF_CHAIN_CMQ) * 4;   // training: [2][128][MSKW] uint ReLU words
     static constexpr int O_RMX = O_ENC + 128 * 64 * 4;        // eval: [4][128] row maxima
-    static constexpr int O_FX = TR ? O_MSK + 2 * 128 * 32 : O_RMX + 4 * 128 * 4;   // head weights, raw4, ...
+    static constexpr int O_FX = TR ? O_MSK + 2 * 128 * MSKW * 4 : O_RMX + 4 * 128 * 4;   // head weights, raw4, ...
     static constexpr int FX_FLOATS = TR ? FX_ENCD : FX_ENCD + (CROWS / 2) * ENCD_REC;
     static constexpr int BYTES = O_FX + FX_FLOATS * 4;
     static_assert(BYTES <= 160 * 1024, "LDS");
@@ -1055,9 +1113,10 @@ __device__ __forceinline__ void dma(const ChainFwdArgs& p, State& st) {
         }
         if constexpr (s == 0) {
             if (st.wave < 4) {
-                const int wr = NO == 256 ? st.wave : (st.wave & 1);
-                dma16(img + ((2 * (2 * ks)) * NO + 64 * wr) * 16, st.voff16,
-                      st.lds0 + Y::O_LEB + (l & 1) * 4096 + 64 * wr * 16);
+                // the layer's weight-row exponents: the compact int array of the chain image
+                // (plane 2, chunk 1), 1 KB, the same bytes from each of waves 0-3 (one vmcnt op
+                // per wave); 128-row layers take the first 512 B of it
+                dma16(img + ((2 * (2 * ks) + 1) * NO) * 16, st.voff16, st.lds0 + Y::O_LEB + (l & 1) * 1024);
             } else if (st.lane < 16) {                   // one instruction, lanes 0-15 active
                 const int wb = NO == 256 ? st.wave - 4 : ((st.wave - 4) & 1);
                 dma16(reinterpret_cast<const char*>(L.bias) + 64 * wb * 4, st.voff16,
@@ -1251,9 +1310,9 @@ __device__ __forceinline__ void save_pieces(const ChainFwdArgs& p, State& st) {
             return reinterpret_cast<uint32_t*>(st.lds + o) + par * 256 + 32 * t + 16 * half;
         };
         auto msk_at = [&](int t) {
-            int o = Y::O_MSK + 32 * st.rl;
+            int o = Y::O_MSK + 4 * MSKW * st.rl;
             asm volatile("" : "+v"(o));
-            return reinterpret_cast<uint32_t*>(st.lds + o) + par * 1024 + t;
+            return reinterpret_cast<uint32_t*>(st.lds + o) + par * 128 * MSKW + t;
         };
         const bool leader = (st.n & (16 / Q - 1)) == 0;
         float* ob = P.out + st.m0 * 256;
@@ -1341,7 +1400,7 @@ __device__ __forceinline__ void layer_start(const ChainFwdArgs& p, State& st) {
     const int tid = fresh(st.tid);
     if (tid < L_OUT[l])   // as the scale 2^-e of the weight row (exact)
         reinterpret_cast<float*>(st.lds + Y::O_EXP)[(l & 1) * 256 + tid] = __builtin_amdgcn_ldexpf(
-            1.f, -*reinterpret_cast<const int*>(st.lds + Y::O_LEB + (l & 1) * 4096 + tid * 16));
+            1.f, -reinterpret_cast<const int*>(st.lds + Y::O_LEB + (l & 1) * 1024)[tid]);
     if constexpr (TR && l >= 2) {
         const int lane = tid & 63;
         if (lane < 32) {
@@ -1352,10 +1411,17 @@ __device__ __forceinline__ void layer_start(const ChainFwdArgs& p, State& st) {
             cm_clear<NERF_CHAIN_CMQ>(cm, cw);
         }
         const int rl = 16 * st.wave + (lane & 15), g = lane >> 4;
-        uint2* mw = reinterpret_cast<uint2*>(st.lds + Y::O_MSK + (l & 1) * 4096 + 32 * rl + 8 * g);
         const nerf_chain_layer& Q = p.L[l - 2];
-        *reinterpret_cast<uint2*>(Q.mask + (st.m0 + rl) * Q.ldmask + 2 * g) = *mw;
-        *mw = make_uint2(0u, 0u);
+        if constexpr (MSKW == 8) {
+            uint2* mw = reinterpret_cast<uint2*>(st.lds + Y::O_MSK + (l & 1) * 4096 + 32 * rl + 8 * g);
+            *reinterpret_cast<uint2*>(Q.mask + (st.m0 + rl) * Q.ldmask + 2 * g) = *mw;
+            *mw = make_uint2(0u, 0u);
+        } else {
+            uint32_t* mw = reinterpret_cast<uint32_t*>(st.lds + Y::O_MSK) + (l & 1) * 128 * MSKW + MSKW * rl + 2 * g;
+            *reinterpret_cast<uint2*>(Q.mask + (st.m0 + rl) * Q.ldmask + 2 * g) = make_uint2(mw[0], mw[1]);
+            mw[0] = 0u;
+            mw[1] = 0u;
+        }
     }
 }
 
@@ -1543,28 +1609,31 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
 // prologue: samples (rendering.py:183-198, no jitter) and the position encoding
 // (official_nerf.py:61, 99-119) of the block's 128 rows into the LDS tile, four threads per
 // row (x and levels 0-2 | 3-5 | 6-7 | 8-9 and the zero pad), with a row max per part and z
-__device__ __forceinline__ void encode_p(const ChainFwdArgs& p, State& st) {
-    using Y = LY<false>;
-    const int row = st.tid & 127, part = st.tid >> 7;
+// the row's sample depth and point (its ray's origin / direction loaded from HBM)
+__device__ __forceinline__ void encode_p_load(const ChainFwdArgs& p, const State& st, float (&x)[3], float& z) {
+    const int row = st.tid & 127;
     const size_t g = st.m0 + row;
-    float* dst = reinterpret_cast<float*>(st.lds + Y::O_ENC) + row * 64;
-    float x[3] = {0.f, 0.f, 0.f}, z = 0.f;
-    const bool live = g < (size_t)p.R * p.S;
-    if (live) {
+    x[0] = x[1] = x[2] = 0.f;
+    z = 0.f;
+    if (g < (size_t)p.R * p.S) {
         const size_t ray = g / (size_t)p.S;
         const int i = (int)(g - ray * (size_t)p.S);
         z = lerp_z(linspace01(i, p.S), p.near_z, p.far_z);
 #pragma unroll
         for (int c = 0; c < 3; ++c) x[c] = ray_point(p.po[3 * ray + c], p.pd[3 * ray + c], z);
     }
+}
+__device__ __forceinline__ void encode_p(const ChainFwdArgs& p, State& st, const float (&x)[3], float z) {
+    using Y = LY<false>;
+    const int row = st.tid & 127, part = st.tid >> 7;
+    float* dst = reinterpret_cast<float*>(st.lds + Y::O_ENC) + row * 64;
     float m = 0.f;
     const int lv0 = part == 0 ? 0 : part == 1 ? 3 : part == 2 ? 6 : 8;
     const int lv1 = part == 0 ? 3 : part == 1 ? 6 : part == 2 ? 8 : 10;
     if (part == 0) {
 #pragma unroll
         for (int c = 0; c < 3; ++c) { dst[c] = x[c]; m = fmaxf(m, fabsf(x[c])); }
-        st.fx[FX_Z + row] = z;
-        if (live) p.z[g] = z;
+        st.fx[FX_Z + row] = z;   // (to HBM in the kernel's tail: a store here would sit in the prologue's vmcnt wait)
     }
     if (part == 3) dst[63] = 0.f;
     for (int lv = lv0; lv < lv1; ++lv) {
@@ -1627,12 +1696,22 @@ __global__ __launch_bounds__(512, 2) void k_render_fused2(ChainFwdArgs p) {
     __shared__ __attribute__((aligned(16))) char smem[Y::BYTES];
     State st;
     init_state<false>(st, smem);
+    // the prologue's HBM loads (head weights, the rows' rays, the view directions) BEFORE the
+    // LDS-DMAs: vmcnt retires in issue order, so a load behind the DMAs would wait for them and
+    // the encodings' sincos could not overlap the weights' flight
+    const float wdv = st.tid < 256 ? p.wd[st.tid] : 0.f;
+    const float wcv = st.tid < 384 ? p.wc[st.tid] : 0.f;
+    float x[3], z, dv[3];
+    encode_p_load(p, st, x, z);
+    encd_load(p, st.tid - 256, 256, st.m0, 0, dv);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (st.tid < 256) st.fx[FX_WD + st.tid] = wdv;
+    if (st.tid < 384) st.fx[FX_WC + st.tid] = wcv;
     dma_n<0, 2 * (npair<false>() - 1), false>(p, st);   // steps 0 .. NPAIR - 2
-    // head weights into LDS, then the samples and both encodings (beside the DMAs)
-    if (st.tid < 256) st.fx[FX_WD + st.tid] = p.wd[st.tid];
-    for (int e = st.tid; e < 384; e += NTH) st.fx[FX_WC + e] = p.wc[e];
-    encode_p(p, st);
-    fused_encode_d(p, st.fx, st.tid, st.m0);
+    // the samples and both encodings beside the DMAs; the view records on waves 4-7 (the encode_p
+    // parts with 6 sincos, not 9): no wave carries 12 sincos more than the others into B_0
+    encode_p(p, st, x, z);
+    fused_encode_d_rows(p, st.fx, st.tid, 256, 256, st.m0, dv);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_prologue<false>()) : "memory");
     __syncthreads();   // B_0 (and the encodings in LDS)
     {
@@ -1647,6 +1726,11 @@ __global__ __launch_bounds__(512, 2) void k_render_fused2(ChainFwdArgs p) {
     chain_layers<false>(p, st);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every DMA landed before the LDS is released
     __syncthreads();   // every row's raw4 in LDS
+    {
+        const int t = fresh(threadIdx.x);
+        const size_t g = (size_t)blockIdx.x * CROWS + t;
+        if (t < CROWS && g < (size_t)p.R * p.S) p.z[g] = st.fx[FX_Z + t];
+    }
     fused_composite<NTH>(p, st.fx, st.tid, st.m0);
     write_stamps(p, st);
 }
@@ -1676,7 +1760,10 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_train2(ChainFwdArgs p) {
     for (int e = st.tid; e < 384; e += NTH) st.fx[FX_WC + e] = p.wc[e];
     // both column-max parities (512 words) and both ReLU-word parities (2048 words) cleared
     for (int e = st.tid; e < cm_words(NERF_CHAIN_CMQ); e += NTH) reinterpret_cast<uint32_t*>(smem + Y::O_CMX)[e] = 0u;
-    reinterpret_cast<uint4*>(smem + Y::O_MSK)[st.tid] = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (MSKW == 8)
+        reinterpret_cast<uint4*>(smem + Y::O_MSK)[st.tid] = make_uint4(0u, 0u, 0u, 0u);
+    else
+        for (int e = st.tid; e < 2 * 128 * MSKW; e += NTH) reinterpret_cast<uint32_t*>(smem + Y::O_MSK)[e] = 0u;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     dma_n<0, 2 * (npair<true>() - 1), true>(p, st);   // steps 0 .. NPAIR - 2
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_prologue<true>()) : "memory");
@@ -1781,8 +1868,8 @@ static_assert(f2::piece_tile<16>(f2::P_STORE) <= TB && f2::piece_tile<16>(f2::P0
               "stores before B");
 
 constexpr int O_RING = 0;
-constexpr int O_LEB = NSLOT * SBYTES;            // [2][256 rows][16 B] weight-row exponent chunks
-constexpr int O_EXP = O_LEB + 2 * 256 * 16;      // [2][256] float 2^-e of the weight rows
+constexpr int O_LEB = NSLOT * SBYTES;            // [2][256] int weight-row exponents (compact array)
+constexpr int O_EXP = O_LEB + 2 * 256 * 4;       // [2][256] float 2^-e of the weight rows
 constexpr int O_MASK = O_EXP + 2 * 256 * 4;      // [2][128 rows][8 words] ReLU words of the layer input
 constexpr int O_CMX = O_MASK + 2 * 128 * 32;     // [2][256] uint column maxima (LDS atomics)
 constexpr int CMQ = NERF_CHAIN_CMQ_BWD;          // column-max copies (f2::cm_words)
@@ -1812,11 +1899,11 @@ __device__ __forceinline__ void dma(const nerf_chain_bwd& p, State& st) {
         }
         if constexpr (s == 0) {
             if (st.wave < 4 || i == 0) {
-                // the weight-row exponents (plane 2, chunk 0 of each image row); the colour
-                // layer (its input f has no ReLU) repeats them on waves 4-7: same bytes, same place
-                const int w = st.wave & 3;
-                f2::dma16(img + ((2 * (2 * ks)) * rows + 64 * w) * 16, st.voff16,
-                          st.lds0 + O_LEB + (i & 1) * 4096 + 64 * w * 16);
+                // the weight-row exponents of image rows 0..255 (the layer's input features the
+                // chain produces gradients for): the compact int array in plane 2, chunk 1, 1 KB,
+                // the same bytes from each of these waves (the colour layer -- its input f has no
+                // ReLU -- repeats them on waves 4-7)
+                f2::dma16(img + ((2 * (2 * ks) + 1) * rows) * 16, st.voff16, st.lds0 + O_LEB + (i & 1) * 1024);
             } else {
                 // the block's ReLU words of the layer input: wave 4 + w rows 32 w .. 32 w + 31
                 // (two lanes per row, 16 bytes each)
@@ -1923,7 +2010,7 @@ __device__ __forceinline__ void layer_start(const nerf_chain_bwd& p, State& st) 
     const int tid = f2::fresh(st.tid);
     if (tid < 256)
         reinterpret_cast<float*>(st.lds + O_EXP)[(i & 1) * 256 + tid] = __builtin_amdgcn_ldexpf(
-            1.f, -*reinterpret_cast<const int*>(st.lds + O_LEB + (i & 1) * 4096 + tid * 16));
+            1.f, -reinterpret_cast<const int*>(st.lds + O_LEB + (i & 1) * 1024)[tid]);
     if constexpr (i >= 1) {
         constexpr int W = i - 1 == 0 ? 128 : 256;
         const int lane = tid & 63;

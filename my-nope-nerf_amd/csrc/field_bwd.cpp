@@ -128,7 +128,7 @@ int weight_grad(const nerf_field_bwd& a, const Work& w, int l, const float* dy, 
 // reduce on the side stream behind an event, so a reduce runs beside the next layer's TN; the
 // ray gradients (pose learning) as three input-gradient GEMMs over the saved dy of the colour
 // layer, l4 and l0.  The head-weight partials were forked to the side stream before the chain.
-int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, void* stream, void* side_stream,
+int chain_schedule(const nerf_field_bwd& a, Work& w, const float* graw4, void* stream, void* side_stream,
                    bool heads_after, const nerf::SlabJobDesc* extra, int n_extra) {
     const int np = a.n_pad;
     hipStream_t main = nerf::as_stream(stream), side = nerf::as_stream(side_stream);
@@ -198,7 +198,8 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
                                         0, nullptr, nullptr, 0, out, 64, np, 64, rm, nullptr, nullptr, stream);
         };
         nerf_wgrad_tile_job tj[nerf::kWgradJobsMax];
-        int nt = 0;
+        int tgrp[nerf::kWgradJobsMax];
+        int nt = 0, cur_grp = 0;
         // layer l's main segment (x = its input; l0: enc_p) and, for l4 / the colour layer, the
         // 64-wide encoding segment at slab column K1[l]
         auto tiles = [&](int l) {
@@ -207,10 +208,13 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
             const int op = OUT_P[l];
             const float* x = l == 0 ? a.enc_p : a.act[l - 1];
             const float* xcm = l == 0 ? a.enc_p_cmax : a.cmax[l - 1];
+            tgrp[nt] = cur_grp;
             tj[nt++] = nerf_wgrad_tile_job{dy, op, op, x, K1[l], K1[l], w.splits[l], w.slab[l], KP[l], 0, w.bslab[l], cm, xcm};
-            if (SEG[l])
+            if (SEG[l]) {
+                tgrp[nt] = cur_grp;
                 tj[nt++] = nerf_wgrad_tile_job{dy, op, op, SEG[l] == 1 ? a.enc_p : a.enc_d, 64, 64, w.splits[l], w.slab[l],
                                                KP[l], K1[l], nullptr, cm, SEG[l] == 1 ? a.enc_p_cmax : a.enc_d_cmax};
+            }
             job(l);
         };
         auto launch = [&]() -> int {
@@ -227,8 +231,25 @@ int chain_schedule(const nerf_field_bwd& a, const Work& w, const float* graw4, v
         const char* b1 = std::getenv("NERF_WGRAD_BATCH1");
         RC(flush(b1 && std::atoi(b1) == 0 ? side : main));
         RC(enc_rows(LR));
-        for (int l : {3, 2, 1, 4, 0}) tiles(l);   // l4's h3 job the last 256 x 256 one: its enc_p job follows
-        RC(launch());
+        // NERF_WGRAD_GROUPS: 1 the second launch as two block groups of 2 S' blocks (S' = S / 2:
+        // half the split-K slab bytes, ~80 MB written and read back per step less), group 0
+        // l4's two segments + l3, group 1 l2 + l1 + l0 (2.25 layer-equivalents each); 0 one list
+        const char* wgg = std::getenv("NERF_WGRAD_GROUPS");
+        const bool grouped = (wgg ? std::atoi(wgg) : 0) != 0 && w.splits[LF] % 16 == 0;
+        if (grouped) {
+            const int s2 = w.splits[LF] / 2;
+            for (int l : {1, 2, 3, 4}) w.splits[l] = s2;   // the slab buffers are sized for S: room to spare
+            w.splits[0] = 2 * s2;
+            for (int l : {3, 4}) tiles(l);   // k_wgrad_jobs runs a group's pairs, then its narrow jobs: l4 h3, l4 enc_p last
+            cur_grp = 1;
+            for (int l : {2, 1, 0}) tiles(l);
+            cur_grp = 0;
+            RC(nerf_linear_bwd_weight_job_groups(tj, tgrp, nt, np, s2, 2, stream));
+            nt = 0;
+        } else {
+            for (int l : {3, 2, 1, 4, 0}) tiles(l);   // l4's h3 job the last 256 x 256 one: its enc_p job follows
+            RC(launch());
+        }
         RC(flush(main));
         RC(enc_rows(4));
         RC(enc_rows(0));

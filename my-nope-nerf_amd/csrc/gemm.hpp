@@ -658,7 +658,9 @@ enum WgradJobKind : int { WJ_PAIR = 0, WJ_WIDE = 1, WJ_ENC = 2, WJ_ENC_HALF = 3,
 struct TNJobs {
     TNArgs a[kWgradJobsMax];
     int kind[kWgradJobsMax];
+    int grp[kWgradJobsMax];   // the block group that runs job i (0 .. ngroups - 1)
     int n;
+    int ngroups;              // the launch is ngroups x 2 S blocks, each group walking its own jobs
 };
 void launch_wgrad_jobs(const TNJobs& m, int splits, hipStream_t s);
 void launch_wgrad_two(const TNArgs& a, int na, const TNArgs& b, int nb, hipStream_t s);

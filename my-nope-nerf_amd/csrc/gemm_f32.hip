@@ -603,13 +603,19 @@ extern "C" int nerf_linear_bwd_weight_multi(const nerf_wgrad_job* j, int n, int 
 
 // weight gradients of several shapes in one launch (k_wgrad_jobs): each job's shape and split
 // count against the launch's S (2 S blocks) pick its tile kind; anything else runs per job
-extern "C" int nerf_linear_bwd_weight_jobs(const nerf_wgrad_tile_job* j, int n, int m, int splits, void* stream) {
+extern "C" int nerf_linear_bwd_weight_job_groups(const nerf_wgrad_tile_job* j, const int* group, int n, int m,
+                                                 int splits, int n_groups, void* stream) {
     NERF_CHECK_PTR(j);
     hipStream_t s = as_stream(stream);
     NERF_CHECK(n >= 1 && n <= kWgradJobsMax, "%s: %d jobs (1..%d)", __func__, n, kWgradJobsMax);
+    NERF_CHECK(n_groups >= 1 && n_groups <= 4, "%s: n_groups %d (1..4)", __func__, n_groups);
+    for (int i = 0; i < n; ++i)
+        NERF_CHECK(group == nullptr ? n_groups == 1 : (group[i] >= 0 && group[i] < n_groups),
+                   "%s: job %d: group %d of %d", __func__, i, group ? group[i] : 0, n_groups);
     const int pol = g_tn_policy ? g_tn_policy : kTnDefault;
     bool fused = g_precision == 2 && pol == 8 && splits > 0 && splits % 8 == 0;
     TNJobs tj{};
+    tj.ngroups = n_groups;
     double bytes = 0.0, flops = 0.0;
     for (int i = 0; i < n && fused; ++i) {
         const nerf_wgrad_tile_job& q = j[i];
@@ -627,6 +633,7 @@ extern "C" int nerf_linear_bwd_weight_jobs(const nerf_wgrad_tile_job* j, int n, 
                          q.bslab, q.dy_cmax, q.x_cmax, tj.a[i]);
         if (rc) return rc;
         tj.kind[i] = kind;
+        tj.grp[i] = group ? group[i] : 0;
         // dy counted once per layer: a second segment over the same dy (col0 > 0) adds its x only
         bytes += 4.0 * m * (q.kin + (q.col0 == 0 ? q.nout : 0)) + 4.0 * q.nout * q.kin + (q.bslab ? 4.0 * q.nout : 0.0);
         flops += 2.0 * m * q.nout * q.kin;
@@ -646,6 +653,10 @@ extern "C" int nerf_linear_bwd_weight_jobs(const nerf_wgrad_tile_job* j, int n, 
     launch_wgrad_jobs(tj, splits, s);
     prof_end(s, flops, 3);
     return check_launch("k_wgrad_jobs");
+}
+
+extern "C" int nerf_linear_bwd_weight_jobs(const nerf_wgrad_tile_job* j, int n, int m, int splits, void* stream) {
+    return nerf_linear_bwd_weight_job_groups(j, nullptr, n, m, splits, 1, stream);
 }
 
 namespace nerf {

@@ -68,8 +68,11 @@ __device__ __forceinline__ void pack_f32(const PackBatch& pb, const nerf_pack_de
 // stays in registers between the max and the split (all its loads in flight at once: one
 // memory latency per row, not one per 64 elements and pass).
 constexpr int PACK_H_MAXK = 16 * kWave;
+// chain images (cexp = true) also get the row exponents as one compact int array in plane 2's
+// chunk 1 (unused otherwise): the chain kernels fetch a layer's 256 exponents with one 1 KB
+// LDS-DMA instead of one 16-byte chunk per row
 template <typename F>
-__device__ __forceinline__ void put_row_h(uint16_t* img, int N, int K, int r, F&& x) {
+__device__ __forceinline__ void put_row_h(uint16_t* img, int N, int K, int r, F&& x, bool cexp = false) {
     const int lane = lane_id();
     float v[PACK_H_MAXK / kWave];
     float m = 0.f;
@@ -95,6 +98,7 @@ __device__ __forceinline__ void put_row_h(uint16_t* img, int N, int K, int r, F&
         img[o + plane] = __builtin_bit_cast(uint16_t, l);
     }
     if (lane == 0) *reinterpret_cast<int*>(img + 2 * plane + (size_t)r * 8) = e;
+    if (cexp && lane == 0) reinterpret_cast<int*>(img + 2 * plane + (size_t)N * 8)[r] = e;
 }
 
 // fp16 pair images of the packed weights (GEMM precision mode 2): one wave per image row,
@@ -116,10 +120,11 @@ __device__ __forceinline__ void pack_h(const nerf_pack_desc& d, int bx, int nb) 
             put_row_h(d.dst_ts, d.rows_t, d.ld_t, c, [&](int r) { return w_at(r, c); });
         } else if (w < ns + nt + ncs) {
             const int r = w - ns - nt;
-            put_row_h(d.dst_cs, rows_s, d.ld_dst, r, [&](int c) { return w_at(r, c < d.perm_k ? chain_perm(c) : c); });
+            put_row_h(d.dst_cs, rows_s, d.ld_dst, r, [&](int c) { return w_at(r, c < d.perm_k ? chain_perm(c) : c); },
+                      true);
         } else {
             const int c = w - ns - nt - ncs;
-            put_row_h(d.dst_cts, d.rows_t, d.ld_t, c, [&](int r) { return w_at(chain_perm(r), c); });
+            put_row_h(d.dst_cts, d.rows_t, d.ld_t, c, [&](int r) { return w_at(chain_perm(r), c); }, true);
         }
     }
 }

@@ -345,12 +345,19 @@ __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_pairs(TNPairs m) {
 // on the set the previous job's epilogue still reads, and the barrier in a job's exponents()
 // orders the rest of it after that epilogue as in k_wgrad_pairs.
 // SH: the shapes compiled in (bit 0 128 x 256, bit 1 128 x 64, bit 2 256 x 64; 256 x 256 always):
-// with all four in one kernel the register allocation spills, with any three it does not
+// with all four in one kernel the register allocation spills, with any three it does not.
+// Block groups (m.ngroups > 1): the grid is ngroups consecutive ranges of 2 S blocks, range g
+// running the jobs with grp == g -- two job lists side by side on half the chip each, at half
+// the split count of one list on the whole chip: the same work per launch, half the split-K
+// slab bytes (written here, read back by the slab reduce).  2 S is a multiple of 8, so a block's
+// XCD pairing within its range is the single-group one.
 template <int SH>
 __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_jobs(TNJobs m) {
     __shared__ __attribute__((aligned(16))) char smem[wg::JOBS_BYTES];
     constexpr int A = wg::JOBS_AUX;
-    const int w = blockIdx.x, q = w >> 3;
+    const int per = gridDim.x / m.ngroups;
+    const int gsel = blockIdx.x / per;
+    const int w = blockIdx.x - gsel * per, q = w >> 3;
     const int jt = q & 1, sp = (q >> 1) * 8 + (w & 7);
     // one loop per tile shape, each group in list order; the exponent set alternates per job run
     // (c).  The order keeps a layer's second segment right behind its first (the same dy rows;
@@ -361,19 +368,21 @@ __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_jobs(TNJobs m) {
     int c = 0;
     auto pairs = [&]() {
         for (int i = 0; i < m.n; ++i)
-            if (m.kind[i] == WJ_PAIR) wg::block_any<256, 128, A, wg::JOBS_SET>(m.a[i], smem, 0, jt, sp, c++ & 1);
+            if (m.kind[i] == WJ_PAIR && m.grp[i] == gsel)
+                wg::block_any<256, 128, A, wg::JOBS_SET>(m.a[i], smem, 0, jt, sp, c++ & 1);
     };
     auto narrow = [&]() {
         for (int i = 0; i < m.n; ++i) {
             const int k = m.kind[i];
-            if (k == WJ_ENC128 || k == WJ_ENC_HALF)
+            if ((k == WJ_ENC128 || k == WJ_ENC_HALF) && m.grp[i] == gsel)
                 wg::block_any<128, 64, A, wg::JOBS_SET>(m.a[i], smem, k == WJ_ENC_HALF ? 128 * jt : 0, 0,
                                           k == WJ_ENC_HALF ? sp : 2 * sp + jt, c++ & 1);
         }
     };
     if constexpr (SH & 1) {
         for (int i = 0; i < m.n; ++i)
-            if (m.kind[i] == WJ_WIDE) wg::block_any<128, 256, A, wg::JOBS_SET>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
+            if (m.kind[i] == WJ_WIDE && m.grp[i] == gsel)
+                wg::block_any<128, 256, A, wg::JOBS_SET>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
         if constexpr (SH & 2) narrow();
         pairs();
     } else {
@@ -382,7 +391,8 @@ __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_jobs(TNJobs m) {
     }
     if constexpr (SH & 4)
         for (int i = 0; i < m.n; ++i)
-            if (m.kind[i] == WJ_ENC) wg::block_any<256, 64, A, wg::JOBS_SET>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
+            if (m.kind[i] == WJ_ENC && m.grp[i] == gsel)
+                wg::block_any<256, 64, A, wg::JOBS_SET>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
 }
 
 // two layers' 256 x 64 tiles in one launch: a's splits (blocks 0 .. na - 1), then b's (l4's
@@ -449,7 +459,7 @@ void launch_wgrad_jobs(const TNJobs& m, int splits, hipStream_t s) {
     int sh = 0;
     for (int i = 0; i < m.n; ++i)
         sh |= m.kind[i] == WJ_WIDE ? 1 : m.kind[i] == WJ_ENC128 || m.kind[i] == WJ_ENC_HALF ? 2 : m.kind[i] == WJ_ENC ? 4 : 0;
-    const dim3 g(2 * splits), b(wg::NTH);
+    const dim3 g(2 * splits * m.ngroups), b(wg::NTH);
     switch (sh) {
     case 0: hipLaunchKernelGGL(k_wgrad_jobs<0>, g, b, 0, s, m); break;
     case 1: hipLaunchKernelGGL(k_wgrad_jobs<1>, g, b, 0, s, m); break;

@@ -46,7 +46,7 @@ class ProfKind(ctypes.Structure):
 
 
 PROF_KINDS = ("fwd", "dx", "dw", "dw_narrow", "chain_fwd", "chain_bwd")   # NERF_PROF_FWD .. _CHAIN_BWD
-ABI_VERSION = 14                   # NERF_HIP_ABI_VERSION
+ABI_VERSION = 15                   # NERF_HIP_ABI_VERSION
 
 
 _P10 = _c_p * 10
@@ -108,6 +108,7 @@ _SIGS = {
                                     _c_p, _c_p, _c_p, _c_p], _c_i),
     "nerf_linear_bwd_weight_multi": ([_c_p, _c_i, _c_i, _c_i, _c_p], _c_i),
     "nerf_linear_bwd_weight_jobs": ([_c_p, _c_i, _c_i, _c_i, _c_p], _c_i),
+    "nerf_linear_bwd_weight_job_groups": ([_c_p, _c_p, _c_i, _c_i, _c_i, _c_i, _c_p], _c_i),
     "nerf_linear_bwd_weight_splits": ([_c_i, _c_i, _c_i], _c_i),
     "nerf_field_bwd_workspace_bytes": ([_c_i, _c_i], ctypes.c_size_t),
     "nerf_field_backward": ([_c_p, _c_p, _c_p], _c_i),
@@ -320,16 +321,22 @@ def linear_bwd_weight_multi(layers, m, splits):
     _call("nerf_linear_bwd_weight_multi", ctypes.addressof(jobs), len(layers), m, splits, _stream())
 
 
-def linear_bwd_weight_jobs(jobs, m, splits):
+def linear_bwd_weight_jobs(jobs, m, splits, groups=None):
     """Weight gradients of several shapes in one launch of 2 * splits blocks (mode 2, TN policy 8):
     jobs is a list of (dy, nout, x, kin, job_splits, slab, ldslab, col0, bslab, dy_cmax, x_cmax), each
     as linear_bwd_weight(dy, nout, x, kin, m, job_splits, slab, ldslab, col0, bslab, dy_cmax, x_cmax)
-    would write it."""
+    would write it.  groups (a list of block-group ids, one per job): the launch runs max + 1 groups
+    of 2 * splits blocks side by side (nerf_linear_bwd_weight_job_groups)."""
     arr = (WgradTileJob * len(jobs))()
     for j, (dy, nout, x, kin, sp, slab, ldslab, col0, bslab, dcm, xcm) in zip(arr, jobs):
         j.dy, j.lddy, j.nout, j.x, j.ldx, j.kin, j.splits = _ptr(dy), _ld(dy), nout, _ptr(x), _ld(x), kin, sp
         j.slab, j.ldslab, j.col0, j.bslab, j.dy_cmax, j.x_cmax = _ptr(slab), ldslab, col0, _ptr(bslab), _ptr(dcm), _ptr(xcm)
-    _call("nerf_linear_bwd_weight_jobs", ctypes.addressof(arr), len(jobs), m, splits, _stream())
+    if groups is None:
+        _call("nerf_linear_bwd_weight_jobs", ctypes.addressof(arr), len(jobs), m, splits, _stream())
+        return
+    grp = (ctypes.c_int * len(jobs))(*groups)
+    _call("nerf_linear_bwd_weight_job_groups", ctypes.addressof(arr), ctypes.addressof(grp), len(jobs), m, splits,
+          max(groups) + 1, _stream())
 
 
 def bwd_weight_splits(nout, kin, m) -> int:

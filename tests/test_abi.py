@@ -37,7 +37,7 @@ def test_binding_covers_the_header():
 
 
 def test_abi_version_and_error_path(lib):
-    assert lib.nerf_hip_abi_version() == 14
+    assert lib.nerf_hip_abi_version() == 15
     rc = lib.nerf_linear_fwd(None, 256, 256, None, 0, 0, None, None, 0, None, None, 256, 128, 256, 1, None, 0,
                              None, None, None, None, None)
     assert rc == -1

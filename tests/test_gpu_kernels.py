@@ -292,9 +292,10 @@ def test_wgrad_multi_matches_single(dev, n, m, splits):
         _hip.gemm_set_precision(prev)
 
 
-@pytest.mark.parametrize("which,m,S", [("colour+trunk", 131072, 128), ("l4+trunk+l0", 131072, 128),
-                                        ("colour+trunk", 32768, 32), ("l4+trunk+l0", 32768, 32)])
-def test_wgrad_jobs_matches_single(dev, which, m, S):
+@pytest.mark.parametrize("which,m,S,grouped", [("colour+trunk", 131072, 128, False), ("l4+trunk+l0", 131072, 128, False),
+                                                ("colour+trunk", 32768, 32, False), ("l4+trunk+l0", 32768, 32, False),
+                                                ("l4+trunk+l0", 131072, 64, True), ("l4+trunk+l0", 32768, 16, True)])
+def test_wgrad_jobs_matches_single(dev, which, m, S, grouped):
     """nerf_linear_bwd_weight_jobs (k_wgrad_jobs: 2 S blocks walk tiles of four shapes -- the
     TN schedule 3 launches of the field backward) against one nerf_linear_bwd_weight per job
     with the same splits and slab columns: every slab and bias partial bit-identical."""
@@ -333,7 +334,13 @@ def test_wgrad_jobs_matches_single(dev, which, m, S):
             s1, b1 = want[-1]
             _hip.linear_bwd_weight(dy, nout, x, kin, m, sp, s1, ld, col0, b1 if col0 == 0 else None,
                                    dy_cmax=dcm, x_cmax=xcm)
-        _hip.linear_bwd_weight_jobs(jobs, m, S)
+        if grouped:
+            # TN schedule 3's second launch in two block groups (field_bwd.cpp): l4 (both
+            # segments) + l3 | l2 + l1 + l0, each group at S splits on its own 2 S blocks
+            grp = [0, 0, 0, 1, 1, 1]
+            _hip.linear_bwd_weight_jobs(jobs, m, S, groups=grp)
+        else:
+            _hip.linear_bwd_weight_jobs(jobs, m, S)
         torch.cuda.synchronize()
         got = [(slab, bslab) for (_, _, _, _, _, slab, _, col0, bslab, _, _) in jobs if col0 == 0]
         assert len(got) == len(want)
