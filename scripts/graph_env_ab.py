@@ -22,7 +22,7 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-KEYS = ("NERF_HEADS_PLACE", "NERF_WGRAD_BATCH1", "NERF_WGRAD_SCHED", "NERF_BWD_CHAIN")
+KEYS = ("NERF_HEADS_PLACE", "NERF_WGRAD_BATCH1", "NERF_WGRAD_SCHED", "NERF_BWD_CHAIN", "NERF_WGRAD_GROUPS")
 
 
 def env_of(name):
