@@ -788,6 +788,9 @@ __global__ __launch_bounds__(256) void k_mlp_chain_fwd(ChainFwdArgs p) {
 // quad) and, in the forward, the ReLU words (from the fp16 hi words: two bits per
 // v_pk_min_u16 + v_dot2_u32_u16, one LDS atomic or per lane and k-step).
 // ---------------------------------------------------------------------------
+#ifndef NERF_CHAIN_MAX3
+#define NERF_CHAIN_MAX3 0   // A/B: the epilogues' row maxima by v_max3_f32 with |.| modifiers
+#endif
 #ifndef NERF_CHAIN_STAMPS
 #define NERF_CHAIN_STAMPS 0   // diagnostic builds only (make EXTRA=-DNERF_CHAIN_STAMPS=1): phase stamps
 #endif
@@ -998,6 +1001,13 @@ __device__ __forceinline__ float rows_sum(float v) {
     const float r = __uint_as_float(a[0]) + __uint_as_float(a[1]);   // own + the partner row's, as a shuffle sum
     const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(r), __float_as_uint(r), false, false);
     return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+// max(m, |a|, |b|) in one v_max3_f32 with |.| source modifiers (the compiler forms ~2.3
+// instructions per value from fmaxf / fabsf chains); max is exact, so the same bits
+__device__ __forceinline__ float max3abs(float m, float a, float b) {
+    float r;
+    asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
 }
 // a fresh copy of a lane value the compiler may not keep live (or spill) across the chain:
 // derived addresses are rebuilt from it where they are used
@@ -1502,7 +1512,7 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
     // in range), one rounding, as ldexp(acc, -(er + ew)) + b
     const float sr = __builtin_amdgcn_ldexpf(1.f, -st.er);
     const pf2 sr2 = {sr, sr};
-    float rmx = 0.f, hs0 = 0.f, hs1 = 0.f, hs2 = 0.f;
+    float rmx = 0.f, rmx1 = 0.f, hs0 = 0.f, hs1 = 0.f, hs2 = 0.f;
     uint32_t mw = 0;
 #pragma unroll
     for (int j = 0; j < ntj; ++j) {
@@ -1523,7 +1533,12 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
             for (int c = 0; c < 4; ++c) x[c] = __int_as_float(max(__float_as_int(x[c]), 0));
         }
         st.xs[j] = x;
-        rmx = fmaxf(rmx, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+        if constexpr (NERF_CHAIN_MAX3) {   // two accumulators (even / odd tiles): half the dependent chain
+            float& r = (j & 1) ? rmx1 : rmx;
+            r = max3abs(max3abs(r, x[0], x[1]), x[2], x[3]);
+        } else {
+            rmx = fmaxf(rmx, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+        }
         if constexpr (last_tr) {   // hr (the f32 epilogue value, as the per-layer kernel) and its ReLU words
             const nerf_chain_layer& L = p.L[l];
             tile_store4<128>(L.out + st.m0 * 128, (fresh(st.rl) * 128 + g4) * 4, 64 * j, x);
@@ -1576,7 +1591,7 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
         // next layer's A operand: row exponent over the row's 256 features (and the encoding
         // the next layer joins), k-step 0's fp16 pairs now, the others during the next layer's
         // k-steps (split_pieces)
-        float m = rows_max(rmx);
+        float m = rows_max(NERF_CHAIN_MAX3 ? fmaxf(rmx, rmx1) : rmx);
         const float* drec = st.fx + FX_ENCD + ENCD_REC * (st.rl / p.S);
         if constexpr (l == 3) {
             if constexpr (TR) {
@@ -2106,7 +2121,11 @@ __device__ __forceinline__ void layer(const nerf_chain_bwd& p, State& st) {
                 x[c] = __int_as_float(__float_as_int(x[c]) & __builtin_amdgcn_sbfe((int)bits, c, 1));
         }
         st.xs[j] = x;
-        rmx = fmaxf(rmx, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+        if constexpr (false) {   // (v_max3 here spills this kernel: 23 scratch ops against 2)
+            rmx = f2::max3abs(f2::max3abs(rmx, x[0], x[1]), x[2], x[3]);
+        } else {
+            rmx = fmaxf(rmx, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+        }
         if constexpr (last) {
             f2::tile_store4<256>(p.dy[NL] + st.m0 * 256, st.vrow, 64 * j, x);
             if constexpr (CMQ == 1)
