@@ -789,7 +789,7 @@ __global__ __launch_bounds__(256) void k_mlp_chain_fwd(ChainFwdArgs p) {
 // v_pk_min_u16 + v_dot2_u32_u16, one LDS atomic or per lane and k-step).
 // ---------------------------------------------------------------------------
 #ifndef NERF_CHAIN_MAX3
-#define NERF_CHAIN_MAX3 0   // A/B: the epilogues' row maxima by v_max3_f32 with |.| modifiers
+#define NERF_CHAIN_MAX3 1   // A/B: the epilogues' row maxima by v_max3_f32 with |.| modifiers
 #endif
 #ifndef NERF_CHAIN_STAMPS
 #define NERF_CHAIN_STAMPS 0   // diagnostic builds only (make EXTRA=-DNERF_CHAIN_STAMPS=1): phase stamps
