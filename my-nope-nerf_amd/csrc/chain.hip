@@ -788,9 +788,6 @@ __global__ __launch_bounds__(256) void k_mlp_chain_fwd(ChainFwdArgs p) {
 // quad) and, in the forward, the ReLU words (from the fp16 hi words: two bits per
 // v_pk_min_u16 + v_dot2_u32_u16, one LDS atomic or per lane and k-step).
 // ---------------------------------------------------------------------------
-#ifndef NERF_CHAIN_MAX3
-#define NERF_CHAIN_MAX3 1   // A/B: the epilogues' row maxima by v_max3_f32 with |.| modifiers
-#endif
 #ifndef NERF_CHAIN_STAMPS
 #define NERF_CHAIN_STAMPS 0   // diagnostic builds only (make EXTRA=-DNERF_CHAIN_STAMPS=1): phase stamps
 #endif
@@ -814,12 +811,9 @@ constexpr int FX_WD = 0, FX_WC = 256;   // fc_density weight [256], fc_rgb weigh
 // two DPP steps, one atomic per 8 / 4 lanes into copy n >> 3 / n >> 2 -- copies CMS words apart, so
 // the leaders' atomics of one instruction hit distinct banks -- and the copies are combined when the
 // maxima leave LDS
-#ifndef NERF_CHAIN_CMQ
-#define NERF_CHAIN_CMQ 1
-#endif
-#ifndef NERF_CHAIN_CMQ_BWD
-#define NERF_CHAIN_CMQ_BWD 4
-#endif
+// (forward: 1 -- 4 copies ran within noise, profiles/r06/fwd_colmax_relu_ab.txt; input-gradient
+// chain: 4 -- 469-472 vs 494-506 us, profiles/r06/colmax_copies_ab.txt)
+constexpr int CMQ_FWD = 1, CMQ_BWD = 4;
 constexpr int CMS = 513;                                     // words per copy (both parities + 1)
 constexpr int cm_words(int q) { return q == 1 ? 512 : q * CMS; }
 // the max of word w (parity * 256 + feature) over the q copies
@@ -836,12 +830,9 @@ __device__ __forceinline__ void cm_clear(uint32_t* cm, int w) {
     for (int c = 0; c < Q; ++c) cm[c * CMS + w] = 0u;
 }
 
-// words per row of the training forward's ReLU-word array: 8, or 9 (A/B) so that the rows' OR
-// atomics of one instruction (16 rows, stride 8 words: 4-way bank conflicts) hit distinct banks
-#ifndef NERF_CHAIN_MSKW
-#define NERF_CHAIN_MSKW 8
-#endif
-constexpr int MSKW = NERF_CHAIN_MSKW;
+// words per row of the training forward's ReLU-word array (rows padded to 9 words against the
+// OR atomics' 4-way bank conflicts ran slower: profiles/r06/fwd_colmax_relu_ab.txt)
+constexpr int MSKW = 8;
 
 template <bool TR>
 struct LY {
@@ -853,7 +844,7 @@ struct LY {
     static constexpr int O_BIAS = O_EXP + 2 * 256 * 4;        // [2][256] float
     static constexpr int O_ENC = O_BIAS + 2 * 256 * 4;        // eval: [128][64] float position encodings
     static constexpr int O_CMX = O_ENC;                       // training: [2][256] uint column maxima
-    static constexpr int O_MSK = O_CMX + cm_words(NERF_CHAIN_CMQ) * 4;   // training: [2][128][MSKW] uint ReLU words
+    static constexpr int O_MSK = O_CMX + cm_words(CMQ_FWD) * 4;   // training: [2][128][MSKW] uint ReLU words
     static constexpr int O_RMX = O_ENC + 128 * 64 * 4;        // eval: [4][128] row maxima
     static constexpr int O_FX = TR ? O_MSK + 2 * 128 * MSKW * 4 : O_RMX + 4 * 128 * 4;   // head weights, raw4, ...
     static constexpr int FX_FLOATS = TR ? FX_ENCD : FX_ENCD + (CROWS / 2) * ENCD_REC;
@@ -1275,21 +1266,18 @@ __device__ __forceinline__ void relu_put(uint32_t* a, uint32_t w, const State&) 
 // tiles, behind its split (which it shares the xs registers with)
 enum Piece { P_SPLIT_HI_A, P_SPLIT_HI_B, P_SPLIT_LO_A, P_SPLIT_LO_B, P_STORE, P_CMAX_A, P_CMAX_B, P_RELU,
              P0_STORE, P0_CMAX_A, P0_CMAX_B, P0_RELU, P_STORE_B, P0_STORE_B };
-#ifndef NERF_CHAIN_DMA2
-#define NERF_CHAIN_DMA2 1      // A/B: the second 16-k step's DMAs DMA2 tiles after the barrier tile
-#endif
-#ifndef NERF_CHAIN_STSPLIT
-#define NERF_CHAIN_STSPLIT 0   // A/B: the second store of a pair STSPLIT tiles after the first
-#endif
+// the second 16-k step's DMAs one tile after the barrier tile (two tiles: within noise; the two
+// stores of a pair on different tiles: +10 us per chain, profiles/r06/chain_store_dma_spread_ab.txt)
+constexpr int DMA2 = 1;
 // (a staggered table for waves 4-7, their pieces at the tiles waves 0-3 leave free, ran 4 %
 // slower: profiles/r05/chain_variants_ab.txt)
 template <int ntj>
 constexpr int piece_tile(int piece) {
     if constexpr (ntj == 16) {
-        constexpr int T[14] = {6, 7, 8, 9, 10, 11, 12, 13, 1, 2, 3, 4, 10 + NERF_CHAIN_STSPLIT, 1 + NERF_CHAIN_STSPLIT};
+        constexpr int T[14] = {6, 7, 8, 9, 10, 11, 12, 13, 1, 2, 3, 4, 10, 1};
         return T[piece];
     } else {
-        constexpr int T[14] = {3, 3, 4, 4, 5, 6, 7, 7, 0, 1, 2, 2, 5, NERF_CHAIN_STSPLIT ? 1 : 0};
+        constexpr int T[14] = {3, 3, 4, 4, 5, 6, 7, 7, 0, 1, 2, 2, 5, 0};
         return T[piece];
     }
 }
@@ -1313,7 +1301,7 @@ __device__ __forceinline__ void save_pieces(const ChainFwdArgs& p, State& st) {
         // a per-piece opaque copy of the lane's LDS offsets (the compiler would otherwise keep
         // every piece's address live across the chain)
         // (the LDS offsets of the arrays are beyond a ds_* immediate: they ride in the base)
-        constexpr int Q = NERF_CHAIN_CMQ;
+        constexpr int Q = CMQ_FWD;
         auto cm_at = [&](int t, int half) {
             int o = Y::O_CMX + 16 * st.g + (Q == 1 ? 0 : 4 * CMS * (st.n >> (Q == 2 ? 3 : 2)));
             asm volatile("" : "+v"(o));
@@ -1417,21 +1405,14 @@ __device__ __forceinline__ void layer_start(const ChainFwdArgs& p, State& st) {
             uint32_t* cm = reinterpret_cast<uint32_t*>(st.lds + Y::O_CMX);
             const int cw = (l & 1) * 256 + 32 * st.wave + lane;
             p.L[l - 2].cmax[(st.m0 / CROWS) * L_OUT[l - 2] + 32 * st.wave + lane] =
-                __uint_as_float(cm_read<NERF_CHAIN_CMQ>(cm, cw));
-            cm_clear<NERF_CHAIN_CMQ>(cm, cw);
+                __uint_as_float(cm_read<CMQ_FWD>(cm, cw));
+            cm_clear<CMQ_FWD>(cm, cw);
         }
         const int rl = 16 * st.wave + (lane & 15), g = lane >> 4;
         const nerf_chain_layer& Q = p.L[l - 2];
-        if constexpr (MSKW == 8) {
-            uint2* mw = reinterpret_cast<uint2*>(st.lds + Y::O_MSK + (l & 1) * 4096 + 32 * rl + 8 * g);
-            *reinterpret_cast<uint2*>(Q.mask + (st.m0 + rl) * Q.ldmask + 2 * g) = *mw;
-            *mw = make_uint2(0u, 0u);
-        } else {
-            uint32_t* mw = reinterpret_cast<uint32_t*>(st.lds + Y::O_MSK) + (l & 1) * 128 * MSKW + MSKW * rl + 2 * g;
-            *reinterpret_cast<uint2*>(Q.mask + (st.m0 + rl) * Q.ldmask + 2 * g) = make_uint2(mw[0], mw[1]);
-            mw[0] = 0u;
-            mw[1] = 0u;
-        }
+        uint2* mw = reinterpret_cast<uint2*>(st.lds + Y::O_MSK + (l & 1) * 4096 + 32 * rl + 8 * g);
+        *reinterpret_cast<uint2*>(Q.mask + (st.m0 + rl) * Q.ldmask + 2 * g) = *mw;
+        *mw = make_uint2(0u, 0u);
     }
 }
 
@@ -1461,7 +1442,7 @@ __device__ __forceinline__ void mstep_tiles(const ChainFwdArgs& p, State& st, co
             tick(p, st, &st.t_bar);
             dma<tt_of_k(k + npair<TR>() - 1), TR>(p, st);
         }
-        if constexpr (k + 1 < NK && j == T + NERF_CHAIN_DMA2) dma<tt_of_k(k + npair<TR>() - 1) + 1, TR>(p, st);
+        if constexpr (k + 1 < NK && j == T + DMA2) dma<tt_of_k(k + npair<TR>() - 1) + 1, TR>(p, st);
         __builtin_amdgcn_sched_barrier(0);
         mstep_tiles<l, u, TR, j + 1, ntj>(p, st, ah, al);
     }
@@ -1533,11 +1514,10 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
             for (int c = 0; c < 4; ++c) x[c] = __int_as_float(max(__float_as_int(x[c]), 0));
         }
         st.xs[j] = x;
-        if constexpr (NERF_CHAIN_MAX3) {   // two accumulators (even / odd tiles): half the dependent chain
+        {   // v_max3 with |.| operands, two accumulators (even / odd tiles): half the dependent chain
+            // (forward chain -2 us, eval -0.17 ms per frame: profiles/r06/max3_ab.txt)
             float& r = (j & 1) ? rmx1 : rmx;
             r = max3abs(max3abs(r, x[0], x[1]), x[2], x[3]);
-        } else {
-            rmx = fmaxf(rmx, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
         }
         if constexpr (last_tr) {   // hr (the f32 epilogue value, as the per-layer kernel) and its ReLU words
             const nerf_chain_layer& L = p.L[l];
@@ -1591,7 +1571,7 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
         // next layer's A operand: row exponent over the row's 256 features (and the encoding
         // the next layer joins), k-step 0's fp16 pairs now, the others during the next layer's
         // k-steps (split_pieces)
-        float m = rows_max(NERF_CHAIN_MAX3 ? fmaxf(rmx, rmx1) : rmx);
+        float m = rows_max(fmaxf(rmx, rmx1));
         const float* drec = st.fx + FX_ENCD + ENCD_REC * (st.rl / p.S);
         if constexpr (l == 3) {
             if constexpr (TR) {
@@ -1774,11 +1754,9 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_train2(ChainFwdArgs p) {
     if (st.tid < 256) st.fx[FX_WD + st.tid] = p.wd[st.tid];
     for (int e = st.tid; e < 384; e += NTH) st.fx[FX_WC + e] = p.wc[e];
     // both column-max parities (512 words) and both ReLU-word parities (2048 words) cleared
-    for (int e = st.tid; e < cm_words(NERF_CHAIN_CMQ); e += NTH) reinterpret_cast<uint32_t*>(smem + Y::O_CMX)[e] = 0u;
-    if constexpr (MSKW == 8)
-        reinterpret_cast<uint4*>(smem + Y::O_MSK)[st.tid] = make_uint4(0u, 0u, 0u, 0u);
-    else
-        for (int e = st.tid; e < 2 * 128 * MSKW; e += NTH) reinterpret_cast<uint32_t*>(smem + Y::O_MSK)[e] = 0u;
+    for (int e = st.tid; e < cm_words(CMQ_FWD); e += NTH) reinterpret_cast<uint32_t*>(smem + Y::O_CMX)[e] = 0u;
+    static_assert(2 * 128 * MSKW == 4 * NTH, "one uint4 per thread");
+    reinterpret_cast<uint4*>(smem + Y::O_MSK)[st.tid] = make_uint4(0u, 0u, 0u, 0u);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     dma_n<0, 2 * (npair<true>() - 1), true>(p, st);   // steps 0 .. NPAIR - 2
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_prologue<true>()) : "memory");
@@ -1795,7 +1773,7 @@ __global__ __launch_bounds__(512, 2) void k_mlp_chain_train2(ChainFwdArgs p) {
         *reinterpret_cast<float4*>(p.raw4 + (m0 + tid) * 4) = *reinterpret_cast<const float4*>(st.fx + FX_RAW + 4 * tid);
     else if (tid < CROWS + 256)
         p.L[8].cmax[(m0 / CROWS) * L_OUT[8] + tid - CROWS] =
-            __uint_as_float(cm_read<NERF_CHAIN_CMQ>(reinterpret_cast<const uint32_t*>(smem + Y::O_CMX), (8 & 1) * 256 + tid - CROWS));
+            __uint_as_float(cm_read<CMQ_FWD>(reinterpret_cast<const uint32_t*>(smem + Y::O_CMX), (8 & 1) * 256 + tid - CROWS));
 }
 
 // ---------------------------------------------------------------------------
@@ -1887,7 +1865,7 @@ constexpr int O_LEB = NSLOT * SBYTES;            // [2][256] int weight-row expo
 constexpr int O_EXP = O_LEB + 2 * 256 * 4;       // [2][256] float 2^-e of the weight rows
 constexpr int O_MASK = O_EXP + 2 * 256 * 4;      // [2][128 rows][8 words] ReLU words of the layer input
 constexpr int O_CMX = O_MASK + 2 * 128 * 32;     // [2][256] uint column maxima (LDS atomics)
-constexpr int CMQ = NERF_CHAIN_CMQ_BWD;          // column-max copies (f2::cm_words)
+constexpr int CMQ = f2::CMQ_BWD;                // column-max copies (f2::cm_words)
 constexpr int O_FX = O_CMX + f2::cm_words(CMQ) * 4;   // fc_density [256], fc_rgb [3][128]
 constexpr int BYTES = O_FX + (256 + 384) * 4;
 static_assert(BYTES <= 160 * 1024, "LDS");
@@ -2058,7 +2036,7 @@ __device__ __forceinline__ void tiles(const nerf_chain_bwd& p, State& st, const 
             __syncthreads();   // B_{k+1}
             dma<tt_of_k(k + NPAIR - 1)>(p, st);
         }
-        if constexpr (k + 1 < NK && j == TB + NERF_CHAIN_DMA2) dma<tt_of_k(k + NPAIR - 1) + 1>(p, st);
+        if constexpr (k + 1 < NK && j == TB + f2::DMA2) dma<tt_of_k(k + NPAIR - 1) + 1>(p, st);
         __builtin_amdgcn_sched_barrier(0);
         tiles<i, u, j + 1>(p, st, ah, al);
     }
