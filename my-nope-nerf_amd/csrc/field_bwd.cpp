@@ -222,8 +222,32 @@ int chain_schedule(const nerf_field_bwd& a, Work& w, const float* graw4, void* s
             nt = 0;
             return NERF_OK;
         };
-        for (int l : {LR, LF, 7, 6, 5}) tiles(l);
-        RC(launch());
+        // NERF_WGRAD_GROUPS: 2 (the default) both launches as two block groups of 2 S' blocks
+        // (S' = S / 2: each job twice the rows per split, half the jobs per block and half the
+        // split-K slab bytes written and read back); 1 the second launch only; 0 one job list per
+        // launch on 2 S blocks.  1.9125 / 1.9525 / 1.9721 ms per cfg2 step (2 / 1 / 0, fresh
+        // processes interleaved, profiles/r06/wgrad_groups_lib_ab.txt)
+        const char* wgg = std::getenv("NERF_WGRAD_GROUPS");
+        const int groups = w.splits[LF] % 16 == 0 ? (wgg ? std::atoi(wgg) : 2) : 0;
+        const int s2 = w.splits[LF] / 2;
+        if (groups >= 2) {
+            // group 0 the colour layer's f segment + l_f + l7, group 1 its enc_d segment + l6 + l5
+            // (5 vs 4.5 1024-row tile-times per block against 4.75 in one list, three jobs each
+            // instead of six); the slab buffers are sized for S: room to spare
+            for (int l : {LF, 7, 6, 5}) w.splits[l] = s2;
+            w.splits[LR] = 2 * s2;
+            tiles(LR);
+            tgrp[nt - 1] = 1;
+            for (int l : {LF, 7}) tiles(l);
+            cur_grp = 1;
+            for (int l : {6, 5}) tiles(l);
+            cur_grp = 0;
+            RC(nerf_linear_bwd_weight_job_groups(tj, tgrp, nt, np, s2, 2, stream));
+            nt = 0;
+        } else {
+            for (int l : {LR, LF, 7, 6, 5}) tiles(l);
+            RC(launch());
+        }
         // NERF_WGRAD_BATCH1: 1 (the default) the first batch on the caller's stream between the two
         // launches; 0 on the side stream (it can only start once the second launch frees CUs).
         // Eager the two are within noise (2.029 vs 2.037 ms/step); replayed as a hipGraph the
@@ -231,13 +255,9 @@ int chain_schedule(const nerf_field_bwd& a, Work& w, const float* graw4, void* s
         const char* b1 = std::getenv("NERF_WGRAD_BATCH1");
         RC(flush(b1 && std::atoi(b1) == 0 ? side : main));
         RC(enc_rows(LR));
-        // NERF_WGRAD_GROUPS: 1 the second launch as two block groups of 2 S' blocks (S' = S / 2:
-        // half the split-K slab bytes, ~80 MB written and read back per step less), group 0
-        // l4's two segments + l3, group 1 l2 + l1 + l0 (2.25 layer-equivalents each); 0 one list
-        const char* wgg = std::getenv("NERF_WGRAD_GROUPS");
-        const bool grouped = (wgg ? std::atoi(wgg) : 0) != 0 && w.splits[LF] % 16 == 0;
-        if (grouped) {
-            const int s2 = w.splits[LF] / 2;
+        // grouped (NERF_WGRAD_GROUPS >= 1): group 0 l4's two segments + l3, group 1 l2 + l1 + l0
+        // (2.25 layer-equivalents each)
+        if (groups >= 1) {
             for (int l : {1, 2, 3, 4}) w.splits[l] = s2;   // the slab buffers are sized for S: room to spare
             w.splits[0] = 2 * s2;
             for (int l : {3, 4}) tiles(l);   // k_wgrad_jobs runs a group's pairs, then its narrow jobs: l4 h3, l4 enc_p last

@@ -26,6 +26,8 @@ KEYS = ("NERF_HEADS_PLACE", "NERF_WGRAD_BATCH1", "NERF_WGRAD_SCHED", "NERF_BWD_C
 
 
 def env_of(name):
+    # (a "#tag" suffix names a repeat of a setting: "default#2" checks the harness's own spread)
+    name = name.split("#", 1)[0]
     return {} if name == "default" else dict(kv.split("=", 1) for kv in name.split(","))
 
 

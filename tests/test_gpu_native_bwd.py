@@ -8,7 +8,7 @@ Training-size batches (Np >= 65536, where the native path runs), with and withou
 gradients (pose learning), from the composite backward and from a given graw4
 (eval_points); the per-layer schedule also under a tail of 0 and 3 deferred weight gradients
 (tail_main applies to it only), and the chain under both weight-gradient schedules
-(NERF_WGRAD_SCHED 1 / 2 / 3)."""
+(NERF_WGRAD_SCHED 1 / 2 / 3; 3 also with NERF_WGRAD_GROUPS 0 / 1 besides its default 2)."""
 import os
 
 import pytest
@@ -70,7 +70,7 @@ def _agree(a, b, chain):
         assert (a - b).abs().max().item() <= 1e-4 * b.abs().max().item() + 1e-30
 
 
-@pytest.mark.parametrize("chain,sched", [("0", "1"), ("1", "1"), ("1", "2"), ("1", "3")])
+@pytest.mark.parametrize("chain,sched", [("0", "1"), ("1", "1"), ("1", "2"), ("1", "3"), ("1", "3g0"), ("1", "3g1")])
 @pytest.mark.parametrize("ray_grad,R,S,tail", [(False, 1024, 128, None), (True, 1024, 128, None),
                                                (False, 600, 128, "0"), (True, 520, 128, "3")])
 def test_native_backward_bit_identical(dev, h16, ray_grad, R, S, tail, chain, sched):
@@ -89,7 +89,9 @@ def test_native_backward_bit_identical(dev, h16, ray_grad, R, S, tail, chain, sc
 
     env = {"NERF_TAIL_MAIN": tail} if tail is not None else {}
     env["NERF_BWD_CHAIN"] = chain
-    env["NERF_WGRAD_SCHED"] = sched      # the chain's weight-gradient schedules (field_bwd.cpp)
+    env["NERF_WGRAD_SCHED"] = sched[0]   # the chain's weight-gradient schedules (field_bwd.cpp)
+    if len(sched) > 1:                   # schedule 3's block groups: none / the second launch (default: both)
+        env["NERF_WGRAD_GROUPS"] = sched[2:]
     g_native = _grads(net, fn, True, env)
     g_python = _grads(net, fn, False, env)
     n_pad = (R * S + 127) // 128 * 128
