@@ -304,6 +304,22 @@ __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int blk, flo
                     acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
                 }
             }
+            // (the grouped weight gradients' 64-split slabs leave 4 splits per lane group: in flight
+            // together, not one dependent load at a time; the same summation order)
+            for (; q + 3 * SR_GROUPS < splits; q += 4 * SR_GROUPS) {
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    typedef float sr_f4 __attribute__((ext_vector_type(4)));
+                    const sr_f4 t = __builtin_nontemporal_load(
+                        reinterpret_cast<const sr_f4*>(src + (size_t)(q + SR_GROUPS * u) * st + c0));
+                    v[u] = make_float4(t.x, t.y, t.z, t.w);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+                }
+            }
             for (; q < splits; q += SR_GROUPS) {
                 const float4 v = *reinterpret_cast<const float4*>(src + (size_t)q * st + c0);
                 acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
