@@ -65,7 +65,7 @@ __host__ __device__ constexpr int chain_perm(int c) {
 // GEMM arithmetic mode (nerf_gemm_set_precision), host side
 int gemm_precision();
 // several split-K slab reduces (nerf_slab_reduce without accumulate) in one launch
-constexpr int kSlabJobsMax = 10;
+constexpr int kSlabJobsMax = 12;   // ten layers + the two head-weight reduces
 struct SlabJobDesc {
     const float* slab;
     int splits, nout, ldslab, nout_ref, kin_ref;

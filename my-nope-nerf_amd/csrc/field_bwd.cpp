@@ -248,12 +248,13 @@ int chain_schedule(const nerf_field_bwd& a, Work& w, const float* graw4, void* s
             for (int l : {LR, LF, 7, 6, 5}) tiles(l);
             RC(launch());
         }
-        // NERF_WGRAD_BATCH1: 1 (the default) the first batch on the caller's stream between the two
-        // launches; 0 on the side stream (it can only start once the second launch frees CUs).
-        // Eager the two are within noise (2.029 vs 2.037 ms/step); replayed as a hipGraph the
-        // side-stream branch costs ~55 us per step (2.093 vs 2.039 ms, profiles/r05/batch1_ab.json)
+        // NERF_WGRAD_BATCH1: the first launch's slab reduces 2 (the default) in ONE reduce launch with
+        // the second's, after it; 1 on the caller's stream between the two launches; 0 on the side
+        // stream (it can only start once the second launch frees CUs; replayed as a hipGraph the
+        // side-stream branch cost ~55 us per step, profiles/r05/batch1_ab.json)
         const char* b1 = std::getenv("NERF_WGRAD_BATCH1");
-        RC(flush(b1 && std::atoi(b1) == 0 ? side : main));
+        const int batch1 = b1 ? std::atoi(b1) : 2;
+        if (batch1 != 2) RC(flush(batch1 == 0 ? side : main));
         RC(enc_rows(LR));
         // grouped (NERF_WGRAD_GROUPS >= 1): group 0 l4's two segments + l3, group 1 l2 + l1 + l0
         // (2.25 layer-equivalents each)

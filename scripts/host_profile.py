@@ -20,8 +20,7 @@ def main():
     _hip.load_library()
     _hip.gemm_set_precision(2)
     if "--full" in sys.argv:
-        import bench_full as bf
-        trainer, datas = bf.setup(dev)
+        trainer, datas = bench.cfg3_setup(dev)
         step = lambda it: trainer.train_step(datas[it % 2], it=it + 1, epoch=0, scheduling_start=0)
     else:
         cfg = bench.make_cfg()
