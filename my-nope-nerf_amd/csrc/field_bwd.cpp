@@ -256,14 +256,19 @@ int chain_schedule(const nerf_field_bwd& a, Work& w, const float* graw4, void* s
         const int batch1 = b1 ? std::atoi(b1) : 2;
         if (batch1 != 2) RC(flush(batch1 == 0 ? side : main));
         RC(enc_rows(LR));
-        // grouped (NERF_WGRAD_GROUPS >= 1): group 0 l4's two segments + l3, group 1 l2 + l1 + l0
-        // (2.25 layer-equivalents each)
+        // grouped (NERF_WGRAD_GROUPS >= 1)
         if (groups >= 1) {
             for (int l : {1, 2, 3, 4}) w.splits[l] = s2;   // the slab buffers are sized for S: room to spare
             w.splits[0] = 2 * s2;
-            for (int l : {3, 4}) tiles(l);   // k_wgrad_jobs runs a group's pairs, then its narrow jobs: l4 h3, l4 enc_p last
+            // group 0 l4's h3 segment + l3 + l0, group 1 l4's enc_p segment + l2 + l1 (4.83 / 5
+            // tile-times): with groups k_wgrad_jobs runs a group's narrow jobs before its pairs, so the
+            // two reads of l4's dy start together (group 0's first job and group 1's): 1.8580 vs 1.8677
+            // ms per cfg2 step (profiles/r06/wgrad_l4_groups_ab.txt)
+            tiles(4);
+            tgrp[nt - 1] = 1;
+            for (int l : {3, 0}) tiles(l);
             cur_grp = 1;
-            for (int l : {2, 1, 0}) tiles(l);
+            for (int l : {2, 1}) tiles(l);
             cur_grp = 0;
             RC(nerf_linear_bwd_weight_job_groups(tj, tgrp, nt, np, s2, 2, stream));
             nt = 0;

@@ -385,6 +385,11 @@ __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_jobs(TNJobs m) {
                 wg::block_any<128, 256, A, wg::JOBS_SET>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
         if constexpr (SH & 2) narrow();
         pairs();
+    } else if (m.ngroups > 1) {
+        // block groups: a group's narrow jobs first, so l4's enc_p job (group 1) reads l4's dy
+        // beside its h3 job (group 0's first) instead of after it
+        if constexpr (SH & 2) narrow();
+        pairs();
     } else {
         pairs();
         if constexpr (SH & 2) narrow();
