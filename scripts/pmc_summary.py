@@ -75,12 +75,12 @@ KINDS = {
         "dw", (4 * M * (D + 128) + 4 * 128 * D + 4 * 128) + (4 * M * 64 + 4 * 128 * 64) +
         4 * (4 * M * 2 * D + 4 * D * D + 4 * D),
         "the colour layer over [f | enc_d] (dyr 67.1 MB + f 134.2 MB + enc_d 33.6 MB) + l_f, l7, l6, l5 (dy + x "
-        "268.4 MB each); measured writes are the split-K slabs (41.9 + 4 x 33.6 MB)"),
+        "268.4 MB each); measured writes are the split-K slabs (round 5: 41.9 + 4 x 33.6 MB; round 6, two block groups at half the splits: 21 + 4 x 16.8 MB)"),
     "k_wgrad_jobs<6>": (
         "dw", (4 * M * 2 * D + 4 * D * D + 4 * D) + (4 * M * 64 + 4 * D * 64) + 3 * (4 * M * 2 * D + 4 * D * D + 4 * D) +
         (4 * M * (64 + D) + 4 * D * 64 + 4 * D),
         "l4 over [h3 | enc_p] (dy + h3 268.4 MB + enc_p 33.6 MB) + l3, l2, l1 (268.4 MB each) + l0 (dy 134.2 MB + "
-        "enc_p 33.6 MB); measured writes are the split-K slabs (41.9 + 3 x 33.6 + 16.8 MB)"),
+        "enc_p 33.6 MB); measured writes are the split-K slabs (round 5: 41.9 + 3 x 33.6 + 16.8 MB; round 6, block groups: 21 + 3 x 16.8 + 8.4 MB)"),
     "k_gemm_tn_x6<256, 256, 2, 2, true, 1>": (
         "dw", 4 * M * D * 2 + 4 * D * D, "dy 134.2 MB + x 134.2 MB + dW 0.26 MB; measured writes are the 256 "
         "split-K slabs (67 MB)"),

@@ -1,6 +1,6 @@
 """The HIP path under a process group, on the one GPU of the box:
 two ranks (gloo carries the collectives; RCCL needs one GPU per rank) each run their share
-of the work through the full HIP path.
+of the work through the full HIP path; and the gradient all-reduce on RCCL itself with one rank.
 
 * config 5 (training): each rank renders half of a ray batch -- NeRF forward / backward, pose
   and distortion learning -- and Trainer.allreduce_grads averages the gradients in place on
@@ -113,14 +113,16 @@ def _spawn(target, world, *args, timeout=300):
     return res
 
 
-def _run_rank(rank, world, port, q, body_name, *args):
-    """Rank entry point (module level: spawn pickles it by name): joins the gloo group on
-    127.0.0.1, runs the named body, reports a traceback instead of leaving the parent waiting."""
+def _run_rank(rank, world, port, q, body_name, *args, backend="gloo"):
+    """Rank entry point (module level: spawn pickles it by name): joins the gloo (or, one rank per
+    GPU, the nccl = RCCL) group on 127.0.0.1, runs the named body, reports a traceback instead of
+    leaving the parent waiting."""
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                **({"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}))
         globals()[body_name](rank, world, q, *args)
         dist.barrier()
         dist.destroy_process_group()
@@ -148,6 +150,51 @@ def _train_body(rank, world, q, case):
     params = [p.detach().cpu().clone().numpy() for p in tr.bucket_params()]
     q.put((rank, grads, params, in_bucket))
 
+
+
+def _run_rank_rccl(rank, world, port, q, body_name, *args):
+    _run_rank(rank, world, port, q, body_name, *args, backend="nccl")
+
+
+def _rccl_body(rank, world, q, case):
+    """The data-parallel gradient path on RCCL itself (one rank: the box has one GPU): the HIP
+    backward writes the NeRF gradients into the Trainer's bucket, allreduce_grads runs the ONE
+    in-place RCCL all-reduce on it, and every gradient must come back bit-identical (a sum over
+    one rank, times 1.0) as a view of the bucket."""
+    dev = torch.device("cuda:0")
+    tr, data, ray_idx, noise, _, _ = _setup(dev, case)
+    assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+    tr.inject = (ray_idx, noise)
+    tr._bucket_buffer(dev)                      # as train_step does under a process group
+    runner = tr.model.renderer.model.hip_runner()
+    runner.release_grad_buffer()
+    for _, o in tr._modules_and_optims():
+        if o is not None:
+            o.zero_grad()
+    ld = tr.compute_loss(data, it=0, epoch=0, scheduling_start=0)
+    ld["loss"].backward()
+    flat = tr._flat
+    base, end = flat.data_ptr(), flat.data_ptr() + 4 * flat.numel()
+    written_in_place = all(base <= p.grad.data_ptr() < end for p in runner.param_list())
+    before = _grads(tr)
+    tr.allreduce_grads()
+    torch.cuda.synchronize()
+    after = _grads(tr)
+    views = all(p.grad is None or base <= p.grad.data_ptr() < end for p in tr.bucket_params())
+    q.put((rank, before, after, written_in_place, views))
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_allreduce_grads_on_rccl(dev, case):
+    res = _spawn(_run_rank_rccl, 1, "_rccl_body", case)
+    before, after, written_in_place, views = res[0]
+    assert written_in_place, "the HIP backward did not write the NeRF gradients into the bucket"
+    assert views, "a gradient is not a view of the all-reduce bucket"
+    assert len(before) == len(after)
+    for i, (b, a) in enumerate(zip(before, after)):
+        assert (b is None) == (a is None), i
+        if b is not None:
+            assert (b == a).all(), i
 
 
 def _nrel(a, b):
