@@ -32,6 +32,7 @@ namespace wg {
 constexpr int NTH = 512;   // 8 waves, two per SIMD: 4 MFMA waves + 4 load / split waves
 constexpr int KS = 32;     // rows per pipeline stage: two 16-row MFMA k-steps
 constexpr int NS = 3;      // register stages of a load wave: loads issued three stages ahead of their split
+                           // (k_wgrad_jobs<3>: four)
 
 template <int BO, int BK>
 struct Cfg {
@@ -103,7 +104,7 @@ __device__ __forceinline__ void put_strip(char* d, int plane_bytes, const float 
 // epilogue may still read the other set's lea / leb, so the two sets must not overlap whatever
 // the two jobs' shapes (with a per-shape stride BO + BK, a 128 x 64 job's set 1 overlapped a
 // 256 x 128 job's set 0)
-template <int BO, int BK, bool BIAS, int AUX = Cfg<BO, BK>::MAIN, int SET = BO + BK>
+template <int BO, int BK, bool BIAS, int AUX = Cfg<BO, BK>::MAIN, int SET = BO + BK, int NS = wg::NS>
 __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int jt, int split, int par) {
     using C = Cfg<BO, BK>;
     constexpr int CA = C::CA, CB = C::CB, TM = C::TM, TN = C::TN;
@@ -288,10 +289,10 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
 }
 
 // the block of column tile jt, with the bias sums where the layer wants them (column tile 0)
-template <int BO, int BK, int AUX = Cfg<BO, BK>::MAIN, int SET = BO + BK>
+template <int BO, int BK, int AUX = Cfg<BO, BK>::MAIN, int SET = BO + BK, int NS = wg::NS>
 __device__ __forceinline__ void block_any(const TNArgs& p, char* smem, int o0, int jt, int split, int par = 0) {
-    if (jt == 0 && p.bslab != nullptr) block<BO, BK, true, AUX, SET>(p, smem, o0, jt, split, par);
-    else block<BO, BK, false, AUX, SET>(p, smem, o0, jt, split, par);
+    if (jt == 0 && p.bslab != nullptr) block<BO, BK, true, AUX, SET, NS>(p, smem, o0, jt, split, par);
+    else block<BO, BK, false, AUX, SET, NS>(p, smem, o0, jt, split, par);
 }
 
 // the LDS of a kernel that runs tiles of every shape (k_wgrad_jobs): the main regions, then two
@@ -355,6 +356,9 @@ template <int SH>
 __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_jobs(TNJobs m) {
     __shared__ __attribute__((aligned(16))) char smem[wg::JOBS_BYTES];
     constexpr int A = wg::JOBS_AUX;
+    // the load waves' stages in flight: 4 in the colour .. l5 launch (shape set 3; 1.8653 vs 1.8702
+    // ms per cfg2 step, profiles/r06/wgrad_ns4_ab.txt), 3 elsewhere (shape set 6 spills at 4)
+    constexpr int NSJ = SH == 3 ? 4 : wg::NS;
     const int per = gridDim.x / m.ngroups;
     const int gsel = blockIdx.x / per;
     const int w = blockIdx.x - gsel * per, q = w >> 3;
@@ -369,20 +373,20 @@ __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_jobs(TNJobs m) {
     auto pairs = [&]() {
         for (int i = 0; i < m.n; ++i)
             if (m.kind[i] == WJ_PAIR && m.grp[i] == gsel)
-                wg::block_any<256, 128, A, wg::JOBS_SET>(m.a[i], smem, 0, jt, sp, c++ & 1);
+                wg::block_any<256, 128, A, wg::JOBS_SET, NSJ>(m.a[i], smem, 0, jt, sp, c++ & 1);
     };
     auto narrow = [&]() {
         for (int i = 0; i < m.n; ++i) {
             const int k = m.kind[i];
             if ((k == WJ_ENC128 || k == WJ_ENC_HALF) && m.grp[i] == gsel)
-                wg::block_any<128, 64, A, wg::JOBS_SET>(m.a[i], smem, k == WJ_ENC_HALF ? 128 * jt : 0, 0,
+                wg::block_any<128, 64, A, wg::JOBS_SET, NSJ>(m.a[i], smem, k == WJ_ENC_HALF ? 128 * jt : 0, 0,
                                           k == WJ_ENC_HALF ? sp : 2 * sp + jt, c++ & 1);
         }
     };
     if constexpr (SH & 1) {
         for (int i = 0; i < m.n; ++i)
             if (m.kind[i] == WJ_WIDE && m.grp[i] == gsel)
-                wg::block_any<128, 256, A, wg::JOBS_SET>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
+                wg::block_any<128, 256, A, wg::JOBS_SET, NSJ>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
         if constexpr (SH & 2) narrow();
         pairs();
     } else if (m.ngroups > 1) {
@@ -397,7 +401,7 @@ __global__ __launch_bounds__(wg::NTH, 2) void k_wgrad_jobs(TNJobs m) {
     if constexpr (SH & 4)
         for (int i = 0; i < m.n; ++i)
             if (m.kind[i] == WJ_ENC && m.grp[i] == gsel)
-                wg::block_any<256, 64, A, wg::JOBS_SET>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
+                wg::block_any<256, 64, A, wg::JOBS_SET, NSJ>(m.a[i], smem, 0, 0, 2 * sp + jt, c++ & 1);
 }
 
 // two layers' 256 x 64 tiles in one launch: a's splits (blocks 0 .. na - 1), then b's (l4's
