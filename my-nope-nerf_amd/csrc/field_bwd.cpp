@@ -485,23 +485,24 @@ int schedule(const nerf_field_bwd& a, void* stream, void* side_stream) {
         graw4 = w.graw4;
     }
     // heads: the head-weight partials (re-reading h8 and hr).  With the input-gradient chain on
-    // the caller's stream BEFORE the chain: NERF_HEADS_PLACE 5 (the default) k_heads_bwd mode 2
-    // there and k_heads_reduce (11 blocks, ~13 us) forked to the side stream beside the chain
-    // (2.009 vs 2.030 ms/step, profiles/r05/heads_reduce_side_ab.json); 1 both on the caller's
-    // stream (~70 + 13 us in-step); 3 by k_heads_part (16-byte buffer loads, 4x the
+    // the caller's stream BEFORE the chain: NERF_HEADS_PLACE 1 (the default since round 6) k_heads_bwd
+    // mode 2 and k_heads_reduce both there (1.8609 vs 1.8665 ms/step against 5 on the round-6 weight-
+    // gradient schedule, profiles/r06/heads_place_r06_ab.txt); 5 the reduce (11 blocks, ~13 us)
+    // forked to the side stream beside the chain (the round-5 default: 2.009 vs 2.030 ms/step then,
+    // profiles/r05/heads_reduce_side_ab.json); 3 by k_heads_part (16-byte buffer loads, 4x the
     // waves: ~62 us in-step) with the reduces in the first slab batch (2.066 vs 2.058 ms/step,
     // profiles/r05/heads_part_ab.json); beside the chain (0, the round-4 placement) the partials and their reduce stretch
     // to ~240 us sharing the CUs with the chain, and the step is 13 us slower than 1
     // (profiles/r05/heads_place_ab.json; 2 = after the chain: 7 us slower).  The per-layer
     // schedule keeps them on the side stream
     const char* hp = std::getenv("NERF_HEADS_PLACE");
-    const int heads_place = a.bwd_chain ? (hp ? std::atoi(hp) : 5) : 0;
+    const int heads_place = a.bwd_chain ? (hp ? std::atoi(hp) : 1) : 0;
     auto heads = [&](hipStream_t s) -> int {
         RC(nerf_heads_bwd_mode(2, graw4, a.act[7], D, a.act[LR], HR, nullptr, 0, D, a.wc, nullptr, 0, w.part, np,
                                nullptr, nullptr, s));
         return nerf_heads_reduce(w.part, D, np, a.g_wd, a.g_bd, a.g_wc, a.g_bc, 0, s);
     };
-    // NERF_HEADS_PLACE 3 (an A/B option; 5 is the default): the partials by k_heads_part (16-byte
+    // NERF_HEADS_PLACE 3 (an A/B option; 1 is the default): the partials by k_heads_part (16-byte
     // loads, 4x the waves) before the chain, their reduces in the weight gradients' first slab batch
     nerf::SlabJobDesc hjobs[2];
     int n_hjobs = 0;
