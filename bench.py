@@ -120,9 +120,10 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 KIND_NAMES = {
     "fwd": "forward NT (nerf_linear_fwd)",
     "dx": "input-gradient NT (nerf_linear_bwd_data)",
-    "dw": "weight-gradient TN (f16x3 default: every layer's, as the two nerf_linear_bwd_weight_jobs launches of TN "
-          "schedule 3 -- [colour f | enc_d, l_f, l7, l6, l5] and [l3, l2, l1, l4 h3 | enc_p, l0]; other modes: the "
-          "256-output layers; algorithmic bytes: dy once per layer + x + dW, the split-K slabs excluded)",
+    "dw": "weight-gradient TN (f16x3 default: every layer's, as the two nerf_linear_bwd_weight_job_groups launches "
+          "of TN schedule 3, each two block groups at half the splits -- [colour f, l_f, l7 | colour enc_d, l6, l5] "
+          "and [l4 h3, l3, l0 | l4 enc_p, l2, l1]; other modes: the 256-output layers; algorithmic bytes: dy once "
+          "per layer + x + dW, the split-K slabs excluded)",
     "dw_narrow": "narrow weight-gradient TN (l0 over enc_p; the colour layer over [f | enc_d] in one launch)",
     "chain_fwd": "training forward chain (nerf_mlp_chain_train: ten linears + heads, every output saved, one launch)",
     "chain_bwd": "input-gradient chain (nerf_mlp_chain_bwd: dyr + nine input gradients, every dy saved, one launch)",
