@@ -75,6 +75,7 @@ class Trainer(object):
         self._flag_cache = {}
         self._submodules = {}      # module -> its submodule list, for the per-step train-mode check
         self._comm_timer = None    # time_collectives: the all-reduces' (start, end) hipEvents / CPU seconds
+        self._seed_one = None      # the backward's persistent d loss / d loss seed (train_step)
 
     def time_collectives(self, on=True):
         """Time every gradient all-reduce from now on (hipEvents on the launch stream around
@@ -125,7 +126,14 @@ class Trainer(object):
             runner.release_grad_buffer()       # the step's first field backward may take the bucket
         loss_dict = self.compute_loss(data, it=it, epoch=epoch, scheduling_start=scheduling_start,
                                       out_render_path=render_path)
-        loss_dict["loss"].backward()
+        loss = loss_dict["loss"]
+        # the backward's seed d loss / d loss = 1 from a persistent tensor: loss.backward() would
+        # fill a fresh one with a kernel launch every step (the same value, so the same gradients;
+        # 1.8700 vs 1.8762 ms per cfg2 step, profiles/r06/backward_seed_ab.txt)
+        seed = self._seed_one
+        if seed is None or seed.device != loss.device or seed.dtype != loss.dtype or seed.shape != loss.shape:
+            seed = self._seed_one = torch.ones_like(loss)
+        loss.backward(seed)
         if self.world_size > 1:
             self.allreduce_grads()
         for _, o in self._modules_and_optims():
