@@ -412,6 +412,13 @@ def init_ranks(args):
         if world > 1:
             dist.init_process_group("gloo")
         return world, rank, local, torch.device("cpu")
+    if world > 1 and os.environ.get("NERF_BENCH_SHARED_GPU") == "1":
+        # rehearsal of the N-rank measurement path on a one-GPU box: every rank on cuda:0, the
+        # collectives on gloo (RCCL refuses two ranks on one GPU); its numbers are not a
+        # measurement (the ranks share the GPU) and the line says so
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+        return world, rank, 0, torch.device("cuda", 0)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
@@ -733,6 +740,9 @@ def main():
                           "parallelism": f"dp{world}"},
                "final_loss": loss, "train_psnr_last_step": psnr,
                "roofline": roof, "cpu_baseline": cpu, "alt_gemm": alt, "render_cfg4": render, "full_cfg3": full}
+        if os.environ.get("NERF_BENCH_SHARED_GPU") == "1" and world > 1:
+            out["rehearsal"] = ("NERF_BENCH_SHARED_GPU: every rank on one GPU over gloo -- a check of the "
+                                "N-rank path, not a measurement")
         att = attributions.get(main_prec)
         if att is not None:
             out["world_size"] = world
