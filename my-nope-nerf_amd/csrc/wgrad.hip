@@ -83,6 +83,14 @@ __device__ __forceinline__ void load_row(float (&v)[C], const __amdgpu_buffer_rs
 // (the stage loads keep the default cache policy: nt on x made a launch 9 % slower, on dy and x
 // 27 %, profiles/r05/nt_loads_ab.txt)
 
+// The operand images hold one 16-byte fragment chunk (8 k values) per column; column col's chunk
+// sits at swz(col) (a permutation within aligned groups of 4 columns).  A load wave's column c of
+// lane l is CA l + c (CB l + c): unswizzled, the 8 lanes of a ds_write_b128 group land CA x 16 bytes
+// apart -- 4-way bank conflicts at CA = 4, more than half the kernel's LDS cycles (SQ_LDS_BANK_CONFLICT,
+// profiles/r06/wgrad_sq_r06cc.json); swizzled they cover 8 distinct 4-bank groups, and the MFMA waves'
+// reads of 32 consecutive columns stay a permutation of the same chunks (the same banks per lane group)
+__device__ __forceinline__ int swz(int col) { return col ^ ((col >> 3) & 3); }
+
 // 8 rows of one column, scaled by 2^e -> one 16-byte fragment chunk per plane
 __device__ __forceinline__ void put_strip(char* d, int plane_bytes, const float (&v)[8], int e) {
     uint32_t h[4], l[4];
@@ -174,7 +182,7 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
                 float v[8];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = va[U][i][c];
-                put_strip(ks + (lw & 1) * C::AH + (CA * lane + c) * 16, C::AP, v, ea[c]);
+                put_strip(ks + (lw & 1) * C::AH + swz(CA * lane + c) * 16, C::AP, v, ea[c]);
                 if constexpr (BIAS) {
                     float sm = 0.f;
 #pragma unroll
@@ -188,7 +196,7 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
                 float v[8];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = vb[U][i][c];
-                put_strip(ks + 2 * C::AP + (lw & 1) * C::BH + (CB * lane + c) * 16, C::BP, v, eb[c]);
+                put_strip(ks + 2 * C::AP + (lw & 1) * C::BH + swz(CB * lane + c) * 16, C::BP, v, eb[c]);
             }
             __builtin_amdgcn_sched_barrier(0);
         };
@@ -243,12 +251,12 @@ __device__ __forceinline__ void block(const TNArgs& p, char* smem, int o0, int j
             for (int j = 0; j < TN; ++j)
 #pragma unroll
                 for (int q = 0; q < 2; ++q)
-                    fb[K][j][q] = *reinterpret_cast<const uint4*>(ks + 2 * C::AP + q * C::BP + hi * C::BH + (wn0 + 32 * j + l32) * 16);
+                    fb[K][j][q] = *reinterpret_cast<const uint4*>(ks + 2 * C::AP + q * C::BP + hi * C::BH + swz(wn0 + 32 * j + l32) * 16);
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int q = 0; q < 2; ++q)
-                    fa[K][i][q] = *reinterpret_cast<const uint4*>(ks + q * C::AP + hi * C::AH + (wm0 + 32 * i + l32) * 16);
+                    fa[K][i][q] = *reinterpret_cast<const uint4*>(ks + q * C::AP + hi * C::AH + swz(wm0 + 32 * i + l32) * 16);
         };
         auto mma = [&](auto kc) {
             constexpr int K = decltype(kc)::value;

@@ -44,6 +44,9 @@ for step in "$@"; do
         wgf) RX=k_wgrad_pair; CT="FETCH_SIZE"; CMD="$R/scripts/wgrad_bench.py --loop 20" ;;
         wgw) RX=k_wgrad_pair; CT="WRITE_SIZE"; CMD="$R/scripts/wgrad_bench.py --loop 20" ;;
         wgh) RX=k_wgrad_pair; CT="TCC_HIT_sum TCC_MISS_sum"; CMD="$R/scripts/wgrad_bench.py --loop 20" ;;
+        wj1) RX=k_wgrad_jobs; CT="$C1"; CMD="$BENCH" ;;
+        wj2) RX=k_wgrad_jobs; CT="$C2"; CMD="$BENCH" ;;
+        wj3) RX=k_wgrad_jobs; CT="SQ_WAVES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES"; CMD="$BENCH" ;;
         ch1) RX=k_mlp_chain; CT="$C1"; CMD="$BENCH" ;;
         ch2) RX=k_mlp_chain; CT="$C2"; CMD="$BENCH" ;;
         ch3) RX=k_mlp_chain; CT="SQ_WAVES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_VALU_MFMA_COEXEC_CYCLES SQ_BUSY_CYCLES"; CMD="$BENCH" ;;
