@@ -47,6 +47,7 @@ for step in "$@"; do
         wj1) RX=k_wgrad_jobs; CT="$C1"; CMD="$BENCH" ;;
         wj2) RX=k_wgrad_jobs; CT="$C2"; CMD="$BENCH" ;;
         wj3) RX=k_wgrad_jobs; CT="SQ_WAVES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES"; CMD="$BENCH" ;;
+        lds) RX='k_'; CT="SQ_WAVES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_WAVE_CYCLES"; CMD="$BENCH" ;;
         ch1) RX=k_mlp_chain; CT="$C1"; CMD="$BENCH" ;;
         ch2) RX=k_mlp_chain; CT="$C2"; CMD="$BENCH" ;;
         ch3) RX=k_mlp_chain; CT="SQ_WAVES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_VALU_MFMA_COEXEC_CYCLES SQ_BUSY_CYCLES"; CMD="$BENCH" ;;
