@@ -1147,6 +1147,20 @@ __device__ __forceinline__ void enc_frag(const float* row, int t, int g, float s
     lo = make_uint4(mlo(a.x, a.y, s, hi.x), mlo(a.z, a.w, s, hi.y), mlo(b.x, b.y, s, hi.z), mlo(b.z, b.w, s, hi.w));
 }
 
+// the eval kernel's encoding tile in LDS ([128 rows][64] floats): row's float4 chunk q at
+// q ^ (row & 15), so the prologue's per-row scalar writes (64 consecutive rows per instruction,
+// 256 bytes apart) spread over the banks instead of all landing on one, and a 16-lane group of
+// enc_frag_lds's 16-byte reads (16 rows) covers 16 distinct chunks
+__device__ __forceinline__ int enc_swz(int row, int k) { return (((k >> 2) ^ (row & 15)) << 2) | (k & 3); }
+__device__ __forceinline__ void enc_frag_lds(const float* tile, int rl, int t, int g, float s, uint4& hi, uint4& lo) {
+    const float* row = tile + rl * 64;
+    const int c0 = 8 * t + 2 * g, sw = rl & 15;
+    const float4 a = *reinterpret_cast<const float4*>(row + 4 * (c0 ^ sw));
+    const float4 b = *reinterpret_cast<const float4*>(row + 4 * ((c0 + 1) ^ sw));
+    hi = make_uint4(mhi(a.x, a.y, s), mhi(a.z, a.w, s), mhi(b.x, b.y, s), mhi(b.z, b.w, s));
+    lo = make_uint4(mlo(a.x, a.y, s, hi.x), mlo(a.z, a.w, s, hi.y), mlo(b.x, b.y, s, hi.z), mlo(b.z, b.w, s, hi.w));
+}
+
 // k-step t's A fragment from tiles 2t, 2t + 1 of xs, in two halves (hi words, lo words)
 template <int t>
 __device__ __forceinline__ void split_hi(State& st) {
@@ -1587,10 +1601,15 @@ __device__ __forceinline__ void layer(const ChainFwdArgs& p, State& st) {
         split_hi<0>(st);
         split_lo<0>(st);
         if constexpr (l == 3) {   // training: the encodings in HBM
-            const float* er_row = TR ? p.enc_p + (st.m0 + st.rl) * 64
-                                     : reinterpret_cast<const float*>(st.lds + Y::O_ENC) + st.rl * 64;
-            enc_frag(er_row, 0, st.g, st.ser, st.enc_hi[0], st.enc_lo[0]);
-            enc_frag(er_row, 1, st.g, st.ser, st.enc_hi[1], st.enc_lo[1]);
+            if constexpr (TR) {
+                const float* er_row = p.enc_p + (st.m0 + st.rl) * 64;
+                enc_frag(er_row, 0, st.g, st.ser, st.enc_hi[0], st.enc_lo[0]);
+                enc_frag(er_row, 1, st.g, st.ser, st.enc_hi[1], st.enc_lo[1]);
+            } else {
+                const float* tile = reinterpret_cast<const float*>(st.lds + Y::O_ENC);
+                enc_frag_lds(tile, st.rl, 0, st.g, st.ser, st.enc_hi[0], st.enc_lo[0]);
+                enc_frag_lds(tile, st.rl, 1, st.g, st.ser, st.enc_hi[1], st.enc_lo[1]);
+            }
         }
         if constexpr (l == 8) {   // the view-direction encoding (27 columns + zeros)
             enc_frag(TR ? p.enc_d + (st.m0 + st.rl) * 64 : drec, 0, st.g, st.ser, st.enc_hi[0], st.enc_lo[0]);
@@ -1621,24 +1640,24 @@ __device__ __forceinline__ void encode_p_load(const ChainFwdArgs& p, const State
 __device__ __forceinline__ void encode_p(const ChainFwdArgs& p, State& st, const float (&x)[3], float z) {
     using Y = LY<false>;
     const int row = st.tid & 127, part = st.tid >> 7;
-    float* dst = reinterpret_cast<float*>(st.lds + Y::O_ENC) + row * 64;
+    float* dst = reinterpret_cast<float*>(st.lds + Y::O_ENC) + row * 64;   // (chunks swizzled: enc_swz)
     float m = 0.f;
     const int lv0 = part == 0 ? 0 : part == 1 ? 3 : part == 2 ? 6 : 8;
     const int lv1 = part == 0 ? 3 : part == 1 ? 6 : part == 2 ? 8 : 10;
     if (part == 0) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) { dst[c] = x[c]; m = fmaxf(m, fabsf(x[c])); }
+        for (int c = 0; c < 3; ++c) { dst[enc_swz(row, c)] = x[c]; m = fmaxf(m, fabsf(x[c])); }
         st.fx[FX_Z + row] = z;   // (to HBM in the kernel's tail: a store here would sit in the prologue's vmcnt wait)
     }
-    if (part == 3) dst[63] = 0.f;
+    if (part == 3) dst[enc_swz(row, 63)] = 0.f;
     for (int lv = lv0; lv < lv1; ++lv) {
         const float f = (float)(1 << lv);
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             float sn, cs;
             sincosf(f * x[c], &sn, &cs);
-            dst[3 + 6 * lv + c] = sn;
-            dst[6 + 6 * lv + c] = cs;
+            dst[enc_swz(row, 3 + 6 * lv + c)] = sn;
+            dst[enc_swz(row, 6 + 6 * lv + c)] = cs;
             m = fmaxf(m, fmaxf(fabsf(sn), fabsf(cs)));
         }
     }
@@ -1713,9 +1732,9 @@ __global__ __launch_bounds__(512, 2) void k_render_fused2(ChainFwdArgs p) {
         const float* rp = reinterpret_cast<const float*>(smem + Y::O_RMX);
         st.er = chain_exp(fmaxf(fmaxf(rp[st.rl], rp[128 + st.rl]), fmaxf(rp[256 + st.rl], rp[384 + st.rl])));
         st.ser = __builtin_amdgcn_ldexpf(1.f, st.er);
-        const float* row = reinterpret_cast<const float*>(smem + Y::O_ENC) + st.rl * 64;
-        enc_frag(row, 0, st.g, st.ser, st.enc_hi[0], st.enc_lo[0]);
-        enc_frag(row, 1, st.g, st.ser, st.enc_hi[1], st.enc_lo[1]);
+        const float* tile = reinterpret_cast<const float*>(smem + Y::O_ENC);
+        enc_frag_lds(tile, st.rl, 0, st.g, st.ser, st.enc_hi[0], st.enc_lo[0]);
+        enc_frag_lds(tile, st.rl, 1, st.g, st.ser, st.enc_hi[1], st.enc_lo[1]);
     }
     tick(p, st, &st.t_pro);
     chain_layers<false>(p, st);
